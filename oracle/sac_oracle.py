@@ -1,0 +1,424 @@
+"""CPU restatement of the reference's SAC / OAC / P-OAC hot path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product (``oac-explore_amd/``) may
+import this module: it is the checker the parity tests compare the HIP path
+against, and the ``cpu_baseline`` leg that ``bench.py`` times on the host.
+
+It restates, with explicit forward and backward passes written out by hand
+(no autograd), the semantics of:
+
+* ``ReplayBuffer.random_batch``        /root/reference/replay_buffer.py:106-115
+* ``np_to_pytorch_batch``              /root/reference/utils/core.py:40-61
+* ``Mlp.forward`` / ``FlattenMlp``     /root/reference/networks.py:62-79,159-161
+* ``TanhGaussianPolicy.forward``       /root/reference/trainer/policies.py:260-316
+* ``TanhNormal.log_prob / rsample``    /root/reference/trainer/policies.py:147-160,175-192
+* ``SACTrainer.train_from_torch``      /root/reference/trainer/trainer.py:126-280
+  with the torch-1.4 update order (the policy
+  gradient back-propagates through the POST-step Q weights with the PRE-step
+  activations / ReLU masks);
+* ``ParticleTrainer.train_from_torch`` /root/reference/trainer/particle_trainer_oac.py:169-363
+  (shared-layer K-head critic);
+* ``get_optimistic_exploration_action_stochastic``
+                                       /root/reference/optimistic_exploration.py:14-109
+* torch 1.4 ``optim.Adam.step`` (constructed at trainer/trainer.py:75-91) and
+  ``soft_update_from_to``              /root/reference/utils/pytorch_util.py:5-9
+
+Pinned against golden vectors produced by running the reference itself in the
+build container (tests/golden/make_golden.py -> tests/golden/*.npz); see
+tests/test_oracle_golden.py.
+
+Everything computes in ``dtype`` (float32 by default, like the reference;
+float64 is used by the tests to measure the fp32 noise floor).
+"""
+import math
+
+import numpy as np
+import torch
+
+LOG_SIG_MAX = 2.0    # trainer/policies.py:10
+LOG_SIG_MIN = -20.0  # trainer/policies.py:11
+TANH_EPS = 1e-6      # TanhNormal(epsilon=1e-6), trainer/policies.py:127
+HALF_LOG_2PI = math.log(math.sqrt(2 * math.pi))  # torch Normal.log_prob constant
+
+
+# --------------------------------------------------------------- helpers
+def _t(x, dtype):
+    if isinstance(x, torch.Tensor):
+        return x.to(dtype)
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dtype)
+
+
+def to_torch_params(d, dtype=torch.float32):
+    return {k: _t(v, dtype).clone() for k, v in d.items()}
+
+
+def linear(x, W, b):
+    """nn.Linear as torch 1.4 ran it: addmm(b, x, W.t())  (networks.py:65)."""
+    return torch.addmm(b, x, W.t())
+
+
+def n_hidden(p):
+    return sum(1 for k in p if k.startswith("fc") and k.endswith(".weight"))
+
+
+# ------------------------------------------------------------- networks
+def mlp_trunk(x, p):
+    """Hidden stack of Mlp.forward (networks.py:63-66): relu(fc_i(h))."""
+    hs = [x]
+    h = x
+    for i in range(n_hidden(p)):
+        h = torch.relu(linear(h, p[f"fc{i}.weight"], p[f"fc{i}.bias"]))
+        hs.append(h)
+    return hs
+
+
+def q_forward(obs, act, p):
+    """FlattenMlp.forward (networks.py:159-161 -> 62-79), identity output."""
+    x = torch.cat([obs, act], dim=1)
+    hs = mlp_trunk(x, p)
+    q = linear(hs[-1], p["last_fc.weight"], p["last_fc.bias"])
+    return dict(hs=hs, q=q)
+
+
+def q_param_grads(cache, dq, p):
+    """Gradient of sum(dq * Q(x)) w.r.t. every Q parameter (MSE backward
+    through Mlp.forward)."""
+    hs = cache["hs"]
+    L = len(hs) - 1
+    g = {}
+    g["last_fc.weight"] = dq.t() @ hs[L]
+    g["last_fc.bias"] = dq.sum(0)
+    dh = (dq @ p["last_fc.weight"]) * (hs[L] > 0)
+    for i in range(L - 1, -1, -1):
+        g[f"fc{i}.weight"] = dh.t() @ hs[i]
+        g[f"fc{i}.bias"] = dh.sum(0)
+        if i > 0:
+            dh = (dh @ p[f"fc{i}.weight"]) * (hs[i] > 0)
+    return g
+
+
+def q_input_grad(cache, dq, p):
+    """d sum(dq*Q)/d x, using the weights in ``p`` and the masks saved in
+    ``cache`` (this is how the torch-1.4 quirk enters: p = post-step)."""
+    hs = cache["hs"]
+    L = len(hs) - 1
+    dh = (dq @ p["last_fc.weight"]) * (hs[L] > 0)
+    for i in range(L - 1, -1, -1):
+        dh = dh @ p[f"fc{i}.weight"]
+        if i > 0:
+            dh = dh * (hs[i] > 0)
+    return dh
+
+
+def policy_forward(obs, p, eps, deterministic=False):
+    """TanhGaussianPolicy.forward(reparameterize=True, return_log_prob=True)
+    (policies.py:272-304) with TanhNormal.rsample / log_prob (175-192, 147-160);
+    ``eps`` is the standard-normal draw of ``Normal(0,1).sample()`` (183-185)."""
+    hs = mlp_trunk(obs, p)
+    h = hs[-1]
+    mean = linear(h, p["last_fc.weight"], p["last_fc.bias"])
+    ls_raw = linear(h, p["last_fc_log_std.weight"], p["last_fc_log_std.bias"])
+    log_std = torch.clamp(ls_raw, LOG_SIG_MIN, LOG_SIG_MAX)
+    std = torch.exp(log_std)
+    if deterministic:
+        a = torch.tanh(mean)
+        return dict(hs=hs, mean=mean, ls_raw=ls_raw, log_std=log_std, std=std, a=a,
+                    z=mean, logp=torch.zeros_like(a), eps=None)
+    z = mean + std * eps
+    a = torch.tanh(z)
+    var = std ** 2
+    u = z - mean
+    lp = -(u ** 2) / (2 * var) - torch.log(std) - HALF_LOG_2PI \
+        - torch.log(1 - a * a + TANH_EPS)
+    logp = lp.sum(dim=1, keepdim=True)
+    return dict(hs=hs, mean=mean, ls_raw=ls_raw, log_std=log_std, std=std, a=a, z=z,
+                logp=logp, eps=eps, u=u, var=var)
+
+
+def policy_backward(c, p, ga, G):
+    """Gradients of  sum(ga * a) + sum(G * logp)  w.r.t. the policy params.
+
+    ga: [B,Da] upstream grad on the tanh action, G: [B,1] upstream grad on
+    log_prob.  Derivatives of policies.py:154-160,179-190,275-279 (clamp passes
+    the gradient where LOG_SIG_MIN <= x <= LOG_SIG_MAX)."""
+    a, std, u, var, eps = c["a"], c["std"], c["u"], c["var"], c["eps"]
+    da = ga + G * (2 * a / (1 - a * a + TANH_EPS))
+    dz = da * (1 - a * a) - G * (u / var)
+    dmean = dz + G * (u / var)
+    dstd = dz * eps + G * (u * u * std / (var * var) - 1.0 / std)
+    dls = dstd * std
+    dls = dls * ((c["ls_raw"] >= LOG_SIG_MIN) & (c["ls_raw"] <= LOG_SIG_MAX))
+    hs = c["hs"]
+    L = len(hs) - 1
+    g = {}
+    g["last_fc.weight"] = dmean.t() @ hs[L]
+    g["last_fc.bias"] = dmean.sum(0)
+    g["last_fc_log_std.weight"] = dls.t() @ hs[L]
+    g["last_fc_log_std.bias"] = dls.sum(0)
+    dh = (dmean @ p["last_fc.weight"] + dls @ p["last_fc_log_std.weight"]) * (hs[L] > 0)
+    for i in range(L - 1, -1, -1):
+        g[f"fc{i}.weight"] = dh.t() @ hs[i]
+        g[f"fc{i}.bias"] = dh.sum(0)
+        if i > 0:
+            dh = (dh @ p[f"fc{i}.weight"]) * (hs[i] > 0)
+    return g
+
+
+# ------------------------------------------------------- optimiser / target
+class Adam14:
+    """torch 1.4.0 optim.Adam.step (no weight decay, no amsgrad)."""
+
+    def __init__(self, params, lr, betas=(0.9, 0.999), eps=1e-8):
+        self.p = params
+        self.lr, self.b1, self.b2, self.eps = lr, betas[0], betas[1], eps
+        self.m = {k: torch.zeros_like(v) for k, v in params.items()}
+        self.v = {k: torch.zeros_like(v) for k, v in params.items()}
+        self.t = 0
+
+    def step(self, grads):
+        self.t += 1
+        bc1 = 1 - self.b1 ** self.t
+        bc2 = 1 - self.b2 ** self.t
+        for k, g in grads.items():
+            m, v = self.m[k], self.v[k]
+            m.mul_(self.b1).add_(g, alpha=1 - self.b1)
+            v.mul_(self.b2).addcmul_(g, g, value=1 - self.b2)
+            denom = (v.sqrt() / math.sqrt(bc2)).add_(self.eps)
+            self.p[k].addcdiv_(m, denom, value=-(self.lr / bc1))
+
+
+def polyak(target, source, tau):
+    """soft_update_from_to (utils/pytorch_util.py:5-9)."""
+    for k in target:
+        target[k].copy_(target[k] * (1.0 - tau) + source[k] * tau)
+
+
+# ---------------------------------------------------------------- replay
+class NumpyReplay:
+    """Host float64 ring buffer + uniform gather (replay_buffer.py:32-48,88-115)
+    and the numpy->fp32 batch conversion (utils/core.py:40-61)."""
+
+    def __init__(self, data):
+        self.d = {k: np.asarray(v) for k, v in data.items()}
+        self.size = len(self.d["observations"])
+
+    def random_batch(self, B, rs=None):
+        idx = (rs or np.random).randint(0, self.size, B)
+        return idx, {k: v[idx] for k, v in self.d.items()}
+
+    @staticmethod
+    def to_torch(batch, dtype=torch.float32):
+        return {k: torch.from_numpy(np.asarray(v)).to(dtype) for k, v in batch.items()}
+
+
+# ------------------------------------------------------------------- SAC
+class SACOracle:
+    """SACTrainer.train_from_torch (trainer/trainer.py:126-280)."""
+
+    def __init__(self, params, obs_dim, act_dim, discount=0.99, reward_scale=1.0,
+                 policy_lr=3e-4, qf_lr=3e-4, tau=5e-3, target_update_period=1,
+                 auto_alpha=True, target_entropy=None, log_alpha0=0.0,
+                 dtype=torch.float32):
+        self.dtype = dtype
+        self.Do, self.Da = obs_dim, act_dim
+        self.P = to_torch_params(params["policy"], dtype)
+        self.Q1 = to_torch_params(params["qf1"], dtype)
+        self.Q2 = to_torch_params(params["qf2"], dtype)
+        self.T1 = to_torch_params(params["target_qf1"], dtype)
+        self.T2 = to_torch_params(params["target_qf2"], dtype)
+        self.discount, self.reward_scale, self.tau = discount, reward_scale, tau
+        self.period = target_update_period
+        self.auto_alpha = auto_alpha
+        self.target_entropy = -float(act_dim) if target_entropy is None else target_entropy
+        self.log_alpha = torch.full((1,), log_alpha0, dtype=dtype)
+        self.opt_p = Adam14(self.P, policy_lr)
+        self.opt_q1 = Adam14(self.Q1, qf_lr)
+        self.opt_q2 = Adam14(self.Q2, qf_lr)
+        self.opt_a = Adam14({"log_alpha": self.log_alpha}, policy_lr)
+        self.n_steps = 0
+        self.last = {}
+
+    def step(self, batch, eps1, eps2):
+        dt = self.dtype
+        obs = _t(batch["observations"], dt)
+        act = _t(batch["actions"], dt)
+        rew = _t(batch["rewards"], dt)
+        term = _t(batch["terminals"], dt)
+        nobs = _t(batch["next_observations"], dt)
+        eps1, eps2 = _t(eps1, dt), _t(eps2, dt)
+        B = obs.shape[0]
+        # E1  policy(obs)                                        trainer.py:136-138
+        pf = policy_forward(obs, self.P, eps1)
+        # E2  alpha                                              trainer.py:139-149
+        if self.auto_alpha:
+            w = (pf["logp"] + self.target_entropy)
+            g_la = (-(w / B)).sum(0)
+            alpha_loss = -(self.log_alpha * w).mean()
+            self.opt_a.step({"log_alpha": g_la})
+            alpha = self.log_alpha.exp()
+        else:
+            g_la, alpha_loss, alpha = None, torch.zeros(()), torch.zeros(1, dtype=dt)
+        # E3  min Q on the fresh actions (pre-step weights)      trainer.py:151-160
+        c1n = q_forward(obs, pf["a"], self.Q1)
+        c2n = q_forward(obs, pf["a"], self.Q2)
+        q_new = torch.min(c1n["q"], c2n["q"])
+        policy_loss = (alpha * pf["logp"] - q_new).mean()
+        # E4                                                     trainer.py:168-169
+        c1 = q_forward(obs, act, self.Q1)
+        c2 = q_forward(obs, act, self.Q2)
+        # E5                                                     trainer.py:172-174
+        pf2 = policy_forward(nobs, self.P, eps2)
+        # E6                                                     trainer.py:178-184
+        t1 = q_forward(nobs, pf2["a"], self.T1)["q"]
+        t2 = q_forward(nobs, pf2["a"], self.T2)["q"]
+        target_q = torch.min(t1, t2) - alpha * pf2["logp"]
+        y = self.reward_scale * rew + (1.0 - term) * self.discount * target_q
+        # E7                                                     trainer.py:194-196
+        qf1_loss = ((c1["q"] - y) ** 2).mean()
+        qf2_loss = ((c2["q"] - y) ** 2).mean()
+        # E8  Q1 step, Q2 step, then the policy backward          trainer.py:200-210
+        g1 = q_param_grads(c1, 2.0 * (c1["q"] - y) / B, self.Q1)
+        self.opt_q1.step(g1)
+        g2 = q_param_grads(c2, 2.0 * (c2["q"] - y) / B, self.Q2)
+        self.opt_q2.step(g2)
+        sel1 = (c1n["q"] <= c2n["q"]).to(dt)          # torch-1.4 min() backward
+        gq = -torch.ones_like(q_new) / B
+        Do = self.Do
+        da = q_input_grad(c1n, gq * sel1, self.Q1)[:, Do:] \
+            + q_input_grad(c2n, gq * (1 - sel1), self.Q2)[:, Do:]
+        G = (alpha / B) * torch.ones_like(pf["logp"])
+        gp = policy_backward(pf, self.P, da, G)
+        self.opt_p.step(gp)
+        # E9  Polyak                                              trainer.py:215-224
+        if self.n_steps % self.period == 0:
+            polyak(self.T1, self.Q1, self.tau)
+            polyak(self.T2, self.Q2, self.tau)
+        stats = self._stats(c1["q"], c2["q"], y, pf, q_new, qf1_loss, qf2_loss, alpha,
+                            alpha_loss)
+        self.n_steps += 1
+        self.last = dict(grads=dict(policy=gp, qf1=g1, qf2=g2, log_alpha=g_la),
+                         qf1_loss=qf1_loss, qf2_loss=qf2_loss, policy_loss=policy_loss,
+                         alpha=alpha, alpha_loss=alpha_loss, y=y, q1=c1["q"], q2=c2["q"],
+                         logp=pf["logp"], logp2=pf2["logp"], a=pf["a"], a2=pf2["a"],
+                         stats=stats)
+        return self.last
+
+    def _stats(self, q1, q2, y, pf, q_new, l1, l2, alpha, alpha_loss):
+        """eval_statistics keys of trainer.py:243-279 (Q5: 'Policy Loss' is
+        recomputed without alpha, :236)."""
+        n = lambda t: t.detach().to(torch.float32).numpy()
+        st = {}
+        qs = np.stack([n(q1), n(q2)], 0)
+        st["QF mean"] = np.mean(qs, axis=0).mean()
+        st["QF std"] = np.std(qs, axis=0).mean()
+        st["QF1 Loss"] = float(l1)
+        st["QF2 Loss"] = float(l2)
+        st["Q Loss"] = float(l1 + l2)
+        st["Policy Loss"] = float((pf["logp"] - q_new).mean())
+        for name, arr in (("Q1 Predictions", q1), ("Q2 Predictions", q2), ("Q Targets", y),
+                          ("Log Pis", pf["logp"]), ("Policy mu", pf["mean"]),
+                          ("Policy log std", pf["log_std"])):
+            a = n(arr)
+            st[name + " Mean"] = np.mean(a)
+            st[name + " Std"] = np.std(a)
+            st[name + " Max"] = np.max(a)
+            st[name + " Min"] = np.min(a)
+        if self.auto_alpha:
+            st["Alpha"] = float(alpha)
+            st["Alpha Loss"] = float(alpha_loss)
+        return st
+
+
+# ----------------------------------------------------------------- P-OAC
+class ParticleOACOracle:
+    """ParticleTrainer (particle_trainer_oac.py) with share_layers=True: one
+    critic with K outputs, per-sample sort over K (lines 169-363)."""
+
+    def __init__(self, params, obs_dim, act_dim, K, discount=0.99, reward_scale=1.0,
+                 policy_lr=3e-4, qf_lr=3e-4, tau=5e-3, target_update_period=1,
+                 target_entropy=None, dtype=torch.float32):
+        self.dtype = dtype
+        self.Do, self.Da, self.K = obs_dim, act_dim, K
+        self.P = to_torch_params(params["policy"], dtype)
+        self.Q = to_torch_params(params["qf1"], dtype)
+        self.T = to_torch_params(params["target_qf1"], dtype)
+        self.discount, self.reward_scale, self.tau = discount, reward_scale, tau
+        self.period = target_update_period
+        self.target_entropy = -float(act_dim) if target_entropy is None else target_entropy
+        self.log_alpha = torch.zeros(1, dtype=dtype)
+        self.opt_p = Adam14(self.P, policy_lr)
+        self.opt_q = Adam14(self.Q, qf_lr)
+        self.opt_a = Adam14({"log_alpha": self.log_alpha}, policy_lr)
+        self.n_steps = 0
+
+    def step(self, batch, eps1, eps2):
+        dt = self.dtype
+        obs = _t(batch["observations"], dt)
+        act = _t(batch["actions"], dt)
+        rew = _t(batch["rewards"], dt)
+        term = _t(batch["terminals"], dt)
+        nobs = _t(batch["next_observations"], dt)
+        eps1, eps2 = _t(eps1, dt), _t(eps2, dt)
+        B = obs.shape[0]
+        c = q_forward(obs, act, self.Q)                      # lines 185-191
+        qs = c["q"].t()                                      # [K,B]
+        sorted_qs, qs_idx = torch.sort(qs, dim=0)            # line 192
+        pf2 = policy_forward(nobs, self.P, eps1)             # 193-195
+        tq = q_forward(nobs, pf2["a"], self.T)["q"].t()      # 198-201
+        tq_sorted, _ = torch.sort(tq, dim=0)                 # 202
+        y = self.reward_scale * rew.t() + (1.0 - term.t()) * self.discount * tq_sorted  # 207-208
+        losses = ((sorted_qs - y) ** 2).mean(dim=1)          # 247-251
+        d_sorted = 2.0 * (sorted_qs - y) / B
+        dq = torch.zeros_like(qs).scatter_(0, qs_idx, d_sorted).t()   # sort backward
+        gq = q_param_grads(c, dq, self.Q)
+        self.opt_q.step(gq)                                  # 252-256
+        pf = policy_forward(obs, self.P, eps2)               # 271-273
+        w = pf["logp"] + self.target_entropy                 # 274-281
+        g_la = (-(w / B)).sum(0)
+        alpha_loss = -(self.log_alpha * w).mean()
+        self.opt_a.step({"log_alpha": g_la})
+        alpha = self.log_alpha.exp()
+        cn = q_forward(obs, pf["a"], self.Q)                 # 286 (post-step Q)
+        pq = cn["q"].t()
+        sq, sidx = torch.sort(pq, dim=0)                     # 291
+        q_new = sq[0]
+        policy_loss = (alpha * pf["logp"][:, 0] - q_new).mean()
+        gsel = torch.zeros_like(pq).scatter_(0, sidx[:1], -torch.ones_like(q_new)[None] / B).t()
+        da = q_input_grad(cn, gsel, self.Q)[:, self.Do:]
+        G = (alpha / B) * torch.ones_like(pf["logp"])
+        gp = policy_backward(pf, self.P, da, G)
+        self.opt_p.step(gp)                                  # 298-300
+        if self.n_steps % self.period == 0:                  # 320-324
+            polyak(self.T, self.Q, self.tau)
+        self.n_steps += 1
+        self.last = dict(grads=dict(policy=gp, qf=gq, log_alpha=g_la), qf_losses=losses,
+                         qf_loss=losses.sum(), policy_loss=policy_loss, alpha=alpha,
+                         alpha_loss=alpha_loss, sorted_qs=sorted_qs, y=y)
+        return self.last
+
+
+# ------------------------------------------------------- OAC exploration
+def oac_exploration_action(ob_np, P, Q1, Q2, beta_UB, delta, eps_discard, eps,
+                           dtype=torch.float32):
+    """get_optimistic_exploration_action_stochastic (optimistic_exploration.py:14-109),
+    trainer=None, two critics.  Returns (action, mu_E, std, grad)."""
+    assert np.ndim(ob_np) == 1
+    ob = _t(np.asarray(ob_np), dtype)[None]                   # from_numpy(...).float() :22
+    pf = policy_forward(ob, P, _t(eps_discard, dtype)[None])  # :27 (draw discarded)
+    mu_T, std = pf["mean"][0], pf["std"][0]
+    a = torch.tanh(mu_T)                                       # :34
+    c1 = q_forward(ob, a[None], Q1)                            # :41-44
+    c2 = q_forward(ob, a[None], Q2)
+    d = c1["q"] - c2["q"]
+    sgn = torch.sign(d)
+    w1 = 0.5 + (beta_UB / 2.0) * sgn                           # dQ_UB/dQ1 (:45-46,60)
+    w2 = 0.5 - (beta_UB / 2.0) * sgn
+    Do = ob.shape[1]
+    ga = q_input_grad(c1, w1, Q1)[0, Do:] + q_input_grad(c2, w2, Q2)[0, Do:]
+    grad = ga * (1 - a * a)                                    # tanh backward, :64
+    Sigma = torch.pow(std, 2)                                  # :71
+    denom = torch.sqrt(torch.sum(torch.mul(torch.pow(grad, 2), Sigma))) + 10e-6   # :76-80
+    mu_C = math.sqrt(2.0 * delta) * torch.mul(Sigma, grad) / denom                # :83
+    mu_E = mu_T + mu_C                                         # :87
+    action = torch.tanh(_t(eps, dtype) * std + mu_E)           # TanhNormal(mu_E,std).sample() :92-94
+    return dict(action=action, mu_E=mu_E, std=std, grad=grad, mu_T=mu_T)

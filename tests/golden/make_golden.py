@@ -1,0 +1,399 @@
+"""Generate the golden parity fixtures by running the REFERENCE itself.
+
+Runs only in the build container (it imports the read-only reference from
+/root/reference; nothing under tests/golden/*.npz contains reference code --
+only inputs and the outputs the reference produced on them).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Harness shims (all on the harness side, the reference files are untouched):
+  * ``gym`` / ``gym.spaces`` stub so ``replay_buffer.ReplayBuffer`` imports
+    (it only needs ``Box``/``Discrete``/``Tuple`` for ``get_dim``,
+    /root/reference/utils/env_utils.py:8-18);
+  * ``Adam14``: torch-1.4 Adam semantics passed through the reference's own
+    ``optimizer_class`` constructor argument (trainer/trainer.py:24,75-91).
+    It updates through ``p.data`` exactly like torch 1.4 did, which is what
+    lets ``policy_loss.backward()`` (trainer/trainer.py:209) run after the Q
+    steps and see the post-step Q weights.
+    It also records the gradient of every parameter at step() time;
+  * ``Normal.sample`` is wrapped to record the standard-normal draw eps
+    behind every sample (replayed from the saved RNG state and checked
+    bit-for-bit against the reference's own output).
+"""
+import math
+import os
+import zlib
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))  # tests/
+from fixtures_lib import sac_params, synthetic_transitions, PARAM_ORDER_POLICY, PARAM_ORDER_Q  # noqa
+
+REF = "/root/reference"
+
+
+# ----------------------------------------------------------------- gym stub
+def _install_gym_stub():
+    gym = types.ModuleType("gym")
+    spaces = types.ModuleType("gym.spaces")
+
+    class Box:
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            shape = shape if shape is not None else np.shape(low)
+            self.low = np.broadcast_to(np.asarray(low, np.float32), shape).copy()
+            self.high = np.broadcast_to(np.asarray(high, np.float32), shape).copy()
+            self.shape = tuple(shape)
+
+    class Discrete:
+        def __init__(self, n):
+            self.n = n
+
+    class Tuple:
+        def __init__(self, spaces_):
+            self.spaces = spaces_
+
+    class Env:
+        pass
+
+    spaces.Box, spaces.Discrete, spaces.Tuple = Box, Discrete, Tuple
+    gym.spaces, gym.Env = spaces, Env
+    sys.modules["gym"] = gym
+    sys.modules["gym.spaces"] = spaces
+    return Box
+
+
+Box = _install_gym_stub()
+sys.path.insert(0, REF)
+import utils.pytorch_util as ptu  # noqa: E402
+
+ptu.set_gpu_mode(False)
+from networks import FlattenMlp  # noqa: E402
+from trainer.policies import TanhGaussianPolicy  # noqa: E402
+from trainer.trainer import SACTrainer  # noqa: E402
+from trainer.particle_trainer_oac import ParticleTrainer as ParticleTrainerOAC  # noqa: E402
+from replay_buffer import ReplayBuffer  # noqa: E402
+import optimistic_exploration as oe  # noqa: E402
+
+
+# ------------------------------------------------------ torch-1.4 Adam shim
+class Adam14(torch.optim.Optimizer):
+    """torch 1.4.0 ``optim.Adam.step`` semantics (p.data updates, no version bump)."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        self.recorded = []
+
+    def step(self, closure=None):
+        rec = []
+        with torch.no_grad():
+            for group in self.param_groups:
+                b1, b2 = group["betas"]
+                for p in group["params"]:
+                    if p.grad is None:
+                        rec.append(None)
+                        continue
+                    g = p.grad.data
+                    rec.append(g.detach().clone())
+                    st = self.state[p]
+                    if len(st) == 0:
+                        st["step"] = 0
+                        st["exp_avg"] = torch.zeros_like(p.data)
+                        st["exp_avg_sq"] = torch.zeros_like(p.data)
+                    m, v = st["exp_avg"], st["exp_avg_sq"]
+                    st["step"] += 1
+                    m.mul_(b1).add_(g, alpha=1 - b1)
+                    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+                    bc1 = 1 - b1 ** st["step"]
+                    bc2 = 1 - b2 ** st["step"]
+                    denom = (v.sqrt() / math.sqrt(bc2)).add_(group["eps"])
+                    p.data.addcdiv_(m, denom, value=-(group["lr"] / bc1))
+        self.recorded.append(rec)
+
+
+# ------------------------------------------------------------ eps recorder
+EPS_LOG = []
+_orig_sample = torch.distributions.Normal.sample
+
+
+def _recording_sample(self, sample_shape=torch.Size()):
+    st = torch.get_rng_state()
+    out = _orig_sample(self, sample_shape)
+    after = torch.get_rng_state()
+    torch.set_rng_state(st)
+    shape = out.shape
+    eps = torch.normal(torch.zeros(shape), torch.ones(shape))
+    torch.set_rng_state(after)
+    recon = eps * self.scale.expand(shape) + self.loc.expand(shape)
+    assert torch.equal(recon, out), "eps replay does not reproduce Normal.sample"
+    EPS_LOG.append(eps.numpy().copy())
+    return out
+
+
+torch.distributions.Normal.sample = _recording_sample
+
+
+# ---------------------------------------------------------------- packing
+SAMPLE_N = 512
+
+
+def pack(out, key, arr, full):
+    arr = np.array(arr, np.float32, copy=True)  # state_dict tensors alias live params
+    if full or arr.size <= 2048:
+        out[key] = arr
+        return
+    flat = arr.reshape(-1)
+    rs = np.random.RandomState(zlib.crc32(key.encode()) % (2 ** 31))
+    idx = np.sort(rs.choice(flat.size, SAMPLE_N, replace=False)).astype(np.int64)
+    out[key + "#norm"] = np.array(np.linalg.norm(flat.astype(np.float64)))
+    out[key + "#idx"] = idx
+    out[key + "#val"] = flat[idx]
+    out[key + "#shape"] = np.array(arr.shape, np.int64)
+
+
+def load_sd(module, d):
+    module.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in d.items()})
+
+
+def _producers(obs_dim, act_dim, hidden, q_out=1):
+    def policy_producer(**kw):
+        return TanhGaussianPolicy(hidden_sizes=hidden, obs_dim=obs_dim, action_dim=act_dim)
+
+    def q_producer(bias=None, positive=False, train_bias=True):
+        return FlattenMlp(input_size=obs_dim + act_dim, output_size=q_out,
+                          hidden_sizes=hidden, bias=bias, positive=positive,
+                          train_bias=train_bias)
+    return policy_producer, q_producer
+
+
+def _fill_buffer(obs_dim, act_dim, n, seed=0):
+    rb = ReplayBuffer(n, Box(-1, 1, (obs_dim,)), Box(-1, 1, (act_dim,)))
+    tr = synthetic_transitions(n, obs_dim, act_dim, seed=seed)
+    for i in range(n):
+        rb.add_sample(tr["observations"][i], tr["actions"][i], tr["rewards"][i],
+                      tr["next_observations"][i], tr["terminals"][i], env_info={})
+    return rb, tr
+
+
+def _record_batch(rb, B):
+    st = np.random.get_state()
+    batch = rb.random_batch(B)
+    rs = np.random.RandomState()
+    rs.set_state(st)
+    idx = rs.randint(0, rb._size, B)
+    assert np.array_equal(batch["observations"], rb._observations[idx])
+    return batch, idx
+
+
+# -------------------------------------------------------------- SAC runs
+def gen_sac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=7,
+            pi_init_w=1e-3, q_init_w=3e-3, auto_alpha=True, log_alpha0=0.0,
+            discount=0.99, reward_scale=1.0, tau=5e-3, lr=3e-4, idx_seed=1,
+            eps_seed=2):
+    pp, qp = _producers(obs_dim, act_dim, hidden)
+    torch.manual_seed(0)
+    tr = SACTrainer(pp, qp, action_space=Box(-1, 1, (act_dim,)), discount=discount,
+                    reward_scale=reward_scale, policy_lr=lr, qf_lr=lr,
+                    optimizer_class=Adam14, soft_target_tau=tau, target_update_period=1,
+                    use_automatic_entropy_tuning=auto_alpha)
+    params = sac_params(obs_dim, act_dim, hidden, seed, pi_init_w=pi_init_w, q_init_w=q_init_w)
+    load_sd(tr.policy, params["policy"])
+    for k in ("qf1", "qf2", "target_qf1", "target_qf2"):
+        load_sd(getattr(tr, k), params[k])
+    if auto_alpha:
+        tr.log_alpha.data.fill_(log_alpha0)
+    rb, _ = _fill_buffer(obs_dim, act_dim, n_replay)
+    np.random.seed(idx_seed)
+    torch.manual_seed(eps_seed)
+    out = {}
+    meta = dict(kind="sac", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, B=B, steps=steps,
+                n_replay=n_replay, seed=seed, pi_init_w=pi_init_w, q_init_w=q_init_w,
+                auto_alpha=auto_alpha, log_alpha0=log_alpha0, discount=discount,
+                reward_scale=reward_scale, tau=tau, lr=lr, idx_seed=idx_seed,
+                eps_seed=eps_seed, target_entropy=-float(act_dim))
+    for s in range(steps):
+        EPS_LOG.clear()
+        batch, idx = _record_batch(rb, B)
+        tr.end_epoch(s)  # force the eval statistics for this step
+        tr.train(dict(batch))
+        assert len(EPS_LOG) == 2
+        out[f"s{s}/idx"] = idx.astype(np.int64)
+        out[f"s{s}/eps1"] = EPS_LOG[0]
+        out[f"s{s}/eps2"] = EPS_LOG[1]
+        stats = tr.get_diagnostics()
+        for k, v in stats.items():
+            out[f"s{s}/stat/{k}"] = np.array(v, np.float64)
+        groups = [("policy", tr.policy_optimizer, PARAM_ORDER_POLICY),
+                  ("qf1", tr.qf1_optimizer, PARAM_ORDER_Q),
+                  ("qf2", tr.qf2_optimizer, PARAM_ORDER_Q)]
+        for gname, opt, order in groups:
+            grads = opt.recorded[-1]
+            for pname, g in zip(order, grads):
+                pack(out, f"s{s}/grad/{gname}/{pname}", g.numpy(), full)
+        if auto_alpha:
+            out[f"s{s}/grad/log_alpha"] = tr.alpha_optimizer.recorded[-1][0].numpy()
+            out[f"s{s}/post/log_alpha"] = tr.log_alpha.detach().numpy().copy()
+        for gname in ("policy", "qf1", "qf2", "target_qf1", "target_qf2"):
+            for pname, t in getattr(tr, gname).state_dict().items():
+                pack(out, f"s{s}/post/{gname}/{pname}", t.numpy(), full)
+        for gname, opt in (("policy", tr.policy_optimizer), ("qf1", tr.qf1_optimizer)):
+            order = PARAM_ORDER_POLICY if gname == "policy" else PARAM_ORDER_Q
+            for pname, p in zip(order, opt.param_groups[0]["params"]):
+                st = opt.state[p]
+                pack(out, f"s{s}/adam/{gname}/{pname}/exp_avg", st["exp_avg"].numpy(), full)
+                pack(out, f"s{s}/adam/{gname}/{pname}/exp_avg_sq", st["exp_avg_sq"].numpy(), full)
+    return meta, out
+
+
+# ------------------------------------------------------------- P-OAC runs
+def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=11,
+             delta=0.95, q_min=0.0, q_max=500.0, discount=0.99, lr=3e-4, tau=5e-3,
+             idx_seed=1, eps_seed=2, pi_init_w=1e-3):
+    pp, qp = _producers(obs_dim, act_dim, hidden, q_out=K)
+    torch.manual_seed(0)
+    tr = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Box(-1, 1, (act_dim,)),
+                            discount=discount, reward_scale=1.0, delta=delta,
+                            policy_lr=lr, qf_lr=lr, optimizer_class=Adam14,
+                            soft_target_tau=tau, target_update_period=1,
+                            use_automatic_entropy_tuning=True, deterministic=False,
+                            q_min=q_min, q_max=q_max, share_layers=True)
+    bias = np.linspace(q_min, q_max, K)
+    params = sac_params(obs_dim, act_dim, hidden, seed, q_out=K, q_last_bias=bias,
+                        pi_init_w=pi_init_w)
+    load_sd(tr.policy, params["policy"])
+    load_sd(tr.qfs[0], params["qf1"])
+    load_sd(tr.tfs[0], params["target_qf1"])
+    rb, _ = _fill_buffer(obs_dim, act_dim, n_replay)
+    np.random.seed(idx_seed)
+    torch.manual_seed(eps_seed)
+    out = {}
+    meta = dict(kind="poac", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, K=K, B=B,
+                steps=steps, n_replay=n_replay, seed=seed, delta=delta, q_min=q_min,
+                q_max=q_max, discount=discount, lr=lr, tau=tau, idx_seed=idx_seed,
+                eps_seed=eps_seed, delta_index=int(tr.delta_index), pi_init_w=pi_init_w,
+                target_entropy=-float(act_dim))
+    for s in range(steps):
+        EPS_LOG.clear()
+        batch, idx = _record_batch(rb, B)
+        tr.end_epoch(s)
+        tr.train(dict(batch))
+        assert len(EPS_LOG) == 2
+        out[f"s{s}/idx"] = idx.astype(np.int64)
+        out[f"s{s}/eps1"] = EPS_LOG[0]   # drawn by policy(next_obs) (line 193)
+        out[f"s{s}/eps2"] = EPS_LOG[1]   # drawn by policy(obs) (line 271)
+        for k, v in tr.get_diagnostics().items():
+            out[f"s{s}/stat/{k}"] = np.array(v, np.float64)
+        for gname, opt, order in (("policy", tr.policy_optimizer, PARAM_ORDER_POLICY),
+                                  ("qf", tr.qf_optimizers[0], PARAM_ORDER_Q)):
+            for pname, g in zip(order, opt.recorded[-1]):
+                pack(out, f"s{s}/grad/{gname}/{pname}", g.numpy(), full)
+        out[f"s{s}/grad/log_alpha"] = tr.alpha_optimizer.recorded[-1][0].numpy()
+        out[f"s{s}/post/log_alpha"] = tr.log_alpha.detach().numpy().copy()
+        for gname, mod in (("policy", tr.policy), ("qf", tr.qfs[0]), ("tf", tr.tfs[0])):
+            for pname, t in mod.state_dict().items():
+                pack(out, f"s{s}/post/{gname}/{pname}", t.numpy(), full)
+    return meta, out
+
+
+# ------------------------------------------------------- OAC exploration
+def gen_oac_expl(name, obs_dim, act_dim, hidden, n_obs, beta_UB, delta, seed=5,
+                 pi_init_w=0.1, q_init_w=0.1, eps_seed=3):
+    pp, qp = _producers(obs_dim, act_dim, hidden)
+    policy = pp()
+    qf1, qf2 = qp(), qp()
+    params = sac_params(obs_dim, act_dim, hidden, seed, pi_init_w=pi_init_w, q_init_w=q_init_w)
+    load_sd(policy, params["policy"])
+    load_sd(qf1, params["qf1"])
+    load_sd(qf2, params["qf2"])
+    rs = np.random.RandomState(seed + 100)
+    obs = rs.standard_normal((n_obs, obs_dim))  # float64, like env observations
+    captured = []
+    orig_tn = oe.TanhNormal
+
+    class CapTN(orig_tn):
+        def __init__(self, mean, std, *a, **k):
+            captured.append((mean.detach().numpy().copy(), std.detach().numpy().copy()))
+            super().__init__(mean, std, *a, **k)
+
+    oe.TanhNormal = CapTN
+    torch.manual_seed(eps_seed)
+    out = {"obs": obs}
+    acts, mu_e, stds, eps_d, eps_s = [], [], [], [], []
+    hp = dict(beta_UB=beta_UB, delta=delta, share_layers=False)
+    try:
+        for i in range(n_obs):
+            EPS_LOG.clear()
+            captured.clear()
+            a, info = oe.get_optimistic_exploration_action(obs[i], policy=policy, qfs=[qf1, qf2],
+                                                           trainer=None, hyper_params=hp)
+            assert len(EPS_LOG) == 2 and len(captured) == 1
+            eps_d.append(EPS_LOG[0])
+            eps_s.append(EPS_LOG[1])
+            mu_e.append(captured[0][0])
+            stds.append(captured[0][1])
+            acts.append(np.asarray(a, np.float32))
+    finally:
+        oe.TanhNormal = orig_tn
+    out.update(action=np.stack(acts), mu_E=np.stack(mu_e), std=np.stack(stds),
+               eps_discard=np.stack(eps_d), eps=np.stack(eps_s))
+    meta = dict(kind="oac_expl", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, n_obs=n_obs,
+                beta_UB=beta_UB, delta=delta, seed=seed, pi_init_w=pi_init_w, q_init_w=q_init_w)
+    return meta, out
+
+
+# -------------------------------------------------------- numpy randint
+def gen_randint():
+    """Legacy MT19937 ``np.random.randint(0, size, B)`` streams, exactly as
+    ``ReplayBuffer.random_batch`` calls it (replay_buffer.py:107)."""
+    cases = [(1, 1000, 256), (1, 10000, 256), (2, 1000000, 4096), (3, 1, 64),
+             (4, 2 ** 20, 1000), (5, 2 ** 20 + 1, 1000), (6, 3, 2000), (7, 2, 100),
+             (8, 4294967295, 50), (9, 123457, 4096), (0, 2 ** 31, 300)]
+    out = {}
+    for n, (seed, size, B) in enumerate(cases):
+        np.random.seed(seed)
+        a = np.random.randint(0, size, B)
+        b = np.random.randint(0, size, B)   # continuity across calls
+        c = np.random.randint(0, 1, 7)      # rng == 0: no draw consumed
+        d = np.random.randint(0, size, B)
+        out[f"c{n}/seed"] = np.array(seed)
+        out[f"c{n}/size"] = np.array(size, np.int64)
+        out[f"c{n}/B"] = np.array(B)
+        out[f"c{n}/idx"] = np.concatenate([a, b, c, d]).astype(np.int64)
+    return dict(kind="randint", n_cases=len(cases)), out
+
+
+def save(name, meta, out):
+    import json
+    out = dict(out)
+    out["meta"] = np.array(json.dumps(meta))
+    path = os.path.join(HERE, name + ".npz")
+    np.savez_compressed(path, **out)
+    print(f"{name}: {os.path.getsize(path) / 1e3:.0f} KB, {len(out)} arrays")
+
+
+def main():
+    torch.set_num_threads(8)
+    save("randint", *gen_randint())
+    save("sac_small", *gen_sac("sac_small", 376, 17, [32, 32], 32, 3, 1000, True))
+    save("sac_stress", *gen_sac("sac_stress", 11, 3, [32, 32], 16, 3, 300, True,
+                                pi_init_w=0.7, q_init_w=0.3, log_alpha0=-0.5,
+                                discount=0.95, reward_scale=2.0, tau=0.01, lr=1e-3))
+    save("sac_noalpha", *gen_sac("sac_noalpha", 5, 2, [16, 16], 8, 2, 100, True,
+                                 auto_alpha=False, pi_init_w=0.2))
+    save("sac_riverswim", *gen_sac("sac_riverswim", 1, 1, [256, 256], 256, 2, 10000, False))
+    save("sac_humanoid", *gen_sac("sac_humanoid", 376, 17, [256, 256], 256, 3, 20000, False))
+    save("sac_humanoid_b4096", *gen_sac("sac_humanoid_b4096", 376, 17, [256, 256], 4096, 1,
+                                        20000, False))
+    save("poac_small", *gen_poac("poac_small", 111, 8, [32, 32], 10, 32, 2, 500, True,
+                                 pi_init_w=0.3))
+    save("poac_ant", *gen_poac("poac_ant", 111, 8, [256, 256], 10, 512, 2, 20000, False))
+    save("oac_expl_humanoid", *gen_oac_expl("oac_expl_humanoid", 376, 17, [256, 256], 16,
+                                            4.66, 23.53))
+    save("oac_expl_small", *gen_oac_expl("oac_expl_small", 11, 3, [32, 32], 16, 0.0, 5.0))
+
+
+if __name__ == "__main__":
+    main()
