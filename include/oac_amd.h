@@ -1,0 +1,157 @@
+/* liboac_amd -- MI355X (gfx950) native OAC/SAC gradient-step hot path.
+ *
+ * Plain C ABI: no C++ or torch types cross this boundary.  All device memory
+ * is owned by the caller (PyTorch allocates it); the library never frees a
+ * caller pointer.  Every call returns 0 on success or nonzero on failure, in
+ * which case oac_last_error() describes it.  Work is stream-ordered on the
+ * hipStream_t passed as `stream` (void*), with no host synchronisation.
+ * One handle per device; a handle is used from one host thread at a time
+ * (the reference trainer is single-threaded, launcher_util.py:90).
+ *
+ * Reference interfaces replaced (paths under /root/reference):
+ *   oac_sac_step          SACTrainer.train / train_from_torch
+ *                         (trainer/trainer.py:99-103, 126-280) incl. the
+ *                         ReplayBuffer.random_batch gather (replay_buffer.py:106-115)
+ *                         and np_to_pytorch_batch (utils/core.py:56-61)
+ *   oac_sac_step_phase    the same step split at the data-parallel exchange points
+ *   oac_particle_*        ParticleTrainer.train_from_torch, share_layers=True
+ *                         (trainer/particle_trainer_oac.py:169-363)
+ *   oac_expl_action       get_optimistic_exploration_action (stochastic branch)
+ *                         (optimistic_exploration.py:7-11, 14-109)
+ *   oac_replay_sample_indices   np.random.randint(0, size, B) (replay_buffer.py:107)
+ *   oac_replay_gather     the fancy-index gather of replay_buffer.py:108-114
+ *   oac_adam_polyak       torch optim.Adam.step (trainer/trainer.py:75-91) +
+ *                         soft_update_from_to (utils/pytorch_util.py:5-9)
+ */
+#ifndef OAC_AMD_H
+#define OAC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OAC_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- config */
+enum oac_kind { OAC_KIND_SAC = 0, OAC_KIND_PARTICLE = 1 };
+
+typedef struct oac_sac_config {
+  int kind;              /* OAC_KIND_SAC (twin critics, q_out=1) or OAC_KIND_PARTICLE */
+  int obs_dim, act_dim;
+  int hidden;            /* width of both hidden layers (reference: [M]*N, N=2) */
+  int q_out;             /* 1 for SAC/OAC; K heads for the shared-layer particle critic */
+  int batch;             /* per-rank batch size */
+  float discount, reward_scale, tau;
+  double policy_lr, qf_lr, beta1, beta2, adam_eps;
+  int auto_alpha;        /* use_automatic_entropy_tuning */
+  float target_entropy;
+  int target_update_period;
+  int row_stride;        /* floats per replay row (multiple of 4) */
+  int off_obs, off_act, off_rew, off_term, off_next_obs; /* row layout; off_act == off_obs+obs_dim */
+  uint64_t seed;         /* Philox key for the policy noise */
+  int gemm_cfg;          /* -1 auto, 0 small tiles + split-K, 1 large tiles */
+  int world_size;        /* data-parallel ranks (alpha / gradient averaging) */
+} oac_sac_config;
+
+/* Flat parameter arena layout (float offsets; every tensor 16-byte aligned).
+ * The policy block holds fc0.weight, fc0.bias, fc1.weight, fc1.bias and the
+ * two heads stacked as one [2*act_dim, hidden] matrix (rows 0..Da-1 =
+ * last_fc.weight, rows Da..2Da-1 = last_fc_log_std.weight) and their biases
+ * likewise.  Each critic block holds fc0.weight, fc0.bias, fc1.weight,
+ * fc1.bias, last_fc.weight, last_fc.bias.  Arenas: params/grads/adam_m/adam_v
+ * = [policy | critic 1 | critic 2] (one critic for PARTICLE);
+ * targets = [target critic 1 | target critic 2]. */
+typedef struct oac_sac_layout {
+  int64_t pol_fc0_w, pol_fc0_b, pol_fc1_w, pol_fc1_b, pol_head_w, pol_head_b, pol_size;
+  int64_t q_fc0_w, q_fc0_b, q_fc1_w, q_fc1_b, q_last_w, q_last_b, q_size;
+  int64_t q1_base, q2_base;   /* critic blocks in the params arena (q2_base < 0: none) */
+  int64_t n_critics;
+  int64_t params_total, targets_total;
+  int64_t workspace_floats;
+} oac_sac_layout;
+
+typedef struct oac_sac_buffers {
+  float* params; float* grads; float* adam_m; float* adam_v; float* targets;
+  void* alpha_state;     /* 8 floats: log_alpha, exp_avg, exp_avg_sq, alpha, alpha_loss, grad */
+  void* step_state;      /* 64-byte device step counters (zeroed by the caller) */
+  float* workspace;      /* layout.workspace_floats */
+  const float* replay;   /* [replay_rows, row_stride] fp32 */
+  int64_t replay_rows;
+  const int32_t* idx_ring; /* [ring_slots * batch] sampled indices */
+  int ring_slots;
+} oac_sac_buffers;
+
+typedef struct oac_sac oac_sac;
+
+/* named workspace buffers (for parity checks and diagnostics) */
+enum oac_ws_buffer {
+  OAC_WS_BATCH = 0, OAC_WS_EPS1, OAC_WS_EPS2,
+  OAC_WS_HEAD1, OAC_WS_HEAD2,          /* policy heads [B, 2Da] = mean | raw log_std */
+  OAC_WS_ACT1, OAC_WS_ACT2, OAC_WS_LOGP1, OAC_WS_LOGP2,
+  OAC_WS_Q1, OAC_WS_Q2, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_TQ2,
+  OAC_WS_Y, OAC_WS_SQE1, OAC_WS_SQE2, OAC_WS_QNEW,
+  OAC_WS_COUNT_PUBLIC
+};
+
+/* step flags */
+#define OAC_STEP_GATHER       1  /* gather the batch from the replay via idx_ring */
+#define OAC_STEP_DEVICE_EPS   2  /* draw eps1/eps2 with Philox (else caller wrote them) */
+#define OAC_STEP_USE_GRAPH    4  /* replay the captured hipGraph of the step */
+
+int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out);
+int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_sac** out);
+int oac_sac_destroy(oac_sac* h);
+int oac_sac_step(oac_sac* h, int flags, void* stream);
+/* data-parallel split: phase 0 = forward through the policy sample (local
+ * alpha partial sum in alpha_state[6]); 1 = alpha update (after the caller's
+ * all-reduce of that sum) through the critic gradients (reduced into the
+ * grads arena); 2 = critic Adam + Polyak (after the critic-grad all-reduce)
+ * through the policy gradient; 3 = policy Adam + step advance. */
+int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream);
+int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows, int64_t* cols);
+/* number of kernel launches of one step (for the launch/graph accounting) */
+int oac_sac_launch_count(oac_sac* h);
+
+/* ---------------------------------------------------------------- replay */
+/* numpy legacy seeding (init_genrand) of a 625-word MT19937 state, on the host */
+int oac_mt_seed_host(uint32_t seed, uint32_t* state625);
+/* device: out[0:count] = np.random.randint(0, size, count), advancing the
+ * device MT19937 state (625 words) bit-exactly like numpy's legacy RandomState */
+int oac_replay_sample_indices(uint32_t* mt_state_dev, uint64_t size, int count, int32_t* out,
+                              void* stream);
+/* device: out[r, :] = replay[idx[r], :] for r < B (row_stride % 4 == 0) */
+int oac_replay_gather(const float* replay, int64_t row_stride, const int32_t* idx, int B,
+                      float* out, void* stream);
+
+/* ------------------------------------------------------------------ Adam */
+int oac_adam_polyak(float* p, const float* g, float* m, float* v, int64_t n, float* target,
+                    float tau, int target_update_period, double lr, double beta1, double beta2,
+                    double eps, void* step_state, int advance, void* stream);
+
+/* -------------------------------------------------------- OAC exploration */
+typedef struct oac_expl oac_expl;
+/* policy / q1 / q2 point at their blocks in a params arena laid out as
+ * oac_sac_layout describes; workspace: oac_expl_workspace_floats() floats. */
+int64_t oac_expl_workspace_floats(int obs_dim, int act_dim, int hidden);
+int oac_expl_create(int obs_dim, int act_dim, int hidden, const float* policy, const float* q1,
+                    const float* q2, float* workspace, void* step_state, uint64_t seed,
+                    oac_expl** out);
+int oac_expl_destroy(oac_expl* h);
+/* ob: device [obs_dim] fp32 (already in the workspace slot returned by
+ * oac_expl_obs_slot, or any device pointer); eps: device [act_dim] or NULL
+ * (Philox).  Writes action[act_dim]; optional mu_E / std / grad outputs. */
+float* oac_expl_obs_slot(oac_expl* h);
+int oac_expl_action(oac_expl* h, const float* eps, float beta_UB, float delta, float* action,
+                    float* mu_E, float* std_out, float* grad_out, void* stream);
+
+/* ---------------------------------------------------------------- errors */
+const char* oac_last_error(void);
+int oac_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OAC_AMD_H */

@@ -1,0 +1,146 @@
+// Fused Adam (torch 1.4 optim.Adam.step semantics, as constructed at
+// /root/reference/trainer/trainer.py:75-91) + Polyak soft update
+// (utils/pytorch_util.py:5-9, called at trainer.py:215-224 with the POST-step
+// parameters).  HBM-bound elementwise.
+//
+// adam_seg_kernel also folds in the split-K reduction of the weight-gradient
+// GEMMs: each (W, b) pair's gradient arrives as S partial slabs
+// [S][M][K_in+1] and is summed in fixed slab order (deterministic), written to
+// the gradient arena, and applied -- one pass over p, m, v, target.
+// adam_flat_kernel is the plain flat form (data-parallel path: gradients are
+// all-reduced in the arena between the reduce pass and this one).
+#include "oac_common.h"
+#include "kernels.h"
+
+namespace oac {
+
+struct AdamConsts { float b1, omb1, b2, omb2, step_size, sbc2, eps, tau, omtau; bool polyak; };
+
+__device__ __forceinline__ AdamConsts adam_consts(const StepState* st, double lr, double beta1,
+                                                  double beta2, double eps, const float* target,
+                                                  float tau, int period) {
+  const long long nsteps = st->n_steps;
+  const double t = (double)(nsteps + 1);
+  const double bc1 = 1.0 - pow(beta1, t);
+  const double bc2 = 1.0 - pow(beta2, t);
+  AdamConsts c;
+  c.b1 = (float)beta1; c.omb1 = (float)(1.0 - beta1);
+  c.b2 = (float)beta2; c.omb2 = (float)(1.0 - beta2);
+  c.step_size = (float)(lr / bc1);
+  c.sbc2 = (float)sqrt(bc2);
+  c.eps = (float)eps;
+  c.tau = tau; c.omtau = (float)(1.0 - (double)tau);
+  c.polyak = target && (period <= 1 || (nsteps % period) == 0);
+  return c;
+}
+
+// m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g g ; p += -(lr/bc1) m / (sqrt(v)/sqrt(bc2) + eps)
+__device__ __forceinline__ void adam1(const AdamConsts& c, float& p, float g, float& m, float& v) {
+  m = __fadd_rn(__fmul_rn(m, c.b1), __fmul_rn(c.omb1, g));
+  v = __fadd_rn(__fmul_rn(v, c.b2), __fmul_rn(__fmul_rn(c.omb2, g), g));
+  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), c.sbc2), c.eps);
+  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(-c.step_size, m), denom));
+}
+
+// target = target*(1-tau) + p*tau
+__device__ __forceinline__ float polyak1(const AdamConsts& c, float t, float p) {
+  return __fadd_rn(__fmul_rn(t, c.omtau), __fmul_rn(p, c.tau));
+}
+
+__device__ __forceinline__ void advance_step(StepState* st, unsigned* ticket) {
+  __syncthreads();
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned prev = atomicAdd(ticket, 1u);
+    last = prev == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    st->n_steps += 1;
+    st->batch_counter += 1;
+    *ticket = 0u;
+  }
+}
+
+__global__ void __launch_bounds__(256) adam_seg_kernel(AdamSegArgs a) {
+  const AdamConsts c = adam_consts(a.state, a.lr, a.beta1, a.beta2, a.eps, a.target, a.tau,
+                                   a.period);
+  const long stride = (long)gridDim.x * 256;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < a.total; e += stride) {
+    int si = 0;
+#pragma unroll 1
+    for (int i = 1; i < a.nseg; ++i)
+      if (e >= a.seg[i].elem_begin) si = i;
+    const AdamSeg& s = a.seg[si];
+    const long local = e - s.elem_begin;
+    const int row = (int)(local / s.ncols);
+    const int col = (int)(local % s.ncols);
+    float g = 0.f;
+    const float* src = s.slab + local;
+#pragma unroll 1
+    for (int k = 0; k < s.S; ++k) g += src[(long)k * s.slab_stride];
+    const long idx = (col < s.ncols - 1) ? s.off_w + (long)row * (s.ncols - 1) + col : s.off_b + row;
+    a.g[idx] = g;
+    if (a.reduce_only) continue;
+    float p = a.p[idx], m = a.m[idx], v = a.v[idx];
+    adam1(c, p, g, m, v);
+    a.p[idx] = p; a.m[idx] = m; a.v[idx] = v;
+    if (c.polyak) a.target[idx] = polyak1(c, a.target[idx], p);
+  }
+  if (a.advance) advance_step(a.state, &a.state->ticket[0]);
+}
+
+__global__ void __launch_bounds__(256) adam_flat_kernel(AdamArgs a) {
+  const AdamConsts c = adam_consts(a.state, a.lr, a.beta1, a.beta2, a.eps, a.target, a.tau,
+                                   a.period);
+  const long n4 = a.n >> 2;
+  const long stride = (long)gridDim.x * 256;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
+    float4 p = reinterpret_cast<float4*>(a.p)[i];
+    const float4 g = reinterpret_cast<const float4*>(a.g)[i];
+    float4 m = reinterpret_cast<float4*>(a.m)[i];
+    float4 v = reinterpret_cast<float4*>(a.v)[i];
+    adam1(c, p.x, g.x, m.x, v.x);
+    adam1(c, p.y, g.y, m.y, v.y);
+    adam1(c, p.z, g.z, m.z, v.z);
+    adam1(c, p.w, g.w, m.w, v.w);
+    reinterpret_cast<float4*>(a.p)[i] = p;
+    reinterpret_cast<float4*>(a.m)[i] = m;
+    reinterpret_cast<float4*>(a.v)[i] = v;
+    if (c.polyak) {
+      float4 t = reinterpret_cast<float4*>(a.target)[i];
+      t.x = polyak1(c, t.x, p.x); t.y = polyak1(c, t.y, p.y);
+      t.z = polyak1(c, t.z, p.z); t.w = polyak1(c, t.w, p.w);
+      reinterpret_cast<float4*>(a.target)[i] = t;
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
+    const long i = (n4 << 2) + threadIdx.x;
+    float p = a.p[i], m = a.m[i], v = a.v[i];
+    adam1(c, p, a.g[i], m, v);
+    a.p[i] = p; a.m[i] = m; a.v[i] = v;
+    if (c.polyak) a.target[i] = polyak1(c, a.target[i], p);
+  }
+  if (a.advance) advance_step(a.state, &a.state->ticket[0]);
+}
+
+static int adam_blocks(long n) {
+  long b = (n + 255) / 256;
+  if (b > 2048) b = 2048;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+hipError_t launch_adam(const AdamArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(adam_flat_kernel, dim3(adam_blocks((a.n + 3) >> 2)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_adam_seg(const AdamSegArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(adam_seg_kernel, dim3(adam_blocks(a.total)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace oac

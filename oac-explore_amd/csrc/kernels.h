@@ -1,0 +1,154 @@
+// Kernel argument structs and launch helpers shared by the plan builders.
+#pragma once
+#include "oac_common.h"
+
+namespace oac {
+
+// ----------------------------------------------------------- Philox4x32-10
+__host__ __device__ __forceinline__ void philox4x32_10(unsigned (&c)[4], unsigned k0, unsigned k1) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    const unsigned long long p0 = (unsigned long long)0xD2511F53u * c[0];
+    const unsigned long long p1 = (unsigned long long)0xCD9E8D57u * c[2];
+    const unsigned hi0 = (unsigned)(p0 >> 32), lo0 = (unsigned)p0;
+    const unsigned hi1 = (unsigned)(p1 >> 32), lo1 = (unsigned)p1;
+    const unsigned n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+
+// One standard normal for element `idx` of draw `stream` at step `counter`
+// (Box-Muller on two 24-bit uniforms in (0,1)).
+__device__ __forceinline__ float philox_normal(unsigned long long seed, unsigned long long counter,
+                                               unsigned stream, unsigned idx) {
+  unsigned c[4] = {idx >> 1, stream, (unsigned)counter, (unsigned)(counter >> 32)};
+  philox4x32_10(c, (unsigned)seed, (unsigned)(seed >> 32));
+  const float u1 = ((float)(c[0] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  const float u2 = ((float)(c[1] >> 8) + 0.5f) * (1.0f / 16777216.0f);
+  const float r = sqrtf(-2.f * logf(u1));
+  const float th = 6.283185307179586f * u2;
+  return (idx & 1) ? r * sinf(th) : r * cosf(th);
+}
+
+// ------------------------------------------------------------- row kernels
+struct PolicySampleSeg {
+  const float* head;   // [B, 2*Da] = mean | ls_raw
+  const float* eps;    // [B, Da]
+  float* act;          // [B, Da]
+  float* stdv;         // [B, Da]
+  float* u;            // [B, Da] z - mean
+  float* logp;         // [B]
+  float* act_row;      // optional strided copy of the action (critic input)
+  long ld_act_row;
+};
+
+struct PolicySampleArgs {
+  PolicySampleSeg seg[2];
+  int B, act_dim, auto_alpha;
+  float target_entropy;
+  double lr, beta1, beta2, adam_eps;
+  float* partials;     // >= gridDim.x*gridDim.y floats
+  StepState* state;
+  AlphaState* alpha;
+};
+
+struct CriticTargetArgs {
+  const float* q1; const float* q2;     // Q_i(obs, actions)
+  const float* qn1; const float* qn2;   // Q_i(obs, a~)
+  const float* tq1; const float* tq2;   // target Q_i(next_obs, a')
+  const float* logp2;
+  const float* batch; long ld_batch; int off_rew, off_term;
+  const AlphaState* alpha;              // null -> alpha = 0
+  float reward_scale, discount;
+  int B;
+  float* y; float* dq1; float* dq2; float* gq1; float* gq2; float* sqe1; float* sqe2;
+  float* qnew;
+};
+
+struct PolicyHeadBwdArgs {
+  const float* da1; const float* da2;
+  const float* act; const float* stdv; const float* u; const float* eps;
+  const float* head;    // [B, 2Da] (ls_raw for the clamp mask)
+  const AlphaState* alpha;
+  int B, act_dim;
+  float* dhead;         // [B, 2Da]
+};
+
+struct OacArgs {
+  const float* head;    // [2Da] policy head of the observation
+  float* xrow;          // [Do+Da] critic input row: ob | tanh(mu_T)
+  float* stdv; float* mu_T;
+  const float* q1; const float* q2;
+  float* w;             // [2] dQ_UB/dQ_i
+  const float* da1; const float* da2;
+  const float* eps;     // [Da] or null -> Philox
+  float* grad; float* mu_E; float* action;
+  StepState* state;
+  unsigned long long seed;
+  float beta_UB, sqrt_2delta;
+  int obs_dim, act_dim;
+};
+
+// ------------------------------------------------------------ replay/adam
+struct GatherArgs {
+  const float* replay; long row_stride;   // [N, row_stride]
+  const int* idx;                         // ring [ring_slots * B] or [B]
+  int ring_slots;                         // 0: use idx[0:B] directly
+  float* out;                             // [B, row_stride]
+  int B;
+  // eps generation (Philox) -- skipped when eps1 == null
+  float* eps1; float* eps2; int n_eps;
+  unsigned long long seed;
+  const StepState* state;
+};
+
+struct AdamArgs {
+  float* p; const float* g; float* m; float* v; long n;
+  float* target; float tau; int period;   // target != null -> Polyak after the step
+  double lr, beta1, beta2, eps;
+  StepState* state;
+  int advance;                            // last block advances the step counters
+};
+
+// Segment-aware reduce + Adam: one segment per (weight, bias) pair whose
+// gradient was produced as split-K slabs [S][M][K_in+1] (last column = bias).
+struct AdamSeg {
+  const float* slab;
+  long slab_stride;
+  int S, M, ncols;        // ncols = K_in + 1
+  long off_w, off_b;      // arena offsets of W [M][K_in] and b [M]
+  long elem_begin;
+};
+constexpr int kMaxAdamSegs = 12;
+struct AdamSegArgs {
+  AdamSeg seg[kMaxAdamSegs];
+  int nseg;
+  long total;
+  float* p; float* g; float* m; float* v; float* target;   // arena bases
+  float tau; int period;
+  double lr, beta1, beta2, eps;
+  StepState* state;
+  int advance;
+  int reduce_only;        // 1: write the reduced gradient only (DP: all-reduce next)
+};
+
+// launchers (defined in the .hip files)
+hipError_t launch_adam_seg(const AdamSegArgs& a, hipStream_t s);
+void gemm_batch_finalize(GemmBatch& b, int cfg);
+hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s);
+int gemm_tile_m(int cfg);
+int gemm_tile_n(int cfg);
+
+hipError_t launch_policy_sample(const PolicySampleArgs& a, int nseg, hipStream_t s);
+hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s);
+hipError_t launch_policy_head_backward(const PolicyHeadBwdArgs& a, hipStream_t s);
+hipError_t launch_gather(const GatherArgs& a, hipStream_t s);
+hipError_t launch_adam(const AdamArgs& a, hipStream_t s);
+hipError_t launch_oac_prep(const OacArgs& a, hipStream_t s);
+hipError_t launch_oac_seed(const OacArgs& a, hipStream_t s);
+hipError_t launch_oac_final(const OacArgs& a, hipStream_t s);
+hipError_t launch_mt_randint(unsigned* mt_state, unsigned long long size, int count, int* out,
+                             hipStream_t s);
+
+}  // namespace oac

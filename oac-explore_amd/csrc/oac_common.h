@@ -1,0 +1,100 @@
+// Shared host/device definitions for liboac_amd (gfx950 / CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace oac {
+
+// ---------------------------------------------------------------------------
+// Grouped fp32 GEMM task:  C(m,n) = sum_k A(m,k) * B(k,n)  (+ fused epilogue)
+//
+// Operand storage is described by (row, col) of the underlying row-major
+// buffer, so one task type covers the three products of an MLP step:
+//   forward  Y  = X  . W^T   A k-contig (row=m,col=k)  B k-contig (row=n,col=k)
+//   dX       dX = dY . W     A k-contig                B n-contig (row=k,col=n)
+//   dW       dW = dY^T . X   A m-contig (row=k,col=m)  B n-contig
+// ---------------------------------------------------------------------------
+enum AMode : int {
+  A_PLAIN = 0,        // A[row*lda + col]
+  A_RANK1_MASK = 1,   // s[row] * v[col] * (mask[row*ld_mask + col] > 0)
+};
+
+enum Epi : int {
+  EPI_STORE = 0,          // C = acc
+  EPI_BIAS = 1,           // C = acc + bias[n]
+  EPI_BIAS_RELU = 2,      // C = relu(acc + bias[n])
+  EPI_BIAS_RANK_RELU = 3, // C = acc + bias[n];  C2 = relu(C + sum_j U[m,j] V[n,j])
+  EPI_ADD_RELU = 4,       // C = relu(acc + aux[m,n])
+  EPI_MASK = 5,           // C = aux[m,n] > 0 ? acc : 0
+  EPI_SLAB = 6,           // C[split*slab_stride + m*ldc + n] = acc (split-K partial)
+};
+
+struct GemmTask {
+  const float* A;
+  const float* a_s;
+  const float* a_v;
+  const float* a_mask;
+  const float* B;
+  float* C;
+  float* C2;
+  const float* bias;
+  const float* aux;
+  const float* U;
+  const float* V;
+  float* bias_grad;
+  long lda, ldb, ldc, ldc2, ld_aux, ldu, ldv, ld_mask;
+  int M, N, K;
+  int a_kc;      // 1: A(m,k) at row=m,col=k ; 0: row=k,col=m
+  int b_kc;      // 1: B(k,n) at row=n,col=k ; 0: row=k,col=n
+  int a_mode;
+  int b_ones;    // 1: column n == N-1 of B is virtual ones (dW bias column)
+  int epi;
+  int R;         // rank of the EPI_BIAS_RANK_RELU update
+  int ksplit;    // K chunks (EPI_SLAB only); chunk = kchunk (multiple of BK)
+  int kchunk;
+  long slab_stride;
+  int tile_begin;
+  int tiles_n;
+};
+
+constexpr int kMaxTasks = 8;
+
+struct GemmBatch {
+  GemmTask t[kMaxTasks];
+  int ntasks;
+  int total_tiles;
+};
+
+// ---------------------------------------------------------------------------
+// Device-resident step state (read by every kernel of a step; advanced by the
+// last block of the step's final kernel, so the launch sequence is static and
+// can be replayed as one hipGraph).
+// ---------------------------------------------------------------------------
+struct StepState {
+  long long n_steps;        // SACTrainer._n_train_steps_total
+  long long batch_counter;  // replay ring cursor / Philox counter
+  long long expl_counter;   // Philox counter for exploration draws
+  unsigned int ticket[8];   // last-block tickets (zero between kernels)
+  unsigned int pad[2];
+};
+
+// alpha state: log_alpha, exp_avg, exp_avg_sq, alpha(out), alpha_loss(out), grad
+struct AlphaState {
+  float log_alpha, m, v, alpha, alpha_loss, grad, pad0, pad1;
+};
+
+}  // namespace oac
+
+#define OAC_HIP_CHECK(expr)                                                     \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess) {                                                     \
+      oac::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr,              \
+                     hipGetErrorString(_e));                                    \
+      return 1;                                                                 \
+    }                                                                           \
+  } while (0)
+
+namespace oac {
+void set_error(const char* fmt, ...);
+}

@@ -1,0 +1,246 @@
+// Per-sample (row-parallel) kernels of the SAC/OAC step: the tanh-Gaussian
+// sample + log-prob, the alpha update, the twin-min TD target and MSE
+// gradients, and the policy-head backward.  All fp32, one thread per row (or
+// per row x action-dim), deterministic fixed-order reductions.
+#include "oac_common.h"
+#include "kernels.h"
+
+namespace oac {
+
+__device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
+
+// --------------------------------------------------------------------------
+// TanhGaussianPolicy.forward tail (trainer/policies.py:275-304):
+//   log_std = clamp(ls_raw, -20, 2); std = exp(log_std); z = mean + std*eps;
+//   a = tanh(z);  logp = sum_j [ -(z-mean)^2/(2 std^2) - log std - log sqrt(2pi)
+//                                - log(1 - a^2 + 1e-6) ]
+// y-dimension 0: obs batch (eps1), 1: next_obs batch (eps2).
+// The last block to finish also performs the alpha update of
+// trainer/trainer.py:139-146 (Adam on log_alpha, then alpha = exp(log_alpha)).
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) policy_sample_kernel(PolicySampleArgs p) {
+  __shared__ float red[256];
+  const int seg = blockIdx.y;
+  const PolicySampleSeg& s = p.seg[seg];
+  const int Da = p.act_dim;
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  float lp_row = 0.f;
+  if (r < p.B) {
+    const float* hd = s.head + (long)r * (2 * Da);
+    const float* eps = s.eps + (long)r * Da;
+    float lp = 0.f;
+    for (int j = 0; j < Da; ++j) {
+      const float mean = hd[j];
+      const float ls = fminf(fmaxf(hd[Da + j], -20.f), 2.f);
+      const float sd = expf(ls);
+      const float e = eps[j];
+      const float z = add_rn(mean, mul_rn(sd, e));
+      const float a = tanhf(z);
+      const float u = z - mean;
+      const float var = mul_rn(sd, sd);
+      const float t1 = -(mul_rn(u, u)) / (2.f * var);
+      const float l = t1 - logf(sd) - 0.918938533204672742f  // log(sqrt(2*pi))
+                      - logf(add_rn(1.f - mul_rn(a, a), 1e-6f));
+      lp += l;
+      s.act[(long)r * Da + j] = a;
+      s.stdv[(long)r * Da + j] = sd;
+      s.u[(long)r * Da + j] = u;
+      if (s.act_row) s.act_row[(long)r * s.ld_act_row + j] = a;
+    }
+    s.logp[r] = lp;
+    lp_row = lp + p.target_entropy;
+  }
+  if (!p.auto_alpha) return;
+  // block partial of sum(logp + target_entropy) over the obs segment
+  red[threadIdx.x] = (seg == 0) ? lp_row : 0.f;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const int nblk = gridDim.x * gridDim.y;
+  const int flat = blockIdx.y * gridDim.x + blockIdx.x;
+  __shared__ int last;
+  if (threadIdx.x == 0) {
+    p.partials[flat] = red[0];
+    __threadfence();
+    const unsigned prev = atomicAdd(&p.state->ticket[1], 1u);
+    last = (prev == (unsigned)(nblk - 1));
+  }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __threadfence();
+  float sum = 0.f;
+  for (int i = 0; i < gridDim.x; ++i) sum += __hip_atomic_load(&p.partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  AlphaState* as = p.alpha;
+  const float la_old = as->log_alpha;
+  const float g = -(sum / (float)p.B);
+  const double t = (double)(p.state->n_steps + 1);
+  const double bc1 = 1.0 - pow((double)p.beta1, t);
+  const double bc2 = 1.0 - pow((double)p.beta2, t);
+  float m = as->m * (float)p.beta1 + (float)(1.0 - p.beta1) * g;
+  float v = as->v * (float)p.beta2 + (float)(1.0 - p.beta2) * g * g;
+  const float denom = sqrtf(v) / (float)sqrt(bc2) + (float)p.adam_eps;
+  const float la = la_old + (-(float)(p.lr / bc1)) * m / denom;
+  as->m = m;
+  as->v = v;
+  as->grad = g;
+  as->log_alpha = la;
+  as->alpha = expf(la);
+  as->alpha_loss = -(la_old * sum) / (float)p.B;
+  p.state->ticket[1] = 0u;
+}
+
+// --------------------------------------------------------------------------
+// Twin-min TD target and critic MSE gradients (trainer/trainer.py:151-196):
+//   y  = reward_scale*r + (1-d)*gamma*(min(tq1,tq2) - alpha*logp')
+//   dq_i = 2 (q_i - y) / B ;  policy seed g_i = -1/B on the min critic
+//   (torch-1.4 min() backward: ties go to the first argument).
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) critic_targets_kernel(CriticTargetArgs p) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= p.B) return;
+  const float alpha = p.alpha ? p.alpha->alpha : 0.f;
+  const float rew = p.batch[(long)r * p.ld_batch + p.off_rew];
+  const float term = p.batch[(long)r * p.ld_batch + p.off_term];
+  const float tq = fminf(p.tq1[r], p.tq2[r]) - mul_rn(alpha, p.logp2[r]);
+  const float y = add_rn(mul_rn(p.reward_scale, rew), mul_rn(mul_rn(1.f - term, p.discount), tq));
+  const float d1 = p.q1[r] - y, d2 = p.q2[r] - y;
+  const float invB = 1.f / (float)p.B;
+  p.y[r] = y;
+  p.dq1[r] = mul_rn(2.f * d1, invB);
+  p.dq2[r] = mul_rn(2.f * d2, invB);
+  p.sqe1[r] = d1 * d1;
+  p.sqe2[r] = d2 * d2;
+  const float a = p.qn1[r], b = p.qn2[r];
+  const bool sel1 = a <= b;
+  p.qnew[r] = sel1 ? a : b;
+  p.gq1[r] = sel1 ? -invB : 0.f;
+  p.gq2[r] = sel1 ? 0.f : -invB;
+}
+
+// --------------------------------------------------------------------------
+// Policy-head backward: upstream dL/da from the critics (da1 + da2) and
+// dL/dlogp = alpha/B, through log_prob (policies.py:154-160), tanh,
+// z = mean + std*eps, std = exp(clamp(ls_raw)) (clamp passes the gradient
+// where -20 <= ls_raw <= 2).  Writes [dmean | dls_raw] per row.
+// --------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) policy_head_backward_kernel(PolicyHeadBwdArgs p) {
+  const int Da = p.act_dim;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= p.B * Da) return;
+  const int r = idx / Da, j = idx % Da;
+  const float alpha = p.alpha ? p.alpha->alpha : 0.f;
+  const float G = alpha * (1.f / (float)p.B);
+  const long e = (long)r * Da + j;
+  float ga = p.da1[e];
+  if (p.da2) ga += p.da2[e];
+  const float a = p.act[e], sd = p.stdv[e], u = p.u[e], eps = p.eps[e];
+  const float var = sd * sd;
+  const float one_m_a2 = 1.f - a * a;
+  const float da = ga + G * (2.f * a / (one_m_a2 + 1e-6f));
+  const float uv = u / var;
+  const float dz = da * one_m_a2 - G * uv;
+  const float dmean = dz + G * uv;
+  const float dstd = dz * eps + G * (u * u * sd / (var * var) - 1.f / sd);
+  const float ls_raw = p.head[(long)r * 2 * Da + Da + j];
+  const float dls = (ls_raw >= -20.f && ls_raw <= 2.f) ? dstd * sd : 0.f;
+  p.dhead[(long)r * 2 * Da + j] = dmean;
+  p.dhead[(long)r * 2 * Da + Da + j] = dls;
+}
+
+// --------------------------------------------------------------------------
+// OAC exploration (optimistic_exploration.py:14-109), batch 1.
+// prep: from the policy head (mean | ls_raw) of one observation:
+//   std = exp(clamp(ls_raw)); a = tanh(mu_T) written into the critic input row
+//   after the observation; the critic seeds w1, w2 = dQ_UB/dQ1, dQ_UB/dQ2 are
+//   computed by oac_seed_kernel once Q1, Q2 are known.
+// --------------------------------------------------------------------------
+__global__ void oac_prep_kernel(OacArgs p) {
+  const int j = threadIdx.x;
+  if (j >= p.act_dim) return;
+  const float mean = p.head[j];
+  const float ls = fminf(fmaxf(p.head[p.act_dim + j], -20.f), 2.f);
+  p.stdv[j] = expf(ls);
+  p.mu_T[j] = mean;
+  p.xrow[p.obs_dim + j] = tanhf(mean);
+}
+
+__global__ void oac_seed_kernel(OacArgs p) {
+  if (threadIdx.x != 0) return;
+  // Q_UB = (Q1+Q2)/2 + beta*|Q1-Q2|/2 ; d|x|/dx = sign(x) (0 at 0)
+  const float d = p.q1[0] - p.q2[0];
+  const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+  const float hb = p.beta_UB / 2.f;
+  p.w[0] = 0.5f + hb * sg;
+  p.w[1] = 0.5f - hb * sg;
+}
+
+// final: grad = (da1 + da2) * (1 - a^2); Sigma = std^2;
+//   denom = sqrt(sum(grad^2 Sigma)) + 1e-5; mu_C = sqrt(2 delta) Sigma grad / denom;
+//   mu_E = mu_T + mu_C;  action = tanh(eps*std + mu_E)
+__global__ void oac_final_kernel(OacArgs p) {
+  __shared__ float red[64];
+  const int j = threadIdx.x;
+  const int Da = p.act_dim;
+  float g = 0.f, sig = 0.f;
+  if (j < Da) {
+    const float a = p.xrow[p.obs_dim + j];
+    g = (p.da1[j] + p.da2[j]) * (1.f - a * a);
+    sig = p.stdv[j] * p.stdv[j];
+    red[j] = g * g * sig;
+  }
+  __syncthreads();
+  if (j == 0) {
+    float s = 0.f;
+    for (int i = 0; i < Da; ++i) s += red[i];
+    red[63] = sqrtf(s) + 10e-6f;
+  }
+  __syncthreads();
+  if (j < Da) {
+    const float denom = red[63];
+    const float mu_C = (p.sqrt_2delta * (sig * g)) / denom;
+    const float mu_E = p.mu_T[j] + mu_C;
+    float e;
+    if (p.eps) e = p.eps[j];
+    else e = philox_normal(p.seed, (unsigned long long)p.state->expl_counter, 3u, (unsigned)j);
+    p.grad[j] = g;
+    p.mu_E[j] = mu_E;
+    p.action[j] = tanhf(add_rn(mul_rn(e, p.stdv[j]), mu_E));
+  }
+  __syncthreads();
+  if (j == 0 && !p.eps) p.state->expl_counter += 1;
+}
+
+}  // namespace oac
+
+namespace oac {
+
+hipError_t launch_policy_sample(const PolicySampleArgs& a, int nseg, hipStream_t s) {
+  hipLaunchKernelGGL(policy_sample_kernel, dim3((a.B + 255) / 256, nseg), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(critic_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_policy_head_backward(const PolicyHeadBwdArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(policy_head_backward_kernel, dim3((a.B * a.act_dim + 255) / 256), dim3(256),
+                     0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_oac_prep(const OacArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(oac_prep_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_oac_seed(const OacArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(oac_seed_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_oac_final(const OacArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(oac_final_kernel, dim3(1), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace oac

@@ -1,0 +1,702 @@
+// SAC / OAC gradient step on MI355X: the launch plan behind oac_sac_step.
+//
+// Restates SACTrainer.train_from_torch (/root/reference/trainer/trainer.py:
+// 126-280) as a fixed sequence of grouped-GEMM / row / fused-Adam kernels over
+// HBM-resident flat buffers, in the reference's torch-1.4 update order:
+//   E1 policy(obs)  E2 alpha  E3 min Q(obs,a~)  E4 Q(obs,a)  E5 policy(next_obs)
+//   E6 y = r*scale + (1-d)*gamma*(min TQ(next_obs,a') - alpha*logp')
+//   E7/E8 Q1 grads -> Adam, Q2 grads -> Adam, then the policy gradient through
+//   the POST-step Q weights with the PRE-step activations,
+//   policy Adam;  E9 Polyak with the post-step critics.
+// The sequence is static (step counters live on the device), so it is
+// captured once into a hipGraph and replayed per step.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/oac_amd.h"
+#include "kernels.h"
+#include "oac_common.h"
+
+namespace oac {
+
+static thread_local char g_err[1024] = "";
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+static inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3); }
+static inline int64_t al64(int64_t x) { return (x + 63) & ~int64_t(63); }
+
+// ---------------------------------------------------------------- layout
+static void compute_layout(const oac_sac_config& c, oac_sac_layout& L) {
+  const int64_t Do = c.obs_dim, Da = c.act_dim, H = c.hidden, Q = c.q_out;
+  int64_t o = 0;
+  L.pol_fc0_w = o; o = al4(o + H * Do);
+  L.pol_fc0_b = o; o = al4(o + H);
+  L.pol_fc1_w = o; o = al4(o + H * H);
+  L.pol_fc1_b = o; o = al4(o + H);
+  L.pol_head_w = o; o = al4(o + 2 * Da * H);
+  L.pol_head_b = o; o = al4(o + 2 * Da);
+  L.pol_size = o;
+  int64_t q = 0;
+  L.q_fc0_w = q; q = al4(q + H * (Do + Da));
+  L.q_fc0_b = q; q = al4(q + H);
+  L.q_fc1_w = q; q = al4(q + H * H);
+  L.q_fc1_b = q; q = al4(q + H);
+  L.q_last_w = q; q = al4(q + Q * H);
+  L.q_last_b = q; q = al4(q + Q);
+  L.q_size = q;
+  L.n_critics = (c.kind == OAC_KIND_SAC) ? 2 : 1;
+  L.q1_base = L.pol_size;
+  L.q2_base = (L.n_critics == 2) ? L.pol_size + L.q_size : -1;
+  L.params_total = L.pol_size + L.n_critics * L.q_size;
+  L.targets_total = L.n_critics * L.q_size;
+}
+
+// Internal workspace buffers (the first OAC_WS_COUNT_PUBLIC are the public ids).
+enum Ws {
+  W_H1P = OAC_WS_COUNT_PUBLIC, W_H2P, W_H1P2, W_H2P2,
+  W_P1, W_P2, W_PT1, W_PT2, W_H1Q1, W_H1Q2, W_H2Q1, W_H2Q2,
+  W_H1N1, W_H1N2, W_H2N1, W_H2N2, W_H1T1, W_H1T2, W_H2T1, W_H2T2,
+  W_STD1, W_U1, W_STD2, W_U2, W_DQ1, W_DQ2, W_GQ1, W_GQ2,
+  W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DA1, W_DA2, W_DHEAD, W_DH2P, W_DH1P,
+  W_PARTIALS,
+  W_SLAB_Q0a, W_SLAB_Q1a, W_SLAB_QLa, W_SLAB_Q0b, W_SLAB_Q1b, W_SLAB_QLb,
+  W_SLAB_P0, W_SLAB_P1, W_SLAB_PH,
+  W_COUNT
+};
+
+struct WsBuf { int64_t off, rows, cols; };
+
+struct Split { int S, kchunk; };
+
+struct SacPlan {
+  oac_sac_config c;
+  oac_sac_layout L;
+  oac_sac_buffers b;
+  WsBuf ws[W_COUNT];
+  int cfg;  // gemm tile config
+  Split sp_q0, sp_q1, sp_ql, sp_p0, sp_p1, sp_ph;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipStream_t graph_stream = nullptr;
+  int graph_flags = -1;
+  int launches = 0;
+
+  float* W(int id) const { return b.workspace + ws[id].off; }
+  float* P(int64_t off) const { return b.params + off; }
+  float* T(int64_t off) const { return b.targets + off; }
+  StepState* state() const { return reinterpret_cast<StepState*>(b.step_state); }
+  AlphaState* alpha() const { return reinterpret_cast<AlphaState*>(b.alpha_state); }
+};
+
+static Split choose_split(int K, int tiles, int cfg) {
+  const int bk = (cfg == 0) ? 64 : 32;
+  int S = 1;
+  if (K >= 512) {
+    int want = (512 + tiles - 1) / tiles;
+    int maxS = K / 256;
+    S = want < maxS ? want : maxS;
+    if (S < 1) S = 1;
+  }
+  int kchunk = (K + S - 1) / S;
+  kchunk = ((kchunk + bk - 1) / bk) * bk;
+  S = (K + kchunk - 1) / kchunk;
+  return {S, kchunk};
+}
+
+static void layout_workspace(SacPlan& p) {
+  const oac_sac_config& c = p.c;
+  const int64_t B = c.batch, H = c.hidden, Da = c.act_dim, Do = c.obs_dim, Q = c.q_out;
+  auto set = [&](int id, int64_t r, int64_t cl) { p.ws[id] = {0, r, cl}; };
+  for (int i = 0; i < W_COUNT; ++i) p.ws[i] = {0, 0, 0};
+  set(OAC_WS_BATCH, B, c.row_stride);
+  set(OAC_WS_EPS1, B, Da); set(OAC_WS_EPS2, B, Da);
+  set(OAC_WS_HEAD1, B, 2 * Da); set(OAC_WS_HEAD2, B, 2 * Da);
+  set(OAC_WS_ACT1, B, Da); set(OAC_WS_ACT2, B, Da);
+  set(OAC_WS_LOGP1, B, 1); set(OAC_WS_LOGP2, B, 1);
+  for (int id : {OAC_WS_Q1, OAC_WS_Q2, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_TQ2}) set(id, B, Q);
+  for (int id : {OAC_WS_Y, OAC_WS_SQE1, OAC_WS_SQE2, OAC_WS_QNEW}) set(id, B, Q);
+  for (int id = W_H1P; id <= W_H2T2; ++id) set(id, B, H);
+  for (int id : {W_STD1, W_U1, W_STD2, W_U2, W_DA1, W_DA2}) set(id, B, Da);
+  for (int id : {W_DQ1, W_DQ2, W_GQ1, W_GQ2}) set(id, B, Q);
+  for (int id : {W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DH2P, W_DH1P}) set(id, B, H);
+  set(W_DHEAD, B, 2 * Da);
+  set(W_PARTIALS, 1, 4096);
+  set(W_SLAB_Q0a, (int64_t)p.sp_q0.S * H, Do + Da + 1);
+  set(W_SLAB_Q1a, (int64_t)p.sp_q1.S * H, H + 1);
+  set(W_SLAB_QLa, (int64_t)p.sp_ql.S * Q, H + 1);
+  if (p.L.n_critics == 2) {
+    set(W_SLAB_Q0b, (int64_t)p.sp_q0.S * H, Do + Da + 1);
+    set(W_SLAB_Q1b, (int64_t)p.sp_q1.S * H, H + 1);
+    set(W_SLAB_QLb, (int64_t)p.sp_ql.S * Q, H + 1);
+  }
+  set(W_SLAB_P0, (int64_t)p.sp_p0.S * H, Do + 1);
+  set(W_SLAB_P1, (int64_t)p.sp_p1.S * H, H + 1);
+  set(W_SLAB_PH, (int64_t)p.sp_ph.S * 2 * Da, H + 1);
+  int64_t off = 0;
+  for (int i = 0; i < W_COUNT; ++i) {
+    p.ws[i].off = off;
+    off = al64(off + p.ws[i].rows * p.ws[i].cols);
+  }
+  p.L.workspace_floats = off;
+}
+
+// ------------------------------------------------------------ task makers
+static GemmTask task0() {
+  GemmTask t;
+  std::memset(&t, 0, sizeof(t));
+  t.ksplit = 1;
+  return t;
+}
+
+// Y[M,N] = X[M,K] . W[N,K]^T   (W row-major [N, ldw])
+static GemmTask t_fwd(const float* X, long ldx, int M, int K, const float* W, long ldw, int N,
+                      float* C, long ldc, int epi, const float* bias) {
+  GemmTask t = task0();
+  t.A = X; t.lda = ldx; t.a_kc = 1;
+  t.B = W; t.ldb = ldw; t.b_kc = 1;
+  t.C = C; t.ldc = ldc; t.M = M; t.N = N; t.K = K;
+  t.epi = epi; t.bias = bias;
+  return t;
+}
+
+// dX[M,N] = dY[M,K] . W[K,N]  (W row-major [K, ldw]); epilogue mask from aux.
+static GemmTask t_dx(const float* dY, long lddy, int M, int K, const float* W, long ldw, int N,
+                     float* C, long ldc, const float* mask_src, long ld_mask_src) {
+  GemmTask t = task0();
+  t.A = dY; t.lda = lddy; t.a_kc = 1;
+  t.B = W; t.ldb = ldw; t.b_kc = 0;
+  t.C = C; t.ldc = ldc; t.M = M; t.N = N; t.K = K;
+  if (mask_src) { t.epi = EPI_MASK; t.aux = mask_src; t.ld_aux = ld_mask_src; }
+  else t.epi = EPI_STORE;
+  return t;
+}
+
+// dY rows given as s[b] * v[n] * (mask[b,n] > 0)  (rank-1 seed through a ReLU)
+static void set_rank1(GemmTask& t, const float* s, const float* v, const float* mask, long ldm) {
+  t.a_mode = A_RANK1_MASK; t.a_s = s; t.a_v = v; t.a_mask = mask; t.ld_mask = ldm;
+}
+
+// dW slab [S][M][Kin+1] = dY^T[M,B] . [X | 1][B, Kin+1]   (dY row-major [B, lddy])
+static GemmTask t_dw(const float* dY, long lddy, int M, int Bn, const float* X, long ldx, int Kin,
+                     float* slab, Split sp) {
+  GemmTask t = task0();
+  t.A = dY; t.lda = lddy; t.a_kc = 0;
+  t.B = X; t.ldb = ldx; t.b_kc = 0; t.b_ones = 1;
+  t.M = M; t.N = Kin + 1; t.K = Bn;
+  t.C = slab; t.ldc = Kin + 1; t.epi = EPI_SLAB;
+  t.ksplit = sp.S; t.kchunk = sp.kchunk; t.slab_stride = (long)M * (Kin + 1);
+  return t;
+}
+
+static int run_gemm(SacPlan& p, GemmBatch& gb, hipStream_t s) {
+  gemm_batch_finalize(gb, p.cfg);
+  OAC_HIP_CHECK(gemm_batch_launch(gb, p.cfg, s));
+  p.launches++;
+  return 0;
+}
+
+static void add(GemmBatch& gb, const GemmTask& t) { gb.t[gb.ntasks++] = t; }
+
+static AdamSeg seg(const float* slab, Split sp, int M, int Kin, int64_t off_w, int64_t off_b) {
+  AdamSeg s;
+  s.slab = slab; s.S = sp.S; s.M = M; s.ncols = Kin + 1;
+  s.slab_stride = (long)M * (Kin + 1);
+  s.off_w = off_w; s.off_b = off_b; s.elem_begin = 0;
+  return s;
+}
+
+static void finalize_segs(AdamSegArgs& a) {
+  long tot = 0;
+  for (int i = 0; i < a.nseg; ++i) {
+    a.seg[i].elem_begin = tot;
+    tot += (long)a.seg[i].M * a.seg[i].ncols;
+  }
+  a.total = tot;
+}
+
+// ----------------------------------------------------------------- phases
+// phase 0: gather, forward of everything that does not need alpha, policy
+//          sample (+ alpha update when world_size == 1)
+static int phase0(SacPlan& p, int flags, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
+  const int Dq = Do + Da;
+  float* X = p.W(OAC_WS_BATCH);
+  const float* obs = X + c.off_obs;
+  const float* nobs = X + c.off_next_obs;
+  const float* act = X + c.off_act;
+  if (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS)) {
+    GatherArgs g;
+    std::memset(&g, 0, sizeof(g));
+    g.replay = p.b.replay; g.row_stride = RS; g.idx = p.b.idx_ring; g.ring_slots = p.b.ring_slots;
+    g.out = X; g.B = (flags & OAC_STEP_GATHER) ? B : 0;
+    if (flags & OAC_STEP_DEVICE_EPS) {
+      g.eps1 = p.W(OAC_WS_EPS1); g.eps2 = p.W(OAC_WS_EPS2); g.n_eps = B * Da;
+    }
+    g.seed = c.seed; g.state = p.state();
+    OAC_HIP_CHECK(launch_gather(g, s));
+    p.launches++;
+  }
+  const float* pol = p.b.params;
+  const float* q1 = p.b.params + L.q1_base;
+  const float* q2 = p.b.params + L.q2_base;
+  const float* t1 = p.b.targets;
+  const float* t2 = p.b.targets + L.q_size;
+  {  // layer 0: policy(obs), policy(next_obs), critic obs-projections
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_fwd(obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
+    add(gb, t_fwd(nobs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
+    const float* qs[2] = {q1, q2};
+    const int P_[2] = {W_P1, W_P2}, H1[2] = {W_H1Q1, W_H1Q2}, PT[2] = {W_PT1, W_PT2};
+    const float* ts[2] = {t1, t2};
+    for (int i = 0; i < 2; ++i) {
+      GemmTask t = t_fwd(obs, RS, B, Do, qs[i] + L.q_fc0_w, Dq, H, p.W(P_[i]), H, EPI_BIAS_RANK_RELU,
+                         qs[i] + L.q_fc0_b);
+      t.U = act; t.ldu = RS; t.V = qs[i] + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
+      t.C2 = p.W(H1[i]); t.ldc2 = H;
+      add(gb, t);
+    }
+    for (int i = 0; i < 2; ++i)
+      add(gb, t_fwd(nobs, RS, B, Do, ts[i] + L.q_fc0_w, Dq, H, p.W(PT[i]), H, EPI_BIAS, ts[i] + L.q_fc0_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {  // layer 1
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_fwd(p.W(W_H1P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_H2P), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
+    add(gb, t_fwd(p.W(W_H1P2), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_H2P2), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
+    add(gb, t_fwd(p.W(W_H1Q1), H, B, H, q1 + L.q_fc1_w, H, H, p.W(W_H2Q1), H, EPI_BIAS_RELU, q1 + L.q_fc1_b));
+    add(gb, t_fwd(p.W(W_H1Q2), H, B, H, q2 + L.q_fc1_w, H, H, p.W(W_H2Q2), H, EPI_BIAS_RELU, q2 + L.q_fc1_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {  // heads: policy mean|log_std for obs/next_obs, q1/q2 predictions
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_fwd(p.W(W_H2P), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD1), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
+    add(gb, t_fwd(p.W(W_H2P2), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD2), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
+    add(gb, t_fwd(p.W(W_H2Q1), H, B, H, q1 + L.q_last_w, H, 1, p.W(OAC_WS_Q1), 1, EPI_BIAS, q1 + L.q_last_b));
+    add(gb, t_fwd(p.W(W_H2Q2), H, B, H, q2 + L.q_last_w, H, 1, p.W(OAC_WS_Q2), 1, EPI_BIAS, q2 + L.q_last_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {  // tanh-Gaussian sample + log-prob (+ alpha update)
+    PolicySampleArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.seg[0] = {p.W(OAC_WS_HEAD1), p.W(OAC_WS_EPS1), p.W(OAC_WS_ACT1), p.W(W_STD1), p.W(W_U1),
+                p.W(OAC_WS_LOGP1), nullptr, 0};
+    a.seg[1] = {p.W(OAC_WS_HEAD2), p.W(OAC_WS_EPS2), p.W(OAC_WS_ACT2), p.W(W_STD2), p.W(W_U2),
+                p.W(OAC_WS_LOGP2), nullptr, 0};
+    a.B = B; a.act_dim = Da; a.auto_alpha = c.auto_alpha; a.target_entropy = c.target_entropy;
+    a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.adam_eps = c.adam_eps;
+    a.partials = p.W(W_PARTIALS); a.state = p.state(); a.alpha = p.alpha();
+    OAC_HIP_CHECK(launch_policy_sample(a, 2, s));
+    p.launches++;
+  }
+  return 0;
+}
+
+// phase 1: fresh-action critics, TD target, critic gradients (split-K slabs)
+static int phase1(SacPlan& p, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
+  const int Dq = Do + Da;
+  float* X = p.W(OAC_WS_BATCH);
+  const float* q1 = p.b.params + L.q1_base;
+  const float* q2 = p.b.params + L.q2_base;
+  const float* t1 = p.b.targets;
+  const float* t2 = p.b.targets + L.q_size;
+  {  // layer 0 action part: h1 = relu(P + a . W0[:, Do:]^T)
+    GemmBatch gb; gb.ntasks = 0;
+    const float* nets[4] = {q1, q2, t1, t2};
+    const int acts[4] = {OAC_WS_ACT1, OAC_WS_ACT1, OAC_WS_ACT2, OAC_WS_ACT2};
+    const int Ps[4] = {W_P1, W_P2, W_PT1, W_PT2};
+    const int outs[4] = {W_H1N1, W_H1N2, W_H1T1, W_H1T2};
+    for (int i = 0; i < 4; ++i) {
+      GemmTask t = t_fwd(p.W(acts[i]), Da, B, Da, nets[i] + L.q_fc0_w + Do, Dq, H, p.W(outs[i]), H,
+                         EPI_ADD_RELU, nullptr);
+      t.aux = p.W(Ps[i]); t.ld_aux = H;
+      add(gb, t);
+    }
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {  // layer 1
+    GemmBatch gb; gb.ntasks = 0;
+    const float* nets[4] = {q1, q2, t1, t2};
+    const int ins[4] = {W_H1N1, W_H1N2, W_H1T1, W_H1T2};
+    const int outs[4] = {W_H2N1, W_H2N2, W_H2T1, W_H2T2};
+    for (int i = 0; i < 4; ++i)
+      add(gb, t_fwd(p.W(ins[i]), H, B, H, nets[i] + L.q_fc1_w, H, H, p.W(outs[i]), H, EPI_BIAS_RELU,
+                    nets[i] + L.q_fc1_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {  // last layer
+    GemmBatch gb; gb.ntasks = 0;
+    const float* nets[4] = {q1, q2, t1, t2};
+    const int ins[4] = {W_H2N1, W_H2N2, W_H2T1, W_H2T2};
+    const int outs[4] = {OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_TQ2};
+    for (int i = 0; i < 4; ++i)
+      add(gb, t_fwd(p.W(ins[i]), H, B, H, nets[i] + L.q_last_w, H, 1, p.W(outs[i]), 1, EPI_BIAS,
+                    nets[i] + L.q_last_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {  // TD target, MSE gradients, policy seeds
+    CriticTargetArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.q1 = p.W(OAC_WS_Q1); a.q2 = p.W(OAC_WS_Q2); a.qn1 = p.W(OAC_WS_QN1); a.qn2 = p.W(OAC_WS_QN2);
+    a.tq1 = p.W(OAC_WS_TQ1); a.tq2 = p.W(OAC_WS_TQ2); a.logp2 = p.W(OAC_WS_LOGP2);
+    a.batch = X; a.ld_batch = RS; a.off_rew = c.off_rew; a.off_term = c.off_term;
+    a.alpha = c.auto_alpha ? p.alpha() : nullptr;
+    a.reward_scale = c.reward_scale; a.discount = c.discount; a.B = B;
+    a.y = p.W(OAC_WS_Y); a.dq1 = p.W(W_DQ1); a.dq2 = p.W(W_DQ2); a.gq1 = p.W(W_GQ1); a.gq2 = p.W(W_GQ2);
+    a.sqe1 = p.W(OAC_WS_SQE1); a.sqe2 = p.W(OAC_WS_SQE2); a.qnew = p.W(OAC_WS_QNEW);
+    OAC_HIP_CHECK(launch_critic_targets(a, s));
+    p.launches++;
+  }
+  {  // critic backward, hidden layer 1 + last layer (dW slabs) and dh1
+    GemmBatch gb; gb.ntasks = 0;
+    const float* qs[2] = {q1, q2};
+    const int dq[2] = {W_DQ1, W_DQ2}, h2[2] = {W_H2Q1, W_H2Q2}, h1[2] = {W_H1Q1, W_H1Q2};
+    const int s1[2] = {W_SLAB_Q1a, W_SLAB_Q1b}, sl[2] = {W_SLAB_QLa, W_SLAB_QLb};
+    const int dh1[2] = {W_DH1Q1, W_DH1Q2};
+    for (int i = 0; i < 2; ++i) {
+      GemmTask t = t_dw(nullptr, 0, H, B, p.W(h1[i]), H, H, p.W(s1[i]), p.sp_q1);
+      set_rank1(t, p.W(dq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
+      add(gb, t);
+      add(gb, t_dw(p.W(dq[i]), 1, 1, B, p.W(h2[i]), H, H, p.W(sl[i]), p.sp_ql));
+      GemmTask d = t_dx(nullptr, 0, B, H, qs[i] + L.q_fc1_w, H, H, p.W(dh1[i]), H, p.W(h1[i]), H);
+      set_rank1(d, p.W(dq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
+      add(gb, d);
+    }
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {  // critic backward, layer 0 (input = [obs | act] contiguous in the row)
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dw(p.W(W_DH1Q1), H, H, B, X + c.off_obs, RS, Dq, p.W(W_SLAB_Q0a), p.sp_q0));
+    add(gb, t_dw(p.W(W_DH1Q2), H, H, B, X + c.off_obs, RS, Dq, p.W(W_SLAB_Q0b), p.sp_q0));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  return 0;
+}
+
+static AdamSegArgs critic_adam_args(SacPlan& p, int reduce_only) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int H = c.hidden, Dq = c.obs_dim + c.act_dim;
+  AdamSegArgs a;
+  std::memset(&a, 0, sizeof(a));
+  const int s0[2] = {W_SLAB_Q0a, W_SLAB_Q0b}, s1[2] = {W_SLAB_Q1a, W_SLAB_Q1b},
+            sl[2] = {W_SLAB_QLa, W_SLAB_QLb};
+  for (int i = 0; i < (int)L.n_critics; ++i) {
+    const int64_t base = (i == 0 ? L.q1_base : L.q2_base) - L.q1_base;  // relative to critic arena
+    a.seg[a.nseg++] = seg(p.W(s0[i]), p.sp_q0, H, Dq, base + L.q_fc0_w, base + L.q_fc0_b);
+    a.seg[a.nseg++] = seg(p.W(s1[i]), p.sp_q1, H, H, base + L.q_fc1_w, base + L.q_fc1_b);
+    a.seg[a.nseg++] = seg(p.W(sl[i]), p.sp_ql, c.q_out, H, base + L.q_last_w, base + L.q_last_b);
+  }
+  finalize_segs(a);
+  a.p = p.b.params + L.q1_base; a.g = p.b.grads + L.q1_base;
+  a.m = p.b.adam_m + L.q1_base; a.v = p.b.adam_v + L.q1_base;
+  a.target = p.b.targets;
+  a.tau = c.tau; a.period = c.target_update_period;
+  a.lr = c.qf_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
+  a.state = p.state(); a.advance = 0; a.reduce_only = reduce_only;
+  return a;
+}
+
+static AdamSegArgs policy_adam_args(SacPlan& p, int reduce_only) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int H = c.hidden, Do = c.obs_dim, Da = c.act_dim;
+  AdamSegArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.seg[a.nseg++] = seg(p.W(W_SLAB_P0), p.sp_p0, H, Do, L.pol_fc0_w, L.pol_fc0_b);
+  a.seg[a.nseg++] = seg(p.W(W_SLAB_P1), p.sp_p1, H, H, L.pol_fc1_w, L.pol_fc1_b);
+  a.seg[a.nseg++] = seg(p.W(W_SLAB_PH), p.sp_ph, 2 * Da, H, L.pol_head_w, L.pol_head_b);
+  finalize_segs(a);
+  a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.target = nullptr;
+  a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
+  a.state = p.state(); a.advance = reduce_only ? 0 : 1; a.reduce_only = reduce_only;
+  return a;
+}
+
+// phase 2: critic Adam + Polyak, policy gradient through the post-step critics
+static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
+  if (dp) {  // gradients already reduced + all-reduced in the arena: flat Adam
+    const oac_sac_layout& L = p.L;
+    AdamArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.p = p.b.params + L.q1_base; a.g = p.b.grads + L.q1_base;
+    a.m = p.b.adam_m + L.q1_base; a.v = p.b.adam_v + L.q1_base; a.n = L.n_critics * L.q_size;
+    a.target = p.b.targets; a.tau = p.c.tau; a.period = p.c.target_update_period;
+    a.lr = p.c.qf_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
+    a.state = p.state(); a.advance = 0;
+    OAC_HIP_CHECK(launch_adam(a, s));
+  } else {
+    AdamSegArgs a = critic_adam_args(p, 0);
+    OAC_HIP_CHECK(launch_adam_seg(a, s));
+  }
+  p.launches++;
+  return 0;
+}
+
+static int phase2(SacPlan& p, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
+  const int Dq = Do + Da;
+  float* X = p.W(OAC_WS_BATCH);
+  const float* pol = p.b.params;
+  const float* q1 = p.b.params + L.q1_base;
+  const float* q2 = p.b.params + L.q2_base;
+  {  // -min Q backward to layer 1 with post-step weights, pre-step masks
+    GemmBatch gb; gb.ntasks = 0;
+    const float* qs[2] = {q1, q2};
+    const int gq[2] = {W_GQ1, W_GQ2}, h2[2] = {W_H2N1, W_H2N2}, h1[2] = {W_H1N1, W_H1N2};
+    const int out[2] = {W_DH1N1, W_DH1N2};
+    for (int i = 0; i < 2; ++i) {
+      GemmTask d = t_dx(nullptr, 0, B, H, qs[i] + L.q_fc1_w, H, H, p.W(out[i]), H, p.W(h1[i]), H);
+      set_rank1(d, p.W(gq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
+      add(gb, d);
+    }
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {  // to the action columns of layer 0
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dx(p.W(W_DH1N1), H, B, H, q1 + L.q_fc0_w + Do, Dq, Da, p.W(W_DA1), Da, nullptr, 0));
+    add(gb, t_dx(p.W(W_DH1N2), H, B, H, q2 + L.q_fc0_w + Do, Dq, Da, p.W(W_DA2), Da, nullptr, 0));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    PolicyHeadBwdArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.da1 = p.W(W_DA1); a.da2 = p.W(W_DA2); a.act = p.W(OAC_WS_ACT1); a.stdv = p.W(W_STD1);
+    a.u = p.W(W_U1); a.eps = p.W(OAC_WS_EPS1); a.head = p.W(OAC_WS_HEAD1);
+    a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.B = B; a.act_dim = Da; a.dhead = p.W(W_DHEAD);
+    OAC_HIP_CHECK(launch_policy_head_backward(a, s));
+    p.launches++;
+  }
+  {  // policy heads: dW_head slab, dh2
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, p.W(W_SLAB_PH), p.sp_ph));
+    add(gb, t_dx(p.W(W_DHEAD), 2 * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(W_DH2P), H, p.W(W_H2P), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {  // policy layer 1
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, p.W(W_SLAB_P1), p.sp_p1));
+    add(gb, t_dx(p.W(W_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_DH1P), H, p.W(W_H1P), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {  // policy layer 0
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dw(p.W(W_DH1P), H, H, B, X + c.off_obs, RS, Do, p.W(W_SLAB_P0), p.sp_p0));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  return 0;
+}
+
+static int run_step(SacPlan& p, int flags, hipStream_t s) {
+  p.launches = 0;
+  if (phase0(p, flags, s)) return 1;
+  if (phase1(p, s)) return 1;
+  if (phase2_adam(p, s, 0)) return 1;
+  if (phase2(p, s)) return 1;
+  AdamSegArgs a = policy_adam_args(p, 0);
+  OAC_HIP_CHECK(launch_adam_seg(a, s));
+  p.launches++;
+  return 0;
+}
+
+}  // namespace oac
+
+using namespace oac;
+
+struct oac_sac {
+  SacPlan plan;
+};
+
+extern "C" {
+
+const char* oac_last_error(void) { return g_err; }
+int oac_abi_version(void) { return OAC_ABI_VERSION; }
+
+static int validate(const oac_sac_config* c) {
+  if (!c) { set_error("null config"); return 1; }
+  if (c->kind != OAC_KIND_SAC && c->kind != OAC_KIND_PARTICLE) { set_error("bad kind %d", c->kind); return 1; }
+  if (c->kind == OAC_KIND_SAC && c->q_out != 1) { set_error("SAC needs q_out == 1"); return 1; }
+  if (c->obs_dim < 1 || c->act_dim < 1 || c->act_dim > 64 || c->hidden < 1 || c->batch < 1) {
+    set_error("bad dims obs=%d act=%d hidden=%d batch=%d", c->obs_dim, c->act_dim, c->hidden, c->batch);
+    return 1;
+  }
+  if (c->row_stride % 4 != 0) { set_error("row_stride must be a multiple of 4"); return 1; }
+  if (c->off_act != c->off_obs + c->obs_dim) { set_error("row layout: act must follow obs"); return 1; }
+  if (c->off_obs < 0 || c->off_next_obs + c->obs_dim > c->row_stride ||
+      c->off_act + c->act_dim > c->row_stride || c->off_rew >= c->row_stride ||
+      c->off_term >= c->row_stride) {
+    set_error("row layout out of bounds");
+    return 1;
+  }
+  return 0;
+}
+
+static void plan_splits(SacPlan& p) {
+  const oac_sac_config& c = p.c;
+  p.cfg = c.gemm_cfg >= 0 ? c.gemm_cfg : (c.batch >= 1024 ? 1 : 0);
+  const int tm = gemm_tile_m(p.cfg), tn = gemm_tile_n(p.cfg);
+  auto tiles = [&](int M, int N) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
+  const int H = c.hidden, Dq = c.obs_dim + c.act_dim, Do = c.obs_dim, Da = c.act_dim;
+  const int nq = (c.kind == OAC_KIND_SAC) ? 2 : 1;
+  p.sp_q1 = choose_split(c.batch, nq * (tiles(H, H + 1) + tiles(c.q_out, H + 1)), p.cfg);
+  p.sp_ql = p.sp_q1;
+  p.sp_q0 = choose_split(c.batch, nq * tiles(H, Dq + 1), p.cfg);
+  p.sp_ph = choose_split(c.batch, tiles(2 * Da, H + 1), p.cfg);
+  p.sp_p1 = choose_split(c.batch, tiles(H, H + 1), p.cfg);
+  p.sp_p0 = choose_split(c.batch, tiles(H, Do + 1), p.cfg);
+}
+
+int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out) {
+  if (validate(cfg)) return 1;
+  SacPlan p;
+  p.c = *cfg;
+  compute_layout(p.c, p.L);
+  plan_splits(p);
+  layout_workspace(p);
+  *out = p.L;
+  return 0;
+}
+
+int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_sac** out) {
+  if (validate(cfg)) return 1;
+  if (!bufs || !out) { set_error("null buffers/out"); return 1; }
+  if (cfg->kind != OAC_KIND_SAC) { set_error("use the particle entry points for kind=PARTICLE"); return 1; }
+  oac_sac* h = new oac_sac();
+  SacPlan& p = h->plan;
+  p.c = *cfg;
+  compute_layout(p.c, p.L);
+  plan_splits(p);
+  layout_workspace(p);
+  p.b = *bufs;
+  *out = h;
+  return 0;
+}
+
+int oac_sac_destroy(oac_sac* h) {
+  if (!h) return 0;
+  if (h->plan.exec) (void)hipGraphExecDestroy(h->plan.exec);
+  if (h->plan.graph) (void)hipGraphDestroy(h->plan.graph);
+  delete h;
+  return 0;
+}
+
+int oac_sac_step(oac_sac* h, int flags, void* stream) {
+  if (!h) { set_error("null handle"); return 1; }
+  SacPlan& p = h->plan;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!(flags & OAC_STEP_USE_GRAPH)) return run_step(p, flags, s);
+  const int gflags = flags & ~OAC_STEP_USE_GRAPH;
+  if (!p.exec || p.graph_stream != s || p.graph_flags != gflags) {
+    if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
+    if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
+    OAC_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    const int rc = run_step(p, gflags, s);
+    hipGraph_t g = nullptr;
+    const hipError_t e = hipStreamEndCapture(s, &g);
+    if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
+    if (e != hipSuccess) { set_error("hipStreamEndCapture: %s", hipGetErrorString(e)); return 1; }
+    p.graph = g;
+    OAC_HIP_CHECK(hipGraphInstantiate(&p.exec, p.graph, nullptr, nullptr, 0));
+    p.graph_stream = s;
+    p.graph_flags = gflags;
+  }
+  OAC_HIP_CHECK(hipGraphLaunch(p.exec, s));
+  return 0;
+}
+
+int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
+  if (!h) { set_error("null handle"); return 1; }
+  SacPlan& p = h->plan;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  switch (phase) {
+    case 0: return phase0(p, flags, s);
+    case 1: return phase1(p, s) ? 1 : [&] {
+        AdamSegArgs a = critic_adam_args(p, 1);
+        OAC_HIP_CHECK(launch_adam_seg(a, s));
+        return 0;
+      }();
+    case 2:
+      if (phase2_adam(p, s, 1)) return 1;
+      if (phase2(p, s)) return 1;
+      {
+        AdamSegArgs a = policy_adam_args(p, 1);
+        OAC_HIP_CHECK(launch_adam_seg(a, s));
+      }
+      return 0;
+    case 3: {
+      const oac_sac_layout& L = p.L;
+      AdamArgs a;
+      std::memset(&a, 0, sizeof(a));
+      a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.n = L.pol_size;
+      a.lr = p.c.policy_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
+      a.state = p.state(); a.advance = 1;
+      OAC_HIP_CHECK(launch_adam(a, s));
+      return 0;
+    }
+    default:
+      set_error("bad phase %d", phase);
+      return 1;
+  }
+}
+
+int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows, int64_t* cols) {
+  if (!h || which < 0 || which >= OAC_WS_COUNT_PUBLIC) { set_error("bad workspace id"); return 1; }
+  const WsBuf& w = h->plan.ws[which];
+  *offset = w.off; *rows = w.rows; *cols = w.cols;
+  return 0;
+}
+
+int oac_sac_launch_count(oac_sac* h) { return h ? h->plan.launches : 0; }
+
+int oac_adam_polyak(float* p, const float* g, float* m, float* v, int64_t n, float* target,
+                    float tau, int period, double lr, double beta1, double beta2, double eps,
+                    void* step_state, int advance, void* stream) {
+  AdamArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.p = p; a.g = g; a.m = m; a.v = v; a.n = n; a.target = target; a.tau = tau; a.period = period;
+  a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps;
+  a.state = reinterpret_cast<StepState*>(step_state); a.advance = advance;
+  OAC_HIP_CHECK(launch_adam(a, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+int oac_mt_seed_host(uint32_t seed, uint32_t* st) {
+  if (!st) { set_error("null state"); return 1; }
+  st[0] = seed;
+  for (int i = 1; i < 624; ++i) st[i] = 1812433253u * (st[i - 1] ^ (st[i - 1] >> 30)) + (uint32_t)i;
+  st[624] = 624;
+  return 0;
+}
+
+int oac_replay_sample_indices(uint32_t* mt_state_dev, uint64_t size, int count, int32_t* out,
+                              void* stream) {
+  if (size == 0 || size > (1ull << 32)) { set_error("size must be in [1, 2^32]"); return 1; }
+  OAC_HIP_CHECK(launch_mt_randint(mt_state_dev, size, count, out, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+int oac_replay_gather(const float* replay, int64_t row_stride, const int32_t* idx, int B,
+                      float* out, void* stream) {
+  if (row_stride % 4) { set_error("row_stride must be a multiple of 4"); return 1; }
+  GatherArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.replay = replay; g.row_stride = row_stride; g.idx = idx; g.ring_slots = 0; g.out = out; g.B = B;
+  g.state = nullptr;  // no ring: the gather reads idx[0:B]
+  OAC_HIP_CHECK(launch_gather(g, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,61 @@
+"""Drop-in ``get_optimistic_exploration_action``
+(/root/reference/optimistic_exploration.py:7-11) -- the OAC action shift,
+computed by liboac_amd's batch-1 kernel sequence (csrc/expl_plan.hip).
+
+Same signature and return value as the reference: ``(action float32[Da], {})``
+for a 1-D observation.  ``policy`` must be the policy of an oac_amd trainer
+(its parameters live in the trainer's HBM arena, which the kernels read in
+place); there is no torch/CPU fallback.
+"""
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr
+
+
+def _owner(policy, qfs, trainer):
+    t = getattr(policy, "oac_trainer", None)
+    if t is None:
+        raise TypeError("get_optimistic_exploration_action: policy is not an oac_amd policy "
+                        "(build the trainer with oac_amd.SACTrainer)")
+    if qfs is not None and (len(qfs) != 2 or qfs[0] is not t.qf1 or qfs[1] is not t.qf2):
+        raise NotImplementedError("oac_amd implements the two-critic (trainer.qfs) OAC shift")
+    if trainer is not None and trainer is not t:
+        raise NotImplementedError("trainer_UB must be the trainer that owns the policy")
+    return t
+
+
+def get_optimistic_exploration_action(ob_np, policy=None, qfs=None, trainer=None,
+                                      hyper_params=None, deterministic=False, eps=None,
+                                      return_info=False):
+    """optimistic_exploration.py:7-11 / 14-109 (stochastic branch).
+
+    ``trainer`` (--trainer_UB) computes the same Q_UB = mean + beta_UB*|Q1-Q2|/2
+    as the qfs branch (trainer/trainer.py:105-123), so both map to the same
+    kernel.  ``eps`` (float32[Da]) replaces the device Philox draw for parity
+    runs; ``return_info`` adds mu_E / std / grad to the info dict."""
+    if deterministic:
+        raise NotImplementedError("the deterministic OAC variant is unreachable from rollout() "
+                                  "(SURVEY 8a quirk Q7) and not implemented")
+    assert np.ndim(ob_np) == 1
+    t = _owner(policy, qfs, trainer)
+    if hyper_params.get("share_layers", False):
+        raise NotImplementedError("share_layers OAC shift: use oac_amd.ParticleTrainer")
+    h, ws, slot, out = t._expl_handle()
+
+    def go(sp):
+        slot.copy_(torch.as_tensor(np.asarray(ob_np)).to(torch.float32), non_blocking=False)
+        e = None
+        if eps is not None:
+            e = out[3]
+            e.copy_(torch.as_tensor(np.asarray(eps, np.float32)))
+        check(_lib.lib().oac_expl_action(h, ptr(e), float(hyper_params["beta_UB"]),
+                                         float(hyper_params["delta"]), ptr(out[0]), ptr(out[1]),
+                                         ptr(out[2]), None, sp))
+        return out[:3].cpu().numpy()
+    res = t._on_stream(go)
+    info = {}
+    if return_info:
+        info = dict(mu_E=res[1].copy(), std=res[2].copy())
+    return res[0].copy(), info

@@ -1,0 +1,235 @@
+"""Drop-in ``ReplayBuffer`` (/root/reference/replay_buffer.py:8-148) with the
+transitions resident in HBM as fp32 rows.
+
+Row layout (``trainer.row_layout``): ``[obs | act | rew | term | next_obs | pad]``.
+Storing fp32 at insert time is bit-identical to the reference's float64 store
+converted at sample time (``ptu.from_numpy(...).float()``, utils/core.py:45,
+utils/pytorch_util.py:77): rounding f64->f32 is the same operation either way.
+
+``random_batch(B)`` draws the indices exactly like the reference
+(``np.random.randint(0, self._size, B)`` on numpy's global legacy MT19937,
+replay_buffer.py:107) and returns a ``DeviceBatch``; ``SACTrainer.train``
+gathers the rows on the GPU inside the step.  ``index_source='device'``
+draws the same stream (np.random.seed(s) semantics) with the device MT19937
+kernel instead, so no host work is needed per step.
+"""
+import ctypes
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, ptr, stream_ptr
+from .trainer import row_layout
+
+BATCH_KEYS = ("observations", "actions", "rewards", "terminals", "next_observations")
+
+
+def get_dim(space):
+    """utils/env_utils.py:8-18."""
+    if isinstance(space, (int, np.integer)):
+        return int(space)
+    if hasattr(space, "low"):
+        return int(np.asarray(space.low).size)
+    if hasattr(space, "n"):
+        return int(space.n)
+    if hasattr(space, "spaces"):
+        return sum(get_dim(s) for s in space.spaces)
+    if hasattr(space, "flat_dim"):
+        return space.flat_dim
+    raise TypeError(f"Unknown space: {space}")
+
+
+class DeviceBatch(dict):
+    """The batch dict ``random_batch`` returns: indices on the device plus a
+    reference to the HBM store.  Reading a key (e.g. rl_algorithm's
+    ``save_sampled_data`` path) gathers that field on the GPU on demand."""
+
+    device_gather = True
+
+    def __init__(self, buffer, indices):
+        super().__init__()
+        self._buffer, self.indices = buffer, indices
+        self.storage = buffer._storage
+        self.batch_size = int(indices.numel())
+
+    def __missing__(self, key):
+        if key not in BATCH_KEYS:
+            raise KeyError(key)
+        rows = self._buffer.gather(self.indices)
+        r = self._buffer.rows
+        spans = dict(observations=(r["off_obs"], self._buffer.ob_dim),
+                     actions=(r["off_act"], self._buffer.ac_dim),
+                     rewards=(r["off_rew"], 1), terminals=(r["off_term"], 1),
+                     next_observations=(r["off_next_obs"], self._buffer.ob_dim))
+        o, n = spans[key]
+        val = rows[:, o:o + n].contiguous()
+        self[key] = val
+        return val
+
+    def keys(self):
+        return list(BATCH_KEYS) + [k for k in dict.keys(self) if k not in BATCH_KEYS]
+
+
+class ReplayBuffer(object):
+    def __init__(self, max_replay_buffer_size, ob_space, action_space, device=None,
+                 index_source="numpy", seed=None):
+        self._ob_space, self._action_space = ob_space, action_space
+        self.ob_dim, self.ac_dim = get_dim(ob_space), get_dim(action_space)
+        self._max_replay_buffer_size = int(max_replay_buffer_size)
+        self.rows = row_layout(self.ob_dim, self.ac_dim)
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self._storage = torch.zeros(self._max_replay_buffer_size, self.rows["row_stride"],
+                                    dtype=torch.float32, device=self.device)
+        self._top = 0
+        self._size = 0
+        self.index_source = index_source
+        self._mt = None
+        if index_source == "device":
+            self.seed_device_stream(0 if seed is None else seed)
+
+    # ------------------------------------------------------------ insert
+    def _rows_from(self, obs, act, rew, nobs, term):
+        n = len(obs)
+        r = self.rows
+        out = np.zeros((n, r["row_stride"]), np.float32)
+        out[:, r["off_obs"]:r["off_obs"] + self.ob_dim] = np.asarray(obs).reshape(n, -1)
+        out[:, r["off_act"]:r["off_act"] + self.ac_dim] = np.asarray(act).reshape(n, -1)
+        out[:, r["off_rew"]] = np.asarray(rew, np.float64).reshape(n)
+        out[:, r["off_term"]] = np.asarray(term).reshape(n).astype(np.float32)
+        out[:, r["off_next_obs"]:r["off_next_obs"] + self.ob_dim] = np.asarray(nobs).reshape(n, -1)
+        return out
+
+    def _write(self, rows_np):
+        n = len(rows_np)
+        t = torch.from_numpy(rows_np)
+        done = 0
+        while done < n:
+            k = min(n - done, self._max_replay_buffer_size - self._top)
+            self._storage[self._top:self._top + k].copy_(t[done:done + k])
+            self._top = (self._top + k) % self._max_replay_buffer_size   # _advance, :101-104
+            self._size = min(self._size + k, self._max_replay_buffer_size)
+            done += k
+
+    def add_sample(self, observation, action, reward, next_observation, terminal,
+                   env_info=None, **kwargs):
+        """replay_buffer.py:88-99."""
+        if hasattr(self._action_space, "n") and not hasattr(self._action_space, "low"):
+            raise AssertionError("discrete action spaces are not supported")
+        self._write(self._rows_from([observation], [action], [reward], [next_observation],
+                                    [terminal]))
+
+    def add_path(self, path):
+        """replay_buffer.py:50-82, one host->device copy per path."""
+        if len(path["observations"]) == 0:
+            return
+        self._write(self._rows_from(path["observations"], path["actions"], path["rewards"],
+                                    path["next_observations"], path["terminals"]))
+
+    def add_paths(self, paths):
+        for path in paths:
+            self.add_path(path)
+
+    def load_transitions(self, rows_fp32):
+        """Bulk insert of pre-built device/host rows [n, row_stride] (synthetic fills)."""
+        n = rows_fp32.shape[0]
+        assert rows_fp32.shape[1] == self.rows["row_stride"] and n <= self._max_replay_buffer_size
+        self._storage[:n].copy_(rows_fp32)
+        self._top = n % self._max_replay_buffer_size
+        self._size = n
+
+    # ------------------------------------------------------------ sample
+    def seed_device_stream(self, seed):
+        st = np.zeros(625, np.uint32)
+        check(_lib.lib().oac_mt_seed_host(ctypes.c_uint32(seed), st.ctypes.data_as(ctypes.c_void_p)))
+        self._mt = torch.from_numpy(st.view(np.int32)).to(self.device)
+
+    def sample_indices_device(self, count, out=None):
+        """``count`` draws of np.random.randint(0, size) from the device stream."""
+        if self._mt is None:
+            raise RuntimeError("device index stream not seeded (index_source='device')")
+        if out is None:
+            out = torch.empty(count, dtype=torch.int32, device=self.device)
+        check(_lib.lib().oac_replay_sample_indices(ptr(self._mt), ctypes.c_uint64(self._size),
+                                                   int(count), ptr(out), stream_ptr()))
+        return out
+
+    def random_batch(self, batch_size):
+        """replay_buffer.py:106-115."""
+        if self.index_source == "device":
+            idx = self.sample_indices_device(batch_size)
+        else:
+            idx_np = np.random.randint(0, self._size, batch_size)
+            idx = torch.from_numpy(idx_np.astype(np.int32)).to(self.device, non_blocking=True)
+        return DeviceBatch(self, idx)
+
+    def gather(self, indices):
+        out = torch.empty(indices.numel(), self.rows["row_stride"], dtype=torch.float32,
+                          device=self.device)
+        check(_lib.lib().oac_replay_gather(ptr(self._storage), self.rows["row_stride"],
+                                           ptr(indices), int(indices.numel()), ptr(out),
+                                           stream_ptr()))
+        return out
+
+    # ------------------------------------------------------------ misc
+    def get_dataset(self):
+        r = self.rows
+        return self._storage[:self._size, r["off_obs"]:r["off_obs"] + self.ob_dim]
+
+    def num_steps_can_sample(self):
+        return self._size
+
+    def get_diagnostics(self):
+        return OrderedDict([("size", self._size)])
+
+    def end_epoch(self, epoch):
+        return
+
+    def get_snapshot(self):
+        """Same keys and dtypes as replay_buffer.py:133-142."""
+        r = self.rows
+        s = self._storage.cpu().numpy().astype(np.float64)
+        return dict(
+            _observations=s[:, r["off_obs"]:r["off_obs"] + self.ob_dim],
+            _next_obs=s[:, r["off_next_obs"]:r["off_next_obs"] + self.ob_dim],
+            _actions=s[:, r["off_act"]:r["off_act"] + self.ac_dim],
+            _rewards=s[:, r["off_rew"]:r["off_rew"] + 1],
+            _terminals=s[:, r["off_term"]:r["off_term"] + 1].astype(np.uint8),
+            _top=self._top, _size=self._size)
+
+    def restore_from_snapshot(self, ss):
+        for key in ss.keys():
+            assert key in ("_observations", "_next_obs", "_actions", "_rewards", "_terminals",
+                           "_top", "_size")
+        rows = self._rows_from(ss["_observations"], ss["_actions"], ss["_rewards"],
+                               ss["_next_obs"], ss["_terminals"])
+        self._storage[:len(rows)].copy_(torch.from_numpy(rows))
+        self._top, self._size = int(ss["_top"]), int(ss["_size"])
+
+
+class DeviceIndexStream:
+    """A ring of pre-drawn batch indices for ``SACTrainer.train_from_ring``:
+    2*chunk step slots, refilled one chunk ahead by the device MT19937 kernel
+    (sequential in the stream, so the index sequence equals
+    ``np.random.seed(seed); randint(0, size, B)`` called once per step)."""
+
+    def __init__(self, buffer, batch_size, chunk=64, seed=1):
+        self.buf, self.B, self.chunk = buffer, int(batch_size), int(chunk)
+        self.slots = 2 * self.chunk
+        self.ring = torch.empty(self.slots * self.B, dtype=torch.int32, device=buffer.device)
+        buffer.seed_device_stream(seed)
+        self.t = 0
+        self._fill(0)
+        self._fill(1)
+
+    def _fill(self, half):
+        view = self.ring[half * self.chunk * self.B:(half + 1) * self.chunk * self.B]
+        self.buf.sample_indices_device(self.chunk * self.B, out=view)
+
+    def before_step(self):
+        """Call before each ring step: refill the half that was just consumed."""
+        if self.t > 0 and self.t % self.chunk == 0:
+            self._fill(((self.t // self.chunk) + 1) % 2)
+        self.t += 1

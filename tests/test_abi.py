@@ -1,0 +1,70 @@
+"""CPU checks of the C-ABI boundary: the library loads and exports every
+symbol include/oac_amd.h declares; host-side layout logic (no GPU compute)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "oac_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(oac_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from oac_amd import _lib
+    L = _lib.lib()
+    decl = declared_functions()
+    assert decl, "no declarations parsed"
+    missing = [f for f in decl if not hasattr(L, f)]
+    assert not missing, missing
+    # and the ctypes binding covers exactly the declared surface
+    assert sorted(_lib.EXPORTED) == decl
+
+
+def test_abi_version_and_error_channel():
+    from oac_amd import _lib
+    L = _lib.lib()
+    assert L.oac_abi_version() == 1
+    cfg = _lib.SacConfig()
+    cfg.kind = 7
+    lay = _lib.SacLayout()
+    assert L.oac_sac_query_layout(ctypes.byref(cfg), ctypes.byref(lay)) != 0
+    assert b"kind" in L.oac_last_error()
+
+
+@pytest.mark.parametrize("dims", [(376, 17, 256), (111, 8, 256), (1, 1, 256), (11, 3, 32)])
+def test_param_layout_matches_reference_parameter_counts(dims):
+    """Arena layout covers exactly the reference's parameter counts
+    (Humanoid policy 171,042, each critic 166,913)."""
+    from oac_amd import _lib, row_layout
+    Do, Da, H = dims
+    cfg = _lib.SacConfig()
+    cfg.kind, cfg.obs_dim, cfg.act_dim, cfg.hidden, cfg.q_out, cfg.batch = 0, Do, Da, H, 1, 256
+    for k, v in row_layout(Do, Da).items():
+        setattr(cfg, k, v)
+    cfg.gemm_cfg = -1
+    lay = _lib.SacLayout()
+    assert _lib.lib().oac_sac_query_layout(ctypes.byref(cfg), ctypes.byref(lay)) == 0
+    n_pol = H * Do + H + H * H + H + 2 * (Da * H + Da)
+    n_q = H * (Do + Da) + H + H * H + H + H + 1
+    assert lay.pol_size >= n_pol and lay.pol_size - n_pol < 4 * 6
+    assert lay.q_size >= n_q and lay.q_size - n_q < 4 * 6
+    if dims == (376, 17, 256):
+        assert n_pol == 171042 and n_q == 166913
+    for f in ("pol_fc0_w", "pol_fc0_b", "pol_fc1_w", "pol_fc1_b", "pol_head_w", "pol_head_b",
+              "q_fc0_w", "q_fc0_b", "q_fc1_w", "q_fc1_b", "q_last_w", "q_last_b", "q1_base",
+              "q2_base"):
+        assert getattr(lay, f) % 4 == 0, f
+    assert lay.workspace_floats > 0
+
+
+def test_row_layout_keeps_critic_input_contiguous():
+    from oac_amd import row_layout
+    r = row_layout(376, 17)
+    assert r["off_act"] == r["off_obs"] + 376
+    assert r["row_stride"] % 4 == 0 and r["row_stride"] >= 2 * 376 + 17 + 2
