@@ -75,7 +75,8 @@ typedef struct oac_sac_layout {
 
 typedef struct oac_sac_buffers {
   float* params; float* grads; float* adam_m; float* adam_v; float* targets;
-  void* alpha_state;     /* 8 floats: log_alpha, exp_avg, exp_avg_sq, alpha, alpha_loss, grad */
+  void* alpha_state;     /* 16 floats: log_alpha, exp_avg, exp_avg_sq, alpha, alpha_loss, grad,
+                            sum (data-parallel all-reduce slot), -, next_* (in-step scratch) */
   void* step_state;      /* 64-byte device step counters (zeroed by the caller) */
   float* workspace;      /* layout.workspace_floats */
   const float* replay;   /* [replay_rows, row_stride] fp32 */
@@ -105,15 +106,24 @@ int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out);
 int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_sac** out);
 int oac_sac_destroy(oac_sac* h);
 int oac_sac_step(oac_sac* h, int flags, void* stream);
-/* data-parallel split: phase 0 = forward through the policy sample (local
- * alpha partial sum in alpha_state[6]); 1 = alpha update (after the caller's
- * all-reduce of that sum) through the critic gradients (reduced into the
- * grads arena); 2 = critic Adam + Polyak (after the critic-grad all-reduce)
- * through the policy gradient; 3 = policy Adam + step advance. */
+/* data-parallel split (config.world_size > 1): phase 0 = forward through the
+ * policy sample and the local sum(logp + target_entropy) into alpha_state[6];
+ * 1 = alpha update from the caller's all-reduced sum through the critic
+ * gradients (reduced into the grads arena); 2 = critic Adam + Polyak (after
+ * the caller's critic-grad all-reduce, averaged) through the policy gradient
+ * (grads arena); 3 = policy Adam + step advance (after the policy-grad
+ * all-reduce).  oac_sac_step (world_size 1) runs the same sequence with the
+ * split-K reduction fused into the Adam passes. */
 int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream);
 int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows, int64_t* cols);
 /* number of kernel launches of one step (for the launch/graph accounting) */
 int oac_sac_launch_count(oac_sac* h);
+/* bench instrumentation: with timing enabled, steps run as direct launches
+ * bracketed by hipEvents; read_timing returns (and resets) the summed device
+ * milliseconds and launch counts per kernel kind: 0 grouped GEMM, 1 row
+ * kernels, 2 fused Adam, 3 gather. */
+int oac_sac_set_timing(oac_sac* h, int enable);
+int oac_sac_read_timing(oac_sac* h, double* ms_by_kind, int64_t* count_by_kind, int nkinds);
 
 /* ---------------------------------------------------------------- replay */
 /* numpy legacy seeding (init_genrand) of a 625-word MT19937 state, on the host */
@@ -127,6 +137,8 @@ int oac_replay_gather(const float* replay, int64_t row_stride, const int32_t* id
                       float* out, void* stream);
 
 /* ------------------------------------------------------------------ Adam */
+/* advance 0: Adam step t = n_steps+1, snapshot t (step_state), Polyak when
+ * n_steps % period == 0; advance 1: t from the snapshot, then n_steps += 1. */
 int oac_adam_polyak(float* p, const float* g, float* m, float* v, int64_t n, float* target,
                     float tau, int target_update_period, double lr, double beta1, double beta2,
                     double eps, void* step_state, int advance, void* stream);

@@ -16,10 +16,10 @@ namespace oac {
 
 struct AdamConsts { float b1, omb1, b2, omb2, step_size, sbc2, eps, tau, omtau; bool polyak; };
 
-__device__ __forceinline__ AdamConsts adam_consts(const StepState* st, double lr, double beta1,
-                                                  double beta2, double eps, const float* target,
-                                                  float tau, int period) {
-  const long long nsteps = st->n_steps;
+__device__ __forceinline__ AdamConsts adam_consts(const StepState* st, int advance, double lr,
+                                                  double beta1, double beta2, double eps,
+                                                  const float* target, float tau, int period) {
+  const long long nsteps = advance ? st->t_snapshot : st->n_steps;
   const double t = (double)(nsteps + 1);
   const double bc1 = 1.0 - pow(beta1, t);
   const double bc2 = 1.0 - pow(beta2, t);
@@ -47,26 +47,23 @@ __device__ __forceinline__ float polyak1(const AdamConsts& c, float t, float p) 
   return __fadd_rn(__fmul_rn(t, c.omtau), __fmul_rn(p, c.tau));
 }
 
-__device__ __forceinline__ void advance_step(StepState* st, unsigned* ticket) {
-  __syncthreads();
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    __threadfence();
-    const unsigned prev = atomicAdd(ticket, 1u);
-    last = prev == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    __threadfence();
-    st->n_steps += 1;
+// Block 0, thread 0 only.  advance == 0 (critic Adam): snapshot t for the
+// final Adam and commit the alpha update; advance == 1 (final policy Adam):
+// advance the step counters.  No other block of the launch reads these fields.
+__device__ __forceinline__ void step_bookkeeping(StepState* st, AlphaState* as, int advance) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  if (advance) {
+    st->n_steps = st->t_snapshot + 1;
     st->batch_counter += 1;
-    *ticket = 0u;
+  } else {
+    st->t_snapshot = st->n_steps;
+    if (as) { as->log_alpha = as->next_log_alpha; as->m = as->next_m; as->v = as->next_v; }
   }
 }
 
 __global__ void __launch_bounds__(256) adam_seg_kernel(AdamSegArgs a) {
-  const AdamConsts c = adam_consts(a.state, a.lr, a.beta1, a.beta2, a.eps, a.target, a.tau,
-                                   a.period);
+  const AdamConsts c = adam_consts(a.state, a.advance, a.lr, a.beta1, a.beta2, a.eps, a.target,
+                                   a.tau, a.period);
   const long stride = (long)gridDim.x * 256;
   for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < a.total; e += stride) {
     int si = 0;
@@ -89,12 +86,12 @@ __global__ void __launch_bounds__(256) adam_seg_kernel(AdamSegArgs a) {
     a.p[idx] = p; a.m[idx] = m; a.v[idx] = v;
     if (c.polyak) a.target[idx] = polyak1(c, a.target[idx], p);
   }
-  if (a.advance) advance_step(a.state, &a.state->ticket[0]);
+  if (!a.reduce_only) step_bookkeeping(a.state, a.alpha, a.advance);
 }
 
 __global__ void __launch_bounds__(256) adam_flat_kernel(AdamArgs a) {
-  const AdamConsts c = adam_consts(a.state, a.lr, a.beta1, a.beta2, a.eps, a.target, a.tau,
-                                   a.period);
+  const AdamConsts c = adam_consts(a.state, a.advance, a.lr, a.beta1, a.beta2, a.eps, a.target,
+                                   a.tau, a.period);
   const long n4 = a.n >> 2;
   const long stride = (long)gridDim.x * 256;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
@@ -123,7 +120,7 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(AdamArgs a) {
     a.p[i] = p; a.m[i] = m; a.v[i] = v;
     if (c.polyak) a.target[i] = polyak1(c, a.target[i], p);
   }
-  if (a.advance) advance_step(a.state, &a.state->ticket[0]);
+  step_bookkeeping(a.state, a.alpha, a.advance);
 }
 
 static int adam_blocks(long n) {

@@ -41,99 +41,151 @@ struct GemmCfg {
   static_assert(BK % (2 * WK) == 0, "k split");
 };
 
-__device__ __forceinline__ float load_a(const GemmTask& t, int m, int k) {
-  if (m >= t.M || k >= t.K) return 0.f;
-  const int row = t.a_kc ? m : k;
-  const int col = t.a_kc ? k : m;
-  if (t.a_mode == A_PLAIN) return t.A[(long)row * t.lda + col];
-  const float mk = t.a_mask[(long)row * t.ld_mask + col];
-  return mk > 0.f ? t.a_s[row] * t.a_v[col] : 0.f;
+// Staging loads.  Every load of the unrolled loop is issued unconditionally
+// (out-of-range elements read a clamped in-bounds address and are zeroed by a
+// select), and the per-task layout branches are hoisted around the whole loop,
+// so hipcc issues all NA+NB loads back to back and waits once -- a per-element
+// branch would make it wait vmcnt(0) per element (one dependent L2 round trip
+// per float).
+template <class C, bool KC>
+__device__ __forceinline__ void idx_mk(int e, int& mn, int& k) {
+  if (KC) { k = e % C::kBK; mn = e / C::kBK; }   // walk the contiguous k
+  else    { mn = e % C::kBM; k = e / C::kBM; }   // walk the contiguous m / n
 }
 
-__device__ __forceinline__ float load_b(const GemmTask& t, int k, int n) {
-  if (n >= t.N || k >= t.K) return 0.f;
-  if (t.b_ones && n == t.N - 1) return 1.f;
-  return t.b_kc ? t.B[(long)n * t.ldb + k] : t.B[(long)k * t.ldb + n];
+template <class C, int TILE, bool KC>
+__device__ __forceinline__ void idx_tile(int e, int& mn, int& k) {
+  if (KC) { k = e % C::kBK; mn = e / C::kBK; }
+  else    { mn = e % TILE; k = e / TILE; }
+}
+
+template <class C, bool KC, bool RANK1>
+__device__ __forceinline__ void load_a_all(const GemmTask& t, int m0, int k0, float (&ra)[C::NA]) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < C::NA; ++i) {
+    int m, k;
+    idx_tile<C, C::kBM, KC>(tid + 256 * i, m, k);
+    m += m0; k += k0;
+    const bool ok = (m < t.M) & (k < t.K);
+    const int row = ok ? (KC ? m : k) : 0;
+    const int col = ok ? (KC ? k : m) : 0;
+    float v;
+    if (!RANK1) {
+      v = t.A[(long)row * t.lda + col];
+    } else {
+      const float mk = t.a_mask[(long)row * t.ld_mask + col];
+      const float sv = t.a_s[row] * t.a_v[col];
+      v = mk > 0.f ? sv : 0.f;
+    }
+    ra[i] = ok ? v : 0.f;
+  }
+}
+
+template <class C, bool KC>
+__device__ __forceinline__ void load_b_all(const GemmTask& t, int n0, int k0, float (&rb)[C::NB]) {
+  const int tid = threadIdx.x;
+  const int nreal = t.b_ones ? t.N - 1 : t.N;
+#pragma unroll
+  for (int i = 0; i < C::NB; ++i) {
+    int n, k;
+    idx_tile<C, C::kBN, KC>(tid + 256 * i, n, k);
+    n += n0; k += k0;
+    const bool ok = (n < nreal) & (k < t.K);
+    const int row = ok ? (KC ? n : k) : 0;
+    const int col = ok ? (KC ? k : n) : 0;
+    const float v = t.B[(long)row * t.ldb + col];
+    const bool one = (n == nreal) & (t.b_ones != 0) & (k < t.K);
+    rb[i] = ok ? v : (one ? 1.f : 0.f);
+  }
 }
 
 template <class C>
 __device__ __forceinline__ void stage_load(const GemmTask& t, int m0, int n0, int k0,
                                            float (&ra)[C::NA], float (&rb)[C::NB]) {
+  if (t.a_mode == A_PLAIN) {
+    if (t.a_kc) load_a_all<C, true, false>(t, m0, k0, ra);
+    else load_a_all<C, false, false>(t, m0, k0, ra);
+  } else {
+    if (t.a_kc) load_a_all<C, true, true>(t, m0, k0, ra);
+    else load_a_all<C, false, true>(t, m0, k0, ra);
+  }
+  if (t.b_kc) load_b_all<C, true>(t, n0, k0, rb);
+  else load_b_all<C, false>(t, n0, k0, rb);
+}
+
+template <class C, bool AKC, bool BKC>
+__device__ __forceinline__ void stage_store_t(float* As, float* Bs, const float (&ra)[C::NA],
+                                              const float (&rb)[C::NB]) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < C::NA; ++i) {
-    const int e = tid + 256 * i;
     int m, k;
-    if (t.a_kc) { k = e % C::kBK; m = e / C::kBK; }   // walk the contiguous k
-    else        { m = e % C::kBM; k = e / C::kBM; }   // walk the contiguous m
-    ra[i] = load_a(t, m0 + m, k0 + k);
+    idx_tile<C, C::kBM, AKC>(tid + 256 * i, m, k);
+    As[k * C::LDA_S + m] = ra[i];
   }
 #pragma unroll
   for (int i = 0; i < C::NB; ++i) {
-    const int e = tid + 256 * i;
     int n, k;
-    if (t.b_kc) { k = e % C::kBK; n = e / C::kBK; }
-    else        { n = e % C::kBN; k = e / C::kBN; }
-    rb[i] = load_b(t, k0 + k, n0 + n);
+    idx_tile<C, C::kBN, BKC>(tid + 256 * i, n, k);
+    Bs[k * C::LDB_S + n] = rb[i];
   }
 }
 
 template <class C>
 __device__ __forceinline__ void stage_store(const GemmTask& t, float* As, float* Bs,
                                             const float (&ra)[C::NA], const float (&rb)[C::NB]) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int i = 0; i < C::NA; ++i) {
-    const int e = tid + 256 * i;
-    int m, k;
-    if (t.a_kc) { k = e % C::kBK; m = e / C::kBK; }
-    else        { m = e % C::kBM; k = e / C::kBM; }
-    As[k * C::LDA_S + m] = ra[i];
-  }
-#pragma unroll
-  for (int i = 0; i < C::NB; ++i) {
-    const int e = tid + 256 * i;
-    int n, k;
-    if (t.b_kc) { k = e % C::kBK; n = e / C::kBK; }
-    else        { n = e % C::kBN; k = e / C::kBN; }
-    Bs[k * C::LDB_S + n] = rb[i];
+  if (t.a_kc) {
+    if (t.b_kc) stage_store_t<C, true, true>(As, Bs, ra, rb);
+    else stage_store_t<C, true, false>(As, Bs, ra, rb);
+  } else {
+    if (t.b_kc) stage_store_t<C, false, true>(As, Bs, ra, rb);
+    else stage_store_t<C, false, false>(As, Bs, ra, rb);
   }
 }
 
-__device__ __forceinline__ void epilogue_elem(const GemmTask& t, int m, int n, float acc) {
+template <int EPI>
+__device__ __forceinline__ void epi_store(const GemmTask& t, int m, int n, float acc,
+                                          const float* lds_u, const float* lds_v, int mt, int nt) {
   if (m >= t.M || n >= t.N) return;
-  switch (t.epi) {
-    case EPI_STORE:
-      t.C[(long)m * t.ldc + n] = acc;
-      break;
-    case EPI_BIAS:
-      t.C[(long)m * t.ldc + n] = acc + t.bias[n];
-      break;
-    case EPI_BIAS_RELU:
-      t.C[(long)m * t.ldc + n] = fmaxf(acc + t.bias[n], 0.f);
-      break;
-    case EPI_BIAS_RANK_RELU: {
-      const float p = acc + t.bias[n];
-      t.C[(long)m * t.ldc + n] = p;
-      const float* u = t.U + (long)m * t.ldu;
-      const float* v = t.V + (long)n * t.ldv;
-      float s = 0.f;
-      for (int j = 0; j < t.R; ++j) s = fmaf(u[j], v[j], s);
-      t.C2[(long)m * t.ldc2 + n] = fmaxf(p + s, 0.f);
-      break;
-    }
-    case EPI_ADD_RELU:
-      t.C[(long)m * t.ldc + n] = fmaxf(acc + t.aux[(long)m * t.ld_aux + n], 0.f);
-      break;
-    case EPI_MASK:
-      t.C[(long)m * t.ldc + n] = t.aux[(long)m * t.ld_aux + n] > 0.f ? acc : 0.f;
-      break;
-    case EPI_SLAB:
-      t.C[(long)m * t.ldc + n] = acc;   // C already offset to this split's slab
-      break;
-    default:
-      break;
+  const long o = (long)m * t.ldc + n;
+  if (EPI == EPI_STORE || EPI == EPI_SLAB) {
+    t.C[o] = acc;
+  } else if (EPI == EPI_BIAS) {
+    t.C[o] = acc + t.bias[n];
+  } else if (EPI == EPI_BIAS_RELU) {
+    t.C[o] = fmaxf(acc + t.bias[n], 0.f);
+  } else if (EPI == EPI_BIAS_RANK_RELU) {
+    const float p = acc + t.bias[n];
+    t.C[o] = p;
+    // U / V tile rows staged in LDS by the caller ([row][R], R odd-padded)
+    const float* u = lds_u + mt * (t.R | 1);
+    const float* v = lds_v + nt * (t.R | 1);
+    float s = 0.f;
+    for (int j = 0; j < t.R; ++j) s = fmaf(u[j], v[j], s);
+    t.C2[(long)m * t.ldc2 + n] = fmaxf(p + s, 0.f);
+  } else if (EPI == EPI_ADD_RELU) {
+    t.C[o] = fmaxf(acc + t.aux[(long)m * t.ld_aux + n], 0.f);
+  } else if (EPI == EPI_MASK) {
+    t.C[o] = t.aux[(long)m * t.ld_aux + n] > 0.f ? acc : 0.f;
   }
+}
+
+template <class C, int EPI>
+__device__ __forceinline__ void epilogue_tile(const GemmTask& t, int m0, int n0, int wm, int wn,
+                                              int lane, const floatx16 (&accf)[C::TI][C::TJ],
+                                              const float* lds_u, const float* lds_v) {
+#pragma unroll
+  for (int i = 0; i < C::TI; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        const int mt = (wm * C::TI + i) * 32 + row;
+        const int nt = (wn * C::TJ + j) * 32 + (lane & 31);
+        epi_store<EPI>(t, m0 + mt, n0 + nt, accf[i][j][r], lds_u, lds_v, mt, nt);
+      }
 }
 
 template <class C>
@@ -246,31 +298,52 @@ __global__ void __launch_bounds__(256) gemm_grouped_kernel(const GemmBatch batch
       }
     }
   }
+  // rank-R epilogue operands (U rows of this M tile, V rows of this N tile)
+  // staged through LDS once per tile instead of strided per-element loads
+  float* lds_u = lds;
+  float* lds_v = lds + C::kBM * (t.R | 1);
+  if (t.epi == EPI_BIAS_RANK_RELU) {
+    __syncthreads();
+    const int Rp = t.R | 1;
+    for (int e = threadIdx.x; e < C::kBM * t.R; e += 256) {
+      const int r = e / t.R, j = e % t.R;
+      const int m = min(m0 + r, t.M - 1);
+      lds_u[r * Rp + j] = t.U[(long)m * t.ldu + j];
+    }
+    for (int e = threadIdx.x; e < C::kBN * t.R; e += 256) {
+      const int r = e / t.R, j = e % t.R;
+      const int n = min(n0 + r, t.N - 1);
+      lds_v[r * Rp + j] = t.V[(long)n * t.ldv + j];
+    }
+    __syncthreads();
+  }
   if (wk != 0) return;
-
-#pragma unroll
-  for (int i = 0; i < C::TI; ++i)
-#pragma unroll
-    for (int j = 0; j < C::TJ; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int m = m0 + (wm * C::TI + i) * 32 + row;
-        const int n = n0 + (wn * C::TJ + j) * 32 + lcol;
-        epilogue_elem(t, m, n, acc[i][j][r]);
-      }
+  const floatx16 (&accf)[C::TI][C::TJ] = acc;
+  switch (t.epi) {
+    case EPI_STORE: epilogue_tile<C, EPI_STORE>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
+    case EPI_BIAS: epilogue_tile<C, EPI_BIAS>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
+    case EPI_BIAS_RELU: epilogue_tile<C, EPI_BIAS_RELU>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
+    case EPI_BIAS_RANK_RELU: epilogue_tile<C, EPI_BIAS_RANK_RELU>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
+    case EPI_ADD_RELU: epilogue_tile<C, EPI_ADD_RELU>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
+    case EPI_MASK: epilogue_tile<C, EPI_MASK>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
+    case EPI_SLAB: epilogue_tile<C, EPI_SLAB>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
+    default: break;
+  }
 }
 
-// Small tiles + split-K over the 4 waves: batch-256 stages (few output tiles,
-// long K).  Large tiles: batch-4096 stages.
-using CfgSmall = GemmCfg<32, 32, 64, 1, 1, 4>;
+// LDS-tiled kernel for the large-batch stages (cfg 1); cfg 0 is the
+// latency-optimised register-direct kernel of gemm_small.hip.
 using CfgLarge = GemmCfg<64, 64, 32, 2, 2, 1>;
 
-int gemm_tile_m(int cfg) { return cfg == 0 ? CfgSmall::kBM : CfgLarge::kBM; }
-int gemm_tile_n(int cfg) { return cfg == 0 ? CfgSmall::kBN : CfgLarge::kBN; }
+int gemm_tile_m(int cfg) { return cfg == 0 ? 32 : CfgLarge::kBM; }
+int gemm_tile_n(int cfg) { return cfg == 0 ? 32 : CfgLarge::kBN; }
+
+void gemm_small_finalize(GemmBatch& b);
+hipError_t gemm_small_launch(const GemmBatch& b, hipStream_t s);
 
 // Fills tile_begin / tiles_n / total_tiles for a tile configuration.
 void gemm_batch_finalize(GemmBatch& b, int cfg) {
+  if (cfg == 0) { gemm_small_finalize(b); return; }
   const int bm = gemm_tile_m(cfg), bn = gemm_tile_n(cfg);
   int tiles = 0;
   for (int i = 0; i < b.ntasks; ++i) {
@@ -287,10 +360,8 @@ void gemm_batch_finalize(GemmBatch& b, int cfg) {
 
 hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   if (b.total_tiles <= 0) return hipSuccess;
-  if (cfg == 0)
-    hipLaunchKernelGGL(gemm_grouped_kernel<CfgSmall>, dim3(b.total_tiles), dim3(256), 0, s, b);
-  else
-    hipLaunchKernelGGL(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b);
+  if (cfg == 0) return gemm_small_launch(b, s);
+  hipLaunchKernelGGL(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 

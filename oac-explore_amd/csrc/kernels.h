@@ -45,12 +45,7 @@ struct PolicySampleSeg {
 
 struct PolicySampleArgs {
   PolicySampleSeg seg[2];
-  int B, act_dim, auto_alpha;
-  float target_entropy;
-  double lr, beta1, beta2, adam_eps;
-  float* partials;     // >= gridDim.x*gridDim.y floats
-  StepState* state;
-  AlphaState* alpha;
+  int B, act_dim;
 };
 
 struct CriticTargetArgs {
@@ -59,7 +54,12 @@ struct CriticTargetArgs {
   const float* tq1; const float* tq2;   // target Q_i(next_obs, a')
   const float* logp2;
   const float* batch; long ld_batch; int off_rew, off_term;
-  const AlphaState* alpha;              // null -> alpha = 0
+  AlphaState* alpha;                    // null -> alpha = 0 (no entropy tuning)
+  const StepState* state;
+  const float* logp1;                   // for the alpha gradient
+  float target_entropy;
+  double lr, beta1, beta2, adam_eps;    // alpha optimiser (policy_lr)
+  int world_size;                       // > 1: use alpha->sum (all-reduced)
   float reward_scale, discount;
   int B;
   float* y; float* dq1; float* dq2; float* gq1; float* gq2; float* sqe1; float* sqe2;
@@ -108,7 +108,9 @@ struct AdamArgs {
   float* target; float tau; int period;   // target != null -> Polyak after the step
   double lr, beta1, beta2, eps;
   StepState* state;
-  int advance;                            // last block advances the step counters
+  int advance;       // 0: critic Adam (t = n_steps; block 0 snapshots t, commits alpha)
+                     // 1: final policy Adam (t = t_snapshot; block 0 advances the step)
+  AlphaState* alpha; // commit next_* (critic Adam only); may be null
 };
 
 // Segment-aware reduce + Adam: one segment per (weight, bias) pair whose
@@ -129,9 +131,13 @@ struct AdamSegArgs {
   float tau; int period;
   double lr, beta1, beta2, eps;
   StepState* state;
-  int advance;
+  int advance;            // as AdamArgs
   int reduce_only;        // 1: write the reduced gradient only (DP: all-reduce next)
+  AlphaState* alpha;
 };
+
+struct LogpSumArgs { const float* logp; int B; float target_entropy; AlphaState* alpha; };
+hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s);
 
 // launchers (defined in the .hip files)
 hipError_t launch_adam_seg(const AdamSegArgs& a, hipStream_t s);

@@ -70,17 +70,29 @@ struct GemmBatch {
 // last block of the step's final kernel, so the launch sequence is static and
 // can be replayed as one hipGraph).
 // ---------------------------------------------------------------------------
+//
+// No kernel writes a field another block of the same launch reads, so no
+// fences or tickets are needed: the critic Adam copies n_steps to t_snapshot
+// (block 0), and the policy Adam -- which reads t_snapshot -- advances
+// n_steps and batch_counter (block 0).
 struct StepState {
   long long n_steps;        // SACTrainer._n_train_steps_total
   long long batch_counter;  // replay ring cursor / Philox counter
   long long expl_counter;   // Philox counter for exploration draws
-  unsigned int ticket[8];   // last-block tickets (zero between kernels)
-  unsigned int pad[2];
+  long long t_snapshot;     // n_steps as seen by this step (for the last Adam)
+  long long pad[4];
 };
 
-// alpha state: log_alpha, exp_avg, exp_avg_sq, alpha(out), alpha_loss(out), grad
+// alpha (auto entropy tuning) state, 16 floats.  critic_targets computes the
+// update (every block, identically) and block 0 publishes next_*; the critic
+// Adam commits next_* -> current (trainer.py:139-146).
 struct AlphaState {
-  float log_alpha, m, v, alpha, alpha_loss, grad, pad0, pad1;
+  float log_alpha, m, v;       // current (log_alpha is the snapshot's 'log_alpha')
+  float alpha, alpha_loss, grad;
+  float sum;                   // data-parallel: all-reduced sum(logp + target_entropy)
+  float pad0;
+  float next_log_alpha, next_m, next_v;
+  float pad1[5];
 };
 
 }  // namespace oac

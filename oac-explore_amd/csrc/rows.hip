@@ -15,81 +15,61 @@ __device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, 
 //   log_std = clamp(ls_raw, -20, 2); std = exp(log_std); z = mean + std*eps;
 //   a = tanh(z);  logp = sum_j [ -(z-mean)^2/(2 std^2) - log std - log sqrt(2pi)
 //                                - log(1 - a^2 + 1e-6) ]
-// y-dimension 0: obs batch (eps1), 1: next_obs batch (eps2).
-// The last block to finish also performs the alpha update of
-// trainer/trainer.py:139-146 (Adam on log_alpha, then alpha = exp(log_alpha)).
+// One half-wave (32 lanes) per row, lane j = action dim j (act_dim <= 32);
+// the sum over j is a 5-step shuffle reduction.  y-dimension 0: obs batch
+// (eps1), 1: next_obs batch (eps2).
 // --------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) policy_sample_kernel(PolicySampleArgs p) {
-  __shared__ float red[256];
-  const int seg = blockIdx.y;
-  const PolicySampleSeg& s = p.seg[seg];
+  const PolicySampleSeg& s = p.seg[blockIdx.y];
   const int Da = p.act_dim;
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  float lp_row = 0.f;
-  if (r < p.B) {
+  const int r = (blockIdx.x * 256 + threadIdx.x) >> 5;
+  const int j = threadIdx.x & 31;
+  float l = 0.f;
+  if (r < p.B && j < Da) {
+    const long e = (long)r * Da + j;
     const float* hd = s.head + (long)r * (2 * Da);
-    const float* eps = s.eps + (long)r * Da;
-    float lp = 0.f;
-    for (int j = 0; j < Da; ++j) {
-      const float mean = hd[j];
-      const float ls = fminf(fmaxf(hd[Da + j], -20.f), 2.f);
-      const float sd = expf(ls);
-      const float e = eps[j];
-      const float z = add_rn(mean, mul_rn(sd, e));
-      const float a = tanhf(z);
-      const float u = z - mean;
-      const float var = mul_rn(sd, sd);
-      const float t1 = -(mul_rn(u, u)) / (2.f * var);
-      const float l = t1 - logf(sd) - 0.918938533204672742f  // log(sqrt(2*pi))
-                      - logf(add_rn(1.f - mul_rn(a, a), 1e-6f));
-      lp += l;
-      s.act[(long)r * Da + j] = a;
-      s.stdv[(long)r * Da + j] = sd;
-      s.u[(long)r * Da + j] = u;
-      if (s.act_row) s.act_row[(long)r * s.ld_act_row + j] = a;
-    }
-    s.logp[r] = lp;
-    lp_row = lp + p.target_entropy;
+    const float mean = hd[j];
+    const float ls = fminf(fmaxf(hd[Da + j], -20.f), 2.f);
+    const float sd = expf(ls);
+    const float z = add_rn(mean, mul_rn(sd, s.eps[e]));
+    const float a = tanhf(z);
+    const float u = z - mean;
+    const float var = mul_rn(sd, sd);
+    const float t1 = -(mul_rn(u, u)) / (2.f * var);
+    l = t1 - logf(sd) - 0.918938533204672742f  // log(sqrt(2*pi))
+        - logf(add_rn(1.f - mul_rn(a, a), 1e-6f));
+    s.act[e] = a;
+    s.stdv[e] = sd;
+    s.u[e] = u;
+    if (s.act_row) s.act_row[(long)r * s.ld_act_row + j] = a;
   }
-  if (!p.auto_alpha) return;
-  // block partial of sum(logp + target_entropy) over the obs segment
-  red[threadIdx.x] = (seg == 0) ? lp_row : 0.f;
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) l += __shfl_xor(l, o, 32);
+  if (j == 0 && r < p.B) s.logp[r] = l;
+}
+
+// Deterministic block sum of (logp + target_entropy) over all B rows (every
+// block computes the same value in the same order).
+__device__ float block_logp_sum(const float* logp, int B, float te, float* red) {
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < B; i += blockDim.x) acc += logp[i] + te;
+  red[threadIdx.x] = acc;
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
     if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  const int nblk = gridDim.x * gridDim.y;
-  const int flat = blockIdx.y * gridDim.x + blockIdx.x;
-  __shared__ int last;
-  if (threadIdx.x == 0) {
-    p.partials[flat] = red[0];
-    __threadfence();
-    const unsigned prev = atomicAdd(&p.state->ticket[1], 1u);
-    last = (prev == (unsigned)(nblk - 1));
-  }
+  const float sum = red[0];
   __syncthreads();
-  if (!last || threadIdx.x != 0) return;
-  __threadfence();
-  float sum = 0.f;
-  for (int i = 0; i < gridDim.x; ++i) sum += __hip_atomic_load(&p.partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  AlphaState* as = p.alpha;
-  const float la_old = as->log_alpha;
-  const float g = -(sum / (float)p.B);
-  const double t = (double)(p.state->n_steps + 1);
-  const double bc1 = 1.0 - pow((double)p.beta1, t);
-  const double bc2 = 1.0 - pow((double)p.beta2, t);
-  float m = as->m * (float)p.beta1 + (float)(1.0 - p.beta1) * g;
-  float v = as->v * (float)p.beta2 + (float)(1.0 - p.beta2) * g * g;
-  const float denom = sqrtf(v) / (float)sqrt(bc2) + (float)p.adam_eps;
-  const float la = la_old + (-(float)(p.lr / bc1)) * m / denom;
-  as->m = m;
-  as->v = v;
-  as->grad = g;
-  as->log_alpha = la;
-  as->alpha = expf(la);
-  as->alpha_loss = -(la_old * sum) / (float)p.B;
-  p.state->ticket[1] = 0u;
+  return sum;
+}
+
+// Data-parallel: local sum(logp + target_entropy) into alpha->sum (all-reduced
+// by the caller before phase 1).
+__global__ void __launch_bounds__(256) logp_sum_kernel(LogpSumArgs a) {
+  __shared__ float red[256];
+  const float s = block_logp_sum(a.logp, a.B, a.target_entropy, red);
+  if (threadIdx.x == 0) a.alpha->sum = s;
 }
 
 // --------------------------------------------------------------------------
@@ -99,9 +79,40 @@ __global__ void __launch_bounds__(256) policy_sample_kernel(PolicySampleArgs p) 
 //   (torch-1.4 min() backward: ties go to the first argument).
 // --------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) critic_targets_kernel(CriticTargetArgs p) {
+  __shared__ float red[256];
+  __shared__ float s_alpha;
+  float alpha = 0.f;
+  if (p.alpha) {
+    // alpha update (trainer.py:139-146): L = -mean(log_alpha * (logp + H)),
+    // Adam on log_alpha with t = n_steps + 1, then alpha = exp(log_alpha).
+    // Every block computes it identically; block 0 publishes next_* (the
+    // critic Adam commits them), so no block reads what another writes.
+    const float S = (p.world_size > 1) ? p.alpha->sum
+                                       : block_logp_sum(p.logp1, p.B, p.target_entropy, red);
+    if (threadIdx.x == 0) {
+      AlphaState* as = p.alpha;
+      const float n = (float)((long long)p.B * (p.world_size > 1 ? p.world_size : 1));
+      const float la_old = as->log_alpha;
+      const float g = -(S / n);
+      const double t = (double)(p.state->n_steps + 1);
+      const double bc1 = 1.0 - pow(p.beta1, t);
+      const double bc2 = 1.0 - pow(p.beta2, t);
+      const float m = __fadd_rn(__fmul_rn(as->m, (float)p.beta1), __fmul_rn((float)(1.0 - p.beta1), g));
+      const float v = __fadd_rn(__fmul_rn(as->v, (float)p.beta2),
+                                __fmul_rn(__fmul_rn((float)(1.0 - p.beta2), g), g));
+      const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), (float)sqrt(bc2)), (float)p.adam_eps);
+      const float la = __fadd_rn(la_old, __fdiv_rn(__fmul_rn(-(float)(p.lr / bc1), m), denom));
+      s_alpha = expf(la);
+      if (blockIdx.x == 0) {
+        as->next_log_alpha = la; as->next_m = m; as->next_v = v;
+        as->alpha = s_alpha; as->grad = g; as->alpha_loss = -(la_old * S) / n;
+      }
+    }
+    __syncthreads();
+    alpha = s_alpha;
+  }
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= p.B) return;
-  const float alpha = p.alpha ? p.alpha->alpha : 0.f;
   const float rew = p.batch[(long)r * p.ld_batch + p.off_rew];
   const float term = p.batch[(long)r * p.ld_batch + p.off_term];
   const float tq = fminf(p.tq1[r], p.tq2[r]) - mul_rn(alpha, p.logp2[r]);
@@ -218,7 +229,11 @@ __global__ void oac_final_kernel(OacArgs p) {
 namespace oac {
 
 hipError_t launch_policy_sample(const PolicySampleArgs& a, int nseg, hipStream_t s) {
-  hipLaunchKernelGGL(policy_sample_kernel, dim3((a.B + 255) / 256, nseg), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(policy_sample_kernel, dim3((a.B + 7) / 8, nseg), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(logp_sum_kernel, dim3(1), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s) {

@@ -73,6 +73,8 @@ enum Ws {
 
 struct WsBuf { int64_t off, rows, cols; };
 
+enum Kind { K_GEMM = 0, K_ROW = 1, K_ADAM = 2, K_GATHER = 3, OAC_NUM_KINDS = 4 };
+
 struct Split { int S, kchunk; };
 
 struct SacPlan {
@@ -87,6 +89,13 @@ struct SacPlan {
   hipStream_t graph_stream = nullptr;
   int graph_flags = -1;
   int launches = 0;
+  // HIP-event kernel timing (bench instrumentation; never inside a graph)
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, int>> ev_pending;   // (kind, index of the start event)
+  int ev_next = 0;
+  double kind_ms[OAC_NUM_KINDS] = {0};
+  long long kind_count[OAC_NUM_KINDS] = {0};
 
   float* W(int id) const { return b.workspace + ws[id].off; }
   float* P(int64_t off) const { return b.params + off; }
@@ -195,9 +204,36 @@ static GemmTask t_dw(const float* dY, long lddy, int M, int Bn, const float* X, 
   return t;
 }
 
+static int tick(SacPlan& p, hipStream_t s) {
+  if (!p.timing) return -1;
+  if (p.ev_next + 2 > (int)p.ev_pool.size()) {
+    for (int i = 0; i < 64; ++i) {
+      hipEvent_t e;
+      OAC_HIP_CHECK(hipEventCreate(&e));
+      p.ev_pool.push_back(e);
+    }
+  }
+  const int i = p.ev_next;
+  p.ev_next += 2;
+  OAC_HIP_CHECK(hipEventRecord(p.ev_pool[i], s));
+  return i;
+}
+static int tock(SacPlan& p, int kind, int i, hipStream_t s) {
+  if (i < 0) return 0;
+  OAC_HIP_CHECK(hipEventRecord(p.ev_pool[i + 1], s));
+  p.ev_pending.push_back({kind, i});
+  return 0;
+}
+#define TIMED(p, kind, s, call)          \
+  do {                                   \
+    const int _t = tick(p, s);           \
+    call;                                \
+    if (tock(p, kind, _t, s)) return 1;  \
+  } while (0)
+
 static int run_gemm(SacPlan& p, GemmBatch& gb, hipStream_t s) {
   gemm_batch_finalize(gb, p.cfg);
-  OAC_HIP_CHECK(gemm_batch_launch(gb, p.cfg, s));
+  TIMED(p, K_GEMM, s, OAC_HIP_CHECK(gemm_batch_launch(gb, p.cfg, s)));
   p.launches++;
   return 0;
 }
@@ -242,7 +278,7 @@ static int phase0(SacPlan& p, int flags, hipStream_t s) {
       g.eps1 = p.W(OAC_WS_EPS1); g.eps2 = p.W(OAC_WS_EPS2); g.n_eps = B * Da;
     }
     g.seed = c.seed; g.state = p.state();
-    OAC_HIP_CHECK(launch_gather(g, s));
+    TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_gather(g, s)));
     p.launches++;
   }
   const float* pol = p.b.params;
@@ -291,10 +327,13 @@ static int phase0(SacPlan& p, int flags, hipStream_t s) {
                 p.W(OAC_WS_LOGP1), nullptr, 0};
     a.seg[1] = {p.W(OAC_WS_HEAD2), p.W(OAC_WS_EPS2), p.W(OAC_WS_ACT2), p.W(W_STD2), p.W(W_U2),
                 p.W(OAC_WS_LOGP2), nullptr, 0};
-    a.B = B; a.act_dim = Da; a.auto_alpha = c.auto_alpha; a.target_entropy = c.target_entropy;
-    a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.adam_eps = c.adam_eps;
-    a.partials = p.W(W_PARTIALS); a.state = p.state(); a.alpha = p.alpha();
-    OAC_HIP_CHECK(launch_policy_sample(a, 2, s));
+    a.B = B; a.act_dim = Da;
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_sample(a, 2, s)));
+    p.launches++;
+  }
+  if (c.world_size > 1 && c.auto_alpha) {  // local alpha partial for the all-reduce
+    LogpSumArgs a{p.W(OAC_WS_LOGP1), B, c.target_entropy, p.alpha()};
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_logp_sum(a, s)));
     p.launches++;
   }
   return 0;
@@ -352,10 +391,13 @@ static int phase1(SacPlan& p, hipStream_t s) {
     a.tq1 = p.W(OAC_WS_TQ1); a.tq2 = p.W(OAC_WS_TQ2); a.logp2 = p.W(OAC_WS_LOGP2);
     a.batch = X; a.ld_batch = RS; a.off_rew = c.off_rew; a.off_term = c.off_term;
     a.alpha = c.auto_alpha ? p.alpha() : nullptr;
+    a.state = p.state(); a.logp1 = p.W(OAC_WS_LOGP1); a.target_entropy = c.target_entropy;
+    a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.adam_eps = c.adam_eps;
+    a.world_size = c.world_size;
     a.reward_scale = c.reward_scale; a.discount = c.discount; a.B = B;
     a.y = p.W(OAC_WS_Y); a.dq1 = p.W(W_DQ1); a.dq2 = p.W(W_DQ2); a.gq1 = p.W(W_GQ1); a.gq2 = p.W(W_GQ2);
     a.sqe1 = p.W(OAC_WS_SQE1); a.sqe2 = p.W(OAC_WS_SQE2); a.qnew = p.W(OAC_WS_QNEW);
-    OAC_HIP_CHECK(launch_critic_targets(a, s));
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_critic_targets(a, s)));
     p.launches++;
   }
   {  // critic backward, hidden layer 1 + last layer (dW slabs) and dh1
@@ -405,6 +447,7 @@ static AdamSegArgs critic_adam_args(SacPlan& p, int reduce_only) {
   a.tau = c.tau; a.period = c.target_update_period;
   a.lr = c.qf_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
   a.state = p.state(); a.advance = 0; a.reduce_only = reduce_only;
+  a.alpha = c.auto_alpha ? p.alpha() : nullptr;
   return a;
 }
 
@@ -434,11 +477,11 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
     a.m = p.b.adam_m + L.q1_base; a.v = p.b.adam_v + L.q1_base; a.n = L.n_critics * L.q_size;
     a.target = p.b.targets; a.tau = p.c.tau; a.period = p.c.target_update_period;
     a.lr = p.c.qf_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
-    a.state = p.state(); a.advance = 0;
+    a.state = p.state(); a.advance = 0; a.alpha = p.c.auto_alpha ? p.alpha() : nullptr;
     OAC_HIP_CHECK(launch_adam(a, s));
   } else {
     AdamSegArgs a = critic_adam_args(p, 0);
-    OAC_HIP_CHECK(launch_adam_seg(a, s));
+    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam_seg(a, s)));
   }
   p.launches++;
   return 0;
@@ -477,7 +520,7 @@ static int phase2(SacPlan& p, hipStream_t s) {
     a.da1 = p.W(W_DA1); a.da2 = p.W(W_DA2); a.act = p.W(OAC_WS_ACT1); a.stdv = p.W(W_STD1);
     a.u = p.W(W_U1); a.eps = p.W(OAC_WS_EPS1); a.head = p.W(OAC_WS_HEAD1);
     a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.B = B; a.act_dim = Da; a.dhead = p.W(W_DHEAD);
-    OAC_HIP_CHECK(launch_policy_head_backward(a, s));
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head_backward(a, s)));
     p.launches++;
   }
   {  // policy heads: dW_head slab, dh2
@@ -507,7 +550,7 @@ static int run_step(SacPlan& p, int flags, hipStream_t s) {
   if (phase2_adam(p, s, 0)) return 1;
   if (phase2(p, s)) return 1;
   AdamSegArgs a = policy_adam_args(p, 0);
-  OAC_HIP_CHECK(launch_adam_seg(a, s));
+  TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam_seg(a, s)));
   p.launches++;
   return 0;
 }
@@ -529,7 +572,7 @@ static int validate(const oac_sac_config* c) {
   if (!c) { set_error("null config"); return 1; }
   if (c->kind != OAC_KIND_SAC && c->kind != OAC_KIND_PARTICLE) { set_error("bad kind %d", c->kind); return 1; }
   if (c->kind == OAC_KIND_SAC && c->q_out != 1) { set_error("SAC needs q_out == 1"); return 1; }
-  if (c->obs_dim < 1 || c->act_dim < 1 || c->act_dim > 64 || c->hidden < 1 || c->batch < 1) {
+  if (c->obs_dim < 1 || c->act_dim < 1 || c->act_dim > 32 || c->hidden < 1 || c->batch < 1) {
     set_error("bad dims obs=%d act=%d hidden=%d batch=%d", c->obs_dim, c->act_dim, c->hidden, c->batch);
     return 1;
   }
@@ -587,6 +630,7 @@ int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_s
 
 int oac_sac_destroy(oac_sac* h) {
   if (!h) return 0;
+  for (hipEvent_t e : h->plan.ev_pool) (void)hipEventDestroy(e);
   if (h->plan.exec) (void)hipGraphExecDestroy(h->plan.exec);
   if (h->plan.graph) (void)hipGraphDestroy(h->plan.graph);
   delete h;
@@ -597,7 +641,7 @@ int oac_sac_step(oac_sac* h, int flags, void* stream) {
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (!(flags & OAC_STEP_USE_GRAPH)) return run_step(p, flags, s);
+  if (!(flags & OAC_STEP_USE_GRAPH) || p.timing) return run_step(p, flags, s);
   const int gflags = flags & ~OAC_STEP_USE_GRAPH;
   if (!p.exec || p.graph_stream != s || p.graph_flags != gflags) {
     if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
@@ -660,6 +704,33 @@ int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows
 }
 
 int oac_sac_launch_count(oac_sac* h) { return h ? h->plan.launches : 0; }
+
+int oac_sac_set_timing(oac_sac* h, int enable) {
+  if (!h) { set_error("null handle"); return 1; }
+  h->plan.timing = enable != 0;
+  return 0;
+}
+
+int oac_sac_read_timing(oac_sac* h, double* ms_by_kind, int64_t* count_by_kind, int nkinds) {
+  if (!h) { set_error("null handle"); return 1; }
+  SacPlan& p = h->plan;
+  for (auto& pr : p.ev_pending) {
+    float ms = 0.f;
+    OAC_HIP_CHECK(hipEventSynchronize(p.ev_pool[pr.second + 1]));
+    OAC_HIP_CHECK(hipEventElapsedTime(&ms, p.ev_pool[pr.second], p.ev_pool[pr.second + 1]));
+    p.kind_ms[pr.first] += ms;
+    p.kind_count[pr.first] += 1;
+  }
+  p.ev_pending.clear();
+  p.ev_next = 0;
+  for (int k = 0; k < nkinds && k < OAC_NUM_KINDS; ++k) {
+    ms_by_kind[k] = p.kind_ms[k];
+    count_by_kind[k] = p.kind_count[k];
+    p.kind_ms[k] = 0;
+    p.kind_count[k] = 0;
+  }
+  return 0;
+}
 
 int oac_adam_polyak(float* p, const float* g, float* m, float* v, int64_t n, float* target,
                     float tau, int period, double lr, double beta1, double beta2, double eps,

@@ -155,7 +155,7 @@ class SACTrainer(object):
         self.params, self.grads = z(lay.params_total), z(lay.params_total)
         self.adam_m, self.adam_v = z(lay.params_total), z(lay.params_total)
         self.targets = z(lay.targets_total)
-        self.alpha_state = z(8)
+        self.alpha_state = z(16)
         self.step_state = torch.zeros(16, dtype=torch.int64, device=dev)
         self.policy = ArenaTanhGaussianPolicy(self.params, 0, lay, Do, Da, H)
         self.qf1 = ArenaFlattenMlp(self.params, lay.q1_base, lay, Do, Da, H, 1)
