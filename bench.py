@@ -209,7 +209,7 @@ def main():
     # sanity: the trained state is finite
     assert torch.isfinite(tr.params).all().item(), "non-finite parameters"
 
-    kt = kernel_timing(tr, rb, stream, B, args.timing_steps) if rank == 0 else None
+    kt = kernel_timing(tr, rb, stream, B, args.timing_steps)   # every rank steps (collectives)
     out = None
     if rank == 0:
         gk = kt["gemm_grouped"]

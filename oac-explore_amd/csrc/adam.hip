@@ -48,8 +48,11 @@ __device__ __forceinline__ float polyak1(const AdamConsts& c, float t, float p) 
 }
 
 // Block 0, thread 0 only.  advance == 0 (critic Adam): snapshot t for the
-// final Adam and commit the alpha update; advance == 1 (final policy Adam):
-// advance the step counters.  No other block of the launch reads these fields.
+// final Adam; advance == 1 (final policy Adam): advance the step counters.
+// Either may commit the alpha update published earlier in the step (`as`
+// non-null: SAC commits in the critic Adam, the particle trainer -- whose
+// alpha update comes after the critic step -- in the policy Adam).  No other
+// block of the launch reads these fields.
 __device__ __forceinline__ void step_bookkeeping(StepState* st, AlphaState* as, int advance) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
   if (advance) {
@@ -57,8 +60,8 @@ __device__ __forceinline__ void step_bookkeeping(StepState* st, AlphaState* as, 
     st->batch_counter += 1;
   } else {
     st->t_snapshot = st->n_steps;
-    if (as) { as->log_alpha = as->next_log_alpha; as->m = as->next_m; as->v = as->next_v; }
   }
+  if (as) { as->log_alpha = as->next_log_alpha; as->m = as->next_m; as->v = as->next_v; }
 }
 
 __global__ void __launch_bounds__(256) adam_seg_kernel(AdamSegArgs a) {
@@ -96,7 +99,8 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(AdamArgs a) {
   const long stride = (long)gridDim.x * 256;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
     float4 p = reinterpret_cast<float4*>(a.p)[i];
-    const float4 g = reinterpret_cast<const float4*>(a.g)[i];
+    float4 g = reinterpret_cast<const float4*>(a.g)[i];
+    if (a.gscale != 1.f) { g.x *= a.gscale; g.y *= a.gscale; g.z *= a.gscale; g.w *= a.gscale; }
     float4 m = reinterpret_cast<float4*>(a.m)[i];
     float4 v = reinterpret_cast<float4*>(a.v)[i];
     adam1(c, p.x, g.x, m.x, v.x);
@@ -116,7 +120,7 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(AdamArgs a) {
   if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
     const long i = (n4 << 2) + threadIdx.x;
     float p = a.p[i], m = a.m[i], v = a.v[i];
-    adam1(c, p, a.g[i], m, v);
+    adam1(c, p, a.g[i] * a.gscale, m, v);
     a.p[i] = p; a.m[i] = m; a.v[i] = v;
     if (c.polyak) a.target[i] = polyak1(c, a.target[i], p);
   }

@@ -182,7 +182,7 @@ int oac_expl_create(int obs_dim, int act_dim, int hidden, const float* policy, c
   c.kind = OAC_KIND_SAC; c.obs_dim = obs_dim; c.act_dim = act_dim; c.hidden = hidden; c.q_out = 1;
   c.batch = 1; c.row_stride = ((2 * obs_dim + act_dim + 2 + 3) / 4) * 4;
   c.off_obs = 0; c.off_act = obs_dim; c.off_rew = obs_dim + act_dim; c.off_term = c.off_rew + 1;
-  c.off_next_obs = c.off_term + 1; c.gemm_cfg = 0;
+  c.off_next_obs = c.off_term + 1; c.gemm_cfg = 0; c.world_size = 1;
   if (oac_sac_query_layout(&c, &p.L)) { delete h; return 1; }
   expl_layout(p);
   *out = h;

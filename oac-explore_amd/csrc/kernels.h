@@ -111,6 +111,7 @@ struct AdamArgs {
   int advance;       // 0: critic Adam (t = n_steps; block 0 snapshots t, commits alpha)
                      // 1: final policy Adam (t = t_snapshot; block 0 advances the step)
   AlphaState* alpha; // commit next_* (critic Adam only); may be null
+  float gscale;      // gradient scale (1/world_size after an all-reduce SUM)
 };
 
 // Segment-aware reduce + Adam: one segment per (weight, bias) pair whose
@@ -135,6 +136,27 @@ struct AdamSegArgs {
   int reduce_only;        // 1: write the reduced gradient only (DP: all-reduce next)
   AlphaState* alpha;
 };
+
+// ParticleTrainer (share_layers) per-sample kernels, particle_trainer_oac.py
+struct ParticleTargetArgs {
+  const float* q; const float* tq;      // [B, K] critic / target critic outputs
+  const float* batch; long ld_batch; int off_rew, off_term;
+  float reward_scale, discount;
+  int B, K;
+  float* dq;                            // [B, K] dL/dq (sort backward scatter)
+  float* sqe;                           // [B, K] (sorted_q - y)^2 per sorted slot
+  float* y;                             // [B, K] quantile targets (sorted slots)
+};
+struct ParticleMinArgs {
+  const float* qn; int B, K;            // [B, K] Q(obs, a~) with the post-step critic
+  float* gq;                            // [B, K] -1/B at the argmin head
+  float* qmin;                          // [B]
+  // alpha update (same as CriticTargetArgs)
+  AlphaState* alpha; const StepState* state; const float* logp; float target_entropy;
+  double lr, beta1, beta2, adam_eps; int world_size;
+};
+hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s);
+hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s);
 
 struct LogpSumArgs { const float* logp; int B; float target_entropy; AlphaState* alpha; };
 hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s);

@@ -1,2 +1,370 @@
-// placeholder -- P-OAC K-head critic plan (filled in below)
+// P-OAC particle trainer step on MI355X (BASELINE configs[4]):
+// ParticleTrainer.train_from_torch with share_layers=True
+// (/root/reference/trainer/particle_trainer_oac.py:169-363) -- one critic with
+// K outputs (quantile "particles"), per-sample sort over K, quantile TD
+// targets without entropy, sum of K MSEs, then (after the critic Adam) the
+// policy forward, alpha update and the policy loss on the min head of the
+// POST-step critic, Polyak.  Reference order:
+//   Q(obs,a) [185-191] -> sort [192] -> pi(next_obs; eps1) [193-195]
+//   -> TQ(next_obs,a') sorted [198-202] -> y = scale*r + (1-d)*gamma*TQ_sorted [207]
+//   -> Adam(Q, grad sum_i MSE(sorted_i, y_i)) [247-256]
+//   -> pi(obs; eps2) [271-273] -> alpha [274-284]
+//   -> min_K Q_new(obs, a~) [286-292] -> Adam(pi) [295-300] -> Polyak [320-324]
+// The policy forward on obs uses the pre-step policy (it is only updated at
+// the end), so it runs in the first forward stage with everything else.
+#include <cstring>
+
+#include "../../include/oac_amd.h"
+#include "kernels.h"
 #include "oac_common.h"
+#include "plan_common.h"
+#include "sac_plan.h"
+
+namespace oac {
+
+enum PWs {
+  // public ids (OAC_WS_*) keep their meaning: HEAD1/ACT1/LOGP1 = policy(obs),
+  // HEAD2/ACT2/LOGP2 = policy(next_obs), EPS1 = next_obs noise (drawn first,
+  // line 193), EPS2 = obs noise (line 271), Q1 = Q(obs,a) [B,K],
+  // QN1 = Q_new(obs,a~) [B,K], TQ1 = TQ(next_obs,a') [B,K], Y / SQE1 [B,K]
+  // in sorted-slot order, QNEW = min_K Q_new [B].
+  X_H1P = OAC_WS_COUNT_PUBLIC, X_H2P, X_H1P2, X_H2P2, X_P, X_H1Q, X_H2Q, X_PT, X_H1T, X_H2T,
+  X_STD1, X_U1, X_STD2, X_U2, X_DQ, X_DH2Q, X_DH1Q, X_PN, X_H1N, X_H2N, X_GQ, X_DH2N, X_DH1N,
+  X_DA, X_DHEAD, X_DH2P, X_DH1P,
+  X_SLAB_Q0, X_SLAB_Q1, X_SLAB_QL, X_SLAB_P0, X_SLAB_P1, X_SLAB_PH,
+  X_COUNT
+};
+static_assert(X_COUNT <= kMaxWs, "workspace ids");
+
+void particle_layout_workspace(SacPlan& p) {
+  const oac_sac_config& c = p.c;
+  const int64_t B = c.batch, H = c.hidden, Da = c.act_dim, Do = c.obs_dim, K = c.q_out;
+  for (int i = 0; i < kMaxWs; ++i) p.ws[i] = {0, 0, 0};
+  auto set = [&](int id, int64_t r, int64_t cl) { p.ws[id] = {0, r, cl}; };
+  set(OAC_WS_BATCH, B, c.row_stride);
+  set(OAC_WS_EPS1, B, Da); set(OAC_WS_EPS2, B, Da);
+  set(OAC_WS_HEAD1, B, 2 * Da); set(OAC_WS_HEAD2, B, 2 * Da);
+  set(OAC_WS_ACT1, B, Da); set(OAC_WS_ACT2, B, Da);
+  set(OAC_WS_LOGP1, B, 1); set(OAC_WS_LOGP2, B, 1);
+  for (int id : {OAC_WS_Q1, OAC_WS_QN1, OAC_WS_TQ1, OAC_WS_Y, OAC_WS_SQE1}) set(id, B, K);
+  set(OAC_WS_QNEW, B, 1);
+  for (int id = X_H1P; id <= X_H2T; ++id) set(id, B, H);
+  for (int id : {X_STD1, X_U1, X_STD2, X_U2, X_DA}) set(id, B, Da);
+  set(X_DQ, B, K); set(X_GQ, B, K);
+  for (int id : {X_DH2Q, X_DH1Q, X_PN, X_H1N, X_H2N, X_DH2N, X_DH1N, X_DH2P, X_DH1P}) set(id, B, H);
+  set(X_DHEAD, B, 2 * Da);
+  set(X_SLAB_Q0, (int64_t)p.sp_q0.S * H, Do + Da + 1);
+  set(X_SLAB_Q1, (int64_t)p.sp_q1.S * H, H + 1);
+  set(X_SLAB_QL, (int64_t)p.sp_ql.S * K, H + 1);
+  set(X_SLAB_P0, (int64_t)p.sp_p0.S * H, Do + 1);
+  set(X_SLAB_P1, (int64_t)p.sp_p1.S * H, H + 1);
+  set(X_SLAB_PH, (int64_t)p.sp_ph.S * 2 * Da, H + 1);
+  int64_t off = 0;
+  for (int i = 0; i < X_COUNT; ++i) {
+    p.ws[i].off = off;
+    off = al64(off + p.ws[i].rows * p.ws[i].cols);
+  }
+  p.L.workspace_floats = off;
+}
+
+// ------------------------------------------------------------------ phases
+static int pphase0(SacPlan& p, int flags, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
+  const int K = c.q_out, Dq = Do + Da;
+  float* X = p.W(OAC_WS_BATCH);
+  const float* obs = X + c.off_obs;
+  const float* nobs = X + c.off_next_obs;
+  if (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS)) {
+    GatherArgs g;
+    std::memset(&g, 0, sizeof(g));
+    g.replay = p.b.replay; g.row_stride = RS; g.idx = p.b.idx_ring; g.ring_slots = p.b.ring_slots;
+    g.out = X; g.B = (flags & OAC_STEP_GATHER) ? B : 0;
+    if (flags & OAC_STEP_DEVICE_EPS) {
+      g.eps1 = p.W(OAC_WS_EPS1); g.eps2 = p.W(OAC_WS_EPS2); g.n_eps = B * Da;
+    }
+    g.seed = c.seed; g.state = p.state();
+    TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_gather(g, s)));
+    p.launches++;
+  }
+  const float* pol = p.b.params;
+  const float* q = p.b.params + L.q1_base;
+  const float* tq = p.b.targets;
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_fwd(obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(X_H1P), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
+    add(gb, t_fwd(nobs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(X_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
+    GemmTask t = t_fwd(obs, RS, B, Do, q + L.q_fc0_w, Dq, H, p.W(X_P), H, EPI_BIAS_RANK_RELU, q + L.q_fc0_b);
+    t.U = X + c.off_act; t.ldu = RS; t.V = q + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
+    t.C2 = p.W(X_H1Q); t.ldc2 = H;
+    add(gb, t);
+    add(gb, t_fwd(nobs, RS, B, Do, tq + L.q_fc0_w, Dq, H, p.W(X_PT), H, EPI_BIAS, tq + L.q_fc0_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_fwd(p.W(X_H1P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(X_H2P), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
+    add(gb, t_fwd(p.W(X_H1P2), H, B, H, pol + L.pol_fc1_w, H, H, p.W(X_H2P2), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
+    add(gb, t_fwd(p.W(X_H1Q), H, B, H, q + L.q_fc1_w, H, H, p.W(X_H2Q), H, EPI_BIAS_RELU, q + L.q_fc1_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_fwd(p.W(X_H2P), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD1), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
+    add(gb, t_fwd(p.W(X_H2P2), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD2), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
+    add(gb, t_fwd(p.W(X_H2Q), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_Q1), K, EPI_BIAS, q + L.q_last_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    PolicySampleArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.seg[0] = {p.W(OAC_WS_HEAD1), p.W(OAC_WS_EPS2), p.W(OAC_WS_ACT1), p.W(X_STD1), p.W(X_U1),
+                p.W(OAC_WS_LOGP1), nullptr, 0};
+    a.seg[1] = {p.W(OAC_WS_HEAD2), p.W(OAC_WS_EPS1), p.W(OAC_WS_ACT2), p.W(X_STD2), p.W(X_U2),
+                p.W(OAC_WS_LOGP2), nullptr, 0};
+    a.B = B; a.act_dim = Da;
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_sample(a, 2, s)));
+    p.launches++;
+  }
+  if (c.world_size > 1 && c.auto_alpha) {
+    LogpSumArgs a{p.W(OAC_WS_LOGP1), B, c.target_entropy, p.alpha()};
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_logp_sum(a, s)));
+    p.launches++;
+  }
+  return 0;
+}
+
+static int pphase1(SacPlan& p, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
+  const int K = c.q_out, Dq = Do + Da;
+  float* X = p.W(OAC_WS_BATCH);
+  const float* q = p.b.params + L.q1_base;
+  const float* tq = p.b.targets;
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    GemmTask t = t_fwd(p.W(OAC_WS_ACT2), Da, B, Da, tq + L.q_fc0_w + Do, Dq, H, p.W(X_H1T), H,
+                       EPI_ADD_RELU, nullptr);
+    t.aux = p.W(X_PT); t.ld_aux = H;
+    add(gb, t);
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_fwd(p.W(X_H1T), H, B, H, tq + L.q_fc1_w, H, H, p.W(X_H2T), H, EPI_BIAS_RELU, tq + L.q_fc1_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_fwd(p.W(X_H2T), H, B, H, tq + L.q_last_w, H, K, p.W(OAC_WS_TQ1), K, EPI_BIAS, tq + L.q_last_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    ParticleTargetArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.q = p.W(OAC_WS_Q1); a.tq = p.W(OAC_WS_TQ1); a.batch = X; a.ld_batch = RS;
+    a.off_rew = c.off_rew; a.off_term = c.off_term; a.reward_scale = c.reward_scale;
+    a.discount = c.discount; a.B = B; a.K = K;
+    a.dq = p.W(X_DQ); a.sqe = p.W(OAC_WS_SQE1); a.y = p.W(OAC_WS_Y);
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_particle_targets(a, s)));
+    p.launches++;
+  }
+  {  // last layer: dW_last slab and dh2 = (dq . W_last) * [h2 > 0]
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dw(p.W(X_DQ), K, K, B, p.W(X_H2Q), H, H, p.W(X_SLAB_QL), p.sp_ql));
+    add(gb, t_dx(p.W(X_DQ), K, B, K, q + L.q_last_w, H, H, p.W(X_DH2Q), H, p.W(X_H2Q), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dw(p.W(X_DH2Q), H, H, B, p.W(X_H1Q), H, H, p.W(X_SLAB_Q1), p.sp_q1));
+    add(gb, t_dx(p.W(X_DH2Q), H, B, H, q + L.q_fc1_w, H, H, p.W(X_DH1Q), H, p.W(X_H1Q), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dw(p.W(X_DH1Q), H, H, B, X + c.off_obs, RS, Dq, p.W(X_SLAB_Q0), p.sp_q0));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  return 0;
+}
+
+static AdamSegArgs pcritic_adam(SacPlan& p, int reduce_only) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int H = c.hidden, Dq = c.obs_dim + c.act_dim;
+  AdamSegArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.seg[a.nseg++] = seg(p.W(X_SLAB_Q0), p.sp_q0, H, Dq, L.q_fc0_w, L.q_fc0_b);
+  a.seg[a.nseg++] = seg(p.W(X_SLAB_Q1), p.sp_q1, H, H, L.q_fc1_w, L.q_fc1_b);
+  a.seg[a.nseg++] = seg(p.W(X_SLAB_QL), p.sp_ql, c.q_out, H, L.q_last_w, L.q_last_b);
+  finalize_segs(a);
+  a.p = p.b.params + L.q1_base; a.g = p.b.grads + L.q1_base;
+  a.m = p.b.adam_m + L.q1_base; a.v = p.b.adam_v + L.q1_base;
+  a.target = p.b.targets; a.tau = c.tau; a.period = c.target_update_period;
+  a.lr = c.qf_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
+  a.state = p.state(); a.advance = 0; a.reduce_only = reduce_only; a.alpha = nullptr;
+  return a;
+}
+
+static AdamSegArgs ppolicy_adam(SacPlan& p, int reduce_only) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int H = c.hidden, Do = c.obs_dim, Da = c.act_dim;
+  AdamSegArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.seg[a.nseg++] = seg(p.W(X_SLAB_P0), p.sp_p0, H, Do, L.pol_fc0_w, L.pol_fc0_b);
+  a.seg[a.nseg++] = seg(p.W(X_SLAB_P1), p.sp_p1, H, H, L.pol_fc1_w, L.pol_fc1_b);
+  a.seg[a.nseg++] = seg(p.W(X_SLAB_PH), p.sp_ph, 2 * Da, H, L.pol_head_w, L.pol_head_b);
+  finalize_segs(a);
+  a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.target = nullptr;
+  a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
+  a.state = p.state(); a.advance = reduce_only ? 0 : 1; a.reduce_only = reduce_only;
+  a.alpha = (!reduce_only && c.auto_alpha) ? p.alpha() : nullptr;
+  return a;
+}
+
+// critic Adam done; post-step critic forward on (obs, a~), alpha, policy grads
+static int pphase2(SacPlan& p, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
+  const int K = c.q_out, Dq = Do + Da;
+  float* X = p.W(OAC_WS_BATCH);
+  const float* pol = p.b.params;
+  const float* q = p.b.params + L.q1_base;
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    GemmTask t = t_fwd(X + c.off_obs, RS, B, Do, q + L.q_fc0_w, Dq, H, p.W(X_PN), H,
+                       EPI_BIAS_RANK_RELU, q + L.q_fc0_b);
+    t.U = p.W(OAC_WS_ACT1); t.ldu = Da; t.V = q + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
+    t.C2 = p.W(X_H1N); t.ldc2 = H;
+    add(gb, t);
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_fwd(p.W(X_H1N), H, B, H, q + L.q_fc1_w, H, H, p.W(X_H2N), H, EPI_BIAS_RELU, q + L.q_fc1_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_fwd(p.W(X_H2N), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_QN1), K, EPI_BIAS, q + L.q_last_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    ParticleMinArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.qn = p.W(OAC_WS_QN1); a.B = B; a.K = K; a.gq = p.W(X_GQ); a.qmin = p.W(OAC_WS_QNEW);
+    a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.state = p.state(); a.logp = p.W(OAC_WS_LOGP1);
+    a.target_entropy = c.target_entropy; a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2;
+    a.adam_eps = c.adam_eps; a.world_size = c.world_size;
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_particle_min(a, s)));
+    p.launches++;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dx(p.W(X_GQ), K, B, K, q + L.q_last_w, H, H, p.W(X_DH2N), H, p.W(X_H2N), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dx(p.W(X_DH2N), H, B, H, q + L.q_fc1_w, H, H, p.W(X_DH1N), H, p.W(X_H1N), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dx(p.W(X_DH1N), H, B, H, q + L.q_fc0_w + Do, Dq, Da, p.W(X_DA), Da, nullptr, 0));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    PolicyHeadBwdArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.da1 = p.W(X_DA); a.da2 = nullptr; a.act = p.W(OAC_WS_ACT1); a.stdv = p.W(X_STD1);
+    a.u = p.W(X_U1); a.eps = p.W(OAC_WS_EPS2); a.head = p.W(OAC_WS_HEAD1);
+    a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.B = B; a.act_dim = Da; a.dhead = p.W(X_DHEAD);
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head_backward(a, s)));
+    p.launches++;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dw(p.W(X_DHEAD), 2 * Da, 2 * Da, B, p.W(X_H2P), H, H, p.W(X_SLAB_PH), p.sp_ph));
+    add(gb, t_dx(p.W(X_DHEAD), 2 * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(X_DH2P), H, p.W(X_H2P), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dw(p.W(X_DH2P), H, H, B, p.W(X_H1P), H, H, p.W(X_SLAB_P1), p.sp_p1));
+    add(gb, t_dx(p.W(X_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(X_DH1P), H, p.W(X_H1P), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb; gb.ntasks = 0;
+    add(gb, t_dw(p.W(X_DH1P), H, H, B, X + c.off_obs, RS, Do, p.W(X_SLAB_P0), p.sp_p0));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  return 0;
+}
+
+int particle_run_step(SacPlan& p, int flags, hipStream_t s) {
+  p.launches = 0;
+  if (pphase0(p, flags, s)) return 1;
+  if (pphase1(p, s)) return 1;
+  {
+    AdamSegArgs a = pcritic_adam(p, 0);
+    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam_seg(a, s)));
+    p.launches++;
+  }
+  if (pphase2(p, s)) return 1;
+  {
+    AdamSegArgs a = ppolicy_adam(p, 0);
+    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam_seg(a, s)));
+    p.launches++;
+  }
+  return 0;
+}
+
+int particle_step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
+  const oac_sac_layout& L = p.L;
+  switch (phase) {
+    case 0: return pphase0(p, flags, s);
+    case 1: {
+      if (pphase1(p, s)) return 1;
+      AdamSegArgs a = pcritic_adam(p, 1);
+      OAC_HIP_CHECK(launch_adam_seg(a, s));
+      return 0;
+    }
+    case 2: {
+      AdamArgs a;
+      std::memset(&a, 0, sizeof(a));
+      a.p = p.b.params + L.q1_base; a.g = p.b.grads + L.q1_base;
+      a.m = p.b.adam_m + L.q1_base; a.v = p.b.adam_v + L.q1_base; a.n = L.q_size;
+      a.target = p.b.targets; a.tau = p.c.tau; a.period = p.c.target_update_period;
+      a.lr = p.c.qf_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
+      a.state = p.state(); a.advance = 0; a.alpha = nullptr;
+      a.gscale = 1.f / (float)(p.c.world_size > 1 ? p.c.world_size : 1);
+      OAC_HIP_CHECK(launch_adam(a, s));
+      if (pphase2(p, s)) return 1;
+      AdamSegArgs b = ppolicy_adam(p, 1);
+      OAC_HIP_CHECK(launch_adam_seg(b, s));
+      return 0;
+    }
+    case 3: {
+      AdamArgs a;
+      std::memset(&a, 0, sizeof(a));
+      a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.n = L.pol_size;
+      a.lr = p.c.policy_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
+      a.state = p.state(); a.advance = 1; a.alpha = p.c.auto_alpha ? p.alpha() : nullptr;
+      a.gscale = 1.f / (float)(p.c.world_size > 1 ? p.c.world_size : 1);
+      OAC_HIP_CHECK(launch_adam(a, s));
+      return 0;
+    }
+    default:
+      set_error("bad phase %d", phase);
+      return 1;
+  }
+}
+
+}  // namespace oac

@@ -1,0 +1,153 @@
+// Shared machinery of the launch plans (SAC / particle trainers): workspace
+// bookkeeping, split-K sizing, GEMM task constructors, HIP-event timing.
+#pragma once
+#include <cstring>
+#include <utility>
+#include <vector>
+
+#include "kernels.h"
+#include "oac_common.h"
+
+namespace oac {
+
+static inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3); }
+static inline int64_t al64(int64_t x) { return (x + 63) & ~int64_t(63); }
+
+enum Kind { K_GEMM = 0, K_ROW = 1, K_ADAM = 2, K_GATHER = 3, OAC_NUM_KINDS = 4 };
+
+struct WsBuf { int64_t off, rows, cols; };
+struct Split { int S, kchunk; };
+
+struct PlanBase {
+  int cfg = 0;  // gemm tile config
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipStream_t graph_stream = nullptr;
+  int graph_flags = -1;
+  int launches = 0;
+  // HIP-event kernel timing (bench instrumentation; never inside a graph)
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, int>> ev_pending;   // (kind, index of the start event)
+  int ev_next = 0;
+  double kind_ms[OAC_NUM_KINDS] = {0};
+  long long kind_count[OAC_NUM_KINDS] = {0};
+};
+
+static inline Split choose_split(int K, int tiles, int cfg) {
+  const int bk = (cfg == 0) ? 64 : 32;
+  int S = 1;
+  if (K >= 512) {
+    int want = (512 + tiles - 1) / tiles;
+    int maxS = K / 256;
+    S = want < maxS ? want : maxS;
+    if (S < 1) S = 1;
+  }
+  int kchunk = (K + S - 1) / S;
+  kchunk = ((kchunk + bk - 1) / bk) * bk;
+  S = (K + kchunk - 1) / kchunk;
+  return {S, kchunk};
+}
+
+// ------------------------------------------------------------ task makers
+static inline GemmTask task0() {
+  GemmTask t;
+  std::memset(&t, 0, sizeof(t));
+  t.ksplit = 1;
+  return t;
+}
+
+// Y[M,N] = X[M,K] . W[N,K]^T   (W row-major [N, ldw])
+static inline GemmTask t_fwd(const float* X, long ldx, int M, int K, const float* W, long ldw, int N,
+                      float* C, long ldc, int epi, const float* bias) {
+  GemmTask t = task0();
+  t.A = X; t.lda = ldx; t.a_kc = 1;
+  t.B = W; t.ldb = ldw; t.b_kc = 1;
+  t.C = C; t.ldc = ldc; t.M = M; t.N = N; t.K = K;
+  t.epi = epi; t.bias = bias;
+  return t;
+}
+
+// dX[M,N] = dY[M,K] . W[K,N]  (W row-major [K, ldw]); epilogue mask from aux.
+static inline GemmTask t_dx(const float* dY, long lddy, int M, int K, const float* W, long ldw, int N,
+                     float* C, long ldc, const float* mask_src, long ld_mask_src) {
+  GemmTask t = task0();
+  t.A = dY; t.lda = lddy; t.a_kc = 1;
+  t.B = W; t.ldb = ldw; t.b_kc = 0;
+  t.C = C; t.ldc = ldc; t.M = M; t.N = N; t.K = K;
+  if (mask_src) { t.epi = EPI_MASK; t.aux = mask_src; t.ld_aux = ld_mask_src; }
+  else t.epi = EPI_STORE;
+  return t;
+}
+
+// dY rows given as s[b] * v[n] * (mask[b,n] > 0)  (rank-1 seed through a ReLU)
+static inline void set_rank1(GemmTask& t, const float* s, const float* v, const float* mask, long ldm) {
+  t.a_mode = A_RANK1_MASK; t.a_s = s; t.a_v = v; t.a_mask = mask; t.ld_mask = ldm;
+}
+
+// dW slab [S][M][Kin+1] = dY^T[M,B] . [X | 1][B, Kin+1]   (dY row-major [B, lddy])
+static inline GemmTask t_dw(const float* dY, long lddy, int M, int Bn, const float* X, long ldx, int Kin,
+                     float* slab, Split sp) {
+  GemmTask t = task0();
+  t.A = dY; t.lda = lddy; t.a_kc = 0;
+  t.B = X; t.ldb = ldx; t.b_kc = 0; t.b_ones = 1;
+  t.M = M; t.N = Kin + 1; t.K = Bn;
+  t.C = slab; t.ldc = Kin + 1; t.epi = EPI_SLAB;
+  t.ksplit = sp.S; t.kchunk = sp.kchunk; t.slab_stride = (long)M * (Kin + 1);
+  return t;
+}
+
+static inline int tick(PlanBase& p, hipStream_t s) {
+  if (!p.timing) return -1;
+  if (p.ev_next + 2 > (int)p.ev_pool.size()) {
+    for (int i = 0; i < 64; ++i) {
+      hipEvent_t e;
+      OAC_HIP_CHECK(hipEventCreate(&e));
+      p.ev_pool.push_back(e);
+    }
+  }
+  const int i = p.ev_next;
+  p.ev_next += 2;
+  OAC_HIP_CHECK(hipEventRecord(p.ev_pool[i], s));
+  return i;
+}
+static inline int tock(PlanBase& p, int kind, int i, hipStream_t s) {
+  if (i < 0) return 0;
+  OAC_HIP_CHECK(hipEventRecord(p.ev_pool[i + 1], s));
+  p.ev_pending.push_back({kind, i});
+  return 0;
+}
+#define TIMED(p, kind, s, call)          \
+  do {                                   \
+    const int _t = tick(p, s);           \
+    call;                                \
+    if (tock(p, kind, _t, s)) return 1;  \
+  } while (0)
+
+static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {
+  gemm_batch_finalize(gb, p.cfg);
+  TIMED(p, K_GEMM, s, OAC_HIP_CHECK(gemm_batch_launch(gb, p.cfg, s)));
+  p.launches++;
+  return 0;
+}
+
+static inline void add(GemmBatch& gb, const GemmTask& t) { gb.t[gb.ntasks++] = t; }
+
+static inline AdamSeg seg(const float* slab, Split sp, int M, int Kin, int64_t off_w, int64_t off_b) {
+  AdamSeg s;
+  s.slab = slab; s.S = sp.S; s.M = M; s.ncols = Kin + 1;
+  s.slab_stride = (long)M * (Kin + 1);
+  s.off_w = off_w; s.off_b = off_b; s.elem_begin = 0;
+  return s;
+}
+
+static inline void finalize_segs(AdamSegArgs& a) {
+  long tot = 0;
+  for (int i = 0; i < a.nseg; ++i) {
+    a.seg[i].elem_begin = tot;
+    tot += (long)a.seg[i].M * a.seg[i].ncols;
+  }
+  a.total = tot;
+}
+
+}  // namespace oac

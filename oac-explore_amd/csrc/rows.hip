@@ -259,3 +259,104 @@ hipError_t launch_oac_final(const OacArgs& a, hipStream_t s) {
 }
 
 }  // namespace oac
+
+namespace oac {
+
+// --------------------------------------------------------------------------
+// ParticleTrainer (OAC flavour, share_layers=True),
+// /root/reference/trainer/particle_trainer_oac.py:185-256:
+//   sorted_qs = sort_K(Q(obs, a));  tq_sorted = sort_K(TQ(next_obs, a'))
+//   y_i = scale*r + (1-d)*gamma*tq_sorted_i                      (207-208)
+//   qf_loss = sum_i MSE(sorted_qs_i, y_i)   (NOT divided by K)   (247-251)
+// The per-sample sort over K (<= 16) is an in-register stable insertion
+// sort; the gradient is scattered back through the sort permutation.
+// --------------------------------------------------------------------------
+constexpr int kMaxHeads = 16;
+
+__device__ __forceinline__ void sort_k(float (&v)[kMaxHeads], int (&ix)[kMaxHeads], int K) {
+  for (int i = 1; i < K; ++i) {
+    const float x = v[i];
+    const int xi = ix[i];
+    int j = i - 1;
+    while (j >= 0 && v[j] > x) { v[j + 1] = v[j]; ix[j + 1] = ix[j]; --j; }
+    v[j + 1] = x;
+    ix[j + 1] = xi;
+  }
+}
+
+__global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArgs p) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= p.B) return;
+  const int K = p.K;
+  float q[kMaxHeads], t[kMaxHeads];
+  int qi[kMaxHeads], tix[kMaxHeads];
+  for (int i = 0; i < K; ++i) {
+    q[i] = p.q[(long)r * K + i]; qi[i] = i;
+    t[i] = p.tq[(long)r * K + i]; tix[i] = i;
+  }
+  sort_k(q, qi, K);
+  sort_k(t, tix, K);
+  const float rew = p.batch[(long)r * p.ld_batch + p.off_rew];
+  const float term = p.batch[(long)r * p.ld_batch + p.off_term];
+  const float invB = 1.f / (float)p.B;
+  const float sr = __fmul_rn(p.reward_scale, rew);
+  const float gd = __fmul_rn(1.f - term, p.discount);
+  for (int i = 0; i < K; ++i) {
+    const float y = __fadd_rn(sr, __fmul_rn(gd, t[i]));
+    const float d = q[i] - y;
+    p.y[(long)r * K + i] = y;
+    p.sqe[(long)r * K + i] = d * d;
+    p.dq[(long)r * K + qi[i]] = __fmul_rn(2.f * d, invB);
+  }
+}
+
+// sorted_qs[0] of Q(obs, a~) with the post-step critic (particle_trainer_oac.py:286-295)
+// -> gradient seed -1/B on the argmin head; plus the alpha update (274-281),
+// computed identically by every block, published by block 0 (committed by
+// the policy Adam, which reads no alpha field).
+__global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
+  __shared__ float red[256];
+  if (p.alpha && blockIdx.x == 0) {
+    const float S = (p.world_size > 1) ? p.alpha->sum
+                                       : block_logp_sum(p.logp, p.B, p.target_entropy, red);
+    if (threadIdx.x == 0) {
+      AlphaState* as = p.alpha;
+      const float n = (float)((long long)p.B * (p.world_size > 1 ? p.world_size : 1));
+      const float la_old = as->log_alpha;
+      const float g = -(S / n);
+      const double t = (double)(p.state->n_steps + 1);
+      const double bc1 = 1.0 - pow(p.beta1, t);
+      const double bc2 = 1.0 - pow(p.beta2, t);
+      const float m = __fadd_rn(__fmul_rn(as->m, (float)p.beta1), __fmul_rn((float)(1.0 - p.beta1), g));
+      const float v = __fadd_rn(__fmul_rn(as->v, (float)p.beta2),
+                                __fmul_rn(__fmul_rn((float)(1.0 - p.beta2), g), g));
+      const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), (float)sqrt(bc2)), (float)p.adam_eps);
+      const float la = __fadd_rn(la_old, __fdiv_rn(__fmul_rn(-(float)(p.lr / bc1), m), denom));
+      as->next_log_alpha = la; as->next_m = m; as->next_v = v;
+      as->alpha = expf(la); as->grad = g; as->alpha_loss = -(la_old * S) / n;
+    }
+  }
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= p.B) return;
+  const int K = p.K;
+  int best = 0;
+  float bv = p.qn[(long)r * K];
+  for (int i = 1; i < K; ++i) {
+    const float x = p.qn[(long)r * K + i];
+    if (x < bv) { bv = x; best = i; }
+  }
+  const float invB = 1.f / (float)p.B;
+  for (int i = 0; i < K; ++i) p.gq[(long)r * K + i] = (i == best) ? -invB : 0.f;
+  p.qmin[r] = bv;
+}
+
+hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(particle_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(particle_min_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace oac

@@ -18,6 +18,8 @@
 #include "../../include/oac_amd.h"
 #include "kernels.h"
 #include "oac_common.h"
+#include "plan_common.h"
+#include "sac_plan.h"
 
 namespace oac {
 
@@ -28,9 +30,6 @@ void set_error(const char* fmt, ...) {
   vsnprintf(g_err, sizeof(g_err), fmt, ap);
   va_end(ap);
 }
-
-static inline int64_t al4(int64_t x) { return (x + 3) & ~int64_t(3); }
-static inline int64_t al64(int64_t x) { return (x + 63) & ~int64_t(63); }
 
 // ---------------------------------------------------------------- layout
 static void compute_layout(const oac_sac_config& c, oac_sac_layout& L) {
@@ -71,54 +70,6 @@ enum Ws {
   W_COUNT
 };
 
-struct WsBuf { int64_t off, rows, cols; };
-
-enum Kind { K_GEMM = 0, K_ROW = 1, K_ADAM = 2, K_GATHER = 3, OAC_NUM_KINDS = 4 };
-
-struct Split { int S, kchunk; };
-
-struct SacPlan {
-  oac_sac_config c;
-  oac_sac_layout L;
-  oac_sac_buffers b;
-  WsBuf ws[W_COUNT];
-  int cfg;  // gemm tile config
-  Split sp_q0, sp_q1, sp_ql, sp_p0, sp_p1, sp_ph;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
-  hipStream_t graph_stream = nullptr;
-  int graph_flags = -1;
-  int launches = 0;
-  // HIP-event kernel timing (bench instrumentation; never inside a graph)
-  bool timing = false;
-  std::vector<hipEvent_t> ev_pool;
-  std::vector<std::pair<int, int>> ev_pending;   // (kind, index of the start event)
-  int ev_next = 0;
-  double kind_ms[OAC_NUM_KINDS] = {0};
-  long long kind_count[OAC_NUM_KINDS] = {0};
-
-  float* W(int id) const { return b.workspace + ws[id].off; }
-  float* P(int64_t off) const { return b.params + off; }
-  float* T(int64_t off) const { return b.targets + off; }
-  StepState* state() const { return reinterpret_cast<StepState*>(b.step_state); }
-  AlphaState* alpha() const { return reinterpret_cast<AlphaState*>(b.alpha_state); }
-};
-
-static Split choose_split(int K, int tiles, int cfg) {
-  const int bk = (cfg == 0) ? 64 : 32;
-  int S = 1;
-  if (K >= 512) {
-    int want = (512 + tiles - 1) / tiles;
-    int maxS = K / 256;
-    S = want < maxS ? want : maxS;
-    if (S < 1) S = 1;
-  }
-  int kchunk = (K + S - 1) / S;
-  kchunk = ((kchunk + bk - 1) / bk) * bk;
-  S = (K + kchunk - 1) / kchunk;
-  return {S, kchunk};
-}
-
 static void layout_workspace(SacPlan& p) {
   const oac_sac_config& c = p.c;
   const int64_t B = c.batch, H = c.hidden, Da = c.act_dim, Do = c.obs_dim, Q = c.q_out;
@@ -154,107 +105,6 @@ static void layout_workspace(SacPlan& p) {
     off = al64(off + p.ws[i].rows * p.ws[i].cols);
   }
   p.L.workspace_floats = off;
-}
-
-// ------------------------------------------------------------ task makers
-static GemmTask task0() {
-  GemmTask t;
-  std::memset(&t, 0, sizeof(t));
-  t.ksplit = 1;
-  return t;
-}
-
-// Y[M,N] = X[M,K] . W[N,K]^T   (W row-major [N, ldw])
-static GemmTask t_fwd(const float* X, long ldx, int M, int K, const float* W, long ldw, int N,
-                      float* C, long ldc, int epi, const float* bias) {
-  GemmTask t = task0();
-  t.A = X; t.lda = ldx; t.a_kc = 1;
-  t.B = W; t.ldb = ldw; t.b_kc = 1;
-  t.C = C; t.ldc = ldc; t.M = M; t.N = N; t.K = K;
-  t.epi = epi; t.bias = bias;
-  return t;
-}
-
-// dX[M,N] = dY[M,K] . W[K,N]  (W row-major [K, ldw]); epilogue mask from aux.
-static GemmTask t_dx(const float* dY, long lddy, int M, int K, const float* W, long ldw, int N,
-                     float* C, long ldc, const float* mask_src, long ld_mask_src) {
-  GemmTask t = task0();
-  t.A = dY; t.lda = lddy; t.a_kc = 1;
-  t.B = W; t.ldb = ldw; t.b_kc = 0;
-  t.C = C; t.ldc = ldc; t.M = M; t.N = N; t.K = K;
-  if (mask_src) { t.epi = EPI_MASK; t.aux = mask_src; t.ld_aux = ld_mask_src; }
-  else t.epi = EPI_STORE;
-  return t;
-}
-
-// dY rows given as s[b] * v[n] * (mask[b,n] > 0)  (rank-1 seed through a ReLU)
-static void set_rank1(GemmTask& t, const float* s, const float* v, const float* mask, long ldm) {
-  t.a_mode = A_RANK1_MASK; t.a_s = s; t.a_v = v; t.a_mask = mask; t.ld_mask = ldm;
-}
-
-// dW slab [S][M][Kin+1] = dY^T[M,B] . [X | 1][B, Kin+1]   (dY row-major [B, lddy])
-static GemmTask t_dw(const float* dY, long lddy, int M, int Bn, const float* X, long ldx, int Kin,
-                     float* slab, Split sp) {
-  GemmTask t = task0();
-  t.A = dY; t.lda = lddy; t.a_kc = 0;
-  t.B = X; t.ldb = ldx; t.b_kc = 0; t.b_ones = 1;
-  t.M = M; t.N = Kin + 1; t.K = Bn;
-  t.C = slab; t.ldc = Kin + 1; t.epi = EPI_SLAB;
-  t.ksplit = sp.S; t.kchunk = sp.kchunk; t.slab_stride = (long)M * (Kin + 1);
-  return t;
-}
-
-static int tick(SacPlan& p, hipStream_t s) {
-  if (!p.timing) return -1;
-  if (p.ev_next + 2 > (int)p.ev_pool.size()) {
-    for (int i = 0; i < 64; ++i) {
-      hipEvent_t e;
-      OAC_HIP_CHECK(hipEventCreate(&e));
-      p.ev_pool.push_back(e);
-    }
-  }
-  const int i = p.ev_next;
-  p.ev_next += 2;
-  OAC_HIP_CHECK(hipEventRecord(p.ev_pool[i], s));
-  return i;
-}
-static int tock(SacPlan& p, int kind, int i, hipStream_t s) {
-  if (i < 0) return 0;
-  OAC_HIP_CHECK(hipEventRecord(p.ev_pool[i + 1], s));
-  p.ev_pending.push_back({kind, i});
-  return 0;
-}
-#define TIMED(p, kind, s, call)          \
-  do {                                   \
-    const int _t = tick(p, s);           \
-    call;                                \
-    if (tock(p, kind, _t, s)) return 1;  \
-  } while (0)
-
-static int run_gemm(SacPlan& p, GemmBatch& gb, hipStream_t s) {
-  gemm_batch_finalize(gb, p.cfg);
-  TIMED(p, K_GEMM, s, OAC_HIP_CHECK(gemm_batch_launch(gb, p.cfg, s)));
-  p.launches++;
-  return 0;
-}
-
-static void add(GemmBatch& gb, const GemmTask& t) { gb.t[gb.ntasks++] = t; }
-
-static AdamSeg seg(const float* slab, Split sp, int M, int Kin, int64_t off_w, int64_t off_b) {
-  AdamSeg s;
-  s.slab = slab; s.S = sp.S; s.M = M; s.ncols = Kin + 1;
-  s.slab_stride = (long)M * (Kin + 1);
-  s.off_w = off_w; s.off_b = off_b; s.elem_begin = 0;
-  return s;
-}
-
-static void finalize_segs(AdamSegArgs& a) {
-  long tot = 0;
-  for (int i = 0; i < a.nseg; ++i) {
-    a.seg[i].elem_begin = tot;
-    tot += (long)a.seg[i].M * a.seg[i].ncols;
-  }
-  a.total = tot;
 }
 
 // ----------------------------------------------------------------- phases
@@ -478,6 +328,7 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
     a.target = p.b.targets; a.tau = p.c.tau; a.period = p.c.target_update_period;
     a.lr = p.c.qf_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
     a.state = p.state(); a.advance = 0; a.alpha = p.c.auto_alpha ? p.alpha() : nullptr;
+    a.gscale = 1.f / (float)(p.c.world_size > 1 ? p.c.world_size : 1);
     OAC_HIP_CHECK(launch_adam(a, s));
   } else {
     AdamSegArgs a = critic_adam_args(p, 0);
@@ -572,11 +423,16 @@ static int validate(const oac_sac_config* c) {
   if (!c) { set_error("null config"); return 1; }
   if (c->kind != OAC_KIND_SAC && c->kind != OAC_KIND_PARTICLE) { set_error("bad kind %d", c->kind); return 1; }
   if (c->kind == OAC_KIND_SAC && c->q_out != 1) { set_error("SAC needs q_out == 1"); return 1; }
+  if (c->kind == OAC_KIND_PARTICLE && (c->q_out < 1 || c->q_out > 16)) {
+    set_error("particle critic: 1 <= q_out <= 16 heads");
+    return 1;
+  }
   if (c->obs_dim < 1 || c->act_dim < 1 || c->act_dim > 32 || c->hidden < 1 || c->batch < 1) {
     set_error("bad dims obs=%d act=%d hidden=%d batch=%d", c->obs_dim, c->act_dim, c->hidden, c->batch);
     return 1;
   }
   if (c->row_stride % 4 != 0) { set_error("row_stride must be a multiple of 4"); return 1; }
+  if (c->world_size < 1) { set_error("world_size must be >= 1"); return 1; }
   if (c->off_act != c->off_obs + c->obs_dim) { set_error("row layout: act must follow obs"); return 1; }
   if (c->off_obs < 0 || c->off_next_obs + c->obs_dim > c->row_stride ||
       c->off_act + c->act_dim > c->row_stride || c->off_rew >= c->row_stride ||
@@ -608,7 +464,8 @@ int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out) {
   p.c = *cfg;
   compute_layout(p.c, p.L);
   plan_splits(p);
-  layout_workspace(p);
+  if (p.c.kind == OAC_KIND_PARTICLE) particle_layout_workspace(p);
+  else layout_workspace(p);
   *out = p.L;
   return 0;
 }
@@ -616,13 +473,13 @@ int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out) {
 int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_sac** out) {
   if (validate(cfg)) return 1;
   if (!bufs || !out) { set_error("null buffers/out"); return 1; }
-  if (cfg->kind != OAC_KIND_SAC) { set_error("use the particle entry points for kind=PARTICLE"); return 1; }
   oac_sac* h = new oac_sac();
   SacPlan& p = h->plan;
   p.c = *cfg;
   compute_layout(p.c, p.L);
   plan_splits(p);
-  layout_workspace(p);
+  if (p.c.kind == OAC_KIND_PARTICLE) particle_layout_workspace(p);
+  else layout_workspace(p);
   p.b = *bufs;
   *out = h;
   return 0;
@@ -640,14 +497,18 @@ int oac_sac_destroy(oac_sac* h) {
 int oac_sac_step(oac_sac* h, int flags, void* stream) {
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
+  if (p.c.world_size > 1) { set_error("world_size > 1: drive the step with oac_sac_step_phase"); return 1; }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (!(flags & OAC_STEP_USE_GRAPH) || p.timing) return run_step(p, flags, s);
+  auto step = [&](int f) {
+    return p.c.kind == OAC_KIND_PARTICLE ? particle_run_step(p, f, s) : run_step(p, f, s);
+  };
+  if (!(flags & OAC_STEP_USE_GRAPH) || p.timing) return step(flags);
   const int gflags = flags & ~OAC_STEP_USE_GRAPH;
   if (!p.exec || p.graph_stream != s || p.graph_flags != gflags) {
     if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
     if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
     OAC_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    const int rc = run_step(p, gflags, s);
+    const int rc = step(gflags);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s, &g);
     if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
@@ -665,6 +526,7 @@ int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (p.c.kind == OAC_KIND_PARTICLE) return particle_step_phase(p, phase, flags, s);
   switch (phase) {
     case 0: return phase0(p, flags, s);
     case 1: return phase1(p, s) ? 1 : [&] {
@@ -687,6 +549,7 @@ int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
       a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.n = L.pol_size;
       a.lr = p.c.policy_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
       a.state = p.state(); a.advance = 1;
+      a.gscale = 1.f / (float)(p.c.world_size > 1 ? p.c.world_size : 1);
       OAC_HIP_CHECK(launch_adam(a, s));
       return 0;
     }
@@ -739,7 +602,7 @@ int oac_adam_polyak(float* p, const float* g, float* m, float* v, int64_t n, flo
   std::memset(&a, 0, sizeof(a));
   a.p = p; a.g = g; a.m = m; a.v = v; a.n = n; a.target = target; a.tau = tau; a.period = period;
   a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps;
-  a.state = reinterpret_cast<StepState*>(step_state); a.advance = advance;
+  a.state = reinterpret_cast<StepState*>(step_state); a.advance = advance; a.gscale = 1.f;
   OAC_HIP_CHECK(launch_adam(a, reinterpret_cast<hipStream_t>(stream)));
   return 0;
 }

@@ -9,6 +9,7 @@ backed by liboac_amd.so (hand-written HIP for gfx950 behind a C ABI).
 """
 from ._lib import lib, LIB_PATH  # noqa: F401
 from .trainer import SACTrainer, row_layout  # noqa: F401
+from .particle_trainer import ParticleTrainer  # noqa: F401
 from .replay_buffer import ReplayBuffer, DeviceBatch, DeviceIndexStream  # noqa: F401
 from .optimistic_exploration import get_optimistic_exploration_action  # noqa: F401
 from .producers import get_policy_producer, get_q_producer  # noqa: F401

@@ -1,0 +1,120 @@
+"""Data-parallel OAC/SAC step over RCCL (BASELINE configs[3]).
+
+One process per GPU, each with its own replay shard and its own index
+stream; parameters, Adam state and targets are replicated.  The reference has
+no distributed path (it runs one independent seed per GPU, main.py:575-578);
+this is the DP scheme the build adds.  Per step there are exactly three
+exchanges, at the points where the single-GPU step needs a whole-batch
+quantity, in the torch-1.4 order of trainer.py:139-210:
+
+  phase 0   forward, policy sample, local sum(logp + H)       -> all-reduce SUM (4 B)
+  phase 1   alpha update (global sum), TD target, critic grads -> all-reduce SUM (1.34 MB)
+  phase 2   critic Adam (grads / world) + Polyak, policy grad
+            through the post-step critics                       -> all-reduce SUM (0.68 MB)
+  phase 3   policy Adam (grads / world), step advance
+
+With equal per-rank batches and mean-reduced losses, the averaged gradients
+are the gradients of the concatenated global batch, so a DP step equals the
+single-process step on the union of the ranks' batches (tests/test_dp.py
+checks this with the CPU oracle over gloo).
+
+``dp_step`` is the transport-agnostic driver: it runs with the GPU executor
+below (liboac_amd phases + torch.distributed over RCCL) and, in the CPU
+tests, with an oracle-backed executor over gloo.
+"""
+import torch
+import torch.distributed as dist
+
+from . import _lib
+from ._lib import check
+from .particle_trainer import ParticleTrainer
+from .trainer import SACTrainer
+
+
+def dp_step(ex, all_reduce):
+    """Drive one data-parallel step.  ``ex`` exposes phase(i) and the views
+    alpha_sum() / critic_grads() / policy_grads(); ``all_reduce(t)`` sums a
+    tensor over ranks in place (the executor's Adam divides by world size)."""
+    ex.phase(0)
+    if ex.auto_alpha:
+        all_reduce(ex.alpha_sum())
+    ex.phase(1)
+    all_reduce(ex.critic_grads())
+    ex.phase(2)
+    all_reduce(ex.policy_grads())
+    ex.phase(3)
+
+
+class _GpuExecutor:
+    def __init__(self, trainer, plan, flags):
+        self.t, self.plan, self.flags = trainer, plan, flags
+        self.auto_alpha = trainer.use_automatic_entropy_tuning
+        lay = trainer.layout
+        self._crit = trainer.grads[lay.q1_base:lay.q1_base + lay.n_critics * lay.q_size]
+        self._pol = trainer.grads[:lay.pol_size]
+
+    def phase(self, i):
+        check(_lib.lib().oac_sac_step_phase(self.plan.handle, i, self.flags if i == 0 else 0,
+                                            _lib.stream_ptr(self.t.stream)))
+
+    def alpha_sum(self):
+        return self.t.alpha_state[6:7]
+
+    def critic_grads(self):
+        return self._crit
+
+    def policy_grads(self):
+        return self._pol
+
+
+class _DataParallel:
+    """Mixin: the trainer's step sharded over the ranks of a process group
+    (NCCL backend = RCCL on ROCm).  Every rank builds the trainer the same way;
+    rank 0's initial state is broadcast."""
+
+    def __init__(self, *args, process_group=None, **kwargs):
+        if not dist.is_initialized():
+            raise RuntimeError("DataParallelSACTrainer needs torch.distributed initialised")
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group)
+        super().__init__(*args, **kwargs)
+        # make sure every rank starts from rank 0's state
+        with torch.no_grad():
+            for t in (self.params, self.targets, self.alpha_state):
+                dist.broadcast(t, src=0, group=process_group)
+
+    def _make_cfg(self, batch):
+        c = super()._make_cfg(batch)
+        c.world_size = self.world
+        return c
+
+    def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None):
+        def all_reduce(t):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+
+        def go(sp):
+            f = flags
+            if batch is not None:
+                self._pack_batch(plan, batch)
+            if idx is not None:
+                self._idx.copy_(idx)
+            if eps1 is not None:
+                plan.views["eps1"].copy_(torch.as_tensor(eps1).reshape(plan.views["eps1"].shape))
+                plan.views["eps2"].copy_(torch.as_tensor(eps2).reshape(plan.views["eps2"].shape))
+            else:
+                f |= _lib.OAC_STEP_DEVICE_EPS
+            dp_step(_GpuExecutor(self, plan, f), all_reduce)
+        self._on_stream(go)
+        self._last_plan = plan
+        if self._need_to_update_eval_statistics:
+            self._need_to_update_eval_statistics = False
+            self._fill_eval_statistics(plan)
+        self._n_train_steps_total += 1
+
+
+class DataParallelSACTrainer(_DataParallel, SACTrainer):
+    """SACTrainer (trainer/trainer.py) with the data-parallel step."""
+
+
+class DataParallelParticleTrainer(_DataParallel, ParticleTrainer):
+    """ParticleTrainer (trainer/particle_trainer_oac.py) with the data-parallel step."""

@@ -109,89 +109,36 @@ class _Plan:
         self.handle, self.ws, self.views, self.key = handle, ws, views, key
 
 
-class SACTrainer(object):
-    """SACTrainer (trainer/trainer.py:14) on liboac_amd."""
+class _ArenaTrainer(object):
+    """Plumbing shared by the oac_amd trainers: flat HBM arenas, per-batch-size
+    launch plans (liboac_amd handles), the dedicated stream, batch packing."""
 
-    def __init__(self, policy_producer, q_producer, action_space=None, discount=0.99,
-                 reward_scale=1.0, policy_lr=1e-3, qf_lr=1e-3, optimizer_class=None,
-                 soft_target_tau=1e-2, target_update_period=1,
-                 use_automatic_entropy_tuning=True, target_entropy=None, deterministic=False,
-                 device=None, seed=0, use_graph=True, gemm_cfg=-1):
+    _kind = _lib.OAC_KIND_SAC
+    _q_out = 1
+
+    def _alloc(self, Do, Da, H, device):
         L = _lib.lib()
-        self.device = torch.device(device) if device is not None else torch.device(
-            "cuda", torch.cuda.current_device())
-        self.use_automatic_entropy_tuning = use_automatic_entropy_tuning
-        if use_automatic_entropy_tuning:
-            if target_entropy:
-                self.target_entropy = target_entropy
-            else:
-                self.target_entropy = -np.prod(action_space.shape).item()  # trainer.py:43-44
-        else:
-            self.target_entropy = 0.0
-        self.soft_target_tau = soft_target_tau
-        self.target_update_period = target_update_period
-        self.deterministic = deterministic
-        self.discount = discount
-        self.reward_scale = reward_scale
-        self.policy_lr, self.qf_lr = policy_lr, qf_lr
-        self.use_graph = use_graph
-        self.seed = int(seed)
-        self._gemm_cfg = gemm_cfg
-
-        ref_pol = policy_producer()
-        ref_q = [q_producer() for _ in range(4)]   # qf1, qf2, target_qf1, target_qf2
-        pol_sd = {k: v.detach() for k, v in ref_pol.state_dict().items()}
-        Do, Da, H, Q = _dims_from_state(pol_sd, ref_q[0].state_dict())
-        if Q != 1:
-            raise ValueError("SACTrainer critics have one output")
         self.obs_dim, self.act_dim, self.hidden = Do, Da, H
         self.rows = row_layout(Do, Da)
-        self._cfg = self._make_cfg(1)
+        cfg = self._make_cfg(1)
         lay = _lib.SacLayout()
-        check(L.oac_sac_query_layout(ctypes.byref(self._cfg), ctypes.byref(lay)))
+        check(L.oac_sac_query_layout(ctypes.byref(cfg), ctypes.byref(lay)))
         self.layout = lay
-        dev = self.device
-        z = lambda n: torch.zeros(int(n), dtype=torch.float32, device=dev)
+        z = lambda n: torch.zeros(int(n), dtype=torch.float32, device=device)
         self.params, self.grads = z(lay.params_total), z(lay.params_total)
         self.adam_m, self.adam_v = z(lay.params_total), z(lay.params_total)
         self.targets = z(lay.targets_total)
         self.alpha_state = z(16)
-        self.step_state = torch.zeros(16, dtype=torch.int64, device=dev)
-        self.policy = ArenaTanhGaussianPolicy(self.params, 0, lay, Do, Da, H)
-        self.qf1 = ArenaFlattenMlp(self.params, lay.q1_base, lay, Do, Da, H, 1)
-        self.qf2 = ArenaFlattenMlp(self.params, lay.q2_base, lay, Do, Da, H, 1)
-        self.target_qf1 = ArenaFlattenMlp(self.targets, 0, lay, Do, Da, H, 1)
-        self.target_qf2 = ArenaFlattenMlp(self.targets, lay.q_size, lay, Do, Da, H, 1)
-        self.policy.load_state_dict(pol_sd)
-        for mod, ref in zip((self.qf1, self.qf2, self.target_qf1, self.target_qf2), ref_q):
-            mod.load_state_dict({k: v.detach() for k, v in ref.state_dict().items()})
-        self.policy.oac_trainer = self
-        self.qfs = [self.qf1, self.qf2]
-        self.tfs = [self.target_qf1, self.target_qf2]
-        # optimizer views (the m / v arenas share the params layout)
-        tw = lambda other, mod: _twin_views(self.params, other, list(mod.parameters()))
-        self.policy_optimizer = AdamStateView(self, list(self.policy.parameters()),
-                                              tw(self.adam_m, self.policy),
-                                              tw(self.adam_v, self.policy), policy_lr,
-                                              (0.9, 0.999), 1e-8)
-        self.qf1_optimizer = AdamStateView(self, list(self.qf1.parameters()),
-                                           tw(self.adam_m, self.qf1), tw(self.adam_v, self.qf1),
-                                           qf_lr, (0.9, 0.999), 1e-8)
-        self.qf2_optimizer = AdamStateView(self, list(self.qf2.parameters()),
-                                           tw(self.adam_m, self.qf2), tw(self.adam_v, self.qf2),
-                                           qf_lr, (0.9, 0.999), 1e-8)
+        self.step_state = torch.zeros(16, dtype=torch.int64, device=device)
         self.log_alpha = self.alpha_state[0:1]
-        self.alpha_optimizer = AdamStateView(self, [self.log_alpha], [self.alpha_state[1:2]],
-                                             [self.alpha_state[2:3]], policy_lr, (0.9, 0.999), 1e-8)
-        self.eval_statistics = OrderedDict()
-        self._n_train_steps_total = 0
-        self._need_to_update_eval_statistics = True
         self._plans = {}
         self._idx = None
         self._expl = None
+        self._last_plan = None
         # all library work runs on a dedicated stream: hipGraph capture needs a
         # non-default stream, and it keeps the step off torch's null stream.
-        self.stream = torch.cuda.Stream(self.device)
+        self.stream = torch.cuda.Stream(device)
+        return lay
 
     def _on_stream(self, fn):
         cur = torch.cuda.current_stream(self.device)
@@ -204,9 +151,9 @@ class SACTrainer(object):
     # ------------------------------------------------------------ plans
     def _make_cfg(self, batch):
         c = _lib.SacConfig()
-        c.kind = _lib.OAC_KIND_SAC
+        c.kind = self._kind
         c.obs_dim, c.act_dim, c.hidden, c.q_out, c.batch = (
-            self.obs_dim, self.act_dim, self.hidden, 1, batch)
+            self.obs_dim, self.act_dim, self.hidden, self._q_out, batch)
         c.discount, c.reward_scale, c.tau = self.discount, self.reward_scale, self.soft_target_tau
         c.policy_lr, c.qf_lr, c.beta1, c.beta2, c.adam_eps = (
             self.policy_lr, self.qf_lr, 0.9, 0.999, 1e-8)
@@ -332,6 +279,70 @@ class SACTrainer(object):
         (indices drawn by the device MT19937 stream, see ReplayBuffer)."""
         plan = self._plan(B, replay=storage, idx=ring, ring_slots=ring_slots)
         self._run(plan, _lib.OAC_STEP_GATHER)
+
+class SACTrainer(_ArenaTrainer):
+    """SACTrainer (trainer/trainer.py:14) on liboac_amd."""
+
+    def __init__(self, policy_producer, q_producer, action_space=None, discount=0.99,
+                 reward_scale=1.0, policy_lr=1e-3, qf_lr=1e-3, optimizer_class=None,
+                 soft_target_tau=1e-2, target_update_period=1,
+                 use_automatic_entropy_tuning=True, target_entropy=None, deterministic=False,
+                 device=None, seed=0, use_graph=True, gemm_cfg=-1):
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.use_automatic_entropy_tuning = use_automatic_entropy_tuning
+        if use_automatic_entropy_tuning:
+            if target_entropy:
+                self.target_entropy = target_entropy
+            else:
+                self.target_entropy = -np.prod(action_space.shape).item()  # trainer.py:43-44
+        else:
+            self.target_entropy = 0.0
+        self.soft_target_tau = soft_target_tau
+        self.target_update_period = target_update_period
+        self.deterministic = deterministic
+        self.discount = discount
+        self.reward_scale = reward_scale
+        self.policy_lr, self.qf_lr = policy_lr, qf_lr
+        self.use_graph = use_graph
+        self.seed = int(seed)
+        self._gemm_cfg = gemm_cfg
+
+        ref_pol = policy_producer()
+        ref_q = [q_producer() for _ in range(4)]   # qf1, qf2, target_qf1, target_qf2
+        pol_sd = {k: v.detach() for k, v in ref_pol.state_dict().items()}
+        Do, Da, H, Q = _dims_from_state(pol_sd, ref_q[0].state_dict())
+        if Q != 1:
+            raise ValueError("SACTrainer critics have one output")
+        lay = self._alloc(Do, Da, H, self.device)
+        self.policy = ArenaTanhGaussianPolicy(self.params, 0, lay, Do, Da, H)
+        self.qf1 = ArenaFlattenMlp(self.params, lay.q1_base, lay, Do, Da, H, 1)
+        self.qf2 = ArenaFlattenMlp(self.params, lay.q2_base, lay, Do, Da, H, 1)
+        self.target_qf1 = ArenaFlattenMlp(self.targets, 0, lay, Do, Da, H, 1)
+        self.target_qf2 = ArenaFlattenMlp(self.targets, lay.q_size, lay, Do, Da, H, 1)
+        self.policy.load_state_dict(pol_sd)
+        for mod, ref in zip((self.qf1, self.qf2, self.target_qf1, self.target_qf2), ref_q):
+            mod.load_state_dict({k: v.detach() for k, v in ref.state_dict().items()})
+        self.policy.oac_trainer = self
+        self.qfs = [self.qf1, self.qf2]
+        self.tfs = [self.target_qf1, self.target_qf2]
+        # optimizer views (the m / v arenas share the params layout)
+        tw = lambda other, mod: _twin_views(self.params, other, list(mod.parameters()))
+        self.policy_optimizer = AdamStateView(self, list(self.policy.parameters()),
+                                              tw(self.adam_m, self.policy),
+                                              tw(self.adam_v, self.policy), policy_lr,
+                                              (0.9, 0.999), 1e-8)
+        self.qf1_optimizer = AdamStateView(self, list(self.qf1.parameters()),
+                                           tw(self.adam_m, self.qf1), tw(self.adam_v, self.qf1),
+                                           qf_lr, (0.9, 0.999), 1e-8)
+        self.qf2_optimizer = AdamStateView(self, list(self.qf2.parameters()),
+                                           tw(self.adam_m, self.qf2), tw(self.adam_v, self.qf2),
+                                           qf_lr, (0.9, 0.999), 1e-8)
+        self.alpha_optimizer = AdamStateView(self, [self.log_alpha], [self.alpha_state[1:2]],
+                                             [self.alpha_state[2:3]], policy_lr, (0.9, 0.999), 1e-8)
+        self.eval_statistics = OrderedDict()
+        self._n_train_steps_total = 0
+        self._need_to_update_eval_statistics = True
 
     # ------------------------------------------------------------ diagnostics
     def _fill_eval_statistics(self, plan):

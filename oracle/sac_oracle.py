@@ -238,69 +238,117 @@ class SACOracle:
         self.n_steps = 0
         self.last = {}
 
+    # The step is written as four phases separated by the only points where a
+    # whole-batch quantity is needed; the single-process step runs them back
+    # to back, the data-parallel test all-reduces alpha_sum / crit_flat /
+    # pol_flat (SUM) between them (oac_amd/dp.py).
     def step(self, batch, eps1, eps2):
+        self.phase0(batch, eps1, eps2)
+        self.phase1()
+        self.phase2()
+        return self.phase3()
+
+    def _flat(self, grads, order):
+        flat = torch.cat([grads[k].reshape(-1) for k in order])
+        views, o = {}, 0
+        for k in order:
+            n = grads[k].numel()
+            views[k] = flat[o:o + n].view(grads[k].shape)
+            o += n
+        return flat, views
+
+    def phase0(self, batch, eps1, eps2):
         dt = self.dtype
-        obs = _t(batch["observations"], dt)
-        act = _t(batch["actions"], dt)
-        rew = _t(batch["rewards"], dt)
-        term = _t(batch["terminals"], dt)
-        nobs = _t(batch["next_observations"], dt)
-        eps1, eps2 = _t(eps1, dt), _t(eps2, dt)
-        B = obs.shape[0]
+        S = self.S = {}
+        S["obs"] = _t(batch["observations"], dt)
+        S["act"] = _t(batch["actions"], dt)
+        S["rew"] = _t(batch["rewards"], dt)
+        S["term"] = _t(batch["terminals"], dt)
+        S["nobs"] = _t(batch["next_observations"], dt)
+        S["B"] = S["obs"].shape[0]
         # E1  policy(obs)                                        trainer.py:136-138
-        pf = policy_forward(obs, self.P, eps1)
+        S["pf"] = policy_forward(S["obs"], self.P, _t(eps1, dt))
+        # E4                                                     trainer.py:168-169
+        S["c1"] = q_forward(S["obs"], S["act"], self.Q1)
+        S["c2"] = q_forward(S["obs"], S["act"], self.Q2)
+        # E5                                                     trainer.py:172-174
+        S["pf2"] = policy_forward(S["nobs"], self.P, _t(eps2, dt))
+        # local sum(logp + H) for the alpha gradient
+        self.alpha_sum = (S["pf"]["logp"] + self.target_entropy).sum(0)
+
+    def phase1(self, world=1):
+        S, dt = self.S, self.dtype
+        B = S["B"]
+        pf, pf2 = S["pf"], S["pf2"]
         # E2  alpha                                              trainer.py:139-149
         if self.auto_alpha:
-            w = (pf["logp"] + self.target_entropy)
-            g_la = (-(w / B)).sum(0)
-            alpha_loss = -(self.log_alpha * w).mean()
+            n = B * world
+            g_la = -(self.alpha_sum / n)
+            alpha_loss = -(self.log_alpha * self.alpha_sum) / n
             self.opt_a.step({"log_alpha": g_la})
             alpha = self.log_alpha.exp()
         else:
             g_la, alpha_loss, alpha = None, torch.zeros(()), torch.zeros(1, dtype=dt)
+        S.update(g_la=g_la, alpha_loss=alpha_loss, alpha=alpha)
         # E3  min Q on the fresh actions (pre-step weights)      trainer.py:151-160
-        c1n = q_forward(obs, pf["a"], self.Q1)
-        c2n = q_forward(obs, pf["a"], self.Q2)
-        q_new = torch.min(c1n["q"], c2n["q"])
-        policy_loss = (alpha * pf["logp"] - q_new).mean()
-        # E4                                                     trainer.py:168-169
-        c1 = q_forward(obs, act, self.Q1)
-        c2 = q_forward(obs, act, self.Q2)
-        # E5                                                     trainer.py:172-174
-        pf2 = policy_forward(nobs, self.P, eps2)
+        S["c1n"] = q_forward(S["obs"], pf["a"], self.Q1)
+        S["c2n"] = q_forward(S["obs"], pf["a"], self.Q2)
+        S["q_new"] = torch.min(S["c1n"]["q"], S["c2n"]["q"])
+        S["policy_loss"] = (alpha * pf["logp"] - S["q_new"]).mean()
         # E6                                                     trainer.py:178-184
-        t1 = q_forward(nobs, pf2["a"], self.T1)["q"]
-        t2 = q_forward(nobs, pf2["a"], self.T2)["q"]
+        t1 = q_forward(S["nobs"], pf2["a"], self.T1)["q"]
+        t2 = q_forward(S["nobs"], pf2["a"], self.T2)["q"]
         target_q = torch.min(t1, t2) - alpha * pf2["logp"]
-        y = self.reward_scale * rew + (1.0 - term) * self.discount * target_q
+        y = self.reward_scale * S["rew"] + (1.0 - S["term"]) * self.discount * target_q
+        S["y"] = y
         # E7                                                     trainer.py:194-196
-        qf1_loss = ((c1["q"] - y) ** 2).mean()
-        qf2_loss = ((c2["q"] - y) ** 2).mean()
-        # E8  Q1 step, Q2 step, then the policy backward          trainer.py:200-210
+        c1, c2 = S["c1"], S["c2"]
+        S["qf1_loss"] = ((c1["q"] - y) ** 2).mean()
+        S["qf2_loss"] = ((c2["q"] - y) ** 2).mean()
         g1 = q_param_grads(c1, 2.0 * (c1["q"] - y) / B, self.Q1)
-        self.opt_q1.step(g1)
         g2 = q_param_grads(c2, 2.0 * (c2["q"] - y) / B, self.Q2)
-        self.opt_q2.step(g2)
-        sel1 = (c1n["q"] <= c2n["q"]).to(dt)          # torch-1.4 min() backward
-        gq = -torch.ones_like(q_new) / B
+        order = list(self.Q1.keys())
+        self.crit_flat, views = self._flat({**{"1/" + k: g1[k] for k in order},
+                                            **{"2/" + k: g2[k] for k in order}},
+                                           ["1/" + k for k in order] + ["2/" + k for k in order])
+        S["g1"] = {k: views["1/" + k] for k in order}
+        S["g2"] = {k: views["2/" + k] for k in order}
+
+    def phase2(self, world=1):
+        S, pf = self.S, self.S["pf"]
+        B = S["B"]
+        # E8  Q1 step, Q2 step, then the policy backward          trainer.py:200-210
+        self.opt_q1.step({k: v / world for k, v in S["g1"].items()})
+        self.opt_q2.step({k: v / world for k, v in S["g2"].items()})
+        c1n, c2n = S["c1n"], S["c2n"]
+        sel1 = (c1n["q"] <= c2n["q"]).to(self.dtype)   # torch-1.4 min() backward
+        gq = -torch.ones_like(S["q_new"]) / B
         Do = self.Do
         da = q_input_grad(c1n, gq * sel1, self.Q1)[:, Do:] \
             + q_input_grad(c2n, gq * (1 - sel1), self.Q2)[:, Do:]
-        G = (alpha / B) * torch.ones_like(pf["logp"])
+        G = (S["alpha"] / B) * torch.ones_like(pf["logp"])
         gp = policy_backward(pf, self.P, da, G)
-        self.opt_p.step(gp)
-        # E9  Polyak                                              trainer.py:215-224
+        order = list(self.P.keys())
+        self.pol_flat, views = self._flat(gp, order)
+        S["gp"] = views
+        # E9  Polyak (uses only the post-step critics)            trainer.py:215-224
         if self.n_steps % self.period == 0:
             polyak(self.T1, self.Q1, self.tau)
             polyak(self.T2, self.Q2, self.tau)
-        stats = self._stats(c1["q"], c2["q"], y, pf, q_new, qf1_loss, qf2_loss, alpha,
-                            alpha_loss)
+
+    def phase3(self, world=1):
+        S = self.S
+        self.opt_p.step({k: v / world for k, v in S["gp"].items()})
+        stats = self._stats(S["c1"]["q"], S["c2"]["q"], S["y"], S["pf"], S["q_new"],
+                            S["qf1_loss"], S["qf2_loss"], S["alpha"], S["alpha_loss"])
         self.n_steps += 1
-        self.last = dict(grads=dict(policy=gp, qf1=g1, qf2=g2, log_alpha=g_la),
-                         qf1_loss=qf1_loss, qf2_loss=qf2_loss, policy_loss=policy_loss,
-                         alpha=alpha, alpha_loss=alpha_loss, y=y, q1=c1["q"], q2=c2["q"],
-                         logp=pf["logp"], logp2=pf2["logp"], a=pf["a"], a2=pf2["a"],
-                         stats=stats)
+        self.last = dict(grads=dict(policy=S["gp"], qf1=S["g1"], qf2=S["g2"],
+                                    log_alpha=S["g_la"]),
+                         qf1_loss=S["qf1_loss"], qf2_loss=S["qf2_loss"],
+                         policy_loss=S["policy_loss"], alpha=S["alpha"],
+                         alpha_loss=S["alpha_loss"], y=S["y"], q1=S["c1"]["q"],
+                         q2=S["c2"]["q"], logp=S["pf"]["logp"], logp2=S["pf2"]["logp"],
+                         a=S["pf"]["a"], a2=S["pf2"]["a"], stats=stats)
         return self.last
 
     def _stats(self, q1, q2, y, pf, q_new, l1, l2, alpha, alpha_loss):

@@ -48,6 +48,7 @@ def test_param_layout_matches_reference_parameter_counts(dims):
     for k, v in row_layout(Do, Da).items():
         setattr(cfg, k, v)
     cfg.gemm_cfg = -1
+    cfg.world_size = 1
     lay = _lib.SacLayout()
     assert _lib.lib().oac_sac_query_layout(ctypes.byref(cfg), ctypes.byref(lay)) == 0
     n_pol = H * Do + H + H * H + H + 2 * (Da * H + Da)

@@ -1,0 +1,84 @@
+"""GPU data-parallel trainer: 2 ranks sharing cuda:0 (gloo transport -- RCCL
+refuses two ranks on one device; the 8-GPU run uses RCCL) must equal the
+single-process GPU trainer on the concatenated batch."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import parity
+from fixtures_lib import sac_params, synthetic_transitions
+
+pytestmark = pytest.mark.gpu
+
+Do, Da, H, BL, STEPS = 11, 3, 32, 32, 3
+META = dict(obs_dim=Do, act_dim=Da, hidden=[H, H], discount=0.99, reward_scale=1.0, lr=1e-3,
+            tau=5e-3, auto_alpha=True, log_alpha0=0.0, seed=3, pi_init_w=0.2, q_init_w=0.1)
+
+
+def _inputs(world):
+    data = synthetic_transitions(500, Do, Da, seed=0)
+    rs = np.random.RandomState(5)
+    out = []
+    for _ in range(STEPS):
+        idx = rs.randint(0, 500, BL * world)
+        e1 = rs.standard_normal((BL * world, Da)).astype(np.float32)
+        e2 = rs.standard_normal((BL * world, Da)).astype(np.float32)
+        out.append(({k: v[idx] for k, v in data.items()}, e1, e2))
+    return out
+
+
+def _trainer(dp):
+    from gpu_helpers import producers, Space
+    from oac_amd import SACTrainer
+    from oac_amd.dp import DataParallelSACTrainer
+    pp, qp = producers(sac_params(Do, Da, [H, H], 3, pi_init_w=0.2, q_init_w=0.1))
+    cls = DataParallelSACTrainer if dp else SACTrainer
+    return cls(pp, qp, action_space=Space(Da), discount=0.99, reward_scale=1.0, policy_lr=1e-3,
+               qf_lr=1e-3, soft_target_tau=5e-3, use_automatic_entropy_tuning=True)
+
+
+def _worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = _trainer(True)
+    for batch, e1, e2 in _inputs(world):
+        sl = slice(rank * BL, (rank + 1) * BL)
+        tr.train_from_torch({k: v[sl] for k, v in batch.items()}, eps1=e1[sl], eps2=e2[sl])
+    torch.cuda.synchronize()
+    if rank == 0:
+        q.put(torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_trainer_two_ranks_equals_single_gpu_on_global_batch():
+    world = 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    tr = _trainer(False)
+    for batch, e1, e2 in _inputs(world):
+        tr.train_from_torch(batch, eps1=e1, eps2=e2)
+    want = torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy()
+    assert parity.rel_err(got, want) < 1e-6, parity.rel_err(got, want)

@@ -1,0 +1,70 @@
+"""GPU parity of the P-OAC particle trainer (share_layers K-head critic)
+against the reference's own outputs (tests/golden/poac_*.npz)."""
+import numpy as np
+import pytest
+import torch
+
+import parity
+from fixtures_lib import PARAM_ORDER_POLICY, PARAM_ORDER_Q, sac_params
+from gpu_helpers import Space, batch_from, module_tensors, producers
+
+pytestmark = pytest.mark.gpu
+
+
+def particle_trainer_for(meta, **kw):
+    from oac_amd import ParticleTrainer
+    K = meta["K"]
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"], q_out=K,
+                        q_last_bias=np.linspace(meta["q_min"], meta["q_max"], K),
+                        pi_init_w=meta["pi_init_w"])
+    pp, qp = producers(params, q_keys=("qf1", "qf2", "target_qf1", "target_qf2", "qf1",
+                                       "target_qf1"))
+    return ParticleTrainer(pp, qp, n_estimators=K, action_space=Space(meta["act_dim"]),
+                           discount=meta["discount"], reward_scale=1.0, delta=meta["delta"],
+                           policy_lr=meta["lr"], qf_lr=meta["lr"], soft_target_tau=meta["tau"],
+                           target_update_period=1, use_automatic_entropy_tuning=True,
+                           deterministic=False, q_min=meta["q_min"], q_max=meta["q_max"],
+                           share_layers=True, **kw)
+
+
+@pytest.mark.parametrize("name", ["poac_small", "poac_ant"])
+def test_particle_step_matches_reference_golden(name):
+    meta, g = parity.load(name)
+    tr = particle_trainer_for(meta)
+    assert tr.delta_index == meta["delta_index"]
+    errs = {}
+    for s in range(meta["steps"]):
+        tr.end_epoch(s)
+        tr.train_from_torch(batch_from(meta, g[f"s{s}/idx"]), eps1=g[f"s{s}/eps1"],
+                            eps2=g[f"s{s}/eps2"])
+        torch.cuda.synchronize()
+        for grp, mod, order in (("policy", tr.policy, PARAM_ORDER_POLICY),
+                                ("qf", tr.qfs[0], PARAM_ORDER_Q)):
+            gv = module_tensors(tr, mod, tr.grads)
+            for pn in order:
+                key = f"s{s}/grad/{grp}/{pn}"
+                errs[key] = parity.compare(g, key, gv[pn].cpu().numpy())
+        a = tr.alpha_state.cpu().numpy()
+        errs[f"s{s}/grad/log_alpha"] = parity.rel_err(a[5:6], g[f"s{s}/grad/log_alpha"])
+        errs[f"s{s}/post/log_alpha"] = parity.rel_err(a[0:1], g[f"s{s}/post/log_alpha"])
+        for grp, mod in (("policy", tr.policy), ("qf", tr.qfs[0]), ("tf", tr.tfs[0])):
+            for pn, t in mod.state_dict().items():
+                key = f"s{s}/post/{grp}/{pn}"
+                gk = f"s{s}/grad/{grp}/{pn}" if s == 0 and grp != "tf" else None
+                errs[key], _ = parity.compare_post(g, key, gk, t.cpu().numpy(), meta["lr"])
+        st = tr.get_diagnostics()
+        for k in list(st.keys()):
+            gk = f"s{s}/stat/{k}"
+            if gk in g and k not in ("QF Unordered", "QF target Undordered"):
+                errs[gk] = parity.rel_err(st[k], g[gk])
+    bad = {k: v for k, v in errs.items() if v > (parity.TOL if k.startswith("s0/") else 1e-4)}
+    print(name, "worst", sorted(errs.items(), key=lambda kv: -kv[1])[:3])
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:10]
+
+
+def test_particle_stats_keys_match_reference_order():
+    meta, g = parity.load("poac_small")
+    tr = particle_trainer_for(meta)
+    tr.train_from_torch(batch_from(meta, g["s0/idx"]), eps1=g["s0/eps1"], eps2=g["s0/eps2"])
+    keys = [k[len("s0/stat/"):] for k in g if k.startswith("s0/stat/")]
+    assert list(tr.get_diagnostics().keys()) == keys
