@@ -3,12 +3,12 @@
 // (utils/pytorch_util.py:5-9, called at trainer.py:215-224 with the POST-step
 // parameters).  HBM-bound elementwise.
 //
-// adam_seg_kernel also folds in the split-K reduction of the weight-gradient
-// GEMMs: each (W, b) pair's gradient arrives as S partial slabs
-// [S][M][K_in+1] and is summed in fixed slab order (deterministic), written to
-// the gradient arena, and applied -- one pass over p, m, v, target.
-// adam_flat_kernel is the plain flat form (data-parallel path: gradients are
-// all-reduced in the arena between the reduce pass and this one).
+// The weight-gradient GEMMs write their results in the parameter-arena
+// layout; with split-K they write S partial slabs shaped like the arena, which
+// this pass sums in fixed slab order (deterministic) before the update -- one
+// float4 pass over g, p, m, v (and target).  Data-parallel: a reduce-only pass
+// writes the summed gradient, the caller all-reduces it, then the update pass
+// runs with gscale = 1/world.
 #include "oac_common.h"
 #include "kernels.h"
 
@@ -64,43 +64,27 @@ __device__ __forceinline__ void step_bookkeeping(StepState* st, AlphaState* as, 
   if (as) { as->log_alpha = as->next_log_alpha; as->m = as->next_m; as->v = as->next_v; }
 }
 
-__global__ void __launch_bounds__(256) adam_seg_kernel(AdamSegArgs a) {
-  const AdamConsts c = adam_consts(a.state, a.advance, a.lr, a.beta1, a.beta2, a.eps, a.target,
-                                   a.tau, a.period);
-  const long stride = (long)gridDim.x * 256;
-  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < a.total; e += stride) {
-    int si = 0;
-#pragma unroll 1
-    for (int i = 1; i < a.nseg; ++i)
-      if (e >= a.seg[i].elem_begin) si = i;
-    const AdamSeg& s = a.seg[si];
-    const long local = e - s.elem_begin;
-    const int row = (int)(local / s.ncols);
-    const int col = (int)(local % s.ncols);
-    float g = 0.f;
-    const float* src = s.slab + local;
-#pragma unroll 1
-    for (int k = 0; k < s.S; ++k) g += src[(long)k * s.slab_stride];
-    const long idx = (col < s.ncols - 1) ? s.off_w + (long)row * (s.ncols - 1) + col : s.off_b + row;
-    a.g[idx] = g;
-    if (a.reduce_only) continue;
-    float p = a.p[idx], m = a.m[idx], v = a.v[idx];
-    adam1(c, p, g, m, v);
-    a.p[idx] = p; a.m[idx] = m; a.v[idx] = v;
-    if (c.polyak) a.target[idx] = polyak1(c, a.target[idx], p);
-  }
-  if (!a.reduce_only) step_bookkeeping(a.state, a.alpha, a.advance);
-}
-
 __global__ void __launch_bounds__(256) adam_flat_kernel(AdamArgs a) {
   const AdamConsts c = adam_consts(a.state, a.advance, a.lr, a.beta1, a.beta2, a.eps, a.target,
                                    a.tau, a.period);
   const long n4 = a.n >> 2;
   const long stride = (long)gridDim.x * 256;
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
-    float4 p = reinterpret_cast<float4*>(a.p)[i];
-    float4 g = reinterpret_cast<const float4*>(a.g)[i];
+    float4 g;
+    if (a.S > 1 || a.gslab != a.g) {
+      g = reinterpret_cast<const float4*>(a.gslab)[i];
+#pragma unroll 1
+      for (int k = 1; k < a.S; ++k) {
+        const float4 x = reinterpret_cast<const float4*>(a.gslab + (long)k * a.slab_stride)[i];
+        g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
+      }
+      reinterpret_cast<float4*>(a.g)[i] = g;
+    } else {
+      g = reinterpret_cast<const float4*>(a.g)[i];
+    }
+    if (a.reduce_only) continue;
     if (a.gscale != 1.f) { g.x *= a.gscale; g.y *= a.gscale; g.z *= a.gscale; g.w *= a.gscale; }
+    float4 p = reinterpret_cast<float4*>(a.p)[i];
     float4 m = reinterpret_cast<float4*>(a.m)[i];
     float4 v = reinterpret_cast<float4*>(a.v)[i];
     adam1(c, p.x, g.x, m.x, v.x);
@@ -117,13 +101,7 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(AdamArgs a) {
       reinterpret_cast<float4*>(a.target)[i] = t;
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) {
-    const long i = (n4 << 2) + threadIdx.x;
-    float p = a.p[i], m = a.m[i], v = a.v[i];
-    adam1(c, p, a.g[i] * a.gscale, m, v);
-    a.p[i] = p; a.m[i] = m; a.v[i] = v;
-    if (c.polyak) a.target[i] = polyak1(c, a.target[i], p);
-  }
+  if (a.reduce_only) return;
   step_bookkeeping(a.state, a.alpha, a.advance);
 }
 
@@ -135,13 +113,10 @@ static int adam_blocks(long n) {
 }
 
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s) {
+  if (a.n & 3) return hipErrorInvalidValue;   // arena ranges are 16-byte multiples
   hipLaunchKernelGGL(adam_flat_kernel, dim3(adam_blocks((a.n + 3) >> 2)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_adam_seg(const AdamSegArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(adam_seg_kernel, dim3(adam_blocks(a.total)), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
 
 }  // namespace oac

@@ -149,8 +149,11 @@ __device__ __forceinline__ void epi_store(const GemmTask& t, int m, int n, float
                                           const float* lds_u, const float* lds_v, int mt, int nt) {
   if (m >= t.M || n >= t.N) return;
   const long o = (long)m * t.ldc + n;
-  if (EPI == EPI_STORE || EPI == EPI_SLAB) {
+  if (EPI == EPI_STORE) {
     t.C[o] = acc;
+  } else if (EPI == EPI_GRAD) {
+    if (t.b_ones && n == t.N - 1) t.bias_grad[m] = acc;
+    else t.C[o] = acc;
   } else if (EPI == EPI_BIAS) {
     t.C[o] = acc + t.bias[n];
   } else if (EPI == EPI_BIAS_RELU) {
@@ -215,6 +218,7 @@ __global__ void __launch_bounds__(256) gemm_grouped_kernel(const GemmBatch batch
     t.B += t.b_kc ? (long)k_lo : (long)k_lo * t.ldb;
     t.K = k_hi - k_lo;
     t.C += (long)split * t.slab_stride;
+    t.bias_grad += (long)split * t.slab_stride;
   }
   const int m0 = (local / t.tiles_n) * C::kBM;
   const int n0 = (local % t.tiles_n) * C::kBN;
@@ -326,7 +330,7 @@ __global__ void __launch_bounds__(256) gemm_grouped_kernel(const GemmBatch batch
     case EPI_BIAS_RANK_RELU: epilogue_tile<C, EPI_BIAS_RANK_RELU>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
     case EPI_ADD_RELU: epilogue_tile<C, EPI_ADD_RELU>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
     case EPI_MASK: epilogue_tile<C, EPI_MASK>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
-    case EPI_SLAB: epilogue_tile<C, EPI_SLAB>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
+    case EPI_GRAD: epilogue_tile<C, EPI_GRAD>(t, m0, n0, wm, wn, lane, accf, lds_u, lds_v); break;
     default: break;
   }
 }

@@ -71,8 +71,11 @@ __device__ __forceinline__ void epi_one(const GemmTask& t, int m, int n, float a
   if (m >= t.M || n >= t.N) return;
   const long o = (long)m * t.ldc + n;
   switch (t.epi) {
-    case EPI_STORE:
-    case EPI_SLAB: t.C[o] = acc; break;
+    case EPI_STORE: t.C[o] = acc; break;
+    case EPI_GRAD:
+      if (t.b_ones && n == t.N - 1) t.bias_grad[m] = acc;
+      else t.C[o] = acc;
+      break;
     case EPI_BIAS: t.C[o] = acc + t.bias[n]; break;
     case EPI_BIAS_RELU: t.C[o] = fmaxf(acc + t.bias[n], 0.f); break;
     case EPI_BIAS_RANK_RELU: {
@@ -113,6 +116,7 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
     k_lo = split * t.kchunk;
     k_hi = min(t.K, k_lo + t.kchunk);
     t.C += (long)split * t.slab_stride;
+    t.bias_grad += (long)split * t.slab_stride;
   }
   const int m0 = (local / t.tiles_n) * 32;
   const int n0 = (local % t.tiles_n) * 32;

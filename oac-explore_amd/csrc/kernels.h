@@ -104,7 +104,10 @@ struct GatherArgs {
 };
 
 struct AdamArgs {
-  float* p; const float* g; float* m; float* v; long n;
+  float* p; float* g; float* m; float* v; long n;
+  // split-K gradient slabs shaped like the arena range: g = sum_s gslab[s*stride + i]
+  // (written back to g); gslab == g with S == 1 reads g directly
+  const float* gslab; int S; long slab_stride;
   float* target; float tau; int period;   // target != null -> Polyak after the step
   double lr, beta1, beta2, eps;
   StepState* state;
@@ -112,29 +115,7 @@ struct AdamArgs {
                      // 1: final policy Adam (t = t_snapshot; block 0 advances the step)
   AlphaState* alpha; // commit next_* (critic Adam only); may be null
   float gscale;      // gradient scale (1/world_size after an all-reduce SUM)
-};
-
-// Segment-aware reduce + Adam: one segment per (weight, bias) pair whose
-// gradient was produced as split-K slabs [S][M][K_in+1] (last column = bias).
-struct AdamSeg {
-  const float* slab;
-  long slab_stride;
-  int S, M, ncols;        // ncols = K_in + 1
-  long off_w, off_b;      // arena offsets of W [M][K_in] and b [M]
-  long elem_begin;
-};
-constexpr int kMaxAdamSegs = 12;
-struct AdamSegArgs {
-  AdamSeg seg[kMaxAdamSegs];
-  int nseg;
-  long total;
-  float* p; float* g; float* m; float* v; float* target;   // arena bases
-  float tau; int period;
-  double lr, beta1, beta2, eps;
-  StepState* state;
-  int advance;            // as AdamArgs
-  int reduce_only;        // 1: write the reduced gradient only (DP: all-reduce next)
-  AlphaState* alpha;
+  int reduce_only;   // data-parallel: only reduce the slabs into g (all-reduce next)
 };
 
 // ParticleTrainer (share_layers) per-sample kernels, particle_trainer_oac.py
@@ -162,7 +143,6 @@ struct LogpSumArgs { const float* logp; int B; float target_entropy; AlphaState*
 hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s);
 
 // launchers (defined in the .hip files)
-hipError_t launch_adam_seg(const AdamSegArgs& a, hipStream_t s);
 void gemm_batch_finalize(GemmBatch& b, int cfg);
 hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s);
 int gemm_tile_m(int cfg);

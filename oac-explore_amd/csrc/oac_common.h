@@ -26,7 +26,9 @@ enum Epi : int {
   EPI_BIAS_RANK_RELU = 3, // C = acc + bias[n];  C2 = relu(C + sum_j U[m,j] V[n,j])
   EPI_ADD_RELU = 4,       // C = relu(acc + aux[m,n])
   EPI_MASK = 5,           // C = aux[m,n] > 0 ? acc : 0
-  EPI_SLAB = 6,           // C[split*slab_stride + m*ldc + n] = acc (split-K partial)
+  EPI_GRAD = 6,           // weight gradient in the parameter-arena layout:
+                          // C[m*ldc + n] (n < N-1), bias_grad[m] (n == N-1, the
+                          // ones column); both offset by split*slab_stride
 };
 
 struct GemmTask {
@@ -50,7 +52,7 @@ struct GemmTask {
   int b_ones;    // 1: column n == N-1 of B is virtual ones (dW bias column)
   int epi;
   int R;         // rank of the EPI_BIAS_RANK_RELU update
-  int ksplit;    // K chunks (EPI_SLAB only); chunk = kchunk (multiple of BK)
+  int ksplit;    // K chunks (EPI_GRAD only); chunk = kchunk (multiple of 64)
   int kchunk;
   long slab_stride;
   int tile_begin;

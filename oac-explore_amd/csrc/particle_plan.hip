@@ -31,7 +31,6 @@ enum PWs {
   X_H1P = OAC_WS_COUNT_PUBLIC, X_H2P, X_H1P2, X_H2P2, X_P, X_H1Q, X_H2Q, X_PT, X_H1T, X_H2T,
   X_STD1, X_U1, X_STD2, X_U2, X_DQ, X_DH2Q, X_DH1Q, X_PN, X_H1N, X_H2N, X_GQ, X_DH2N, X_DH1N,
   X_DA, X_DHEAD, X_DH2P, X_DH1P,
-  X_SLAB_Q0, X_SLAB_Q1, X_SLAB_QL, X_SLAB_P0, X_SLAB_P1, X_SLAB_PH,
   X_COUNT
 };
 static_assert(X_COUNT <= kMaxWs, "workspace ids");
@@ -53,14 +52,10 @@ void particle_layout_workspace(SacPlan& p) {
   set(X_DQ, B, K); set(X_GQ, B, K);
   for (int id : {X_DH2Q, X_DH1Q, X_PN, X_H1N, X_H2N, X_DH2N, X_DH1N, X_DH2P, X_DH1P}) set(id, B, H);
   set(X_DHEAD, B, 2 * Da);
-  set(X_SLAB_Q0, (int64_t)p.sp_q0.S * H, Do + Da + 1);
-  set(X_SLAB_Q1, (int64_t)p.sp_q1.S * H, H + 1);
-  set(X_SLAB_QL, (int64_t)p.sp_ql.S * K, H + 1);
-  set(X_SLAB_P0, (int64_t)p.sp_p0.S * H, Do + 1);
-  set(X_SLAB_P1, (int64_t)p.sp_p1.S * H, H + 1);
-  set(X_SLAB_PH, (int64_t)p.sp_ph.S * 2 * Da, H + 1);
+  if (p.S_q > 1) set(WS_GSLAB_Q, p.S_q, p.L.n_critics * p.L.q_size);
+  if (p.S_p > 1) set(WS_GSLAB_P, p.S_p, p.L.pol_size);
   int64_t off = 0;
-  for (int i = 0; i < X_COUNT; ++i) {
+  for (int i = 0; i < kMaxWs; ++i) {
     p.ws[i].off = off;
     off = al64(off + p.ws[i].rows * p.ws[i].cols);
   }
@@ -173,57 +168,28 @@ static int pphase1(SacPlan& p, hipStream_t s) {
   }
   {  // last layer: dW_last slab and dh2 = (dq . W_last) * [h2 > 0]
     GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_dw(p.W(X_DQ), K, K, B, p.W(X_H2Q), H, H, p.W(X_SLAB_QL), p.sp_ql));
+    float* gq = grad_q(p);
+    add(gb, t_dw(p.W(X_DQ), K, K, B, p.W(X_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
+                 q_group(p), p.sp_ql));
     add(gb, t_dx(p.W(X_DQ), K, B, K, q + L.q_last_w, H, H, p.W(X_DH2Q), H, p.W(X_H2Q), H));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
     GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_dw(p.W(X_DH2Q), H, H, B, p.W(X_H1Q), H, H, p.W(X_SLAB_Q1), p.sp_q1));
+    float* gq = grad_q(p);
+    add(gb, t_dw(p.W(X_DH2Q), H, H, B, p.W(X_H1Q), H, H, gq + L.q_fc1_w, gq + L.q_fc1_b,
+                 q_group(p), p.sp_q1));
     add(gb, t_dx(p.W(X_DH2Q), H, B, H, q + L.q_fc1_w, H, H, p.W(X_DH1Q), H, p.W(X_H1Q), H));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
     GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_dw(p.W(X_DH1Q), H, H, B, X + c.off_obs, RS, Dq, p.W(X_SLAB_Q0), p.sp_q0));
+    float* gq = grad_q(p);
+    add(gb, t_dw(p.W(X_DH1Q), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_fc0_w, gq + L.q_fc0_b,
+                 q_group(p), p.sp_q0));
     if (run_gemm(p, gb, s)) return 1;
   }
   return 0;
-}
-
-static AdamSegArgs pcritic_adam(SacPlan& p, int reduce_only) {
-  const oac_sac_config& c = p.c;
-  const oac_sac_layout& L = p.L;
-  const int H = c.hidden, Dq = c.obs_dim + c.act_dim;
-  AdamSegArgs a;
-  std::memset(&a, 0, sizeof(a));
-  a.seg[a.nseg++] = seg(p.W(X_SLAB_Q0), p.sp_q0, H, Dq, L.q_fc0_w, L.q_fc0_b);
-  a.seg[a.nseg++] = seg(p.W(X_SLAB_Q1), p.sp_q1, H, H, L.q_fc1_w, L.q_fc1_b);
-  a.seg[a.nseg++] = seg(p.W(X_SLAB_QL), p.sp_ql, c.q_out, H, L.q_last_w, L.q_last_b);
-  finalize_segs(a);
-  a.p = p.b.params + L.q1_base; a.g = p.b.grads + L.q1_base;
-  a.m = p.b.adam_m + L.q1_base; a.v = p.b.adam_v + L.q1_base;
-  a.target = p.b.targets; a.tau = c.tau; a.period = c.target_update_period;
-  a.lr = c.qf_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
-  a.state = p.state(); a.advance = 0; a.reduce_only = reduce_only; a.alpha = nullptr;
-  return a;
-}
-
-static AdamSegArgs ppolicy_adam(SacPlan& p, int reduce_only) {
-  const oac_sac_config& c = p.c;
-  const oac_sac_layout& L = p.L;
-  const int H = c.hidden, Do = c.obs_dim, Da = c.act_dim;
-  AdamSegArgs a;
-  std::memset(&a, 0, sizeof(a));
-  a.seg[a.nseg++] = seg(p.W(X_SLAB_P0), p.sp_p0, H, Do, L.pol_fc0_w, L.pol_fc0_b);
-  a.seg[a.nseg++] = seg(p.W(X_SLAB_P1), p.sp_p1, H, H, L.pol_fc1_w, L.pol_fc1_b);
-  a.seg[a.nseg++] = seg(p.W(X_SLAB_PH), p.sp_ph, 2 * Da, H, L.pol_head_w, L.pol_head_b);
-  finalize_segs(a);
-  a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.target = nullptr;
-  a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
-  a.state = p.state(); a.advance = reduce_only ? 0 : 1; a.reduce_only = reduce_only;
-  a.alpha = (!reduce_only && c.auto_alpha) ? p.alpha() : nullptr;
-  return a;
 }
 
 // critic Adam done; post-step critic forward on (obs, a~), alpha, policy grads
@@ -290,19 +256,25 @@ static int pphase2(SacPlan& p, hipStream_t s) {
   }
   {
     GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_dw(p.W(X_DHEAD), 2 * Da, 2 * Da, B, p.W(X_H2P), H, H, p.W(X_SLAB_PH), p.sp_ph));
+    float* gp = grad_p(p);
+    add(gb, t_dw(p.W(X_DHEAD), 2 * Da, 2 * Da, B, p.W(X_H2P), H, H, gp + L.pol_head_w,
+                 gp + L.pol_head_b, L.pol_size, p.sp_ph));
     add(gb, t_dx(p.W(X_DHEAD), 2 * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(X_DH2P), H, p.W(X_H2P), H));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
     GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_dw(p.W(X_DH2P), H, H, B, p.W(X_H1P), H, H, p.W(X_SLAB_P1), p.sp_p1));
+    float* gp = grad_p(p);
+    add(gb, t_dw(p.W(X_DH2P), H, H, B, p.W(X_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
+                 L.pol_size, p.sp_p1));
     add(gb, t_dx(p.W(X_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(X_DH1P), H, p.W(X_H1P), H));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
     GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_dw(p.W(X_DH1P), H, H, B, X + c.off_obs, RS, Do, p.W(X_SLAB_P0), p.sp_p0));
+    float* gp = grad_p(p);
+    add(gb, t_dw(p.W(X_DH1P), H, H, B, X + c.off_obs, RS, Do, gp + L.pol_fc0_w, gp + L.pol_fc0_b,
+                 L.pol_size, p.sp_p0));
     if (run_gemm(p, gb, s)) return 1;
   }
   return 0;
@@ -313,51 +285,41 @@ int particle_run_step(SacPlan& p, int flags, hipStream_t s) {
   if (pphase0(p, flags, s)) return 1;
   if (pphase1(p, s)) return 1;
   {
-    AdamSegArgs a = pcritic_adam(p, 0);
-    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam_seg(a, s)));
+    AdamArgs a = critic_adam(p, 0, nullptr);   // alpha is updated after the critic step
+    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
   }
   if (pphase2(p, s)) return 1;
   {
-    AdamSegArgs a = ppolicy_adam(p, 0);
-    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam_seg(a, s)));
+    AdamArgs a = policy_adam(p, 0, p.c.auto_alpha ? p.alpha() : nullptr);
+    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
   }
   return 0;
 }
 
 int particle_step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
-  const oac_sac_layout& L = p.L;
   switch (phase) {
     case 0: return pphase0(p, flags, s);
-    case 1: {
+    case 1:
       if (pphase1(p, s)) return 1;
-      AdamSegArgs a = pcritic_adam(p, 1);
-      OAC_HIP_CHECK(launch_adam_seg(a, s));
+      if (p.S_q > 1) {
+        AdamArgs a = critic_adam(p, 1, nullptr);
+        OAC_HIP_CHECK(launch_adam(a, s));
+      }
       return 0;
-    }
     case 2: {
-      AdamArgs a;
-      std::memset(&a, 0, sizeof(a));
-      a.p = p.b.params + L.q1_base; a.g = p.b.grads + L.q1_base;
-      a.m = p.b.adam_m + L.q1_base; a.v = p.b.adam_v + L.q1_base; a.n = L.q_size;
-      a.target = p.b.targets; a.tau = p.c.tau; a.period = p.c.target_update_period;
-      a.lr = p.c.qf_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
-      a.state = p.state(); a.advance = 0; a.alpha = nullptr;
-      a.gscale = 1.f / (float)(p.c.world_size > 1 ? p.c.world_size : 1);
+      AdamArgs a = critic_adam(p, -1, nullptr);
       OAC_HIP_CHECK(launch_adam(a, s));
       if (pphase2(p, s)) return 1;
-      AdamSegArgs b = ppolicy_adam(p, 1);
-      OAC_HIP_CHECK(launch_adam_seg(b, s));
+      if (p.S_p > 1) {
+        AdamArgs b = policy_adam(p, 1, nullptr);
+        OAC_HIP_CHECK(launch_adam(b, s));
+      }
       return 0;
     }
     case 3: {
-      AdamArgs a;
-      std::memset(&a, 0, sizeof(a));
-      a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.n = L.pol_size;
-      a.lr = p.c.policy_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
-      a.state = p.state(); a.advance = 1; a.alpha = p.c.auto_alpha ? p.alpha() : nullptr;
-      a.gscale = 1.f / (float)(p.c.world_size > 1 ? p.c.world_size : 1);
+      AdamArgs a = policy_adam(p, -1, p.c.auto_alpha ? p.alpha() : nullptr);
       OAC_HIP_CHECK(launch_adam(a, s));
       return 0;
     }

@@ -85,15 +85,17 @@ static inline void set_rank1(GemmTask& t, const float* s, const float* v, const 
   t.a_mode = A_RANK1_MASK; t.a_s = s; t.a_v = v; t.a_mask = mask; t.ld_mask = ldm;
 }
 
-// dW slab [S][M][Kin+1] = dY^T[M,B] . [X | 1][B, Kin+1]   (dY row-major [B, lddy])
-static inline GemmTask t_dw(const float* dY, long lddy, int M, int Bn, const float* X, long ldx, int Kin,
-                     float* slab, Split sp) {
+// dW[M, Kin] and db[M] = dY^T[M,B] . [X | 1][B, Kin+1], written in the
+// parameter-arena layout (gw / gb point into the gradient arena, or into
+// split-K slab `split` at +split*slab_stride).  dY row-major [B, lddy].
+static inline GemmTask t_dw(const float* dY, long lddy, int M, int Bn, const float* X, long ldx,
+                            int Kin, float* gw, float* gb, long slab_stride, Split sp) {
   GemmTask t = task0();
   t.A = dY; t.lda = lddy; t.a_kc = 0;
   t.B = X; t.ldb = ldx; t.b_kc = 0; t.b_ones = 1;
   t.M = M; t.N = Kin + 1; t.K = Bn;
-  t.C = slab; t.ldc = Kin + 1; t.epi = EPI_SLAB;
-  t.ksplit = sp.S; t.kchunk = sp.kchunk; t.slab_stride = (long)M * (Kin + 1);
+  t.C = gw; t.ldc = Kin; t.bias_grad = gb; t.epi = EPI_GRAD;
+  t.ksplit = sp.S; t.kchunk = sp.kchunk; t.slab_stride = slab_stride;
   return t;
 }
 
@@ -132,22 +134,5 @@ static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {
 }
 
 static inline void add(GemmBatch& gb, const GemmTask& t) { gb.t[gb.ntasks++] = t; }
-
-static inline AdamSeg seg(const float* slab, Split sp, int M, int Kin, int64_t off_w, int64_t off_b) {
-  AdamSeg s;
-  s.slab = slab; s.S = sp.S; s.M = M; s.ncols = Kin + 1;
-  s.slab_stride = (long)M * (Kin + 1);
-  s.off_w = off_w; s.off_b = off_b; s.elem_begin = 0;
-  return s;
-}
-
-static inline void finalize_segs(AdamSegArgs& a) {
-  long tot = 0;
-  for (int i = 0; i < a.nseg; ++i) {
-    a.seg[i].elem_begin = tot;
-    tot += (long)a.seg[i].M * a.seg[i].ncols;
-  }
-  a.total = tot;
-}
 
 }  // namespace oac

@@ -3,11 +3,15 @@
 // launch sequence).
 #pragma once
 #include "../../include/oac_amd.h"
+#include <cstring>
 #include "plan_common.h"
 
 namespace oac {
 
 constexpr int kMaxWs = 128;
+// split-K weight-gradient slabs shaped like the critic / policy arena ranges
+constexpr int WS_GSLAB_Q = kMaxWs - 2;
+constexpr int WS_GSLAB_P = kMaxWs - 1;
 
 struct SacPlan : PlanBase {
   oac_sac_config c;
@@ -15,6 +19,7 @@ struct SacPlan : PlanBase {
   oac_sac_buffers b;
   WsBuf ws[kMaxWs];
   Split sp_q0, sp_q1, sp_ql, sp_p0, sp_p1, sp_ph;
+  int S_q = 1, S_p = 1;   // slab counts per group (max over the group's dW tasks)
 
   float* W(int id) const { return b.workspace + ws[id].off; }
   float* P(int64_t off) const { return b.params + off; }
@@ -23,6 +28,49 @@ struct SacPlan : PlanBase {
   AlphaState* alpha() const { return reinterpret_cast<AlphaState*>(b.alpha_state); }
 };
 
+
+// gradient destinations: the grads arena (no split) or the group's slabs
+inline float* grad_q(SacPlan& p) {
+  return p.S_q > 1 ? p.W(WS_GSLAB_Q) : p.b.grads + p.L.q1_base;
+}
+inline float* grad_p(SacPlan& p) { return p.S_p > 1 ? p.W(WS_GSLAB_P) : p.b.grads; }
+inline long q_group(const SacPlan& p) { return (long)(p.L.n_critics * p.L.q_size); }
+
+// critic update: reduce slabs, Adam (t = n_steps + 1), Polyak, snapshot t
+inline AdamArgs critic_adam(SacPlan& p, int reduce_only, AlphaState* commit) {
+  const oac_sac_config& c = p.c;
+  AdamArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.p = p.b.params + p.L.q1_base; a.g = p.b.grads + p.L.q1_base;
+  a.m = p.b.adam_m + p.L.q1_base; a.v = p.b.adam_v + p.L.q1_base; a.n = q_group(p);
+  a.gslab = reduce_only < 0 ? a.g : grad_q(p);
+  a.S = reduce_only < 0 ? 1 : p.S_q;
+  a.slab_stride = q_group(p);
+  a.target = p.b.targets; a.tau = c.tau; a.period = c.target_update_period;
+  a.lr = c.qf_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
+  a.state = p.state(); a.advance = 0; a.alpha = commit;
+  a.gscale = reduce_only < 0 ? 1.f / (float)c.world_size : 1.f;
+  a.reduce_only = reduce_only > 0;
+  return a;
+}
+
+// policy update: reduce slabs, Adam (t = snapshot + 1), advance the step
+// reduce_only: 1 = reduce slabs into the grads arena only; -1 = the update from
+// the (all-reduced) grads arena with gscale = 1/world; 0 = both in one pass.
+inline AdamArgs policy_adam(SacPlan& p, int reduce_only, AlphaState* commit) {
+  const oac_sac_config& c = p.c;
+  AdamArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.n = p.L.pol_size;
+  a.gslab = reduce_only < 0 ? a.g : grad_p(p);
+  a.S = reduce_only < 0 ? 1 : p.S_p;
+  a.slab_stride = p.L.pol_size;
+  a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
+  a.state = p.state(); a.advance = 1; a.alpha = commit;
+  a.gscale = reduce_only < 0 ? 1.f / (float)c.world_size : 1.f;
+  a.reduce_only = reduce_only > 0;
+  return a;
+}
 
 // particle trainer (particle_plan.hip)
 void particle_layout_workspace(SacPlan& p);

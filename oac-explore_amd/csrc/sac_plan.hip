@@ -10,6 +10,7 @@
 //   policy Adam;  E9 Polyak with the post-step critics.
 // The sequence is static (step counters live on the device), so it is
 // captured once into a hipGraph and replayed per step.
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -65,8 +66,6 @@ enum Ws {
   W_STD1, W_U1, W_STD2, W_U2, W_DQ1, W_DQ2, W_GQ1, W_GQ2,
   W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DA1, W_DA2, W_DHEAD, W_DH2P, W_DH1P,
   W_PARTIALS,
-  W_SLAB_Q0a, W_SLAB_Q1a, W_SLAB_QLa, W_SLAB_Q0b, W_SLAB_Q1b, W_SLAB_QLb,
-  W_SLAB_P0, W_SLAB_P1, W_SLAB_PH,
   W_COUNT
 };
 
@@ -74,7 +73,7 @@ static void layout_workspace(SacPlan& p) {
   const oac_sac_config& c = p.c;
   const int64_t B = c.batch, H = c.hidden, Da = c.act_dim, Do = c.obs_dim, Q = c.q_out;
   auto set = [&](int id, int64_t r, int64_t cl) { p.ws[id] = {0, r, cl}; };
-  for (int i = 0; i < W_COUNT; ++i) p.ws[i] = {0, 0, 0};
+  for (int i = 0; i < kMaxWs; ++i) p.ws[i] = {0, 0, 0};
   set(OAC_WS_BATCH, B, c.row_stride);
   set(OAC_WS_EPS1, B, Da); set(OAC_WS_EPS2, B, Da);
   set(OAC_WS_HEAD1, B, 2 * Da); set(OAC_WS_HEAD2, B, 2 * Da);
@@ -88,19 +87,10 @@ static void layout_workspace(SacPlan& p) {
   for (int id : {W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DH2P, W_DH1P}) set(id, B, H);
   set(W_DHEAD, B, 2 * Da);
   set(W_PARTIALS, 1, 4096);
-  set(W_SLAB_Q0a, (int64_t)p.sp_q0.S * H, Do + Da + 1);
-  set(W_SLAB_Q1a, (int64_t)p.sp_q1.S * H, H + 1);
-  set(W_SLAB_QLa, (int64_t)p.sp_ql.S * Q, H + 1);
-  if (p.L.n_critics == 2) {
-    set(W_SLAB_Q0b, (int64_t)p.sp_q0.S * H, Do + Da + 1);
-    set(W_SLAB_Q1b, (int64_t)p.sp_q1.S * H, H + 1);
-    set(W_SLAB_QLb, (int64_t)p.sp_ql.S * Q, H + 1);
-  }
-  set(W_SLAB_P0, (int64_t)p.sp_p0.S * H, Do + 1);
-  set(W_SLAB_P1, (int64_t)p.sp_p1.S * H, H + 1);
-  set(W_SLAB_PH, (int64_t)p.sp_ph.S * 2 * Da, H + 1);
+  if (p.S_q > 1) set(WS_GSLAB_Q, p.S_q, p.L.n_critics * p.L.q_size);
+  if (p.S_p > 1) set(WS_GSLAB_P, p.S_p, p.L.pol_size);
   int64_t off = 0;
-  for (int i = 0; i < W_COUNT; ++i) {
+  for (int i = 0; i < kMaxWs; ++i) {
     p.ws[i].off = off;
     off = al64(off + p.ws[i].rows * p.ws[i].cols);
   }
@@ -254,13 +244,15 @@ static int phase1(SacPlan& p, hipStream_t s) {
     GemmBatch gb; gb.ntasks = 0;
     const float* qs[2] = {q1, q2};
     const int dq[2] = {W_DQ1, W_DQ2}, h2[2] = {W_H2Q1, W_H2Q2}, h1[2] = {W_H1Q1, W_H1Q2};
-    const int s1[2] = {W_SLAB_Q1a, W_SLAB_Q1b}, sl[2] = {W_SLAB_QLa, W_SLAB_QLb};
     const int dh1[2] = {W_DH1Q1, W_DH1Q2};
+    float* gq = grad_q(p);
+    const long gs = q_group(p);
     for (int i = 0; i < 2; ++i) {
-      GemmTask t = t_dw(nullptr, 0, H, B, p.W(h1[i]), H, H, p.W(s1[i]), p.sp_q1);
+      float* g = gq + i * L.q_size;   // critic i's block in the gradient (slab) layout
+      GemmTask t = t_dw(nullptr, 0, H, B, p.W(h1[i]), H, H, g + L.q_fc1_w, g + L.q_fc1_b, gs, p.sp_q1);
       set_rank1(t, p.W(dq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
       add(gb, t);
-      add(gb, t_dw(p.W(dq[i]), 1, 1, B, p.W(h2[i]), H, H, p.W(sl[i]), p.sp_ql));
+      add(gb, t_dw(p.W(dq[i]), 1, 1, B, p.W(h2[i]), H, H, g + L.q_last_w, g + L.q_last_b, gs, p.sp_ql));
       GemmTask d = t_dx(nullptr, 0, B, H, qs[i] + L.q_fc1_w, H, H, p.W(dh1[i]), H, p.W(h1[i]), H);
       set_rank1(d, p.W(dq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
       add(gb, d);
@@ -269,71 +261,21 @@ static int phase1(SacPlan& p, hipStream_t s) {
   }
   {  // critic backward, layer 0 (input = [obs | act] contiguous in the row)
     GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_dw(p.W(W_DH1Q1), H, H, B, X + c.off_obs, RS, Dq, p.W(W_SLAB_Q0a), p.sp_q0));
-    add(gb, t_dw(p.W(W_DH1Q2), H, H, B, X + c.off_obs, RS, Dq, p.W(W_SLAB_Q0b), p.sp_q0));
+    float* gq = grad_q(p);
+    const long gs = q_group(p);
+    add(gb, t_dw(p.W(W_DH1Q1), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_fc0_w, gq + L.q_fc0_b, gs, p.sp_q0));
+    add(gb, t_dw(p.W(W_DH1Q2), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_size + L.q_fc0_w,
+                 gq + L.q_size + L.q_fc0_b, gs, p.sp_q0));
     if (run_gemm(p, gb, s)) return 1;
   }
   return 0;
 }
 
-static AdamSegArgs critic_adam_args(SacPlan& p, int reduce_only) {
-  const oac_sac_config& c = p.c;
-  const oac_sac_layout& L = p.L;
-  const int H = c.hidden, Dq = c.obs_dim + c.act_dim;
-  AdamSegArgs a;
-  std::memset(&a, 0, sizeof(a));
-  const int s0[2] = {W_SLAB_Q0a, W_SLAB_Q0b}, s1[2] = {W_SLAB_Q1a, W_SLAB_Q1b},
-            sl[2] = {W_SLAB_QLa, W_SLAB_QLb};
-  for (int i = 0; i < (int)L.n_critics; ++i) {
-    const int64_t base = (i == 0 ? L.q1_base : L.q2_base) - L.q1_base;  // relative to critic arena
-    a.seg[a.nseg++] = seg(p.W(s0[i]), p.sp_q0, H, Dq, base + L.q_fc0_w, base + L.q_fc0_b);
-    a.seg[a.nseg++] = seg(p.W(s1[i]), p.sp_q1, H, H, base + L.q_fc1_w, base + L.q_fc1_b);
-    a.seg[a.nseg++] = seg(p.W(sl[i]), p.sp_ql, c.q_out, H, base + L.q_last_w, base + L.q_last_b);
-  }
-  finalize_segs(a);
-  a.p = p.b.params + L.q1_base; a.g = p.b.grads + L.q1_base;
-  a.m = p.b.adam_m + L.q1_base; a.v = p.b.adam_v + L.q1_base;
-  a.target = p.b.targets;
-  a.tau = c.tau; a.period = c.target_update_period;
-  a.lr = c.qf_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
-  a.state = p.state(); a.advance = 0; a.reduce_only = reduce_only;
-  a.alpha = c.auto_alpha ? p.alpha() : nullptr;
-  return a;
-}
-
-static AdamSegArgs policy_adam_args(SacPlan& p, int reduce_only) {
-  const oac_sac_config& c = p.c;
-  const oac_sac_layout& L = p.L;
-  const int H = c.hidden, Do = c.obs_dim, Da = c.act_dim;
-  AdamSegArgs a;
-  std::memset(&a, 0, sizeof(a));
-  a.seg[a.nseg++] = seg(p.W(W_SLAB_P0), p.sp_p0, H, Do, L.pol_fc0_w, L.pol_fc0_b);
-  a.seg[a.nseg++] = seg(p.W(W_SLAB_P1), p.sp_p1, H, H, L.pol_fc1_w, L.pol_fc1_b);
-  a.seg[a.nseg++] = seg(p.W(W_SLAB_PH), p.sp_ph, 2 * Da, H, L.pol_head_w, L.pol_head_b);
-  finalize_segs(a);
-  a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.target = nullptr;
-  a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
-  a.state = p.state(); a.advance = reduce_only ? 0 : 1; a.reduce_only = reduce_only;
-  return a;
-}
-
 // phase 2: critic Adam + Polyak, policy gradient through the post-step critics
 static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
-  if (dp) {  // gradients already reduced + all-reduced in the arena: flat Adam
-    const oac_sac_layout& L = p.L;
-    AdamArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.p = p.b.params + L.q1_base; a.g = p.b.grads + L.q1_base;
-    a.m = p.b.adam_m + L.q1_base; a.v = p.b.adam_v + L.q1_base; a.n = L.n_critics * L.q_size;
-    a.target = p.b.targets; a.tau = p.c.tau; a.period = p.c.target_update_period;
-    a.lr = p.c.qf_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
-    a.state = p.state(); a.advance = 0; a.alpha = p.c.auto_alpha ? p.alpha() : nullptr;
-    a.gscale = 1.f / (float)(p.c.world_size > 1 ? p.c.world_size : 1);
-    OAC_HIP_CHECK(launch_adam(a, s));
-  } else {
-    AdamSegArgs a = critic_adam_args(p, 0);
-    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam_seg(a, s)));
-  }
+  // SAC commits the alpha update here (no kernel after this reads next_*)
+  AdamArgs a = critic_adam(p, dp ? -1 : 0, p.c.auto_alpha ? p.alpha() : nullptr);
+  TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
   p.launches++;
   return 0;
 }
@@ -376,19 +318,25 @@ static int phase2(SacPlan& p, hipStream_t s) {
   }
   {  // policy heads: dW_head slab, dh2
     GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, p.W(W_SLAB_PH), p.sp_ph));
+    float* gp = grad_p(p);
+    add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, gp + L.pol_head_w,
+                 gp + L.pol_head_b, L.pol_size, p.sp_ph));
     add(gb, t_dx(p.W(W_DHEAD), 2 * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(W_DH2P), H, p.W(W_H2P), H));
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 1
     GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, p.W(W_SLAB_P1), p.sp_p1));
+    float* gp = grad_p(p);
+    add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
+                 L.pol_size, p.sp_p1));
     add(gb, t_dx(p.W(W_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_DH1P), H, p.W(W_H1P), H));
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 0
     GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_dw(p.W(W_DH1P), H, H, B, X + c.off_obs, RS, Do, p.W(W_SLAB_P0), p.sp_p0));
+    float* gp = grad_p(p);
+    add(gb, t_dw(p.W(W_DH1P), H, H, B, X + c.off_obs, RS, Do, gp + L.pol_fc0_w, gp + L.pol_fc0_b,
+                 L.pol_size, p.sp_p0));
     if (run_gemm(p, gb, s)) return 1;
   }
   return 0;
@@ -400,8 +348,8 @@ static int run_step(SacPlan& p, int flags, hipStream_t s) {
   if (phase1(p, s)) return 1;
   if (phase2_adam(p, s, 0)) return 1;
   if (phase2(p, s)) return 1;
-  AdamSegArgs a = policy_adam_args(p, 0);
-  TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam_seg(a, s)));
+  AdamArgs a = policy_adam(p, 0, nullptr);
+  TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
   p.launches++;
   return 0;
 }
@@ -456,6 +404,8 @@ static void plan_splits(SacPlan& p) {
   p.sp_ph = choose_split(c.batch, tiles(2 * Da, H + 1), p.cfg);
   p.sp_p1 = choose_split(c.batch, tiles(H, H + 1), p.cfg);
   p.sp_p0 = choose_split(c.batch, tiles(H, Do + 1), p.cfg);
+  p.S_q = std::max(std::max(p.sp_q0.S, p.sp_q1.S), p.sp_ql.S);
+  p.S_p = std::max(std::max(p.sp_p0.S, p.sp_p1.S), p.sp_ph.S);
 }
 
 int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out) {
@@ -529,27 +479,23 @@ int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
   if (p.c.kind == OAC_KIND_PARTICLE) return particle_step_phase(p, phase, flags, s);
   switch (phase) {
     case 0: return phase0(p, flags, s);
-    case 1: return phase1(p, s) ? 1 : [&] {
-        AdamSegArgs a = critic_adam_args(p, 1);
-        OAC_HIP_CHECK(launch_adam_seg(a, s));
-        return 0;
-      }();
+    case 1:
+      if (phase1(p, s)) return 1;
+      if (p.S_q > 1) {
+        AdamArgs a = critic_adam(p, 1, nullptr);
+        OAC_HIP_CHECK(launch_adam(a, s));
+      }
+      return 0;
     case 2:
       if (phase2_adam(p, s, 1)) return 1;
       if (phase2(p, s)) return 1;
-      {
-        AdamSegArgs a = policy_adam_args(p, 1);
-        OAC_HIP_CHECK(launch_adam_seg(a, s));
+      if (p.S_p > 1) {
+        AdamArgs a = policy_adam(p, 1, nullptr);
+        OAC_HIP_CHECK(launch_adam(a, s));
       }
       return 0;
     case 3: {
-      const oac_sac_layout& L = p.L;
-      AdamArgs a;
-      std::memset(&a, 0, sizeof(a));
-      a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.n = L.pol_size;
-      a.lr = p.c.policy_lr; a.beta1 = p.c.beta1; a.beta2 = p.c.beta2; a.eps = p.c.adam_eps;
-      a.state = p.state(); a.advance = 1;
-      a.gscale = 1.f / (float)(p.c.world_size > 1 ? p.c.world_size : 1);
+      AdamArgs a = policy_adam(p, -1, nullptr);
       OAC_HIP_CHECK(launch_adam(a, s));
       return 0;
     }
@@ -600,9 +546,11 @@ int oac_adam_polyak(float* p, const float* g, float* m, float* v, int64_t n, flo
                     void* step_state, int advance, void* stream) {
   AdamArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.p = p; a.g = g; a.m = m; a.v = v; a.n = n; a.target = target; a.tau = tau; a.period = period;
+  a.p = p; a.g = const_cast<float*>(g); a.m = m; a.v = v; a.n = n;  // g is only read (S == 1)
+  a.target = target; a.tau = tau; a.period = period;
   a.lr = lr; a.beta1 = beta1; a.beta2 = beta2; a.eps = eps;
   a.state = reinterpret_cast<StepState*>(step_state); a.advance = advance; a.gscale = 1.f;
+  a.gslab = a.g; a.S = 1; a.slab_stride = n;
   OAC_HIP_CHECK(launch_adam(a, reinterpret_cast<hipStream_t>(stream)));
   return 0;
 }

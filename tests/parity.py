@@ -55,6 +55,22 @@ def ref_view(gold, key):
                        tuple(gold[key + "#shape"]))
 
 
+def stat_err(got, g, key):
+    """Relative error of a diagnostics statistic.  A "... Std" of tightly
+    clustered values (e.g. the P-OAC heads initialised at fixed biases) is a
+    cancellation: |std(a) - std(b)| <= rms(a - b), so its error is measured
+    against the rms of the values, sqrt(mean^2 + std^2), not against the std."""
+    ref = float(np.asarray(g[key], np.float64).reshape(-1)[0])
+    if key.endswith(" Std"):
+        mk = key[:-4] + " Mean"
+        if mk in g:
+            mean = float(np.asarray(g[mk], np.float64).reshape(-1)[0])
+            scale = float(np.hypot(mean, ref))
+            if scale > 0:
+                return abs(float(np.asarray(got, np.float64).reshape(-1)[0]) - ref) / scale
+    return rel_err(got, ref)
+
+
 def rel_err(got, ref):
     got = np.asarray(got, np.float64).reshape(-1)
     ref = np.asarray(ref, np.float64).reshape(-1)

@@ -50,7 +50,7 @@ def _gpu_errors(meta, g, tr, use_device_batch=False):
         for k in ("QF1 Loss", "QF2 Loss", "Q Loss", "Policy Loss", "Alpha", "Alpha Loss",
                   "QF mean", "Log Pis Mean", "Q Targets Mean", "Policy log std Mean"):
             if f"s{s}/stat/{k}" in g:
-                errs[f"s{s}/stat/{k}"] = parity.rel_err(st[k], g[f"s{s}/stat/{k}"])
+                errs[f"s{s}/stat/{k}"] = parity.stat_err(st[k], g, f"s{s}/stat/{k}")
     return errs
 
 

@@ -56,7 +56,7 @@ def test_particle_step_matches_reference_golden(name):
         for k in list(st.keys()):
             gk = f"s{s}/stat/{k}"
             if gk in g and k not in ("QF Unordered", "QF target Undordered"):
-                errs[gk] = parity.rel_err(st[k], g[gk])
+                errs[gk] = parity.stat_err(st[k], g, gk)
     bad = {k: v for k, v in errs.items() if v > (parity.TOL if k.startswith("s0/") else 1e-4)}
     print(name, "worst", sorted(errs.items(), key=lambda kv: -kv[1])[:3])
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:10]
