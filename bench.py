@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--timing-steps", type=int, default=50)
     ap.add_argument("--gemm-cfg", type=int, default=-1)
+    ap.add_argument("--steps-per-launch", type=int, default=8,
+                    help="gradient steps per graph launch (1 = one graph per step)")
     return ap.parse_args()
 
 
@@ -95,10 +97,12 @@ def build(args, rank, world, device):
     return tr, rb, stream
 
 
-def step_fn(tr, rb, stream, B):
+def step_fn(tr, rb, stream, B, n=1):
+    """One call = n consecutive gradient steps (n divides the 64-step index
+    chunk), each on its own minibatch; n > 1 replays one n-step graph."""
     def step():
-        stream.before_step()
-        tr.train_from_ring(rb._storage, stream.ring, stream.slots, B)
+        stream.before_step(n)
+        tr.train_from_ring(rb._storage, stream.ring, stream.slots, B, n_steps=n)
     return step
 
 
@@ -118,7 +122,7 @@ def kernel_timing(tr, rb, stream, B, n):
     torch.cuda.synchronize()
     _lib.check(L.oac_sac_read_timing(plan.handle, ms, cnt, 4))
     _lib.check(L.oac_sac_set_timing(plan.handle, 0))
-    names = ["gemm_grouped", "row", "adam_seg", "gather"]
+    names = ["gemm_grouped", "row", "adam", "gather"]
     return {names[k]: dict(ms=ms[k], launches=int(cnt[k]),
                            avg_us=1e3 * ms[k] / max(cnt[k], 1)) for k in range(4)}
 
@@ -184,7 +188,11 @@ def main():
     torch.cuda.set_device(device)
     B = args.batch
     tr, rb, stream = build(args, rank, world, device)
-    step = step_fn(tr, rb, stream, B)
+    # data-parallel steps exchange gradients from the host between phases: one step per call
+    n = max(1, args.steps_per_launch) if world == 1 else 1
+    if args.steps % n or args.warmup % n or stream.chunk % n:
+        raise SystemExit("--steps / --warmup must be multiples of --steps-per-launch (which divides 64)")
+    step = step_fn(tr, rb, stream, B, n)
 
     def barrier():
         torch.cuda.synchronize()
@@ -192,11 +200,11 @@ def main():
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup):
+    for _ in range(args.warmup // n):
         step()
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.steps // n):
         step()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -231,6 +239,7 @@ def main():
                        "replay_per_rank": args.replay,
                        "parallelism": "dp%d" % world if world > 1 else "single"},
             "samples_per_s": round(value * B, 1),
+            "steps_per_launch": n,
             "roofline": {"bound": "mfma", "kernel": "gemm_grouped_kernel",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
@@ -242,7 +251,7 @@ def main():
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv
                             for kk, vv in v.items()} for k, v in kt.items()},
         }
-        ga, ad = kt["gather"], kt["adam_seg"]
+        ga, ad = kt["gather"], kt["adam"]
         if ga["launches"]:
             out["gather_GBps"] = round(GATHER_BYTES_PER_SAMPLE * B / (ga["avg_us"] * 1e-6) / 1e9, 1)
         if ad["launches"]:

@@ -106,6 +106,13 @@ int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out);
 int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_sac** out);
 int oac_sac_destroy(oac_sac* h);
 int oac_sac_step(oac_sac* h, int flags, void* stream);
+
+/* n_steps consecutive steps (each its own minibatch from the device index
+ * ring, exactly as n calls of oac_sac_step); with OAC_STEP_USE_GRAPH they are
+ * captured into one graph, so the per-launch host/graph cost is paid once per
+ * n steps.  Used by rl_algorithm-style loops that run num_trains_per_train_loop
+ * steps back to back (rl_algorithm.py: trainer.train per step). */
+int oac_sac_step_n(oac_sac* h, int flags, int n_steps, void* stream);
 /* data-parallel split (config.world_size > 1): phase 0 = forward through the
  * policy sample and the local sum(logp + target_entropy) into alpha_state[6];
  * 1 = alpha update from the caller's all-reduced sum through the critic

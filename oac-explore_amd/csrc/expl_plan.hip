@@ -75,17 +75,17 @@ static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta,
   const oac_sac_layout& L = p.L;
   float* w = p.ws;
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     gb.t[gb.ntasks++] = e_fwd(w + p.o_x, Do, p.pol + L.pol_fc0_w, Do, H, w + p.o_h1p, EPI_BIAS_RELU, p.pol + L.pol_fc0_b);
     if (e_run(gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     gb.t[gb.ntasks++] = e_fwd(w + p.o_h1p, H, p.pol + L.pol_fc1_w, H, H, w + p.o_h2p, EPI_BIAS_RELU, p.pol + L.pol_fc1_b);
     if (e_run(gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     gb.t[gb.ntasks++] = e_fwd(w + p.o_h2p, H, p.pol + L.pol_head_w, H, 2 * Da, w + p.o_head, EPI_BIAS, p.pol + L.pol_head_b);
     if (e_run(gb, s)) return 1;
   }
@@ -100,19 +100,19 @@ static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta,
   const float* qs[2] = {p.q1, p.q2};
   const int64_t h1[2] = {p.o_h1q1, p.o_h1q2}, h2[2] = {p.o_h2q1, p.o_h2q2}, qo[2] = {p.o_q1, p.o_q2};
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     for (int i = 0; i < 2; ++i)
       gb.t[gb.ntasks++] = e_fwd(w + p.o_x, Dq, qs[i] + L.q_fc0_w, Dq, H, w + h1[i], EPI_BIAS_RELU, qs[i] + L.q_fc0_b);
     if (e_run(gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     for (int i = 0; i < 2; ++i)
       gb.t[gb.ntasks++] = e_fwd(w + h1[i], H, qs[i] + L.q_fc1_w, H, H, w + h2[i], EPI_BIAS_RELU, qs[i] + L.q_fc1_b);
     if (e_run(gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     for (int i = 0; i < 2; ++i)
       gb.t[gb.ntasks++] = e_fwd(w + h2[i], H, qs[i] + L.q_last_w, H, 1, w + qo[i], EPI_BIAS, qs[i] + L.q_last_b);
     if (e_run(gb, s)) return 1;
@@ -120,7 +120,7 @@ static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta,
   OAC_HIP_CHECK(launch_oac_seed(a, s));
   const int64_t dh[2] = {p.o_dh1, p.o_dh2}, da[2] = {p.o_da1, p.o_da2};
   {  // dQ_i/dh1 = (w_i * wl_i * [h2 > 0]) . W1_i  masked by h1 > 0
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     for (int i = 0; i < 2; ++i) {
       GemmTask t = e_task();
       t.a_mode = A_RANK1_MASK; t.a_s = w + p.o_w + i; t.a_v = qs[i] + L.q_last_w;
@@ -133,7 +133,7 @@ static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta,
     if (e_run(gb, s)) return 1;
   }
   {  // dQ_i/da = dh1_i . W0_i[:, Do:]
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     for (int i = 0; i < 2; ++i) {
       GemmTask t = e_task();
       t.A = w + dh[i]; t.lda = H; t.a_kc = 1;

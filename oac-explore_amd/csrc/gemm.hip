@@ -17,6 +17,7 @@
 // the K loop across waves (for the small-M/N stages of a batch-256 step),
 // reduced through LDS in fixed order (deterministic).
 #include "oac_common.h"
+#include "adam_common.h"
 
 namespace oac {
 
@@ -198,6 +199,8 @@ __global__ void __launch_bounds__(256) gemm_grouped_kernel(const GemmBatch batch
   // task lookup (uniform)
   int ti = 0;
   const int bid = blockIdx.x;
+  if (batch.publish && bid == 0 && threadIdx.x == 0)
+    publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
 #pragma unroll 1
   for (int i = 1; i < batch.ntasks; ++i)
     if (bid >= batch.t[i].tile_begin) ti = i;
@@ -365,6 +368,7 @@ void gemm_batch_finalize(GemmBatch& b, int cfg) {
 hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   if (b.total_tiles <= 0) return hipSuccess;
   if (cfg == 0) return gemm_small_launch(b, s);
+  if (b.fuse_adam) return hipErrorInvalidValue;   // fused optimizer: small-batch kernel only
   hipLaunchKernelGGL(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b);
   return hipGetLastError();
 }

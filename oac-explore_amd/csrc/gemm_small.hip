@@ -15,71 +15,189 @@
 //   are issued before the current group's MFMAs (register double buffer).
 #include "oac_common.h"
 #include "kernels.h"
+#include "adam_common.h"
+
+#include <algorithm>
 
 namespace oac {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-// Operand fetch for one k-group: out[c] = X(mn, k = kbase + c), c = 0..3,
-// where kbase = 8g + 4*(lane>>5).  `kc`: k contiguous in memory.
-struct OpDesc {
-  const float* p;     // base
-  long ld;            // row stride
-  int kc;             // 1: element (mn,k) at p[mn*ld + k]; 0: p[k*ld + mn]
-  int vec;            // kc && ld%4==0 && aligned: one float4 load
-  int rank1;          // value = s[row]*v[col]*(mask[row*ldm+col] > 0)
-  const float* s; const float* v; long ldm;
-  int n_mn;           // rows (M or N) in range
-  int ones;           // virtual ones column at mn == n_mn (dW bias column)
-  int K;
+// Operand kinds (compile-time, so the k loop is straight-line code: every
+// load of a wave's k-groups is issued before the first MFMA and fixed up
+// -- masking, rank-1 products -- only afterwards).
+//   OP_KC     X(mn,k) = p[mn*ld + k]                      (one 16-B load / 4 k)
+//   OP_KC_R1  X(mn,k) = s[mn] * v[k] * (mask[mn*ld+k] > 0)
+//   OP_MN     X(mn,k) = p[k*ld + mn]                      (dword, coalesced over mn)
+//   OP_MN_R1  X(mn,k) = s[k] * v[mn] * (mask[k*ld+mn] > 0)
+// k-contiguous loads are dword-aligned dwordx4 (gfx950 global memory takes
+// them, so odd row strides such as the critic's 393-wide layer 0 stay
+// vectorised) and may read up to 7 floats past a row's last k; those lanes
+// are masked.  Every operand buffer is followed by >= 8 readable floats
+// (workspace tail pad, arena neighbours, replay row padding).
+enum OpKind { OP_KC = 0, OP_KC_R1 = 1, OP_MN = 2, OP_MN_R1 = 3 };
+
+struct Lane {
+  const float* p;     // kc: &X(mn, 0) ; mn: &X(0, mn)   (rank-1: of the mask)
+  const float* s;     // rank-1 factor indexed by k
+  long ld;
+  float f;            // rank-1 factor indexed by mn
+  bool valid;         // mn in range
+  bool ones;          // virtual ones column (dW bias)
 };
 
-__device__ __forceinline__ void fetch4(const OpDesc& d, int mn, int kbase, float (&out)[4]) {
-  const bool mn_ok = mn < d.n_mn;
-  const int mnc = mn_ok ? mn : 0;
-  if (d.vec) {
-    const bool ok = mn_ok && (kbase < d.K);          // K % 4 == 0 on the vec path
-    const float4 x = *reinterpret_cast<const float4*>(d.p + (long)mnc * d.ld + (ok ? kbase : 0));
-    out[0] = ok ? x.x : 0.f; out[1] = ok ? x.y : 0.f;
-    out[2] = ok ? x.z : 0.f; out[3] = ok ? x.w : 0.f;
-    if (d.ones && mn == d.n_mn) {
-#pragma unroll
-      for (int c = 0; c < 4; ++c) out[c] = (kbase + c < d.K) ? 1.f : 0.f;
+template <int KIND>
+__device__ __forceinline__ Lane lane_init(int mn, int n_mn, bool ones, const float* p, long ld,
+                                          const float* s, const float* v) {
+  Lane o;
+  o.valid = mn < n_mn;
+  o.ones = ones && mn == n_mn;
+  const int m = o.valid ? mn : 0;
+  o.ld = ld;
+  o.p = (KIND == OP_KC || KIND == OP_KC_R1) ? p + (long)m * ld : p + m;
+  o.s = KIND == OP_KC_R1 ? v : s;
+  o.f = KIND == OP_KC_R1 ? s[m] : (KIND == OP_MN_R1 ? v[m] : 1.f);
+  return o;
+}
+
+typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+
+// raw loads of X(mn, kb..kb+3); kmax = last valid k (clamp for mn-major rows)
+template <int KIND>
+__device__ __forceinline__ void load4(const Lane& o, int kb, int kmax, float (&x)[4],
+                                      float (&y)[4]) {
+  if (KIND == OP_KC || KIND == OP_KC_R1) {
+    const f4u a = *reinterpret_cast<const f4u*>(o.p + kb);
+    x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+    if (KIND == OP_KC_R1) {
+      const f4u b = *reinterpret_cast<const f4u*>(o.s + kb);
+      y[0] = b.x; y[1] = b.y; y[2] = b.z; y[3] = b.w;
     }
-    return;
-  }
+  } else {
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const int k = kbase + c;
-    const bool ok = mn_ok && (k < d.K);
-    const int kk = ok ? k : 0;
-    const int row = d.kc ? mnc : kk;
-    const int col = d.kc ? kk : mnc;
-    float x;
-    if (!d.rank1) {
-      x = d.p[(long)row * d.ld + col];
-    } else {
-      const float mk = d.p[(long)row * d.ldm + col];
-      x = mk > 0.f ? d.s[row] * d.v[col] : 0.f;
+    for (int c = 0; c < 4; ++c) {
+      const int k = min(kb + c, kmax);
+      x[c] = o.p[(long)k * o.ld];
+      if (KIND == OP_MN_R1) y[c] = o.s[k];
     }
-    out[c] = ok ? x : ((d.ones && mn == d.n_mn && k < d.K) ? 1.f : 0.f);
   }
 }
 
-__device__ __forceinline__ void epi_one(const GemmTask& t, int m, int n, float acc,
+template <int KIND>
+__device__ __forceinline__ float fix1(const Lane& o, int k, int k_hi, float x, float y) {
+  float val = x;
+  if (KIND == OP_KC_R1 || KIND == OP_MN_R1) val = x > 0.f ? o.f * y : 0.f;
+  val = o.valid ? val : (o.ones ? 1.f : 0.f);
+  return k < k_hi ? val : 0.f;
+}
+
+// acc += A[m0.., k_lo..k_hi) . B[k_lo..k_hi), n0..]  for this wave's k-groups
+template <int NW, int AK, int BK>
+__device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
+                                       floatx16& acc) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+  const int l32 = lane & 31;
+  const int half = lane >> 5;
+  const bool ar1 = (AK == OP_KC_R1 || AK == OP_MN_R1);
+  const Lane la = lane_init<AK>(m0 + l32, t.M, false, ar1 ? t.a_mask : t.A,
+                                ar1 ? t.ld_mask : t.lda, t.a_s, t.a_v);
+  const Lane lb = lane_init<BK>(n0 + l32, t.b_ones ? t.N - 1 : t.N, t.b_ones != 0, t.B, t.ldb,
+                                nullptr, nullptr);
+  constexpr int kGPW = NW >= 16 ? 4 : 5;      // k-groups in flight per wave (<= 128 VGPRs at 8 waves)
+  const int g_lo = k_lo >> 3;                 // k_lo is a multiple of 8 (kchunk % 8 == 0)
+  const int g_hi = (k_hi + 7) >> 3;
+  const int kmax = k_hi - 1;
+#pragma unroll 1
+  for (int g0 = g_lo + wave; g0 < g_hi; g0 += kGPW * NW) {
+    float ax[kGPW][4], ay[kGPW][4], bx[kGPW][4], by[kGPW][4];
+#pragma unroll
+    for (int j = 0; j < kGPW; ++j)
+      if (g0 + j * NW < g_hi) {
+        const int kb = 8 * (g0 + j * NW) + 4 * half;
+        load4<AK>(la, kb, kmax, ax[j], ay[j]);
+        load4<BK>(lb, kb, kmax, bx[j], by[j]);
+      }
+#pragma unroll
+    for (int j = 0; j < kGPW; ++j)
+      if (g0 + j * NW < g_hi) {
+        const int kb = 8 * (g0 + j * NW) + 4 * half;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float a = fix1<AK>(la, kb + c, k_hi, ax[j][c], ay[j][c]);
+          const float b = fix1<BK>(lb, kb + c, k_hi, bx[j][c], by[j][c]);
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+        }
+      }
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void k_dispatch(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
+                                           floatx16& acc) {
+  const bool r1 = t.a_mode == A_RANK1_MASK;
+  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC>(t, m0, n0, k_lo, k_hi, acc);      // forward
+  else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN>(t, m0, n0, k_lo, k_hi, acc);      // dX
+  else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN>(t, m0, n0, k_lo, k_hi, acc);   // dX, rank-1 seed
+  else if (!r1)                k_loop<NW, OP_MN, OP_MN>(t, m0, n0, k_lo, k_hi, acc);      // dW
+  else                         k_loop<NW, OP_MN_R1, OP_MN>(t, m0, n0, k_lo, k_hi, acc);   // dW, rank-1 seed
+}
+
+// Epilogue operands of one output element, loaded before the k loop so their
+// latency hides behind it: xb = bias[n] (or the fused-Adam p), xa = aux[m,n]
+// (EPI_ADD_RELU / EPI_MASK), aux[n] (EPI_BIAS_RELU_DOT).
+// EPI_GRAD with the fused optimizer: p, m, v (and the Polyak target) of the element.
+struct EpiIn { float xb, xa, am, av, at; };
+
+__device__ __forceinline__ EpiIn epi_prefetch(const GemmBatch& batch, const GemmTask& t, int m,
+                                              int n) {
+  EpiIn x{0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool in = m < t.M && n < t.N;
+  const int mc = in ? m : 0, nc = in ? n : 0;
+  switch (t.epi) {
+    case EPI_GRAD:
+      if (batch.fuse_adam) {
+        const float* g = (t.b_ones && nc == t.N - 1) ? t.bias_grad + mc : t.C + (long)mc * t.ldc + nc;
+        const long i = g - batch.adam.g;
+        x.xb = batch.adam.p[i]; x.am = batch.adam.m[i]; x.av = batch.adam.v[i];
+        if (batch.adam.target) x.at = batch.adam.target[i];
+      }
+      break;
+    case EPI_BIAS: case EPI_BIAS_RELU: case EPI_BIAS_RANK_RELU:
+      x.xb = t.bias[nc]; break;
+    case EPI_BIAS_RELU_DOT:
+      x.xb = t.bias[nc]; x.xa = t.aux[nc]; break;
+    case EPI_ADD_RELU: case EPI_MASK:
+      x.xa = t.aux[(long)mc * t.ld_aux + nc]; break;
+    default: break;
+  }
+  return x;
+}
+
+__device__ __forceinline__ void epi_one(const GemmBatch& batch, const AdamConsts& ac,
+                                        const GemmTask& t, int m, int n, float acc, EpiIn x,
                                         const float* lds_u, const float* lds_v, int mt, int nt) {
   if (m >= t.M || n >= t.N) return;
   const long o = (long)m * t.ldc + n;
   switch (t.epi) {
     case EPI_STORE: t.C[o] = acc; break;
-    case EPI_GRAD:
-      if (t.b_ones && n == t.N - 1) t.bias_grad[m] = acc;
-      else t.C[o] = acc;
+    case EPI_GRAD: {
+      float* g = (t.b_ones && n == t.N - 1) ? t.bias_grad + m : t.C + o;
+      *g = acc;
+      if (batch.fuse_adam) {   // adam_elem on the prefetched p, m, v, target
+        const long i = g - batch.adam.g;
+        float p = x.xb, m = x.am, v = x.av;
+        adam1(ac, p, acc, m, v);
+        batch.adam.p[i] = p; batch.adam.m[i] = m; batch.adam.v[i] = v;
+        if (ac.polyak) batch.adam.target[i] = polyak1(ac, x.at, p);
+      }
       break;
-    case EPI_BIAS: t.C[o] = acc + t.bias[n]; break;
-    case EPI_BIAS_RELU: t.C[o] = fmaxf(acc + t.bias[n], 0.f); break;
+    }
+    case EPI_BIAS: t.C[o] = acc + x.xb; break;
+    case EPI_BIAS_RELU:
+    case EPI_BIAS_RELU_DOT: t.C[o] = fmaxf(acc + x.xb, 0.f); break;
     case EPI_BIAS_RANK_RELU: {
-      const float p = acc + t.bias[n];
+      const float p = acc + x.xb;
       t.C[o] = p;
       const int Rp = t.R | 1;
       const float* u = lds_u + mt * Rp;
@@ -89,8 +207,8 @@ __device__ __forceinline__ void epi_one(const GemmTask& t, int m, int n, float a
       t.C2[(long)m * t.ldc2 + n] = fmaxf(p + s, 0.f);
       break;
     }
-    case EPI_ADD_RELU: t.C[o] = fmaxf(acc + t.aux[(long)m * t.ld_aux + n], 0.f); break;
-    case EPI_MASK: t.C[o] = t.aux[(long)m * t.ld_aux + n] > 0.f ? acc : 0.f; break;
+    case EPI_ADD_RELU: t.C[o] = fmaxf(acc + x.xa, 0.f); break;
+    case EPI_MASK: t.C[o] = x.xa > 0.f ? acc : 0.f; break;
     default: break;
   }
 }
@@ -102,8 +220,26 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
   constexpr int LDS = RED > 2 * 32 * 65 ? RED : 2 * 32 * 65;
   constexpr int PER = 1024 / (64 * NW);   // epilogue elements per thread
   __shared__ __attribute__((aligned(16))) float red[LDS];
-  int ti = 0;
   const int bid = blockIdx.x;
+  if (batch.publish && bid == 0 && threadIdx.x == 0)
+    publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
+  if (bid >= batch.total_tiles) {   // fused optimizer: flat Adam over the other ranges
+    const AdamArgs& a = batch.adam;
+    const AdamConsts c = adam_consts(a.state, a.advance, a.lr, a.beta1, a.beta2, a.eps,
+                                     a.target, a.tau, a.period);
+    const long stride = (long)batch.adam_blocks * 64 * NW;
+    for (int sgi = 0; sgi < batch.nseg; ++sgi) {
+      AdamArgs r = a;
+      r.p += batch.seg_off[sgi]; r.m += batch.seg_off[sgi]; r.v += batch.seg_off[sgi];
+      if (r.target) r.target += batch.seg_off[sgi];
+      const float* g = a.g + batch.seg_off[sgi];
+      const long n4 = batch.seg_n[sgi] >> 2;
+      for (long i = (long)(bid - batch.total_tiles) * 64 * NW + threadIdx.x; i < n4; i += stride)
+        adam_float4(c, r, i, reinterpret_cast<const float4*>(g)[i]);
+    }
+    return;
+  }
+  int ti = 0;
 #pragma unroll 1
   for (int i = 1; i < batch.ntasks; ++i)
     if (bid >= batch.t[i].tile_begin) ti = i;
@@ -121,58 +257,19 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
   const int m0 = (local / t.tiles_n) * 32;
   const int n0 = (local % t.tiles_n) * 32;
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int l32 = lane & 31;
-  const int half = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
 
-  // operand descriptors (the k origin is folded into K: k indices are absolute)
-  OpDesc da, db;
-  da.p = t.a_mode == A_PLAIN ? t.A : t.a_mask;
-  da.ld = t.a_mode == A_PLAIN ? t.lda : t.ld_mask;
-  da.ldm = t.ld_mask;
-  da.kc = t.a_kc;
-  da.rank1 = t.a_mode == A_RANK1_MASK;
-  da.s = t.a_s; da.v = t.a_v;
-  da.n_mn = t.M; da.ones = 0; da.K = k_hi;
-  da.vec = (!da.rank1) && t.a_kc && ((t.lda & 3) == 0) &&
-           ((reinterpret_cast<unsigned long>(t.A) & 15) == 0) && ((t.K & 3) == 0);
-  db.p = t.B; db.ld = t.ldb; db.ldm = 0; db.kc = t.b_kc; db.rank1 = 0; db.s = nullptr;
-  db.v = nullptr; db.K = k_hi;
-  db.n_mn = t.b_ones ? t.N - 1 : t.N; db.ones = t.b_ones;
-  db.vec = t.b_kc && ((t.ldb & 3) == 0) && ((reinterpret_cast<unsigned long>(t.B) & 15) == 0) &&
-           ((t.K & 3) == 0);
-  if (da.rank1 && t.a_kc) {  // K-contiguous rank-1 view: row = m (s), col = k (v)
-    da.vec = 0;
+  EpiIn xin[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int e = threadIdx.x + i * 64 * NW;
+    const int r = e >> 6, l = e & 63;
+    xin[i] = epi_prefetch(batch, t, m0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), n0 + (l & 31));
   }
-
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-
-  // k-groups of 8 owned by this wave: g = g_lo + wave, wave + NW, ...
-  const int g_lo = k_lo >> 3;                 // k_lo is a multiple of 8 (kchunk % 8 == 0)
-  const int g_hi = (k_hi + 7) >> 3;
-  const int mrow = m0 + l32;                  // A row of this lane
-  const int ncol = n0 + l32;                  // B column of this lane
-  float a_cur[4], b_cur[4], a_nxt[4], b_nxt[4];
-  int g = g_lo + wave;
-  if (g < g_hi) {
-    fetch4(da, mrow, 8 * g + 4 * half, a_cur);
-    fetch4(db, ncol, 8 * g + 4 * half, b_cur);
-  }
-#pragma unroll 1
-  for (; g < g_hi; g += NW) {
-    const int gn = g + NW;
-    if (gn < g_hi) {
-      fetch4(da, mrow, 8 * gn + 4 * half, a_nxt);
-      fetch4(db, ncol, 8 * gn + 4 * half, b_nxt);
-    }
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a_cur[c], b_cur[c], acc, 0, 0, 0);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) { a_cur[c] = a_nxt[c]; b_cur[c] = b_nxt[c]; }
-  }
+  k_dispatch<NW>(t, m0, n0, k_lo, k_hi, acc);
 
   // fixed-order split-K reduction through LDS
 #pragma unroll
@@ -200,14 +297,29 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
     }
     __syncthreads();
   }
+  AdamConsts ac{};
+  if (batch.fuse_adam)
+    ac = adam_consts(batch.adam.state, batch.adam.advance, batch.adam.lr, batch.adam.beta1,
+                     batch.adam.beta2, batch.adam.eps, batch.adam.target, batch.adam.tau,
+                     batch.adam.period);
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int e = threadIdx.x + i * 64 * NW;
     const int r = e >> 6, l = e & 63;
     const int mt = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
     const int nt = l & 31;
-    epi_one(t, m0 + mt, n0 + nt, vals[i], lds_u, lds_v, mt, nt);
+    epi_one(batch, ac, t, m0 + mt, n0 + nt, vals[i], xin[i], lds_u, lds_v, mt, nt);
+    if (t.epi == EPI_BIAS_RELU_DOT) {
+      // the 32 lanes of a half-wave hold one row's 32 columns: fixed butterfly
+      const int m = m0 + mt, n = n0 + nt;
+      float x = (m < t.M && n < t.N) ? fmaxf(vals[i] + xin[i].xb, 0.f) * xin[i].xa : 0.f;
+#pragma unroll
+      for (int off = 16; off > 0; off >>= 1) x += __shfl_xor(x, off, 32);
+      if (nt == 0 && m < t.M) t.C2[(long)(n0 >> 5) * t.ldc2 + m] = x;   // tile-major
+    }
   }
+  if (batch.fuse_adam && bid == 0 && threadIdx.x == 0)
+    step_bookkeeping(batch.adam.state, batch.adam.alpha, batch.adam.advance);
 }
 
 // tile geometry shared with the plan builder
@@ -220,6 +332,9 @@ int gemm_small_waves(const GemmBatch& b) {
   const int groups = (kmax + 7) / 8;
   int nw = 1;
   while (nw < 16 && nw * 2 <= groups) nw *= 2;   // >= 1 group per wave... up to 16 waves
+  // a 16-wave workgroup holds a whole CU (VGPRs); past 256 tiles the grid
+  // would run in two rounds, so take 8 waves (two workgroups per CU)
+  if (nw == 16 && b.total_tiles > 256) nw = 8;
   return nw;
 }
 
@@ -235,15 +350,27 @@ void gemm_small_finalize(GemmBatch& b) {
   b.total_tiles = tiles;
 }
 
-hipError_t gemm_small_launch(const GemmBatch& b, hipStream_t s) {
-  if (b.total_tiles <= 0) return hipSuccess;
+hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
+  if (b0.total_tiles <= 0) return hipSuccess;
+  GemmBatch b = b0;
   const int nw = gemm_small_waves(b);
+  b.adam_blocks = 0;
+  if (b.fuse_adam) {
+    long n4 = 0;
+    for (int i = 0; i < b.nseg; ++i) {
+      if ((b.seg_n[i] | b.seg_off[i]) & 3) return hipErrorInvalidValue;
+      n4 = std::max(n4, b.seg_n[i] >> 2);
+    }
+    b.adam_blocks = (int)std::min<long>((n4 + 64 * nw - 1) / (64 * nw), 1024);
+    if (b.adam_blocks < 1) b.adam_blocks = 1;
+  }
+  const int grid = b.total_tiles + b.adam_blocks;
   switch (nw) {
-    case 1: hipLaunchKernelGGL(gemm_small_kernel<1>, dim3(b.total_tiles), dim3(64), 0, s, b); break;
-    case 2: hipLaunchKernelGGL(gemm_small_kernel<2>, dim3(b.total_tiles), dim3(128), 0, s, b); break;
-    case 4: hipLaunchKernelGGL(gemm_small_kernel<4>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-    case 8: hipLaunchKernelGGL(gemm_small_kernel<8>, dim3(b.total_tiles), dim3(512), 0, s, b); break;
-    default: hipLaunchKernelGGL(gemm_small_kernel<16>, dim3(b.total_tiles), dim3(1024), 0, s, b); break;
+    case 1: hipLaunchKernelGGL(gemm_small_kernel<1>, dim3(grid), dim3(64), 0, s, b); break;
+    case 2: hipLaunchKernelGGL(gemm_small_kernel<2>, dim3(grid), dim3(128), 0, s, b); break;
+    case 4: hipLaunchKernelGGL(gemm_small_kernel<4>, dim3(grid), dim3(256), 0, s, b); break;
+    case 8: hipLaunchKernelGGL(gemm_small_kernel<8>, dim3(grid), dim3(512), 0, s, b); break;
+    default: hipLaunchKernelGGL(gemm_small_kernel<16>, dim3(grid), dim3(1024), 0, s, b); break;
   }
   return hipGetLastError();
 }

@@ -43,15 +43,38 @@ struct PolicySampleSeg {
   long ld_act_row;
 };
 
+// fused policy head + sample + critics' action columns (head.hip)
+struct HeadSeg {
+  const float* h2;        // [B, H] policy hidden layer 2
+  const float* eps;       // [B, Da]
+  float* head; float* act; float* stdv; float* u; float* logp;   // per-row outputs
+  int n_nets;             // critics fed with this batch's actions (0..2)
+  const float* wa[2];     // W0[:, Do:] of each critic (row n at wa + n*ld_wa)
+  const float* pre[2];    // [B, H] saved obs projection (+ bias) of each critic
+  float* h1[2];           // [B, H] relu(pre + a . wa^T)
+};
+struct HeadArgs {
+  HeadSeg seg[2];
+  const float* wh; const float* bh;   // stacked heads [2*Da, H], [2*Da]
+  long ld_wa;
+  int B, H, Da;
+  int col_chunks;                     // workgroups per 32-row block
+  long long* stage_clock;             // tools/micro builds only (-DOAC_STAGE_CLOCK)
+};
+hipError_t launch_policy_head(const HeadArgs& a, int nseg, hipStream_t s);
+
 struct PolicySampleArgs {
   PolicySampleSeg seg[2];
   int B, act_dim;
 };
 
+enum { QV_Q1 = 0, QV_Q2, QV_QN1, QV_QN2, QV_TQ1, QV_TQ2, QV_COUNT };
 struct CriticTargetArgs {
-  const float* q1; const float* q2;     // Q_i(obs, actions)
-  const float* qn1; const float* qn2;   // Q_i(obs, a~)
-  const float* tq1; const float* tq2;   // target Q_i(next_obs, a')
+  // Q_i(obs, actions), Q_i(obs, a~), target Q_i(next_obs, a')  (QV_* order).
+  // n_part > 0: q[k] is an output, assembled as part_bias[k] + sum_t
+  // part[k][t*B + r] (per-tile partial dots of the last hidden layer)
+  float* q[QV_COUNT];
+  const float* part[QV_COUNT]; const float* part_bias[QV_COUNT]; int n_part;
   const float* logp2;
   const float* batch; long ld_batch; int off_rew, off_term;
   AlphaState* alpha;                    // null -> alpha = 0 (no entropy tuning)
@@ -103,20 +126,6 @@ struct GatherArgs {
   const StepState* state;
 };
 
-struct AdamArgs {
-  float* p; float* g; float* m; float* v; long n;
-  // split-K gradient slabs shaped like the arena range: g = sum_s gslab[s*stride + i]
-  // (written back to g); gslab == g with S == 1 reads g directly
-  const float* gslab; int S; long slab_stride;
-  float* target; float tau; int period;   // target != null -> Polyak after the step
-  double lr, beta1, beta2, eps;
-  StepState* state;
-  int advance;       // 0: critic Adam (t = n_steps; block 0 snapshots t, commits alpha)
-                     // 1: final policy Adam (t = t_snapshot; block 0 advances the step)
-  AlphaState* alpha; // commit next_* (critic Adam only); may be null
-  float gscale;      // gradient scale (1/world_size after an all-reduce SUM)
-  int reduce_only;   // data-parallel: only reduce the slabs into g (all-reduce next)
-};
 
 // ParticleTrainer (share_layers) per-sample kernels, particle_trainer_oac.py
 struct ParticleTargetArgs {

@@ -29,6 +29,9 @@ enum Epi : int {
   EPI_GRAD = 6,           // weight gradient in the parameter-arena layout:
                           // C[m*ldc + n] (n < N-1), bias_grad[m] (n == N-1, the
                           // ones column); both offset by split*slab_stride
+  EPI_BIAS_RELU_DOT = 7,  // C = relu(acc + bias[n]) and, per row, the partial
+                          // dot of this 32-column tile with aux[n] (a width-1
+                          // output layer): C2[(n0/32)*ldc2 + m]  (small kernel)
 };
 
 struct GemmTask {
@@ -59,12 +62,42 @@ struct GemmTask {
   int tiles_n;
 };
 
+struct StepState;
+struct AlphaState;
+
+struct AdamArgs {
+  float* p; float* g; float* m; float* v; long n;
+  // split-K gradient slabs shaped like the arena range: g = sum_s gslab[s*stride + i]
+  // (written back to g); gslab == g with S == 1 reads g directly
+  const float* gslab; int S; long slab_stride;
+  float* target; float tau; int period;   // target != null -> Polyak after the step
+  double lr, beta1, beta2, eps;
+  StepState* state;
+  int advance;       // 0: critic Adam (t = n_steps; block 0 snapshots t, commits alpha)
+                     // 1: final policy Adam (t = t_snapshot; block 0 advances the step)
+  AlphaState* alpha; // commit next_* (critic Adam only); may be null
+  float gscale;      // gradient scale (1/world_size after an all-reduce SUM)
+  int reduce_only;   // data-parallel: only reduce the slabs into g (all-reduce next)
+};
+
 constexpr int kMaxTasks = 8;
 
 struct GemmBatch {
   GemmTask t[kMaxTasks];
   int ntasks;
   int total_tiles;
+  // Fused optimizer (small-batch kernel, unsplit K): every EPI_GRAD element is
+  // also Adam(+Polyak)-updated in the epilogue (its index in the group is its
+  // gradient pointer minus adam.g), and blocks [total_tiles, +adam_blocks) run
+  // the flat Adam over the group's other ranges (gradients finished by earlier
+  // launches of the step).  adam.state / adam.alpha bookkeeping: block 0.
+  int fuse_adam;
+  int nseg;
+  StepState* publish;        // non-null: block 0 publishes the step's Adam constants
+  double pub_beta1, pub_beta2;
+  int adam_blocks;           // set by the launcher
+  long seg_off[2], seg_n[2]; // flat ranges (floats, multiples of 4) from the group base
+  AdamArgs adam;
 };
 
 // ---------------------------------------------------------------------------
@@ -82,7 +115,11 @@ struct StepState {
   long long batch_counter;  // replay ring cursor / Philox counter
   long long expl_counter;   // Philox counter for exploration draws
   long long t_snapshot;     // n_steps as seen by this step (for the last Adam)
-  long long pad[4];
+  // Adam bias corrections for t = bc_t (= n_steps + 1: all three optimisers of
+  // a step share t), published by the step's first launch so no later kernel
+  // evaluates pow() per thread
+  double bc1, bc2, sbc2;    // 1 - beta1^t, 1 - beta2^t, sqrt(bc2)
+  long long bc_t;
 };
 
 // alpha (auto entropy tuning) state, 16 floats.  critic_targets computes the

@@ -37,7 +37,7 @@ static_assert(X_COUNT <= kMaxWs, "workspace ids");
 
 void particle_layout_workspace(SacPlan& p) {
   const oac_sac_config& c = p.c;
-  const int64_t B = c.batch, H = c.hidden, Da = c.act_dim, Do = c.obs_dim, K = c.q_out;
+  const int64_t B = c.batch, H = c.hidden, Da = c.act_dim, K = c.q_out;
   for (int i = 0; i < kMaxWs; ++i) p.ws[i] = {0, 0, 0};
   auto set = [&](int id, int64_t r, int64_t cl) { p.ws[id] = {0, r, cl}; };
   set(OAC_WS_BATCH, B, c.row_stride);
@@ -59,7 +59,7 @@ void particle_layout_workspace(SacPlan& p) {
     p.ws[i].off = off;
     off = al64(off + p.ws[i].rows * p.ws[i].cols);
   }
-  p.L.workspace_floats = off;
+  p.L.workspace_floats = off + 64;   // tail pad: GEMM k-contiguous loads may read 7 floats past a row
 }
 
 // ------------------------------------------------------------------ phases
@@ -87,8 +87,9 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
   const float* q = p.b.params + L.q1_base;
   const float* tq = p.b.targets;
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_fwd(obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(X_H1P), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
+    gb.publish = p.state(); gb.pub_beta1 = c.beta1; gb.pub_beta2 = c.beta2;   // step's Adam constants
     add(gb, t_fwd(nobs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(X_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
     GemmTask t = t_fwd(obs, RS, B, Do, q + L.q_fc0_w, Dq, H, p.W(X_P), H, EPI_BIAS_RANK_RELU, q + L.q_fc0_b);
     t.U = X + c.off_act; t.ldu = RS; t.V = q + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
@@ -98,14 +99,14 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_fwd(p.W(X_H1P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(X_H2P), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
     add(gb, t_fwd(p.W(X_H1P2), H, B, H, pol + L.pol_fc1_w, H, H, p.W(X_H2P2), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
     add(gb, t_fwd(p.W(X_H1Q), H, B, H, q + L.q_fc1_w, H, H, p.W(X_H2Q), H, EPI_BIAS_RELU, q + L.q_fc1_b));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_fwd(p.W(X_H2P), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD1), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
     add(gb, t_fwd(p.W(X_H2P2), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD2), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
     add(gb, t_fwd(p.W(X_H2Q), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_Q1), K, EPI_BIAS, q + L.q_last_b));
@@ -139,7 +140,7 @@ static int pphase1(SacPlan& p, hipStream_t s) {
   const float* q = p.b.params + L.q1_base;
   const float* tq = p.b.targets;
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     GemmTask t = t_fwd(p.W(OAC_WS_ACT2), Da, B, Da, tq + L.q_fc0_w + Do, Dq, H, p.W(X_H1T), H,
                        EPI_ADD_RELU, nullptr);
     t.aux = p.W(X_PT); t.ld_aux = H;
@@ -147,12 +148,12 @@ static int pphase1(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_fwd(p.W(X_H1T), H, B, H, tq + L.q_fc1_w, H, H, p.W(X_H2T), H, EPI_BIAS_RELU, tq + L.q_fc1_b));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_fwd(p.W(X_H2T), H, B, H, tq + L.q_last_w, H, K, p.W(OAC_WS_TQ1), K, EPI_BIAS, tq + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -167,7 +168,7 @@ static int pphase1(SacPlan& p, hipStream_t s) {
     p.launches++;
   }
   {  // last layer: dW_last slab and dh2 = (dq . W_last) * [h2 > 0]
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     float* gq = grad_q(p);
     add(gb, t_dw(p.W(X_DQ), K, K, B, p.W(X_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
                  q_group(p), p.sp_ql));
@@ -175,7 +176,7 @@ static int pphase1(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     float* gq = grad_q(p);
     add(gb, t_dw(p.W(X_DH2Q), H, H, B, p.W(X_H1Q), H, H, gq + L.q_fc1_w, gq + L.q_fc1_b,
                  q_group(p), p.sp_q1));
@@ -183,7 +184,7 @@ static int pphase1(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     float* gq = grad_q(p);
     add(gb, t_dw(p.W(X_DH1Q), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_fc0_w, gq + L.q_fc0_b,
                  q_group(p), p.sp_q0));
@@ -202,7 +203,7 @@ static int pphase2(SacPlan& p, hipStream_t s) {
   const float* pol = p.b.params;
   const float* q = p.b.params + L.q1_base;
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     GemmTask t = t_fwd(X + c.off_obs, RS, B, Do, q + L.q_fc0_w, Dq, H, p.W(X_PN), H,
                        EPI_BIAS_RANK_RELU, q + L.q_fc0_b);
     t.U = p.W(OAC_WS_ACT1); t.ldu = Da; t.V = q + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
@@ -211,12 +212,12 @@ static int pphase2(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_fwd(p.W(X_H1N), H, B, H, q + L.q_fc1_w, H, H, p.W(X_H2N), H, EPI_BIAS_RELU, q + L.q_fc1_b));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_fwd(p.W(X_H2N), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_QN1), K, EPI_BIAS, q + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -231,17 +232,17 @@ static int pphase2(SacPlan& p, hipStream_t s) {
     p.launches++;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_dx(p.W(X_GQ), K, B, K, q + L.q_last_w, H, H, p.W(X_DH2N), H, p.W(X_H2N), H));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_dx(p.W(X_DH2N), H, B, H, q + L.q_fc1_w, H, H, p.W(X_DH1N), H, p.W(X_H1N), H));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_dx(p.W(X_DH1N), H, B, H, q + L.q_fc0_w + Do, Dq, Da, p.W(X_DA), Da, nullptr, 0));
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -255,7 +256,7 @@ static int pphase2(SacPlan& p, hipStream_t s) {
     p.launches++;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(X_DHEAD), 2 * Da, 2 * Da, B, p.W(X_H2P), H, H, gp + L.pol_head_w,
                  gp + L.pol_head_b, L.pol_size, p.sp_ph));
@@ -263,7 +264,7 @@ static int pphase2(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(X_DH2P), H, H, B, p.W(X_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
                  L.pol_size, p.sp_p1));
@@ -271,7 +272,7 @@ static int pphase2(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(X_DH1P), H, H, B, X + c.off_obs, RS, Do, gp + L.pol_fc0_w, gp + L.pol_fc0_b,
                  L.pol_size, p.sp_p0));

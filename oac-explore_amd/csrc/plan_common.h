@@ -24,6 +24,7 @@ struct PlanBase {
   hipGraphExec_t exec = nullptr;
   hipStream_t graph_stream = nullptr;
   int graph_flags = -1;
+  int graph_n = 0;          // steps captured in the graph
   int launches = 0;
   // HIP-event kernel timing (bench instrumentation; never inside a graph)
   bool timing = false;

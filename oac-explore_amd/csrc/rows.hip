@@ -4,6 +4,7 @@
 // per row x action-dim), deterministic fixed-order reductions.
 #include "oac_common.h"
 #include "kernels.h"
+#include "adam_common.h"
 
 namespace oac {
 
@@ -94,13 +95,12 @@ __global__ void __launch_bounds__(256) critic_targets_kernel(CriticTargetArgs p)
       const float n = (float)((long long)p.B * (p.world_size > 1 ? p.world_size : 1));
       const float la_old = as->log_alpha;
       const float g = -(S / n);
-      const double t = (double)(p.state->n_steps + 1);
-      const double bc1 = 1.0 - pow(p.beta1, t);
-      const double bc2 = 1.0 - pow(p.beta2, t);
+      double bc1, sbc2;
+      bias_corrections(p.state, p.state->n_steps + 1, p.beta1, p.beta2, bc1, sbc2);
       const float m = __fadd_rn(__fmul_rn(as->m, (float)p.beta1), __fmul_rn((float)(1.0 - p.beta1), g));
       const float v = __fadd_rn(__fmul_rn(as->v, (float)p.beta2),
                                 __fmul_rn(__fmul_rn((float)(1.0 - p.beta2), g), g));
-      const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), (float)sqrt(bc2)), (float)p.adam_eps);
+      const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), (float)sbc2), (float)p.adam_eps);
       const float la = __fadd_rn(la_old, __fdiv_rn(__fmul_rn(-(float)(p.lr / bc1), m), denom));
       s_alpha = expf(la);
       if (blockIdx.x == 0) {
@@ -111,20 +111,45 @@ __global__ void __launch_bounds__(256) critic_targets_kernel(CriticTargetArgs p)
     __syncthreads();
     alpha = s_alpha;
   }
-  const int r = blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= p.B) return;
+  float qv[QV_COUNT];
+  if (p.n_part > 0) {
+    // all partial loads in flight at once (n_part <= 16), then the fixed-order sums
+    constexpr int kMaxPart = 16;
+    float pv[QV_COUNT][kMaxPart];
+#pragma unroll
+    for (int k = 0; k < QV_COUNT; ++k) {
+      const float* pp = p.part[k] + r;
+#pragma unroll
+      for (int t = 0; t < kMaxPart; ++t)   // unconditional, coalesced over rows
+        pv[k][t] = pp[(long)min(t, p.n_part - 1) * p.B];
+    }
+#pragma unroll
+    for (int k = 0; k < QV_COUNT; ++k) {
+      float s = p.part_bias[k][0];
+#pragma unroll
+      for (int t = 0; t < kMaxPart; ++t)
+        if (t < p.n_part) s += pv[k][t];
+      qv[k] = s;
+      p.q[k][r] = s;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < QV_COUNT; ++k) qv[k] = p.q[k][r];
+  }
   const float rew = p.batch[(long)r * p.ld_batch + p.off_rew];
   const float term = p.batch[(long)r * p.ld_batch + p.off_term];
-  const float tq = fminf(p.tq1[r], p.tq2[r]) - mul_rn(alpha, p.logp2[r]);
+  const float tq = fminf(qv[QV_TQ1], qv[QV_TQ2]) - mul_rn(alpha, p.logp2[r]);
   const float y = add_rn(mul_rn(p.reward_scale, rew), mul_rn(mul_rn(1.f - term, p.discount), tq));
-  const float d1 = p.q1[r] - y, d2 = p.q2[r] - y;
+  const float d1 = qv[QV_Q1] - y, d2 = qv[QV_Q2] - y;
   const float invB = 1.f / (float)p.B;
   p.y[r] = y;
   p.dq1[r] = mul_rn(2.f * d1, invB);
   p.dq2[r] = mul_rn(2.f * d2, invB);
   p.sqe1[r] = d1 * d1;
   p.sqe2[r] = d2 * d2;
-  const float a = p.qn1[r], b = p.qn2[r];
+  const float a = qv[QV_QN1], b = qv[QV_QN2];
   const bool sel1 = a <= b;
   p.qnew[r] = sel1 ? a : b;
   p.gq1[r] = sel1 ? -invB : 0.f;
@@ -237,7 +262,9 @@ hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(critic_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  // 64 rows per block: the per-row work spreads over CUs (every block redoes
+  // the 4-byte-per-row alpha reduction, which is cheap)
+  hipLaunchKernelGGL(critic_targets_kernel, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_policy_head_backward(const PolicyHeadBwdArgs& a, hipStream_t s) {
@@ -324,13 +351,12 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
       const float n = (float)((long long)p.B * (p.world_size > 1 ? p.world_size : 1));
       const float la_old = as->log_alpha;
       const float g = -(S / n);
-      const double t = (double)(p.state->n_steps + 1);
-      const double bc1 = 1.0 - pow(p.beta1, t);
-      const double bc2 = 1.0 - pow(p.beta2, t);
+      double bc1, sbc2;
+      bias_corrections(p.state, p.state->n_steps + 1, p.beta1, p.beta2, bc1, sbc2);
       const float m = __fadd_rn(__fmul_rn(as->m, (float)p.beta1), __fmul_rn((float)(1.0 - p.beta1), g));
       const float v = __fadd_rn(__fmul_rn(as->v, (float)p.beta2),
                                 __fmul_rn(__fmul_rn((float)(1.0 - p.beta2), g), g));
-      const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), (float)sqrt(bc2)), (float)p.adam_eps);
+      const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), (float)sbc2), (float)p.adam_eps);
       const float la = __fadd_rn(la_old, __fdiv_rn(__fmul_rn(-(float)(p.lr / bc1), m), denom));
       as->next_log_alpha = la; as->next_m = m; as->next_v = v;
       as->alpha = expf(la); as->grad = g; as->alpha_loss = -(la_old * S) / n;

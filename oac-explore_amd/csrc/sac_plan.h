@@ -72,6 +72,22 @@ inline AdamArgs policy_adam(SacPlan& p, int reduce_only, AlphaState* commit) {
   return a;
 }
 
+// Fold a group's Adam into the launch that produces its last gradients (the
+// layer-0 weight gradients): possible on the single-process path with the
+// small-batch kernel and no split-K (a data-parallel step all-reduces first).
+inline bool can_fuse_adam(const SacPlan& p) {
+  return p.cfg == 0 && p.S_q == 1 && p.S_p == 1 && p.c.world_size == 1;
+}
+
+// attach `a` to batch `gb`: EPI_GRAD tiles update their own elements, tail
+// blocks the given flat ranges (offsets from the group base a.p)
+inline void fuse_adam(GemmBatch& gb, const AdamArgs& a, int nseg, const long* off, const long* n) {
+  gb.fuse_adam = 1;
+  gb.adam = a;
+  gb.nseg = nseg;
+  for (int i = 0; i < nseg; ++i) { gb.seg_off[i] = off[i]; gb.seg_n[i] = n[i]; }
+}
+
 // particle trainer (particle_plan.hip)
 void particle_layout_workspace(SacPlan& p);
 int particle_run_step(SacPlan& p, int flags, hipStream_t s);

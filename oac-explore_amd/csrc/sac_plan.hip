@@ -65,13 +65,13 @@ enum Ws {
   W_H1N1, W_H1N2, W_H2N1, W_H2N2, W_H1T1, W_H1T2, W_H2T1, W_H2T2,
   W_STD1, W_U1, W_STD2, W_U2, W_DQ1, W_DQ2, W_GQ1, W_GQ2,
   W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DA1, W_DA2, W_DHEAD, W_DH2P, W_DH1P,
-  W_PARTIALS,
+  W_QPART,   // [6][B][tiles]: per-tile partial dots of the width-1 critic heads
   W_COUNT
 };
 
 static void layout_workspace(SacPlan& p) {
   const oac_sac_config& c = p.c;
-  const int64_t B = c.batch, H = c.hidden, Da = c.act_dim, Do = c.obs_dim, Q = c.q_out;
+  const int64_t B = c.batch, H = c.hidden, Da = c.act_dim, Q = c.q_out;
   auto set = [&](int id, int64_t r, int64_t cl) { p.ws[id] = {0, r, cl}; };
   for (int i = 0; i < kMaxWs; ++i) p.ws[i] = {0, 0, 0};
   set(OAC_WS_BATCH, B, c.row_stride);
@@ -86,7 +86,7 @@ static void layout_workspace(SacPlan& p) {
   for (int id : {W_DQ1, W_DQ2, W_GQ1, W_GQ2}) set(id, B, Q);
   for (int id : {W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DH2P, W_DH1P}) set(id, B, H);
   set(W_DHEAD, B, 2 * Da);
-  set(W_PARTIALS, 1, 4096);
+  set(W_QPART, QV_COUNT * B, (H + 31) / 32);
   if (p.S_q > 1) set(WS_GSLAB_Q, p.S_q, p.L.n_critics * p.L.q_size);
   if (p.S_p > 1) set(WS_GSLAB_P, p.S_p, p.L.pol_size);
   int64_t off = 0;
@@ -94,12 +94,28 @@ static void layout_workspace(SacPlan& p) {
     p.ws[i].off = off;
     off = al64(off + p.ws[i].rows * p.ws[i].cols);
   }
-  p.L.workspace_floats = off;
+  p.L.workspace_floats = off + 64;   // tail pad: GEMM k-contiguous loads may read 7 floats past a row
 }
 
 // ----------------------------------------------------------------- phases
 // phase 0: gather, forward of everything that does not need alpha, policy
 //          sample (+ alpha update when world_size == 1)
+// The width-1 critic heads ride on the layer-1 epilogue (EPI_BIAS_RELU_DOT;
+// critic_targets adds the per-tile partials) on the small-batch kernel.
+static bool qdot(const SacPlan& p) {
+  return p.cfg == 0 && p.c.q_out == 1 && (p.c.hidden + 31) / 32 <= 16;
+}
+static GemmTask q_l1(SacPlan& p, const float* in, const float* net, float* out, int qv) {
+  const oac_sac_config& c = p.c;
+  const int B = c.batch, H = c.hidden;
+  GemmTask t = t_fwd(in, H, B, H, net + p.L.q_fc1_w, H, H, out, H, EPI_BIAS_RELU, net + p.L.q_fc1_b);
+  if (qdot(p)) {
+    t.epi = EPI_BIAS_RELU_DOT; t.aux = net + p.L.q_last_w;
+    t.C2 = p.W(W_QPART) + (long)qv * B * p.ws[W_QPART].cols; t.ldc2 = B;   // [tile][row]
+  }
+  return t;
+}
+
 static int phase0(SacPlan& p, int flags, hipStream_t s) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
@@ -127,7 +143,8 @@ static int phase0(SacPlan& p, int flags, hipStream_t s) {
   const float* t1 = p.b.targets;
   const float* t2 = p.b.targets + L.q_size;
   {  // layer 0: policy(obs), policy(next_obs), critic obs-projections
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
+    gb.publish = p.state(); gb.pub_beta1 = c.beta1; gb.pub_beta2 = c.beta2;   // step's Adam constants
     add(gb, t_fwd(obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
     add(gb, t_fwd(nobs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
     const float* qs[2] = {q1, q2};
@@ -145,30 +162,37 @@ static int phase0(SacPlan& p, int flags, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // layer 1
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_fwd(p.W(W_H1P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_H2P), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
     add(gb, t_fwd(p.W(W_H1P2), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_H2P2), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
-    add(gb, t_fwd(p.W(W_H1Q1), H, B, H, q1 + L.q_fc1_w, H, H, p.W(W_H2Q1), H, EPI_BIAS_RELU, q1 + L.q_fc1_b));
-    add(gb, t_fwd(p.W(W_H1Q2), H, B, H, q2 + L.q_fc1_w, H, H, p.W(W_H2Q2), H, EPI_BIAS_RELU, q2 + L.q_fc1_b));
+    add(gb, q_l1(p, p.W(W_H1Q1), q1, p.W(W_H2Q1), QV_Q1));
+    add(gb, q_l1(p, p.W(W_H1Q2), q2, p.W(W_H2Q2), QV_Q2));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {  // heads: policy mean|log_std for obs/next_obs, q1/q2 predictions
-    GemmBatch gb; gb.ntasks = 0;
-    add(gb, t_fwd(p.W(W_H2P), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD1), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
-    add(gb, t_fwd(p.W(W_H2P2), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD2), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
+  if (!qdot(p)) {  // q1/q2 predictions (the small-batch path has them from layer 1)
+    GemmBatch gb{};
     add(gb, t_fwd(p.W(W_H2Q1), H, B, H, q1 + L.q_last_w, H, 1, p.W(OAC_WS_Q1), 1, EPI_BIAS, q1 + L.q_last_b));
     add(gb, t_fwd(p.W(W_H2Q2), H, B, H, q2 + L.q_last_w, H, 1, p.W(OAC_WS_Q2), 1, EPI_BIAS, q2 + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {  // tanh-Gaussian sample + log-prob (+ alpha update)
-    PolicySampleArgs a;
+  {  // policy heads, tanh-Gaussian sample + log-prob, critics' action columns
+    HeadArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.seg[0] = {p.W(OAC_WS_HEAD1), p.W(OAC_WS_EPS1), p.W(OAC_WS_ACT1), p.W(W_STD1), p.W(W_U1),
-                p.W(OAC_WS_LOGP1), nullptr, 0};
-    a.seg[1] = {p.W(OAC_WS_HEAD2), p.W(OAC_WS_EPS2), p.W(OAC_WS_ACT2), p.W(W_STD2), p.W(W_U2),
-                p.W(OAC_WS_LOGP2), nullptr, 0};
-    a.B = B; a.act_dim = Da;
-    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_sample(a, 2, s)));
+    a.wh = pol + L.pol_head_w; a.bh = pol + L.pol_head_b; a.ld_wa = Dq;
+    a.B = B; a.H = H; a.Da = Da; a.col_chunks = H >= 128 ? 2 : 1;
+    HeadSeg& s0 = a.seg[0];   // policy(obs; eps1) -> Q1/Q2(obs, a~)
+    s0.h2 = p.W(W_H2P); s0.eps = p.W(OAC_WS_EPS1); s0.head = p.W(OAC_WS_HEAD1);
+    s0.act = p.W(OAC_WS_ACT1); s0.stdv = p.W(W_STD1); s0.u = p.W(W_U1); s0.logp = p.W(OAC_WS_LOGP1);
+    s0.n_nets = 2;
+    s0.wa[0] = q1 + L.q_fc0_w + Do; s0.pre[0] = p.W(W_P1); s0.h1[0] = p.W(W_H1N1);
+    s0.wa[1] = q2 + L.q_fc0_w + Do; s0.pre[1] = p.W(W_P2); s0.h1[1] = p.W(W_H1N2);
+    HeadSeg& s1 = a.seg[1];   // policy(next_obs; eps2) -> TQ1/TQ2(next_obs, a')
+    s1.h2 = p.W(W_H2P2); s1.eps = p.W(OAC_WS_EPS2); s1.head = p.W(OAC_WS_HEAD2);
+    s1.act = p.W(OAC_WS_ACT2); s1.stdv = p.W(W_STD2); s1.u = p.W(W_U2); s1.logp = p.W(OAC_WS_LOGP2);
+    s1.n_nets = 2;
+    s1.wa[0] = t1 + L.q_fc0_w + Do; s1.pre[0] = p.W(W_PT1); s1.h1[0] = p.W(W_H1T1);
+    s1.wa[1] = t2 + L.q_fc0_w + Do; s1.pre[1] = p.W(W_PT2); s1.h1[1] = p.W(W_H1T2);
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head(a, 2, s)));
     p.launches++;
   }
   if (c.world_size > 1 && c.auto_alpha) {  // local alpha partial for the all-reduce
@@ -179,8 +203,9 @@ static int phase0(SacPlan& p, int flags, hipStream_t s) {
   return 0;
 }
 
-// phase 1: fresh-action critics, TD target, critic gradients (split-K slabs)
-static int phase1(SacPlan& p, hipStream_t s) {
+// phase 1: fresh-action critics, TD target, critic gradients (split-K slabs);
+// fused: the critic Adam + Polyak runs inside the layer-0 gradient launch
+static int phase1(SacPlan& p, hipStream_t s, bool fused) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -190,32 +215,17 @@ static int phase1(SacPlan& p, hipStream_t s) {
   const float* q2 = p.b.params + L.q2_base;
   const float* t1 = p.b.targets;
   const float* t2 = p.b.targets + L.q_size;
-  {  // layer 0 action part: h1 = relu(P + a . W0[:, Do:]^T)
-    GemmBatch gb; gb.ntasks = 0;
-    const float* nets[4] = {q1, q2, t1, t2};
-    const int acts[4] = {OAC_WS_ACT1, OAC_WS_ACT1, OAC_WS_ACT2, OAC_WS_ACT2};
-    const int Ps[4] = {W_P1, W_P2, W_PT1, W_PT2};
-    const int outs[4] = {W_H1N1, W_H1N2, W_H1T1, W_H1T2};
-    for (int i = 0; i < 4; ++i) {
-      GemmTask t = t_fwd(p.W(acts[i]), Da, B, Da, nets[i] + L.q_fc0_w + Do, Dq, H, p.W(outs[i]), H,
-                         EPI_ADD_RELU, nullptr);
-      t.aux = p.W(Ps[i]); t.ld_aux = H;
-      add(gb, t);
-    }
-    if (run_gemm(p, gb, s)) return 1;
-  }
   {  // layer 1
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     const float* nets[4] = {q1, q2, t1, t2};
     const int ins[4] = {W_H1N1, W_H1N2, W_H1T1, W_H1T2};
     const int outs[4] = {W_H2N1, W_H2N2, W_H2T1, W_H2T2};
-    for (int i = 0; i < 4; ++i)
-      add(gb, t_fwd(p.W(ins[i]), H, B, H, nets[i] + L.q_fc1_w, H, H, p.W(outs[i]), H, EPI_BIAS_RELU,
-                    nets[i] + L.q_fc1_b));
+    const int qv[4] = {QV_QN1, QV_QN2, QV_TQ1, QV_TQ2};
+    for (int i = 0; i < 4; ++i) add(gb, q_l1(p, p.W(ins[i]), nets[i], p.W(outs[i]), qv[i]));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {  // last layer
-    GemmBatch gb; gb.ntasks = 0;
+  if (!qdot(p)) {  // last layer
+    GemmBatch gb{};
     const float* nets[4] = {q1, q2, t1, t2};
     const int ins[4] = {W_H2N1, W_H2N2, W_H2T1, W_H2T2};
     const int outs[4] = {OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_TQ2};
@@ -227,8 +237,17 @@ static int phase1(SacPlan& p, hipStream_t s) {
   {  // TD target, MSE gradients, policy seeds
     CriticTargetArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.q1 = p.W(OAC_WS_Q1); a.q2 = p.W(OAC_WS_Q2); a.qn1 = p.W(OAC_WS_QN1); a.qn2 = p.W(OAC_WS_QN2);
-    a.tq1 = p.W(OAC_WS_TQ1); a.tq2 = p.W(OAC_WS_TQ2); a.logp2 = p.W(OAC_WS_LOGP2);
+    const int qid[QV_COUNT] = {OAC_WS_Q1, OAC_WS_Q2, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_TQ2};
+    const float* nets[QV_COUNT] = {q1, q2, q1, q2, t1, t2};
+    for (int k = 0; k < QV_COUNT; ++k) {
+      a.q[k] = p.W(qid[k]);
+      if (qdot(p)) {
+        a.part[k] = p.W(W_QPART) + (long)k * B * p.ws[W_QPART].cols;
+        a.part_bias[k] = nets[k] + L.q_last_b;
+      }
+    }
+    a.n_part = qdot(p) ? (int)p.ws[W_QPART].cols : 0;
+    a.logp2 = p.W(OAC_WS_LOGP2);
     a.batch = X; a.ld_batch = RS; a.off_rew = c.off_rew; a.off_term = c.off_term;
     a.alpha = c.auto_alpha ? p.alpha() : nullptr;
     a.state = p.state(); a.logp1 = p.W(OAC_WS_LOGP1); a.target_entropy = c.target_entropy;
@@ -241,7 +260,7 @@ static int phase1(SacPlan& p, hipStream_t s) {
     p.launches++;
   }
   {  // critic backward, hidden layer 1 + last layer (dW slabs) and dh1
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     const float* qs[2] = {q1, q2};
     const int dq[2] = {W_DQ1, W_DQ2}, h2[2] = {W_H2Q1, W_H2Q2}, h1[2] = {W_H1Q1, W_H1Q2};
     const int dh1[2] = {W_DH1Q1, W_DH1Q2};
@@ -260,12 +279,17 @@ static int phase1(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // critic backward, layer 0 (input = [obs | act] contiguous in the row)
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     float* gq = grad_q(p);
     const long gs = q_group(p);
     add(gb, t_dw(p.W(W_DH1Q1), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_fc0_w, gq + L.q_fc0_b, gs, p.sp_q0));
     add(gb, t_dw(p.W(W_DH1Q2), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_size + L.q_fc0_w,
                  gq + L.q_size + L.q_fc0_b, gs, p.sp_q0));
+    if (fused) {  // SAC commits the alpha update in the critic Adam
+      const long off[2] = {(long)L.q_fc1_w, (long)(L.q_size + L.q_fc1_w)};
+      const long n[2] = {(long)(L.q_size - L.q_fc1_w), (long)(L.q_size - L.q_fc1_w)};
+      fuse_adam(gb, critic_adam(p, 0, c.auto_alpha ? p.alpha() : nullptr), 2, off, n);
+    }
     if (run_gemm(p, gb, s)) return 1;
   }
   return 0;
@@ -280,7 +304,7 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
   return 0;
 }
 
-static int phase2(SacPlan& p, hipStream_t s) {
+static int phase2(SacPlan& p, hipStream_t s, bool fused) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -290,7 +314,7 @@ static int phase2(SacPlan& p, hipStream_t s) {
   const float* q1 = p.b.params + L.q1_base;
   const float* q2 = p.b.params + L.q2_base;
   {  // -min Q backward to layer 1 with post-step weights, pre-step masks
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     const float* qs[2] = {q1, q2};
     const int gq[2] = {W_GQ1, W_GQ2}, h2[2] = {W_H2N1, W_H2N2}, h1[2] = {W_H1N1, W_H1N2};
     const int out[2] = {W_DH1N1, W_DH1N2};
@@ -302,7 +326,7 @@ static int phase2(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // to the action columns of layer 0
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     add(gb, t_dx(p.W(W_DH1N1), H, B, H, q1 + L.q_fc0_w + Do, Dq, Da, p.W(W_DA1), Da, nullptr, 0));
     add(gb, t_dx(p.W(W_DH1N2), H, B, H, q2 + L.q_fc0_w + Do, Dq, Da, p.W(W_DA2), Da, nullptr, 0));
     if (run_gemm(p, gb, s)) return 1;
@@ -317,7 +341,7 @@ static int phase2(SacPlan& p, hipStream_t s) {
     p.launches++;
   }
   {  // policy heads: dW_head slab, dh2
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, gp + L.pol_head_w,
                  gp + L.pol_head_b, L.pol_size, p.sp_ph));
@@ -325,7 +349,7 @@ static int phase2(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 1
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
                  L.pol_size, p.sp_p1));
@@ -333,10 +357,15 @@ static int phase2(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 0
-    GemmBatch gb; gb.ntasks = 0;
+    GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(W_DH1P), H, H, B, X + c.off_obs, RS, Do, gp + L.pol_fc0_w, gp + L.pol_fc0_b,
                  L.pol_size, p.sp_p0));
+    if (fused) {
+      const long off[1] = {(long)L.pol_fc1_w};
+      const long n[1] = {(long)(L.pol_size - L.pol_fc1_w)};
+      fuse_adam(gb, policy_adam(p, 0, nullptr), 1, off, n);
+    }
     if (run_gemm(p, gb, s)) return 1;
   }
   return 0;
@@ -344,13 +373,16 @@ static int phase2(SacPlan& p, hipStream_t s) {
 
 static int run_step(SacPlan& p, int flags, hipStream_t s) {
   p.launches = 0;
+  const bool fused = can_fuse_adam(p);
   if (phase0(p, flags, s)) return 1;
-  if (phase1(p, s)) return 1;
-  if (phase2_adam(p, s, 0)) return 1;
-  if (phase2(p, s)) return 1;
-  AdamArgs a = policy_adam(p, 0, nullptr);
-  TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
-  p.launches++;
+  if (phase1(p, s, fused)) return 1;
+  if (!fused && phase2_adam(p, s, 0)) return 1;
+  if (phase2(p, s, fused)) return 1;
+  if (!fused) {
+    AdamArgs a = policy_adam(p, 0, nullptr);
+    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
+    p.launches++;
+  }
   return 0;
 }
 
@@ -444,21 +476,28 @@ int oac_sac_destroy(oac_sac* h) {
   return 0;
 }
 
-int oac_sac_step(oac_sac* h, int flags, void* stream) {
+int oac_sac_step_n(oac_sac* h, int flags, int n_steps, void* stream) {
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
   if (p.c.world_size > 1) { set_error("world_size > 1: drive the step with oac_sac_step_phase"); return 1; }
+  if (n_steps < 1 || n_steps > 1024) { set_error("n_steps %d out of range", n_steps); return 1; }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  auto step = [&](int f) {
-    return p.c.kind == OAC_KIND_PARTICLE ? particle_run_step(p, f, s) : run_step(p, f, s);
+  auto steps = [&](int f) {
+    for (int i = 0; i < n_steps; ++i) {
+      const int rc = p.c.kind == OAC_KIND_PARTICLE ? particle_run_step(p, f, s) : run_step(p, f, s);
+      if (rc) return rc;
+    }
+    return 0;
   };
-  if (!(flags & OAC_STEP_USE_GRAPH) || p.timing) return step(flags);
+  if (!(flags & OAC_STEP_USE_GRAPH) || p.timing) return steps(flags);
   const int gflags = flags & ~OAC_STEP_USE_GRAPH;
-  if (!p.exec || p.graph_stream != s || p.graph_flags != gflags) {
+  if (!p.exec || p.graph_stream != s || p.graph_flags != gflags || p.graph_n != n_steps) {
     if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
     if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
+    // the step sequence is static (counters live on the device), so n
+    // consecutive steps capture into one graph
     OAC_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    const int rc = step(gflags);
+    const int rc = steps(gflags);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s, &g);
     if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
@@ -467,10 +506,13 @@ int oac_sac_step(oac_sac* h, int flags, void* stream) {
     OAC_HIP_CHECK(hipGraphInstantiate(&p.exec, p.graph, nullptr, nullptr, 0));
     p.graph_stream = s;
     p.graph_flags = gflags;
+    p.graph_n = n_steps;
   }
   OAC_HIP_CHECK(hipGraphLaunch(p.exec, s));
   return 0;
 }
+
+int oac_sac_step(oac_sac* h, int flags, void* stream) { return oac_sac_step_n(h, flags, 1, stream); }
 
 int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
   if (!h) { set_error("null handle"); return 1; }
@@ -480,7 +522,7 @@ int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
   switch (phase) {
     case 0: return phase0(p, flags, s);
     case 1:
-      if (phase1(p, s)) return 1;
+      if (phase1(p, s, false)) return 1;
       if (p.S_q > 1) {
         AdamArgs a = critic_adam(p, 1, nullptr);
         OAC_HIP_CHECK(launch_adam(a, s));
@@ -488,7 +530,7 @@ int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
       return 0;
     case 2:
       if (phase2_adam(p, s, 1)) return 1;
-      if (phase2(p, s)) return 1;
+      if (phase2(p, s, false)) return 1;
       if (p.S_p > 1) {
         AdamArgs a = policy_adam(p, 1, nullptr);
         OAC_HIP_CHECK(launch_adam(a, s));

@@ -66,6 +66,8 @@ _SIGS = {
                                       ctypes.POINTER(ctypes.c_void_p)]),
     "oac_sac_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "oac_sac_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "oac_sac_step_n": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                      ctypes.c_void_p]),
     "oac_sac_step_phase": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_void_p]),
     "oac_sac_workspace_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,

@@ -228,8 +228,11 @@ class DeviceIndexStream:
         view = self.ring[half * self.chunk * self.B:(half + 1) * self.chunk * self.B]
         self.buf.sample_indices_device(self.chunk * self.B, out=view)
 
-    def before_step(self):
-        """Call before each ring step: refill the half that was just consumed."""
+    def before_step(self, n_steps=1):
+        """Call before each ring step (or block of n_steps consecutive steps,
+        n_steps dividing the chunk): refill the half that was just consumed."""
+        if self.chunk % n_steps or self.t % n_steps:
+            raise ValueError("n_steps must divide the ring chunk and the step count")
         if self.t > 0 and self.t % self.chunk == 0:
             self._fill(((self.t // self.chunk) + 1) % 2)
-        self.t += 1
+        self.t += n_steps

@@ -226,7 +226,7 @@ class _ArenaTrainer(object):
         put(r["off_term"], 1, batch["terminals"])
         put(r["off_next_obs"], Do, batch["next_observations"])
 
-    def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None):
+    def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None, n_steps=1):
         def go(sp):
             f = flags
             if batch is not None:
@@ -240,13 +240,16 @@ class _ArenaTrainer(object):
                 f |= _lib.OAC_STEP_DEVICE_EPS
             if self.use_graph:
                 f |= _lib.OAC_STEP_USE_GRAPH
-            check(_lib.lib().oac_sac_step(plan.handle, f, sp))
+            if n_steps == 1:
+                check(_lib.lib().oac_sac_step(plan.handle, f, sp))
+            else:
+                check(_lib.lib().oac_sac_step_n(plan.handle, f, n_steps, sp))
         self._on_stream(go)
         self._last_plan = plan
         if self._need_to_update_eval_statistics:
             self._need_to_update_eval_statistics = False
             self._fill_eval_statistics(plan)
-        self._n_train_steps_total += 1
+        self._n_train_steps_total += n_steps
 
     def train(self, np_batch):
         """trainer.py:99-103.  Accepts the reference's numpy batch dict, or the
@@ -274,11 +277,15 @@ class _ArenaTrainer(object):
         plan = self._plan(B, replay=dbatch.storage, idx=self._idx)
         self._run(plan, _lib.OAC_STEP_GATHER, eps1, eps2, idx=dbatch.indices)
 
-    def train_from_ring(self, storage, ring, ring_slots, B):
+    def train_from_ring(self, storage, ring, ring_slots, B, n_steps=1):
         """Fast path for a device-resident replay with a device index ring
-        (indices drawn by the device MT19937 stream, see ReplayBuffer)."""
+        (indices drawn by the device MT19937 stream, see ReplayBuffer):
+        n_steps consecutive gradient steps, each on its own minibatch --
+        rl_algorithm.py's inner loop of num_trains_per_train_loop train()
+        calls -- in one graph launch.  Diagnostics (on the first step after
+        end_epoch in the reference) come from the last step of the call."""
         plan = self._plan(B, replay=storage, idx=ring, ring_slots=ring_slots)
-        self._run(plan, _lib.OAC_STEP_GATHER)
+        self._run(plan, _lib.OAC_STEP_GATHER, n_steps=n_steps)
 
 class SACTrainer(_ArenaTrainer):
     """SACTrainer (trainer/trainer.py:14) on liboac_amd."""
