@@ -16,6 +16,7 @@
 #include "oac_common.h"
 #include "kernels.h"
 #include "adam_common.h"
+#include "policy_math.h"
 
 #include <algorithm>
 
@@ -147,14 +148,21 @@ __device__ __forceinline__ void k_dispatch(const GemmTask& t, int m0, int n0, in
 // latency hides behind it: xb = bias[n] (or the fused-Adam p), xa = aux[m,n]
 // (EPI_ADD_RELU / EPI_MASK), aux[n] (EPI_BIAS_RELU_DOT).
 // EPI_GRAD with the fused optimizer: p, m, v (and the Polyak target) of the element.
-struct EpiIn { float xb, xa, am, av, at; };
+struct EpiIn { float xb, xa, am, av, at, s; };
 
 __device__ __forceinline__ EpiIn epi_prefetch(const GemmBatch& batch, const GemmTask& t, int m,
                                               int n) {
-  EpiIn x{0.f, 0.f, 0.f, 0.f, 0.f};
+  EpiIn x{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const bool in = m < t.M && n < t.N;
   const int mc = in ? m : 0, nc = in ? n : 0;
   switch (t.epi) {
+    case EPI_HEAD_BWD: {   // act, std, u, eps [B, Da]; ls_raw from the head; alpha
+      const long e = (long)mc * t.N + nc;
+      x.xb = t.ex[0][e]; x.xa = t.ex[1][e]; x.am = t.ex[2][e]; x.av = t.ex[3][e];
+      x.at = t.ex[4][(long)mc * 2 * t.N + t.N + nc];
+      x.s = t.ex[5] ? t.ex[5][0] : 0.f;
+      break;
+    }
     case EPI_GRAD:
       if (batch.fuse_adam) {
         const float* g = (t.b_ones && nc == t.N - 1) ? t.bias_grad + mc : t.C + (long)mc * t.ldc + nc;
@@ -209,6 +217,13 @@ __device__ __forceinline__ void epi_one(const GemmBatch& batch, const AdamConsts
     }
     case EPI_ADD_RELU: t.C[o] = fmaxf(acc + x.xa, 0.f); break;
     case EPI_MASK: t.C[o] = x.xa > 0.f ? acc : 0.f; break;
+    case EPI_HEAD_BWD: {
+      float dmean, dls;
+      tanh_gauss_backward(acc, x.xb, x.xa, x.am, x.av, x.at, x.s * (1.f / (float)t.M), dmean, dls);
+      t.C[o] = dmean;
+      t.C[o + t.N] = dls;
+      break;
+    }
     default: break;
   }
 }
@@ -270,6 +285,11 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   k_dispatch<NW>(t, m0, n0, k_lo, k_hi, acc);
+  if (t.K2 > 0) {   // second product into the same accumulator (unsplit dX tasks only)
+    GemmTask t2 = t;
+    t2.A = t.A2; t2.B = t.B2; t2.K = t.K2;
+    k_loop<NW, OP_KC, OP_MN>(t2, m0, n0, 0, t.K2, acc);
+  }
 
   // fixed-order split-K reduction through LDS
 #pragma unroll
@@ -326,7 +346,7 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
 int gemm_small_waves(const GemmBatch& b) {
   int kmax = 1;
   for (int i = 0; i < b.ntasks; ++i) {
-    const int k = b.t[i].ksplit > 1 ? b.t[i].kchunk : b.t[i].K;
+    const int k = b.t[i].ksplit > 1 ? b.t[i].kchunk : std::max(b.t[i].K, b.t[i].K2);
     kmax = k > kmax ? k : kmax;
   }
   const int groups = (kmax + 7) / 8;
@@ -353,6 +373,10 @@ void gemm_small_finalize(GemmBatch& b) {
 hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   if (b0.total_tiles <= 0) return hipSuccess;
   GemmBatch b = b0;
+  for (int i = 0; i < b.ntasks; ++i)   // second products: plain unsplit dX tasks
+    if (b.t[i].K2 > 0 && (b.t[i].ksplit > 1 || !b.t[i].a_kc || b.t[i].b_kc ||
+                          b.t[i].a_mode != A_PLAIN))
+      return hipErrorInvalidValue;
   const int nw = gemm_small_waves(b);
   b.adam_blocks = 0;
   if (b.fuse_adam) {

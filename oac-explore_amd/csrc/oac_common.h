@@ -29,6 +29,9 @@ enum Epi : int {
   EPI_GRAD = 6,           // weight gradient in the parameter-arena layout:
                           // C[m*ldc + n] (n < N-1), bias_grad[m] (n == N-1, the
                           // ones column); both offset by split*slab_stride
+  EPI_HEAD_BWD = 8,       // acc = dL/da (N = act_dim): tanh-Gaussian head backward
+                          // (policy_math.h) -> C[m*ldc + n] = dmean, C[m*ldc + N + n]
+                          // = dls_raw; ex[] = act, std, u, eps, head, &alpha (small kernel)
   EPI_BIAS_RELU_DOT = 7,  // C = relu(acc + bias[n]) and, per row, the partial
                           // dot of this 32-column tile with aux[n] (a width-1
                           // output layer): C2[(n0/32)*ldc2 + m]  (small kernel)
@@ -60,6 +63,12 @@ struct GemmTask {
   long slab_stride;
   int tile_begin;
   int tiles_n;
+  // optional second product accumulated into the same tile (same layouts and
+  // leading dimensions, K2 > 0, unsplit): acc = A.B + A2.B2
+  const float* A2;
+  const float* B2;
+  int K2;
+  const float* ex[6];   // extra epilogue operands (EPI_HEAD_BWD)
 };
 
 struct StepState;

@@ -5,6 +5,7 @@
 #include "oac_common.h"
 #include "kernels.h"
 #include "adam_common.h"
+#include "policy_math.h"
 
 namespace oac {
 
@@ -29,16 +30,8 @@ __global__ void __launch_bounds__(256) policy_sample_kernel(PolicySampleArgs p) 
   if (r < p.B && j < Da) {
     const long e = (long)r * Da + j;
     const float* hd = s.head + (long)r * (2 * Da);
-    const float mean = hd[j];
-    const float ls = fminf(fmaxf(hd[Da + j], -20.f), 2.f);
-    const float sd = expf(ls);
-    const float z = add_rn(mean, mul_rn(sd, s.eps[e]));
-    const float a = tanhf(z);
-    const float u = z - mean;
-    const float var = mul_rn(sd, sd);
-    const float t1 = -(mul_rn(u, u)) / (2.f * var);
-    l = t1 - logf(sd) - 0.918938533204672742f  // log(sqrt(2*pi))
-        - logf(add_rn(1.f - mul_rn(a, a), 1e-6f));
+    float a, sd, u;
+    l = tanh_gauss_sample(hd[j], hd[Da + j], s.eps[e], a, sd, u);
     s.act[e] = a;
     s.stdv[e] = sd;
     s.u[e] = u;
@@ -82,6 +75,31 @@ __global__ void __launch_bounds__(256) logp_sum_kernel(LogpSumArgs a) {
 __global__ void __launch_bounds__(256) critic_targets_kernel(CriticTargetArgs p) {
   __shared__ float red[256];
   __shared__ float s_alpha;
+  // this row's inputs first (clamped row, all loads in flight together), so
+  // their latency overlaps the alpha reduction below
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int rc = min(r, p.B - 1);
+  constexpr int kMaxPart = 16;                 // n_part <= 16
+  float pv[QV_COUNT][kMaxPart];
+  if (p.n_part > 0) {
+#pragma unroll
+    for (int k = 0; k < QV_COUNT; ++k) {
+      const float* pp = p.part[k] + rc;
+#pragma unroll
+      for (int t = 0; t < kMaxPart; ++t)   // unconditional, coalesced over rows
+        pv[k][t] = pp[(long)min(t, p.n_part - 1) * p.B];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < QV_COUNT; ++k) pv[k][0] = p.q[k][rc];
+  }
+  float pb[QV_COUNT];
+#pragma unroll
+  for (int k = 0; k < QV_COUNT; ++k) pb[k] = p.n_part > 0 ? p.part_bias[k][0] : 0.f;
+  const float rew = p.batch[(long)rc * p.ld_batch + p.off_rew];
+  const float term = p.batch[(long)rc * p.ld_batch + p.off_term];
+  const float logp2 = p.logp2[rc];
+
   float alpha = 0.f;
   if (p.alpha) {
     // alpha update (trainer.py:139-146): L = -mean(log_alpha * (logp + H)),
@@ -111,36 +129,22 @@ __global__ void __launch_bounds__(256) critic_targets_kernel(CriticTargetArgs p)
     __syncthreads();
     alpha = s_alpha;
   }
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= p.B) return;
   float qv[QV_COUNT];
-  if (p.n_part > 0) {
-    // all partial loads in flight at once (n_part <= 16), then the fixed-order sums
-    constexpr int kMaxPart = 16;
-    float pv[QV_COUNT][kMaxPart];
 #pragma unroll
-    for (int k = 0; k < QV_COUNT; ++k) {
-      const float* pp = p.part[k] + r;
-#pragma unroll
-      for (int t = 0; t < kMaxPart; ++t)   // unconditional, coalesced over rows
-        pv[k][t] = pp[(long)min(t, p.n_part - 1) * p.B];
-    }
-#pragma unroll
-    for (int k = 0; k < QV_COUNT; ++k) {
-      float s = p.part_bias[k][0];
+  for (int k = 0; k < QV_COUNT; ++k) {
+    if (p.n_part > 0) {   // fixed-order sum of the per-tile partials
+      float s = pb[k];
 #pragma unroll
       for (int t = 0; t < kMaxPart; ++t)
         if (t < p.n_part) s += pv[k][t];
       qv[k] = s;
       p.q[k][r] = s;
+    } else {
+      qv[k] = pv[k][0];
     }
-  } else {
-#pragma unroll
-    for (int k = 0; k < QV_COUNT; ++k) qv[k] = p.q[k][r];
   }
-  const float rew = p.batch[(long)r * p.ld_batch + p.off_rew];
-  const float term = p.batch[(long)r * p.ld_batch + p.off_term];
-  const float tq = fminf(qv[QV_TQ1], qv[QV_TQ2]) - mul_rn(alpha, p.logp2[r]);
+  const float tq = fminf(qv[QV_TQ1], qv[QV_TQ2]) - mul_rn(alpha, logp2);
   const float y = add_rn(mul_rn(p.reward_scale, rew), mul_rn(mul_rn(1.f - term, p.discount), tq));
   const float d1 = qv[QV_Q1] - y, d2 = qv[QV_Q2] - y;
   const float invB = 1.f / (float)p.B;
@@ -172,16 +176,9 @@ __global__ void __launch_bounds__(256) policy_head_backward_kernel(PolicyHeadBwd
   const long e = (long)r * Da + j;
   float ga = p.da1[e];
   if (p.da2) ga += p.da2[e];
-  const float a = p.act[e], sd = p.stdv[e], u = p.u[e], eps = p.eps[e];
-  const float var = sd * sd;
-  const float one_m_a2 = 1.f - a * a;
-  const float da = ga + G * (2.f * a / (one_m_a2 + 1e-6f));
-  const float uv = u / var;
-  const float dz = da * one_m_a2 - G * uv;
-  const float dmean = dz + G * uv;
-  const float dstd = dz * eps + G * (u * u * sd / (var * var) - 1.f / sd);
-  const float ls_raw = p.head[(long)r * 2 * Da + Da + j];
-  const float dls = (ls_raw >= -20.f && ls_raw <= 2.f) ? dstd * sd : 0.f;
+  float dmean, dls;
+  tanh_gauss_backward(ga, p.act[e], p.stdv[e], p.u[e], p.eps[e], p.head[(long)r * 2 * Da + Da + j], G,
+                      dmean, dls);
   p.dhead[(long)r * 2 * Da + j] = dmean;
   p.dhead[(long)r * 2 * Da + Da + j] = dls;
 }

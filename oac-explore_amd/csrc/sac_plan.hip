@@ -179,7 +179,7 @@ static int phase0(SacPlan& p, int flags, hipStream_t s) {
     HeadArgs a;
     std::memset(&a, 0, sizeof(a));
     a.wh = pol + L.pol_head_w; a.bh = pol + L.pol_head_b; a.ld_wa = Dq;
-    a.B = B; a.H = H; a.Da = Da; a.col_chunks = H >= 128 ? 2 : 1;
+    a.B = B; a.H = H; a.Da = Da; a.col_chunks = std::max(1, (H + 63) / 64);   // 64 columns each
     HeadSeg& s0 = a.seg[0];   // policy(obs; eps1) -> Q1/Q2(obs, a~)
     s0.h2 = p.W(W_H2P); s0.eps = p.W(OAC_WS_EPS1); s0.head = p.W(OAC_WS_HEAD1);
     s0.act = p.W(OAC_WS_ACT1); s0.stdv = p.W(W_STD1); s0.u = p.W(W_U1); s0.logp = p.W(OAC_WS_LOGP1);
@@ -325,20 +325,33 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused) {
     }
     if (run_gemm(p, gb, s)) return 1;
   }
-  {  // to the action columns of layer 0
+  if (p.cfg == 0) {  // dL/da through both critics' action columns + head backward, one launch
     GemmBatch gb{};
-    add(gb, t_dx(p.W(W_DH1N1), H, B, H, q1 + L.q_fc0_w + Do, Dq, Da, p.W(W_DA1), Da, nullptr, 0));
-    add(gb, t_dx(p.W(W_DH1N2), H, B, H, q2 + L.q_fc0_w + Do, Dq, Da, p.W(W_DA2), Da, nullptr, 0));
+    GemmTask t = t_dx(p.W(W_DH1N1), H, B, H, q1 + L.q_fc0_w + Do, Dq, Da, p.W(W_DHEAD), 2 * Da,
+                      nullptr, 0);
+    t.A2 = p.W(W_DH1N2); t.B2 = q2 + L.q_fc0_w + Do; t.K2 = H;   // same leading dims
+    t.epi = EPI_HEAD_BWD;
+    t.ex[0] = p.W(OAC_WS_ACT1); t.ex[1] = p.W(W_STD1); t.ex[2] = p.W(W_U1);
+    t.ex[3] = p.W(OAC_WS_EPS1); t.ex[4] = p.W(OAC_WS_HEAD1);
+    t.ex[5] = c.auto_alpha ? &p.alpha()->alpha : nullptr;
+    add(gb, t);
     if (run_gemm(p, gb, s)) return 1;
-  }
-  {
-    PolicyHeadBwdArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.da1 = p.W(W_DA1); a.da2 = p.W(W_DA2); a.act = p.W(OAC_WS_ACT1); a.stdv = p.W(W_STD1);
-    a.u = p.W(W_U1); a.eps = p.W(OAC_WS_EPS1); a.head = p.W(OAC_WS_HEAD1);
-    a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.B = B; a.act_dim = Da; a.dhead = p.W(W_DHEAD);
-    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head_backward(a, s)));
-    p.launches++;
+  } else {
+    {  // to the action columns of layer 0
+      GemmBatch gb{};
+      add(gb, t_dx(p.W(W_DH1N1), H, B, H, q1 + L.q_fc0_w + Do, Dq, Da, p.W(W_DA1), Da, nullptr, 0));
+      add(gb, t_dx(p.W(W_DH1N2), H, B, H, q2 + L.q_fc0_w + Do, Dq, Da, p.W(W_DA2), Da, nullptr, 0));
+      if (run_gemm(p, gb, s)) return 1;
+    }
+    {
+      PolicyHeadBwdArgs a;
+      std::memset(&a, 0, sizeof(a));
+      a.da1 = p.W(W_DA1); a.da2 = p.W(W_DA2); a.act = p.W(OAC_WS_ACT1); a.stdv = p.W(W_STD1);
+      a.u = p.W(W_U1); a.eps = p.W(OAC_WS_EPS1); a.head = p.W(OAC_WS_HEAD1);
+      a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.B = B; a.act_dim = Da; a.dhead = p.W(W_DHEAD);
+      TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head_backward(a, s)));
+      p.launches++;
+    }
   }
   {  // policy heads: dW_head slab, dh2
     GemmBatch gb{};

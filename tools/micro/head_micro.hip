@@ -23,7 +23,7 @@ static float* dev_rand(size_t n, float scale) {
 
 int main(int argc, char** argv) {
   const int B = argc > 1 ? atoi(argv[1]) : 256, H = 256, Da = 17, Do = 376, Dq = Do + Da;
-  const int cc = argc > 2 ? atoi(argv[2]) : 2;
+  const int cc = argc > 2 ? atoi(argv[2]) : 4;
   HeadArgs a{};
   a.wh = dev_rand(2 * Da * H, 0.1f); a.bh = dev_rand(2 * Da, 0.1f); a.ld_wa = Dq;
   a.B = B; a.H = H; a.Da = Da; a.col_chunks = cc;
@@ -38,7 +38,7 @@ int main(int argc, char** argv) {
       g.h1[i] = dev_rand((size_t)B * H, 0);
     }
   }
-  const int nblk = ((B + 31) / 32) * cc * 2;
+  const int nblk = ((B + 15) / 16) * cc * 2;
   CK(hipMalloc(&a.stage_clock, nblk * 8 * sizeof(long long)));
   hipStream_t st; CK(hipStreamCreate(&st));
   for (int i = 0; i < 20; ++i) CK(launch_policy_head(a, 2, st));
@@ -60,6 +60,11 @@ int main(int argc, char** argv) {
     tend = std::max(tend, clk[b * 8 + 4]);
     for (int i = 1; i < 5; ++i) st_sum[i] += (clk[b * 8 + i] - clk[b * 8 + i - 1]) * us_per_tick;
   }
+  double pf = 0;
+  for (int b = 0; b < nblk; ++b) pf += (clk[b * 8 + 5] - clk[b * 8]) * us_per_tick;
+  double hl = 0;
+  for (int b = 0; b < nblk; ++b) hl += (clk[b * 8 + 6] - clk[b * 8 + 5]) * us_per_tick;
+  printf("prefetch-drain %.2f us (from start), head-operand loads %.2f us after that\n", pf / nblk, hl / nblk);
   printf("stage means (us): heads %.2f  reduce %.2f  sample %.2f  critic-cols %.2f ; first start -> last end %.2f us\n",
          st_sum[1] / nblk, st_sum[2] / nblk, st_sum[3] / nblk, st_sum[4] / nblk, (tend - t0) * us_per_tick);
   return 0;
