@@ -110,6 +110,8 @@ def kernel_timing(tr, rb, stream, B, n):
     """HIP-event timing of every kernel of n steps (direct launches)."""
     from oac_amd import _lib
     step = step_fn(tr, rb, stream, B)
+    if hasattr(tr, "capture"):
+        tr.capture = False   # data-parallel: eager phases while the per-kernel events record
     step()  # build the plan
     plan = tr._last_plan
     L = _lib.lib()
@@ -188,8 +190,9 @@ def main():
     torch.cuda.set_device(device)
     B = args.batch
     tr, rb, stream = build(args, rank, world, device)
-    # data-parallel steps exchange gradients from the host between phases: one step per call
-    n = max(1, args.steps_per_launch) if world == 1 else 1
+    # n steps per graph replay (data-parallel: the phases and RCCL all-reduces
+    # of n steps captured together, oac_amd/dp.py)
+    n = max(1, args.steps_per_launch)
     if args.steps % n or args.warmup % n or stream.chunk % n:
         raise SystemExit("--steps / --warmup must be multiples of --steps-per-launch (which divides 64)")
     step = step_fn(tr, rb, stream, B, n)

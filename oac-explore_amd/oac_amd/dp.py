@@ -46,8 +46,8 @@ def dp_step(ex, all_reduce):
 
 
 class _GpuExecutor:
-    def __init__(self, trainer, plan, flags):
-        self.t, self.plan, self.flags = trainer, plan, flags
+    def __init__(self, trainer, plan, flags, stream):
+        self.t, self.plan, self.flags, self.stream = trainer, plan, flags, stream
         self.auto_alpha = trainer.use_automatic_entropy_tuning
         lay = trainer.layout
         self._crit = trainer.grads[lay.q1_base:lay.q1_base + lay.n_critics * lay.q_size]
@@ -55,7 +55,7 @@ class _GpuExecutor:
 
     def phase(self, i):
         check(_lib.lib().oac_sac_step_phase(self.plan.handle, i, self.flags if i == 0 else 0,
-                                            _lib.stream_ptr(self.t.stream)))
+                                            _lib.stream_ptr(self.stream)))
 
     def alpha_sum(self):
         return self.t.alpha_state[6:7]
@@ -70,13 +70,21 @@ class _GpuExecutor:
 class _DataParallel:
     """Mixin: the trainer's step sharded over the ranks of a process group
     (NCCL backend = RCCL on ROCm).  Every rank builds the trainer the same way;
-    rank 0's initial state is broadcast."""
+    rank 0's initial state is broadcast.
 
-    def __init__(self, *args, process_group=None, **kwargs):
+    With RCCL, the ring fast path (``train_from_ring``) captures whole steps --
+    the four phase launch sequences AND the three all-reduces -- into one
+    hipGraph per (plan, n_steps) after one eager call, so a step costs one
+    graph replay instead of ~20 host-issued launches and collectives
+    (``capture=False`` keeps every step eager)."""
+
+    def __init__(self, *args, process_group=None, capture=None, **kwargs):
         if not dist.is_initialized():
             raise RuntimeError("DataParallelSACTrainer needs torch.distributed initialised")
         self.pg = process_group
         self.world = dist.get_world_size(process_group)
+        self.capture = (dist.get_backend(process_group) == "nccl") if capture is None else capture
+        self._graphs, self._eager_seen = {}, set()
         super().__init__(*args, **kwargs)
         # make sure every rank starts from rank 0's state
         with torch.no_grad():
@@ -88,10 +96,15 @@ class _DataParallel:
         c.world_size = self.world
         return c
 
-    def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None):
-        def all_reduce(t):
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+    def _all_reduce(self, t):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
 
+    def _steps(self, plan, f, n_steps, stream):
+        ex = _GpuExecutor(self, plan, f, stream)
+        for _ in range(n_steps):
+            dp_step(ex, self._all_reduce)
+
+    def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None, n_steps=1):
         def go(sp):
             f = flags
             if batch is not None:
@@ -103,13 +116,27 @@ class _DataParallel:
                 plan.views["eps2"].copy_(torch.as_tensor(eps2).reshape(plan.views["eps2"].shape))
             else:
                 f |= _lib.OAC_STEP_DEVICE_EPS
-            dp_step(_GpuExecutor(self, plan, f), all_reduce)
+            static = batch is None and idx is None and eps1 is None   # ring path
+            key = (id(plan), f, n_steps)
+            if not (self.capture and static):
+                self._steps(plan, f, n_steps, self.stream)
+            elif key in self._graphs:
+                self._graphs[key].replay()
+            elif key not in self._eager_seen:   # first call eager (communicator warm-up)
+                self._eager_seen.add(key)
+                self._steps(plan, f, n_steps, self.stream)
+            else:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=self.stream):
+                    self._steps(plan, f, n_steps, torch.cuda.current_stream(self.device))
+                self._graphs[key] = g
+                g.replay()
         self._on_stream(go)
         self._last_plan = plan
         if self._need_to_update_eval_statistics:
             self._need_to_update_eval_statistics = False
             self._fill_eval_statistics(plan)
-        self._n_train_steps_total += 1
+        self._n_train_steps_total += n_steps
 
 
 class DataParallelSACTrainer(_DataParallel, SACTrainer):

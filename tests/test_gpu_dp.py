@@ -82,3 +82,61 @@ def test_dp_trainer_two_ranks_equals_single_gpu_on_global_batch():
         tr.train_from_torch(batch, eps1=e1, eps2=e2)
     want = torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy()
     assert parity.rel_err(got, want) < 1e-6, parity.rel_err(got, want)
+
+
+def _ring_run(tr, n_calls, n_steps):
+    """n_calls train_from_ring calls of n_steps each on a seeded device replay."""
+    from oac_amd import DeviceIndexStream, ReplayBuffer
+    from gpu_helpers import Space
+    rb = ReplayBuffer(2000, Space(Do), Space(Da), device="cuda:0")
+    data = synthetic_transitions(2000, Do, Da, seed=1)
+    rb.load_transitions(torch.from_numpy(rb._rows_from(
+        data["observations"], data["actions"], data["rewards"], data["next_observations"],
+        data["terminals"])).cuda())
+    st = DeviceIndexStream(rb, BL, chunk=8, seed=4)
+    for _ in range(n_calls):
+        st.before_step(n_steps)
+        tr.train_from_ring(rb._storage, st.ring, st.slots, BL, n_steps=n_steps)
+    torch.cuda.synchronize()
+    return torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy()
+
+
+def _nccl_worker(port, q):
+    import faulthandler
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.makedirs(os.path.join(os.path.dirname(here), "gpurun_out"), exist_ok=True)
+    trace = open(os.path.join(os.path.dirname(here), "gpurun_out", "dp_nccl_worker_stack.txt"), "w")
+    faulthandler.dump_traceback_later(90, exit=True, file=trace)   # a hang leaves its stack
+    for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    tr = _trainer(True)
+    assert tr.capture
+    got = _ring_run(tr, 4, 4)          # call 1 eager, calls 2.. captured (RCCL inside the graph)
+    n_graphs = len(tr._graphs)
+    dist.destroy_process_group()
+    q.put((got, n_graphs))
+
+
+def test_dp_rccl_graph_capture_single_rank_equals_single_gpu():
+    """The captured data-parallel step (phases + RCCL all-reduces in one
+    hipGraph, 4 steps per replay) on one rank equals the single-GPU trainer on
+    the same device index stream."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    p = ctx.Process(target=_nccl_worker, args=(port, q))
+    p.start()
+    p.join(timeout=150)
+    assert p.exitcode == 0, p.exitcode
+    got, n_graphs = q.get()
+    assert n_graphs == 1
+    want = _ring_run(_trainer(False), 4, 4)
+    assert parity.rel_err(got, want) < 1e-6, parity.rel_err(got, want)
