@@ -50,7 +50,7 @@ static int adam_blocks(long n) {
 
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s) {
   if (a.n & 3) return hipErrorInvalidValue;   // arena ranges are 16-byte multiples
-  hipLaunchKernelGGL(adam_flat_kernel, dim3(adam_blocks((a.n + 3) >> 2)), dim3(256), 0, s, a);
+  OAC_LAUNCH(adam_flat_kernel, dim3(adam_blocks((a.n + 3) >> 2)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

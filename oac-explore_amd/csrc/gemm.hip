@@ -372,7 +372,7 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   for (int i = 0; i < b.ntasks; ++i)               // dual products / head backward: small kernel
     if (b.t[i].K2 > 0 || b.t[i].epi == EPI_HEAD_BWD || b.t[i].epi == EPI_BIAS_RELU_DOT)
       return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b);
+  OAC_LAUNCH(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 

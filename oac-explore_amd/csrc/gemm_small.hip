@@ -390,11 +390,11 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   }
   const int grid = b.total_tiles + b.adam_blocks;
   switch (nw) {
-    case 1: hipLaunchKernelGGL(gemm_small_kernel<1>, dim3(grid), dim3(64), 0, s, b); break;
-    case 2: hipLaunchKernelGGL(gemm_small_kernel<2>, dim3(grid), dim3(128), 0, s, b); break;
-    case 4: hipLaunchKernelGGL(gemm_small_kernel<4>, dim3(grid), dim3(256), 0, s, b); break;
-    case 8: hipLaunchKernelGGL(gemm_small_kernel<8>, dim3(grid), dim3(512), 0, s, b); break;
-    default: hipLaunchKernelGGL(gemm_small_kernel<16>, dim3(grid), dim3(1024), 0, s, b); break;
+    case 1: OAC_LAUNCH(gemm_small_kernel<1>, dim3(grid), dim3(64), 0, s, b); break;
+    case 2: OAC_LAUNCH(gemm_small_kernel<2>, dim3(grid), dim3(128), 0, s, b); break;
+    case 4: OAC_LAUNCH(gemm_small_kernel<4>, dim3(grid), dim3(256), 0, s, b); break;
+    case 8: OAC_LAUNCH(gemm_small_kernel<8>, dim3(grid), dim3(512), 0, s, b); break;
+    default: OAC_LAUNCH(gemm_small_kernel<16>, dim3(grid), dim3(1024), 0, s, b); break;
   }
   return hipGetLastError();
 }

@@ -227,10 +227,10 @@ hipError_t launch_policy_head(const HeadArgs& a, int nseg, hipStream_t s) {
   const int rblocks = (a.B + kRows - 1) / kRows;
   const dim3 grid(rblocks * a.col_chunks, nseg), block(64 * kHeadWaves);
   switch ((2 * a.Da + 15) / 16) {
-    case 1: hipLaunchKernelGGL(policy_head_kernel<1>, grid, block, 0, s, a); break;
-    case 2: hipLaunchKernelGGL(policy_head_kernel<2>, grid, block, 0, s, a); break;
-    case 3: hipLaunchKernelGGL(policy_head_kernel<3>, grid, block, 0, s, a); break;
-    default: hipLaunchKernelGGL(policy_head_kernel<4>, grid, block, 0, s, a); break;
+    case 1: OAC_LAUNCH(policy_head_kernel<1>, grid, block, 0, s, a); break;
+    case 2: OAC_LAUNCH(policy_head_kernel<2>, grid, block, 0, s, a); break;
+    case 3: OAC_LAUNCH(policy_head_kernel<3>, grid, block, 0, s, a); break;
+    default: OAC_LAUNCH(policy_head_kernel<4>, grid, block, 0, s, a); break;
   }
   return hipGetLastError();
 }

@@ -157,4 +157,27 @@ struct AlphaState {
 
 namespace oac {
 void set_error(const char* fmt, ...);
+
+// Kernel-exact timing (bench instrumentation, never inside a graph): when
+// g_ext_timing.start is set, the next OAC_LAUNCH records the pair on the
+// dispatch itself (hipExtLaunchKernel start/stop events = the kernel's begin
+// and end timestamps, the same interval rocprofv3's kernel trace reports) and
+// marks the pair consumed.
+struct ExtTiming {
+  hipEvent_t start = nullptr, stop = nullptr;
+  bool consumed = false;
+};
+extern thread_local ExtTiming g_ext_timing;
 }
+
+#include <hip/hip_ext.h>
+#define OAC_LAUNCH(kernel, grid, block, shmem, stream, ...)                                  \
+  do {                                                                                      \
+    if (oac::g_ext_timing.start && !oac::g_ext_timing.consumed) {                           \
+      hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, oac::g_ext_timing.start,    \
+                            oac::g_ext_timing.stop, 0, __VA_ARGS__);                        \
+      oac::g_ext_timing.consumed = true;                                                    \
+    } else {                                                                                \
+      hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);                  \
+    }                                                                                       \
+  } while (0)

@@ -111,13 +111,18 @@ static inline int tick(PlanBase& p, hipStream_t s) {
   }
   const int i = p.ev_next;
   p.ev_next += 2;
-  OAC_HIP_CHECK(hipEventRecord(p.ev_pool[i], s));
+  // the launch records the pair on its dispatch (OAC_LAUNCH, hipExtLaunchKernel)
+  g_ext_timing.start = p.ev_pool[i];
+  g_ext_timing.stop = p.ev_pool[i + 1];
+  g_ext_timing.consumed = false;
   return i;
 }
 static inline int tock(PlanBase& p, int kind, int i, hipStream_t s) {
+  (void)s;
   if (i < 0) return 0;
-  OAC_HIP_CHECK(hipEventRecord(p.ev_pool[i + 1], s));
-  p.ev_pending.push_back({kind, i});
+  if (g_ext_timing.consumed) p.ev_pending.push_back({kind, i});
+  g_ext_timing.start = g_ext_timing.stop = nullptr;
+  g_ext_timing.consumed = false;
   return 0;
 }
 #define TIMED(p, kind, s, call)          \

@@ -251,34 +251,34 @@ __global__ void oac_final_kernel(OacArgs p) {
 namespace oac {
 
 hipError_t launch_policy_sample(const PolicySampleArgs& a, int nseg, hipStream_t s) {
-  hipLaunchKernelGGL(policy_sample_kernel, dim3((a.B + 7) / 8, nseg), dim3(256), 0, s, a);
+  OAC_LAUNCH(policy_sample_kernel, dim3((a.B + 7) / 8, nseg), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(logp_sum_kernel, dim3(1), dim3(256), 0, s, a);
+  OAC_LAUNCH(logp_sum_kernel, dim3(1), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s) {
   // 64 rows per block: the per-row work spreads over CUs (every block redoes
   // the 4-byte-per-row alpha reduction, which is cheap)
-  hipLaunchKernelGGL(critic_targets_kernel, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
+  OAC_LAUNCH(critic_targets_kernel, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_policy_head_backward(const PolicyHeadBwdArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(policy_head_backward_kernel, dim3((a.B * a.act_dim + 255) / 256), dim3(256),
+  OAC_LAUNCH(policy_head_backward_kernel, dim3((a.B * a.act_dim + 255) / 256), dim3(256),
                      0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_oac_prep(const OacArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(oac_prep_kernel, dim3(1), dim3(64), 0, s, a);
+  OAC_LAUNCH(oac_prep_kernel, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_oac_seed(const OacArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(oac_seed_kernel, dim3(1), dim3(64), 0, s, a);
+  OAC_LAUNCH(oac_seed_kernel, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_oac_final(const OacArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(oac_final_kernel, dim3(1), dim3(64), 0, s, a);
+  OAC_LAUNCH(oac_final_kernel, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 
@@ -374,11 +374,11 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
 }
 
 hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(particle_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  OAC_LAUNCH(particle_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(particle_min_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  OAC_LAUNCH(particle_min_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

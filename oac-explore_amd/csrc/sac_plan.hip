@@ -25,6 +25,7 @@
 namespace oac {
 
 static thread_local char g_err[1024] = "";
+thread_local ExtTiming g_ext_timing;
 void set_error(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);

@@ -10,7 +10,7 @@
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
 
-namespace oac { void set_error(const char*, ...) {} }
+namespace oac { void set_error(const char*, ...) {} thread_local ExtTiming g_ext_timing; }
 using namespace oac;
 
 static float* dev_rand(size_t n, float scale) {

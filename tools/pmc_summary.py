@@ -3,7 +3,11 @@
 FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch; on gfx950 FETCH_SIZE
 counts wide coalesced reads at half their bytes (MI355X_MICROARCH.md, HBM),
 so HBM bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
-usage: python tools/pmc_summary.py <tag> [json-out]"""
+
+usage: python tools/pmc_summary.py <tag> [json-out] [--traffic BATCH FILE]
+  --traffic: also merge {BATCH: HBM bytes per GEMM launch} (the mean over every
+  dispatch of the step's GEMM kernel, gemm_small_kernel / gemm_grouped_kernel)
+  into FILE -- the `roofline.traffic` bench.py reports."""
 import collections
 import csv
 import glob
@@ -29,13 +33,32 @@ def load(kind):
 
 
 out = {}
+gemm = collections.defaultdict(list)   # counter -> per-dispatch values of the GEMM kernel
 for kind in ("fetch", "write", "sq"):
     for k, d in load(kind).items():
         for c, v in d.items():
             out.setdefault(k, {})[c] = sum(v) / len(v)
+            if "gemm_small_kernel" in k or "gemm_grouped_kernel" in k:
+                gemm[c].extend(v)
 for k, d in sorted(out.items()):
     if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
         d["hbm_bytes"] = 2 * d["FETCH_SIZE"] * 1024 + d["WRITE_SIZE"] * 1024
     print(k.ljust(40), " ".join(f"{c}={v:.4g}" for c, v in sorted(d.items())))
-if len(sys.argv) > 2:
-    json.dump(out, open(sys.argv[2], "w"), indent=1, sort_keys=True)
+args = [a for a in sys.argv[2:]]
+if "--traffic" in args:
+    i = args.index("--traffic")
+    batch, path = args[i + 1], args[i + 2]
+    del args[i:i + 3]
+    if gemm.get("FETCH_SIZE") and gemm.get("WRITE_SIZE"):
+        f = sum(gemm["FETCH_SIZE"]) / len(gemm["FETCH_SIZE"])
+        w = sum(gemm["WRITE_SIZE"]) / len(gemm["WRITE_SIZE"])
+        per_launch = 2 * f * 1024 + w * 1024
+        d = {}
+        if os.path.exists(path):
+            d = json.load(open(path))
+        d[str(batch)] = round(per_launch)
+        json.dump(d, open(path, "w"), indent=1, sort_keys=True)
+        print(f"GEMM launches: {len(gemm['FETCH_SIZE'])} dispatches, "
+              f"HBM bytes per launch {per_launch:.4g} -> {path}")
+if args:
+    json.dump(out, open(args[0], "w"), indent=1, sort_keys=True)
