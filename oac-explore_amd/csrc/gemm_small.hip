@@ -24,6 +24,14 @@ namespace oac {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+#ifdef OAC_STAGE_CLOCK   // per-stage wall clock of thread 0 of each block (tools/micro only)
+__device__ long long g_gs_clock[4096 * 8];
+#define GS_STAGE(i) do { __builtin_amdgcn_s_waitcnt(0); \
+  if (threadIdx.x == 0 && blockIdx.x < 4096) g_gs_clock[blockIdx.x * 8 + (i)] = wall_clock64(); } while (0)
+#else
+#define GS_STAGE(i)
+#endif
+
 // Operand kinds (compile-time, so the k loop is straight-line code: every
 // load of a wave's k-groups is issued before the first MFMA and fixed up
 // -- masking, rank-1 products -- only afterwards).
@@ -93,7 +101,7 @@ __device__ __forceinline__ float fix1(const Lane& o, int k, int k_hi, float x, f
 }
 
 // acc += A[m0.., k_lo..k_hi) . B[k_lo..k_hi), n0..]  for this wave's k-groups
-template <int NW, int AK, int BK>
+template <int NW, int AK, int BK, int GPW = (NW >= 16 ? 4 : 5)>
 __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
                                        floatx16& acc) {
   const int lane = threadIdx.x & 63;
@@ -105,7 +113,7 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
                                 ar1 ? t.ld_mask : t.lda, t.a_s, t.a_v);
   const Lane lb = lane_init<BK>(n0 + l32, t.b_ones ? t.N - 1 : t.N, t.b_ones != 0, t.B, t.ldb,
                                 nullptr, nullptr);
-  constexpr int kGPW = NW >= 16 ? 4 : 5;      // k-groups in flight per wave (<= 128 VGPRs at 8 waves)
+  constexpr int kGPW = GPW;                   // k-groups in flight per wave (<= 128 VGPRs at 8 waves)
   const int g_lo = k_lo >> 3;                 // k_lo is a multiple of 8 (kchunk % 8 == 0)
   const int g_hi = (k_hi + 7) >> 3;
   const int kmax = k_hi - 1;
@@ -133,15 +141,15 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
   }
 }
 
-template <int NW>
+template <int NW, int GPW>
 __device__ __forceinline__ void k_dispatch(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
                                            floatx16& acc) {
   const bool r1 = t.a_mode == A_RANK1_MASK;
-  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC>(t, m0, n0, k_lo, k_hi, acc);      // forward
-  else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN>(t, m0, n0, k_lo, k_hi, acc);      // dX
-  else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN>(t, m0, n0, k_lo, k_hi, acc);   // dX, rank-1 seed
-  else if (!r1)                k_loop<NW, OP_MN, OP_MN>(t, m0, n0, k_lo, k_hi, acc);      // dW
-  else                         k_loop<NW, OP_MN_R1, OP_MN>(t, m0, n0, k_lo, k_hi, acc);   // dW, rank-1 seed
+  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW>(t, m0, n0, k_lo, k_hi, acc);      // forward
+  else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dX
+  else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dX, rank-1 seed
+  else if (!r1)                k_loop<NW, OP_MN, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dW
+  else                         k_loop<NW, OP_MN_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dW, rank-1 seed
 }
 
 // Epilogue operands of one output element, loaded before the k loop so their
@@ -228,17 +236,35 @@ __device__ __forceinline__ void epi_one(const GemmBatch& batch, const AdamConsts
   }
 }
 
-template <int NW>
-__global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch batch) {
+// Launch header as leading scalar kernel arguments: with
+// -mllvm -amdgpu-kernarg-preload-count they arrive in SGPRs, so a block finds
+// its task without a dependent kernarg round trip; only the task record itself
+// is then loaded (one scalar round trip).
+struct GemmHead { int total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6, tb7; };
+
+static GemmHead gemm_head(const GemmBatch& b) {
+  GemmHead h;
+  int tb[8];
+  for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
+  h.total_tiles = b.total_tiles; h.publish = b.publish != nullptr;
+  h.tb1 = tb[1]; h.tb2 = tb[2]; h.tb3 = tb[3]; h.tb4 = tb[4]; h.tb5 = tb[5]; h.tb6 = tb[6]; h.tb7 = tb[7];
+  return h;
+}
+
+template <int NW, int GPW>
+__global__ void __launch_bounds__(64 * NW)
+gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6,
+                  int tb7, const GemmBatch batch) {
   // partial tiles: NW x 16 regs x 64 lanes ; reused for the epilogue operands
   constexpr int RED = NW * 16 * 64;
   constexpr int LDS = RED > 2 * 32 * 65 ? RED : 2 * 32 * 65;
   constexpr int PER = 1024 / (64 * NW);   // epilogue elements per thread
   __shared__ __attribute__((aligned(16))) float red[LDS];
   const int bid = blockIdx.x;
-  if (batch.publish && bid == 0 && threadIdx.x == 0)
+  GS_STAGE(0);
+  if (publish && bid == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
-  if (bid >= batch.total_tiles) {   // fused optimizer: flat Adam over the other ranges
+  if (bid >= total_tiles) {   // fused optimizer: flat Adam over the other ranges
     const AdamArgs& a = batch.adam;
     const AdamConsts c = adam_consts(a.state, a.advance, a.lr, a.beta1, a.beta2, a.eps,
                                      a.target, a.tau, a.period);
@@ -249,15 +275,16 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
       if (r.target) r.target += batch.seg_off[sgi];
       const float* g = a.g + batch.seg_off[sgi];
       const long n4 = batch.seg_n[sgi] >> 2;
-      for (long i = (long)(bid - batch.total_tiles) * 64 * NW + threadIdx.x; i < n4; i += stride)
+      for (long i = (long)(bid - total_tiles) * 64 * NW + threadIdx.x; i < n4; i += stride)
         adam_float4(c, r, i, reinterpret_cast<const float4*>(g)[i]);
     }
     return;
   }
-  int ti = 0;
-#pragma unroll 1
-  for (int i = 1; i < batch.ntasks; ++i)
-    if (bid >= batch.t[i].tile_begin) ti = i;
+  int ti = 0;   // task of this block from the preloaded tile starts (no memory access)
+  ti = bid >= tb1 ? 1 : ti; ti = bid >= tb2 ? 2 : ti; ti = bid >= tb3 ? 3 : ti;
+  ti = bid >= tb4 ? 4 : ti; ti = bid >= tb5 ? 5 : ti; ti = bid >= tb6 ? 6 : ti;
+  ti = bid >= tb7 ? 7 : ti;
+  ti = __builtin_amdgcn_readfirstlane(ti);
   GemmTask t = batch.t[ti];
   int local = bid - t.tile_begin;
   int k_lo = 0, k_hi = t.K;
@@ -273,6 +300,7 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
   const int n0 = (local % t.tiles_n) * 32;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+  GS_STAGE(1);
 
   EpiIn xin[PER];
 #pragma unroll
@@ -284,13 +312,14 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  k_dispatch<NW>(t, m0, n0, k_lo, k_hi, acc);
+  k_dispatch<NW, GPW>(t, m0, n0, k_lo, k_hi, acc);
   if (t.K2 > 0) {   // second product into the same accumulator (unsplit dX tasks only)
     GemmTask t2 = t;
     t2.A = t.A2; t2.B = t.B2; t2.K = t.K2;
-    k_loop<NW, OP_KC, OP_MN>(t2, m0, n0, 0, t.K2, acc);
+    k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc);
   }
 
+  GS_STAGE(2);
   // fixed-order split-K reduction through LDS
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = acc[r];
@@ -305,6 +334,7 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
     for (int w = 0; w < NW; ++w) s += red[(w * 16 + r) * 64 + l];
     vals[i] = s;
   }
+  GS_STAGE(3);
   float* lds_u = red;
   float* lds_v = red + 32 * 65;
   if (t.epi == EPI_BIAS_RANK_RELU) {   // stage the rank-R operands (reusing the LDS)
@@ -340,6 +370,7 @@ __global__ void __launch_bounds__(64 * NW) gemm_small_kernel(const GemmBatch bat
   }
   if (batch.fuse_adam && bid == 0 && threadIdx.x == 0)
     step_bookkeeping(batch.adam.state, batch.adam.alpha, batch.adam.advance);
+  GS_STAGE(4);
 }
 
 // tile geometry shared with the plan builder
@@ -377,7 +408,8 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
     if (b.t[i].K2 > 0 && (b.t[i].ksplit > 1 || !b.t[i].a_kc || b.t[i].b_kc ||
                           b.t[i].a_mode != A_PLAIN))
       return hipErrorInvalidValue;
-  const int nw = gemm_small_waves(b);
+  const int nw = b.force_nw > 0 ? b.force_nw : gemm_small_waves(b);
+  const int gpw = b.force_gpw > 0 ? b.force_gpw : (nw >= 16 ? 4 : 5);
   b.adam_blocks = 0;
   if (b.fuse_adam) {
     long n4 = 0;
@@ -389,14 +421,18 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
     if (b.adam_blocks < 1) b.adam_blocks = 1;
   }
   const int grid = b.total_tiles + b.adam_blocks;
-  switch (nw) {
-    case 1: OAC_LAUNCH(gemm_small_kernel<1>, dim3(grid), dim3(64), 0, s, b); break;
-    case 2: OAC_LAUNCH(gemm_small_kernel<2>, dim3(grid), dim3(128), 0, s, b); break;
-    case 4: OAC_LAUNCH(gemm_small_kernel<4>, dim3(grid), dim3(256), 0, s, b); break;
-    case 8: OAC_LAUNCH(gemm_small_kernel<8>, dim3(grid), dim3(512), 0, s, b); break;
-    default: OAC_LAUNCH(gemm_small_kernel<16>, dim3(grid), dim3(1024), 0, s, b); break;
-  }
-  return hipGetLastError();
+  const GemmHead h = gemm_head(b);
+#define OAC_GS(NW_, G_) \
+  if (nw == NW_ && gpw == G_) { \
+    OAC_LAUNCH((gemm_small_kernel<NW_, G_>), dim3(grid), dim3(64 * NW_), 0, s, h.total_tiles, h.publish, \
+               h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b); \
+    return hipGetLastError(); }
+  OAC_GS(1, 5) OAC_GS(2, 5) OAC_GS(4, 5) OAC_GS(8, 5) OAC_GS(16, 4)
+  OAC_GS(4, 3) OAC_GS(4, 4) OAC_GS(4, 6) OAC_GS(4, 8)
+  OAC_GS(8, 3) OAC_GS(8, 4) OAC_GS(8, 6) OAC_GS(8, 8)
+  OAC_GS(16, 2) OAC_GS(16, 3) OAC_GS(16, 5) OAC_GS(16, 6)
+#undef OAC_GS
+  return hipErrorInvalidValue;
 }
 
 }  // namespace oac

@@ -105,6 +105,7 @@ struct GemmBatch {
   StepState* publish;        // non-null: block 0 publishes the step's Adam constants
   double pub_beta1, pub_beta2;
   int adam_blocks;           // set by the launcher
+  int force_nw, force_gpw;   // small kernel: waves per workgroup / k-groups in flight (0 = auto)
   long seg_off[2], seg_n[2]; // flat ranges (floats, multiples of 4) from the group base
   AdamArgs adam;
 };

@@ -1,6 +1,8 @@
 // Shared machinery of the launch plans (SAC / particle trainers): workspace
 // bookkeeping, split-K sizing, GEMM task constructors, HIP-event timing.
 #pragma once
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <utility>
 #include <vector>
@@ -26,6 +28,9 @@ struct PlanBase {
   int graph_flags = -1;
   int graph_n = 0;          // steps captured in the graph
   int launches = 0;
+  // per-launch small-GEMM geometry overrides (tuning experiments: env
+  // OAC_TUNE="launch:nw:gpw,..." read at plan creation; 0 = automatic)
+  int tune_nw[64] = {0}, tune_gpw[64] = {0};
   // HIP-event kernel timing (bench instrumentation; never inside a graph)
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -132,8 +137,20 @@ static inline int tock(PlanBase& p, int kind, int i, hipStream_t s) {
     if (tock(p, kind, _t, s)) return 1;  \
   } while (0)
 
+static inline void read_tuning(PlanBase& p) {
+  const char* e = getenv("OAC_TUNE");
+  while (e && *e) {
+    int i = 0, nw = 0, g = 0, used = 0;
+    if (sscanf(e, "%d:%d:%d%n", &i, &nw, &g, &used) != 3) break;
+    if (i >= 0 && i < 64) { p.tune_nw[i] = nw; p.tune_gpw[i] = g; }
+    e += used;
+    if (*e == ',') ++e;
+  }
+}
+
 static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {
   gemm_batch_finalize(gb, p.cfg);
+  if (p.launches < 64) { gb.force_nw = p.tune_nw[p.launches]; gb.force_gpw = p.tune_gpw[p.launches]; }
   TIMED(p, K_GEMM, s, OAC_HIP_CHECK(gemm_batch_launch(gb, p.cfg, s)));
   p.launches++;
   return 0;

@@ -477,6 +477,7 @@ int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_s
   if (p.c.kind == OAC_KIND_PARTICLE) particle_layout_workspace(p);
   else layout_workspace(p);
   p.b = *bufs;
+  read_tuning(p);
   *out = h;
   return 0;
 }
