@@ -118,8 +118,11 @@ struct GatherArgs {
   const float* replay; long row_stride;   // [N, row_stride]
   const int* idx;                         // ring [ring_slots * B] or [B]
   int ring_slots;                         // 0: use idx[0:B] directly
-  float* out;                             // [B, row_stride]
+  float* out;                             // [n_steps][B, row_stride]
   int B;
+  int n_steps;                            // consecutive steps gathered (0 = 1): step j uses
+                                          // ring slot / Philox counter batch_counter + j
+  long out_stride, eps_stride;            // floats between the steps' batches / eps
   // eps generation (Philox) -- skipped when eps1 == null
   float* eps1; float* eps2; int n_eps;
   unsigned long long seed;

@@ -6,6 +6,7 @@
 #include "kernels.h"
 #include "adam_common.h"
 #include "policy_math.h"
+#include "target_math.h"
 
 namespace oac {
 
@@ -74,90 +75,21 @@ __global__ void __launch_bounds__(256) logp_sum_kernel(LogpSumArgs a) {
 // --------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) critic_targets_kernel(CriticTargetArgs p) {
   __shared__ float red[256];
-  __shared__ float s_alpha;
   // this row's inputs first (clamped row, all loads in flight together), so
   // their latency overlaps the alpha reduction below
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  const int rc = min(r, p.B - 1);
-  constexpr int kMaxPart = 16;                 // n_part <= 16
-  float pv[QV_COUNT][kMaxPart];
-  if (p.n_part > 0) {
-#pragma unroll
-    for (int k = 0; k < QV_COUNT; ++k) {
-      const float* pp = p.part[k] + rc;
-#pragma unroll
-      for (int t = 0; t < kMaxPart; ++t)   // unconditional, coalesced over rows
-        pv[k][t] = pp[(long)min(t, p.n_part - 1) * p.B];
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < QV_COUNT; ++k) pv[k][0] = p.q[k][rc];
-  }
-  float pb[QV_COUNT];
-#pragma unroll
-  for (int k = 0; k < QV_COUNT; ++k) pb[k] = p.n_part > 0 ? p.part_bias[k][0] : 0.f;
-  const float rew = p.batch[(long)rc * p.ld_batch + p.off_rew];
-  const float term = p.batch[(long)rc * p.ld_batch + p.off_term];
-  const float logp2 = p.logp2[rc];
-
+  TargetRowIn x;
+  target_row_load(p, min(r, p.B - 1), x);
   float alpha = 0.f;
   if (p.alpha) {
-    // alpha update (trainer.py:139-146): L = -mean(log_alpha * (logp + H)),
-    // Adam on log_alpha with t = n_steps + 1, then alpha = exp(log_alpha).
-    // Every block computes it identically; block 0 publishes next_* (the
-    // critic Adam commits them), so no block reads what another writes.
-    const float S = (p.world_size > 1) ? p.alpha->sum
-                                       : block_logp_sum(p.logp1, p.B, p.target_entropy, red);
-    if (threadIdx.x == 0) {
-      AlphaState* as = p.alpha;
-      const float n = (float)((long long)p.B * (p.world_size > 1 ? p.world_size : 1));
-      const float la_old = as->log_alpha;
-      const float g = -(S / n);
-      double bc1, sbc2;
-      bias_corrections(p.state, p.state->n_steps + 1, p.beta1, p.beta2, bc1, sbc2);
-      const float m = __fadd_rn(__fmul_rn(as->m, (float)p.beta1), __fmul_rn((float)(1.0 - p.beta1), g));
-      const float v = __fadd_rn(__fmul_rn(as->v, (float)p.beta2),
-                                __fmul_rn(__fmul_rn((float)(1.0 - p.beta2), g), g));
-      const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), (float)sbc2), (float)p.adam_eps);
-      const float la = __fadd_rn(la_old, __fdiv_rn(__fmul_rn(-(float)(p.lr / bc1), m), denom));
-      s_alpha = expf(la);
-      if (blockIdx.x == 0) {
-        as->next_log_alpha = la; as->next_m = m; as->next_v = v;
-        as->alpha = s_alpha; as->grad = g; as->alpha_loss = -(la_old * S) / n;
-      }
-    }
-    __syncthreads();
-    alpha = s_alpha;
+    // every block computes the update identically; block 0 publishes next_*
+    // (the critic Adam commits them), so no block reads what another writes
+    const float S = (p.world_size > 1) ? p.alpha->sum : logp_sum256(p.logp1, p.B, p.target_entropy, red);
+    alpha = alpha_update(p, S, blockIdx.x == 0 && threadIdx.x == 0);
   }
   if (r >= p.B) return;
-  float qv[QV_COUNT];
-#pragma unroll
-  for (int k = 0; k < QV_COUNT; ++k) {
-    if (p.n_part > 0) {   // fixed-order sum of the per-tile partials
-      float s = pb[k];
-#pragma unroll
-      for (int t = 0; t < kMaxPart; ++t)
-        if (t < p.n_part) s += pv[k][t];
-      qv[k] = s;
-      p.q[k][r] = s;
-    } else {
-      qv[k] = pv[k][0];
-    }
-  }
-  const float tq = fminf(qv[QV_TQ1], qv[QV_TQ2]) - mul_rn(alpha, logp2);
-  const float y = add_rn(mul_rn(p.reward_scale, rew), mul_rn(mul_rn(1.f - term, p.discount), tq));
-  const float d1 = qv[QV_Q1] - y, d2 = qv[QV_Q2] - y;
-  const float invB = 1.f / (float)p.B;
-  p.y[r] = y;
-  p.dq1[r] = mul_rn(2.f * d1, invB);
-  p.dq2[r] = mul_rn(2.f * d2, invB);
-  p.sqe1[r] = d1 * d1;
-  p.sqe2[r] = d2 * d2;
-  const float a = qv[QV_QN1], b = qv[QV_QN2];
-  const bool sel1 = a <= b;
-  p.qnew[r] = sel1 ? a : b;
-  p.gq1[r] = sel1 ? -invB : 0.f;
-  p.gq2[r] = sel1 ? 0.f : -invB;
+  float dq1, dq2;
+  target_row(p, r, x, alpha, true, dq1, dq2);
 }
 
 // --------------------------------------------------------------------------
@@ -261,7 +193,7 @@ hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s) {
 hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s) {
   // 64 rows per block: the per-row work spreads over CUs (every block redoes
   // the 4-byte-per-row alpha reduction, which is cheap)
-  OAC_LAUNCH(critic_targets_kernel, dim3((a.B + 63) / 64), dim3(64), 0, s, a);
+  OAC_LAUNCH(critic_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_policy_head_backward(const PolicyHeadBwdArgs& a, hipStream_t s) {

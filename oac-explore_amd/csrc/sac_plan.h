@@ -9,6 +9,9 @@
 namespace oac {
 
 constexpr int kMaxWs = 128;
+// batch / eps slots: one gather launch fills the minibatches of up to
+// kXSlots consecutive steps (slot i % kXSlots is step i's batch)
+constexpr int kXSlots = 8;
 // split-K weight-gradient slabs shaped like the critic / policy arena ranges
 constexpr int WS_GSLAB_Q = kMaxWs - 2;
 constexpr int WS_GSLAB_P = kMaxWs - 1;
@@ -20,8 +23,12 @@ struct SacPlan : PlanBase {
   WsBuf ws[kMaxWs];
   Split sp_q0, sp_q1, sp_ql, sp_p0, sp_p1, sp_ph;
   int S_q = 1, S_p = 1;   // slab counts per group (max over the group's dW tasks)
+  int slot = 0;           // batch / eps slot of the step being issued
 
   float* W(int id) const { return b.workspace + ws[id].off; }
+  float* X() const { return W(OAC_WS_BATCH) + (long)slot * c.batch * c.row_stride; }
+  float* E1() const { return W(OAC_WS_EPS1) + (long)slot * c.batch * c.act_dim; }
+  float* E2() const { return W(OAC_WS_EPS2) + (long)slot * c.batch * c.act_dim; }
   float* P(int64_t off) const { return b.params + off; }
   float* T(int64_t off) const { return b.targets + off; }
   StepState* state() const { return reinterpret_cast<StepState*>(b.step_state); }

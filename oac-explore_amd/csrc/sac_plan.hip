@@ -75,8 +75,8 @@ static void layout_workspace(SacPlan& p) {
   const int64_t B = c.batch, H = c.hidden, Da = c.act_dim, Q = c.q_out;
   auto set = [&](int id, int64_t r, int64_t cl) { p.ws[id] = {0, r, cl}; };
   for (int i = 0; i < kMaxWs; ++i) p.ws[i] = {0, 0, 0};
-  set(OAC_WS_BATCH, B, c.row_stride);
-  set(OAC_WS_EPS1, B, Da); set(OAC_WS_EPS2, B, Da);
+  set(OAC_WS_BATCH, kXSlots * B, c.row_stride);   // public view: slot 0 (B rows)
+  set(OAC_WS_EPS1, kXSlots * B, Da); set(OAC_WS_EPS2, kXSlots * B, Da);
   set(OAC_WS_HEAD1, B, 2 * Da); set(OAC_WS_HEAD2, B, 2 * Da);
   set(OAC_WS_ACT1, B, Da); set(OAC_WS_ACT2, B, Da);
   set(OAC_WS_LOGP1, B, 1); set(OAC_WS_LOGP2, B, 1);
@@ -117,27 +117,35 @@ static GemmTask q_l1(SacPlan& p, const float* in, const float* net, float* out, 
   return t;
 }
 
-static int phase0(SacPlan& p, int flags, hipStream_t s) {
+// the minibatches (and Philox eps) of steps [i, i + n) into slots 0..n-1
+static int gather_steps(SacPlan& p, int flags, int n, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  const int B = c.batch, Da = c.act_dim;
+  GatherArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.replay = p.b.replay; g.row_stride = c.row_stride; g.idx = p.b.idx_ring; g.ring_slots = p.b.ring_slots;
+  g.out = p.W(OAC_WS_BATCH); g.B = (flags & OAC_STEP_GATHER) ? B : 0;
+  g.n_steps = n; g.out_stride = (long)B * c.row_stride; g.eps_stride = (long)B * Da;
+  if (flags & OAC_STEP_DEVICE_EPS) {
+    g.eps1 = p.W(OAC_WS_EPS1); g.eps2 = p.W(OAC_WS_EPS2); g.n_eps = B * Da;
+  }
+  g.seed = c.seed; g.state = p.state();
+  TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_gather(g, s)));
+  p.launches++;
+  return 0;
+}
+
+static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
   const int Dq = Do + Da;
-  float* X = p.W(OAC_WS_BATCH);
+  float* X = p.X();
   const float* obs = X + c.off_obs;
   const float* nobs = X + c.off_next_obs;
   const float* act = X + c.off_act;
-  if (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS)) {
-    GatherArgs g;
-    std::memset(&g, 0, sizeof(g));
-    g.replay = p.b.replay; g.row_stride = RS; g.idx = p.b.idx_ring; g.ring_slots = p.b.ring_slots;
-    g.out = X; g.B = (flags & OAC_STEP_GATHER) ? B : 0;
-    if (flags & OAC_STEP_DEVICE_EPS) {
-      g.eps1 = p.W(OAC_WS_EPS1); g.eps2 = p.W(OAC_WS_EPS2); g.n_eps = B * Da;
-    }
-    g.seed = c.seed; g.state = p.state();
-    TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_gather(g, s)));
-    p.launches++;
-  }
+  if (gather_n > 0 && (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS)))
+    if (gather_steps(p, flags, gather_n, s)) return 1;
   const float* pol = p.b.params;
   const float* q1 = p.b.params + L.q1_base;
   const float* q2 = p.b.params + L.q2_base;
@@ -182,13 +190,13 @@ static int phase0(SacPlan& p, int flags, hipStream_t s) {
     a.wh = pol + L.pol_head_w; a.bh = pol + L.pol_head_b; a.ld_wa = Dq;
     a.B = B; a.H = H; a.Da = Da; a.col_chunks = std::max(1, (H + 63) / 64);   // 64 columns each
     HeadSeg& s0 = a.seg[0];   // policy(obs; eps1) -> Q1/Q2(obs, a~)
-    s0.h2 = p.W(W_H2P); s0.eps = p.W(OAC_WS_EPS1); s0.head = p.W(OAC_WS_HEAD1);
+    s0.h2 = p.W(W_H2P); s0.eps = p.E1(); s0.head = p.W(OAC_WS_HEAD1);
     s0.act = p.W(OAC_WS_ACT1); s0.stdv = p.W(W_STD1); s0.u = p.W(W_U1); s0.logp = p.W(OAC_WS_LOGP1);
     s0.n_nets = 2;
     s0.wa[0] = q1 + L.q_fc0_w + Do; s0.pre[0] = p.W(W_P1); s0.h1[0] = p.W(W_H1N1);
     s0.wa[1] = q2 + L.q_fc0_w + Do; s0.pre[1] = p.W(W_P2); s0.h1[1] = p.W(W_H1N2);
     HeadSeg& s1 = a.seg[1];   // policy(next_obs; eps2) -> TQ1/TQ2(next_obs, a')
-    s1.h2 = p.W(W_H2P2); s1.eps = p.W(OAC_WS_EPS2); s1.head = p.W(OAC_WS_HEAD2);
+    s1.h2 = p.W(W_H2P2); s1.eps = p.E2(); s1.head = p.W(OAC_WS_HEAD2);
     s1.act = p.W(OAC_WS_ACT2); s1.stdv = p.W(W_STD2); s1.u = p.W(W_U2); s1.logp = p.W(OAC_WS_LOGP2);
     s1.n_nets = 2;
     s1.wa[0] = t1 + L.q_fc0_w + Do; s1.pre[0] = p.W(W_PT1); s1.h1[0] = p.W(W_H1T1);
@@ -211,7 +219,7 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused) {
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
   const int Dq = Do + Da;
-  float* X = p.W(OAC_WS_BATCH);
+  float* X = p.X();
   const float* q1 = p.b.params + L.q1_base;
   const float* q2 = p.b.params + L.q2_base;
   const float* t1 = p.b.targets;
@@ -310,7 +318,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused) {
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
   const int Dq = Do + Da;
-  float* X = p.W(OAC_WS_BATCH);
+  float* X = p.X();
   const float* pol = p.b.params;
   const float* q1 = p.b.params + L.q1_base;
   const float* q2 = p.b.params + L.q2_base;
@@ -333,7 +341,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused) {
     t.A2 = p.W(W_DH1N2); t.B2 = q2 + L.q_fc0_w + Do; t.K2 = H;   // same leading dims
     t.epi = EPI_HEAD_BWD;
     t.ex[0] = p.W(OAC_WS_ACT1); t.ex[1] = p.W(W_STD1); t.ex[2] = p.W(W_U1);
-    t.ex[3] = p.W(OAC_WS_EPS1); t.ex[4] = p.W(OAC_WS_HEAD1);
+    t.ex[3] = p.E1(); t.ex[4] = p.W(OAC_WS_HEAD1);
     t.ex[5] = c.auto_alpha ? &p.alpha()->alpha : nullptr;
     add(gb, t);
     if (run_gemm(p, gb, s)) return 1;
@@ -348,7 +356,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused) {
       PolicyHeadBwdArgs a;
       std::memset(&a, 0, sizeof(a));
       a.da1 = p.W(W_DA1); a.da2 = p.W(W_DA2); a.act = p.W(OAC_WS_ACT1); a.stdv = p.W(W_STD1);
-      a.u = p.W(W_U1); a.eps = p.W(OAC_WS_EPS1); a.head = p.W(OAC_WS_HEAD1);
+      a.u = p.W(W_U1); a.eps = p.E1(); a.head = p.W(OAC_WS_HEAD1);
       a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.B = B; a.act_dim = Da; a.dhead = p.W(W_DHEAD);
       TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head_backward(a, s)));
       p.launches++;
@@ -385,10 +393,14 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused) {
   return 0;
 }
 
-static int run_step(SacPlan& p, int flags, hipStream_t s) {
+// step i of an n-step sequence: the gather of steps [i, i + kXSlots) runs at
+// slot 0 (one launch per kXSlots steps), step i uses slot i % kXSlots
+static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) {
   p.launches = 0;
   const bool fused = can_fuse_adam(p);
-  if (phase0(p, flags, s)) return 1;
+  p.slot = i % kXSlots;
+  const int gather_n = p.slot == 0 ? std::min(kXSlots, n - i) : 0;
+  if (phase0(p, flags, s, gather_n)) return 1;
   if (phase1(p, s, fused)) return 1;
   if (!fused && phase2_adam(p, s, 0)) return 1;
   if (phase2(p, s, fused)) return 1;
@@ -397,6 +409,7 @@ static int run_step(SacPlan& p, int flags, hipStream_t s) {
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
   }
+  p.slot = 0;
   return 0;
 }
 
@@ -499,7 +512,7 @@ int oac_sac_step_n(oac_sac* h, int flags, int n_steps, void* stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   auto steps = [&](int f) {
     for (int i = 0; i < n_steps; ++i) {
-      const int rc = p.c.kind == OAC_KIND_PARTICLE ? particle_run_step(p, f, s) : run_step(p, f, s);
+      const int rc = p.c.kind == OAC_KIND_PARTICLE ? particle_run_step(p, f, s) : run_step(p, f, s, i, n_steps);
       if (rc) return rc;
     }
     return 0;
@@ -566,6 +579,8 @@ int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows
   if (!h || which < 0 || which >= OAC_WS_COUNT_PUBLIC) { set_error("bad workspace id"); return 1; }
   const WsBuf& w = h->plan.ws[which];
   *offset = w.off; *rows = w.rows; *cols = w.cols;
+  if (which == OAC_WS_BATCH || which == OAC_WS_EPS1 || which == OAC_WS_EPS2)
+    *rows = h->plan.c.batch;   // slot 0: the batch / eps of a single-step call
   return 0;
 }
 
