@@ -135,7 +135,47 @@ static int gather_steps(SacPlan& p, int flags, int n, hipStream_t s) {
   return 0;
 }
 
-static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1) {
+// The step's critic-side forward that needs only the critic parameters and the
+// batch -- Q_i(obs, a) (obs projection + the batch actions' rank-Da part; the
+// projection P_i is kept for Q_i(obs, a~)) and the target critics' next_obs
+// projections.  Issued by phase 0, or, on the small-batch ring path, ahead of
+// time inside the previous step's policy-backward launches (the critic Adam +
+// Polyak of that step are done by then; nothing later in it reads these
+// buffers), which takes four of the six layer-0 and two of the four layer-1
+// products off the step's dependency chain.
+static void add_critic_l0(SacPlan& p, GemmBatch& gb, const float* X) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
+  const int Dq = Do + Da;
+  const float* qs[2] = {p.b.params + L.q1_base, p.b.params + L.q2_base};
+  const int P_[2] = {W_P1, W_P2}, H1[2] = {W_H1Q1, W_H1Q2};
+  for (int i = 0; i < 2; ++i) {
+    GemmTask t = t_fwd(X + c.off_obs, RS, B, Do, qs[i] + L.q_fc0_w, Dq, H, p.W(P_[i]), H,
+                       EPI_BIAS_RANK_RELU, qs[i] + L.q_fc0_b);
+    t.U = X + c.off_act; t.ldu = RS; t.V = qs[i] + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
+    t.C2 = p.W(H1[i]); t.ldc2 = H;
+    add(gb, t);
+  }
+}
+static void add_target_l0(SacPlan& p, GemmBatch& gb, const float* X) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Dq = c.obs_dim + c.act_dim, RS = c.row_stride;
+  const float* ts[2] = {p.b.targets, p.b.targets + L.q_size};
+  const int PT[2] = {W_PT1, W_PT2};
+  for (int i = 0; i < 2; ++i)
+    add(gb, t_fwd(X + c.off_next_obs, RS, B, Do, ts[i] + L.q_fc0_w, Dq, H, p.W(PT[i]), H, EPI_BIAS,
+                  ts[i] + L.q_fc0_b));
+}
+static void add_critic_l1(SacPlan& p, GemmBatch& gb) {
+  const float* q1 = p.b.params + p.L.q1_base;
+  const float* q2 = p.b.params + p.L.q2_base;
+  add(gb, q_l1(p, p.W(W_H1Q1), q1, p.W(W_H2Q1), QV_Q1));
+  add(gb, q_l1(p, p.W(W_H1Q2), q2, p.W(W_H2Q2), QV_Q2));
+}
+
+static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool critic_done = false) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -143,7 +183,6 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1) {
   float* X = p.X();
   const float* obs = X + c.off_obs;
   const float* nobs = X + c.off_next_obs;
-  const float* act = X + c.off_act;
   if (gather_n > 0 && (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS)))
     if (gather_steps(p, flags, gather_n, s)) return 1;
   const float* pol = p.b.params;
@@ -156,26 +195,17 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1) {
     gb.publish = p.state(); gb.pub_beta1 = c.beta1; gb.pub_beta2 = c.beta2;   // step's Adam constants
     add(gb, t_fwd(obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
     add(gb, t_fwd(nobs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
-    const float* qs[2] = {q1, q2};
-    const int P_[2] = {W_P1, W_P2}, H1[2] = {W_H1Q1, W_H1Q2}, PT[2] = {W_PT1, W_PT2};
-    const float* ts[2] = {t1, t2};
-    for (int i = 0; i < 2; ++i) {
-      GemmTask t = t_fwd(obs, RS, B, Do, qs[i] + L.q_fc0_w, Dq, H, p.W(P_[i]), H, EPI_BIAS_RANK_RELU,
-                         qs[i] + L.q_fc0_b);
-      t.U = act; t.ldu = RS; t.V = qs[i] + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
-      t.C2 = p.W(H1[i]); t.ldc2 = H;
-      add(gb, t);
+    if (!critic_done) {
+      add_critic_l0(p, gb, X);
+      add_target_l0(p, gb, X);
     }
-    for (int i = 0; i < 2; ++i)
-      add(gb, t_fwd(nobs, RS, B, Do, ts[i] + L.q_fc0_w, Dq, H, p.W(PT[i]), H, EPI_BIAS, ts[i] + L.q_fc0_b));
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // layer 1
     GemmBatch gb{};
     add(gb, t_fwd(p.W(W_H1P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_H2P), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
     add(gb, t_fwd(p.W(W_H1P2), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_H2P2), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
-    add(gb, q_l1(p, p.W(W_H1Q1), q1, p.W(W_H2Q1), QV_Q1));
-    add(gb, q_l1(p, p.W(W_H1Q2), q2, p.W(W_H2Q2), QV_Q2));
+    if (!critic_done) add_critic_l1(p, gb);
     if (run_gemm(p, gb, s)) return 1;
   }
   if (!qdot(p)) {  // q1/q2 predictions (the small-batch path has them from layer 1)
@@ -313,7 +343,9 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
   return 0;
 }
 
-static int phase2(SacPlan& p, hipStream_t s, bool fused) {
+// prefetch: batch of the next step (its critic-side forward rides on this
+// step's policy-backward launches, small-batch path only), or null
+static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch = nullptr) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -332,6 +364,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused) {
       set_rank1(d, p.W(gq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
       add(gb, d);
     }
+    if (prefetch) add_critic_l0(p, gb, prefetch);
     if (run_gemm(p, gb, s)) return 1;
   }
   if (p.cfg == 0) {  // dL/da through both critics' action columns + head backward, one launch
@@ -344,6 +377,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused) {
     t.ex[3] = p.E1(); t.ex[4] = p.W(OAC_WS_HEAD1);
     t.ex[5] = c.auto_alpha ? &p.alpha()->alpha : nullptr;
     add(gb, t);
+    if (prefetch) add_target_l0(p, gb, prefetch);
     if (run_gemm(p, gb, s)) return 1;
   } else {
     {  // to the action columns of layer 0
@@ -368,6 +402,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused) {
     add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, gp + L.pol_head_w,
                  gp + L.pol_head_b, L.pol_size, p.sp_ph));
     add(gb, t_dx(p.W(W_DHEAD), 2 * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(W_DH2P), H, p.W(W_H2P), H));
+    if (prefetch) add_critic_l1(p, gb);
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 1
@@ -395,15 +430,21 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused) {
 
 // step i of an n-step sequence: the gather of steps [i, i + kXSlots) runs at
 // slot 0 (one launch per kXSlots steps), step i uses slot i % kXSlots
+static long c_batch_rows(const SacPlan& p) { return (long)p.c.batch * p.c.row_stride; }
+
 static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) {
   p.launches = 0;
   const bool fused = can_fuse_adam(p);
   p.slot = i % kXSlots;
   const int gather_n = p.slot == 0 ? std::min(kXSlots, n - i) : 0;
-  if (phase0(p, flags, s, gather_n)) return 1;
+  // steps after the first of a gather batch had their critic-side forward
+  // issued inside the previous step's policy backward (small-batch path)
+  const bool ahead = p.cfg == 0 && (flags & OAC_STEP_GATHER);
+  if (phase0(p, flags, s, gather_n, ahead && p.slot > 0)) return 1;
   if (phase1(p, s, fused)) return 1;
   if (!fused && phase2_adam(p, s, 0)) return 1;
-  if (phase2(p, s, fused)) return 1;
+  const bool pf = ahead && i + 1 < n && p.slot + 1 < kXSlots;
+  if (phase2(p, s, fused, pf ? p.W(OAC_WS_BATCH) + (long)(p.slot + 1) * c_batch_rows(p) : nullptr)) return 1;
   if (!fused) {
     AdamArgs a = policy_adam(p, 0, nullptr);
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
