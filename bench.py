@@ -37,8 +37,8 @@ PEAK_HBM_GBS = 8000.0
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=640)
+    ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--obs-dim", type=int, default=376)
     ap.add_argument("--act-dim", type=int, default=17)
@@ -49,8 +49,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--timing-steps", type=int, default=50)
     ap.add_argument("--gemm-cfg", type=int, default=-1)
-    ap.add_argument("--steps-per-launch", type=int, default=8,
-                    help="gradient steps per graph launch (1 = one graph per step)")
+    ap.add_argument("--steps-per-launch", type=int, default=64,
+                    help="gradient steps per graph launch (1 = one graph per step); the "
+                         "default is the device index ring's refill period, i.e. one "
+                         "rl_algorithm train-loop stretch of 64 train() calls per launch")
     return ap.parse_args()
 
 
@@ -197,7 +199,7 @@ def main():
     # n steps per graph replay (data-parallel: the phases and RCCL all-reduces
     # of n steps captured together, oac_amd/dp.py)
     # (the largest n <= --steps-per-launch dividing the ring chunk, K and W, so
-    # any --steps / --warmup work; the defaults keep n = 8)
+    # any --steps / --warmup work; the defaults keep n = 64)
     n = max(1, args.steps_per_launch)
     while n > 1 and (stream.chunk % n or args.steps % n or args.warmup % n):
         n -= 1

@@ -150,7 +150,10 @@ static inline void read_tuning(PlanBase& p) {
 
 static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {
   gemm_batch_finalize(gb, p.cfg);
-  if (p.launches < 64) { gb.force_nw = p.tune_nw[p.launches]; gb.force_gpw = p.tune_gpw[p.launches]; }
+  if (p.launches < 64 && p.tune_nw[p.launches] > 0) {
+    gb.force_nw = p.tune_nw[p.launches];
+    gb.force_gpw = p.tune_gpw[p.launches];
+  }
   TIMED(p, K_GEMM, s, OAC_HIP_CHECK(gemm_batch_launch(gb, p.cfg, s)));
   p.launches++;
   return 0;

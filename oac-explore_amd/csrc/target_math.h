@@ -2,10 +2,15 @@
 // (/root/reference/trainer/trainer.py:139-196), per row / per block, for
 // critic_targets_kernel (rows.hip).
 //
-// (Measured and rejected: folding this into the critic-backward GEMM launch as
-// a prologue every workgroup runs over all B rows -- the dW tiles need every
-// row's dq -- made that launch ~14 us slower at B=256 than the two launches it
-// replaced: ~290 workgroups re-reading the same 32 KB of head partials.)
+// (Measured and rejected at B=256: (1) folding this into the critic-backward
+// GEMM launch as a prologue every workgroup runs over all B rows -- the dW
+// tiles need every row's dq -- made that launch ~14 us slower than the two
+// launches it replaced (~290 workgroups re-reading the same 32 KB of head
+// partials); (2) running it as the row-block tail of the layer-1 launch (the
+// last arriving tile of each 32-row block, partials handed off write-through
+// + an agent-scope arrival counter) removed the launch but not the time: the
+// step stayed at 98-99 us, the tail's own dependent round trips costing what
+// the launch boundary did.)
 #pragma once
 #include "adam_common.h"
 #include "kernels.h"
