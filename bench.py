@@ -201,6 +201,8 @@ def main():
     # (the largest n <= --steps-per-launch dividing the ring chunk, K and W, so
     # any --steps / --warmup work; the defaults keep n = 64)
     n = max(1, args.steps_per_launch)
+    if world > 1:
+        n = min(n, 8)   # data parallel: at most 8 steps (24 RCCL all-reduces) per captured graph
     while n > 1 and (stream.chunk % n or args.steps % n or args.warmup % n):
         n -= 1
     step = step_fn(tr, rb, stream, B, n)
