@@ -143,6 +143,31 @@ int oac_replay_sample_indices(uint32_t* mt_state_dev, uint64_t size, int count, 
 int oac_replay_gather(const float* replay, int64_t row_stride, const int32_t* idx, int B,
                       float* out, void* stream);
 
+/* device insert (ReplayBuffer.add_path / add_sample, replay_buffer.py:50-104):
+ * n transitions in the reference's host dtypes -- obs / act / next_obs
+ * float64 [n, dim], rew float64 [n], term uint8 [n] -- rounded to fp32 and
+ * packed into the ring rows (top + i) % capacity of the row layout
+ * [obs | act | rew | term | next_obs | pad] (offsets in floats) */
+int oac_replay_insert(float* storage, int64_t row_stride, int64_t capacity, int64_t top, int n,
+                      const double* obs, const double* act, const double* rew,
+                      const double* next_obs, const uint8_t* term, int obs_dim, int act_dim,
+                      int off_obs, int off_act, int off_rew, int off_term, int off_next_obs,
+                      void* stream);
+/* ReplayBufferCount.random_batch bookkeeping (replay_buffer.py:186-197):
+ * counts_out[i] = counts[idx[i]] (float, before the update; may be NULL), then
+ * counts[j] += 1 once per distinct j of idx (numpy fancy-index `+=`).  tags:
+ * int32 [capacity] owned by the caller, epoch: a value this buffer never
+ * passed before (dedupe tags are never cleared) */
+int oac_replay_counts_update(int32_t* counts, int32_t* tags, const int32_t* idx, int B,
+                             int32_t epoch, float* counts_out, void* stream);
+/* priority sampling (replay_buffer.py:180-184, np.random.choice(p = 1/(c+1),
+ * normalised)): idx_out[i] = the inverse-cdf index of the caller's uniform
+ * u[i] (numpy random_sample draws) over counts[0:size]; scratch: device fp64
+ * [oac_replay_priority_scratch_doubles(size)], size <= 4,194,304 */
+int64_t oac_replay_priority_scratch_doubles(int64_t size);
+int oac_replay_priority_sample(const int32_t* counts, int64_t size, const double* u, int B,
+                               double* scratch, int32_t* idx_out, void* stream);
+
 /* ------------------------------------------------------------------ Adam */
 /* advance 0: Adam step t = n_steps+1, snapshot t (step_state), Polyak when
  * n_steps % period == 0; advance 1: t from the snapshot, then n_steps += 1. */

@@ -130,6 +130,21 @@ struct GatherArgs {
 };
 
 
+// replay insert / ReplayBufferCount (replay_count.hip)
+struct ReplayInsertArgs {
+  float* storage; long row_stride, capacity, top;
+  int n;                                   // transitions
+  const double* obs; const double* act; const double* rew; const double* next_obs;
+  const unsigned char* term;
+  int obs_dim, act_dim, off_obs, off_act, off_rew, off_term, off_next_obs;
+};
+hipError_t launch_replay_insert(const ReplayInsertArgs& a, hipStream_t s);
+hipError_t launch_counts_update(int* counts, int* tags, const int* idx, int B, int epoch,
+                                float* counts_out, hipStream_t s);
+long prio_scratch_doubles(long size);
+hipError_t launch_priority_sample(const int* counts, long size, const double* u, int B,
+                                  double* scratch, int* idx_out, hipStream_t s);
+
 // ParticleTrainer (share_layers) per-sample kernels, particle_trainer_oac.py
 struct ParticleTargetArgs {
   const float* q; const float* tq;      // [B, K] critic / target critic outputs

@@ -683,6 +683,48 @@ int oac_replay_sample_indices(uint32_t* mt_state_dev, uint64_t size, int count, 
   return 0;
 }
 
+int oac_replay_insert(float* storage, int64_t row_stride, int64_t capacity, int64_t top, int n,
+                      const double* obs, const double* act, const double* rew,
+                      const double* next_obs, const uint8_t* term, int obs_dim, int act_dim,
+                      int off_obs, int off_act, int off_rew, int off_term, int off_next_obs,
+                      void* stream) {
+  if (!storage || capacity < 1 || top < 0 || top >= capacity || n < 0 || n > capacity) {
+    set_error("replay insert: bad storage / top / n");
+    return 1;
+  }
+  if (off_obs + obs_dim > row_stride || off_act + act_dim > row_stride || off_rew >= row_stride ||
+      off_term >= row_stride || off_next_obs + obs_dim > row_stride) {
+    set_error("replay insert: row layout out of bounds");
+    return 1;
+  }
+  ReplayInsertArgs a;
+  a.storage = storage; a.row_stride = row_stride; a.capacity = capacity; a.top = top; a.n = n;
+  a.obs = obs; a.act = act; a.rew = rew; a.next_obs = next_obs; a.term = term;
+  a.obs_dim = obs_dim; a.act_dim = act_dim; a.off_obs = off_obs; a.off_act = off_act;
+  a.off_rew = off_rew; a.off_term = off_term; a.off_next_obs = off_next_obs;
+  OAC_HIP_CHECK(launch_replay_insert(a, reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+int oac_replay_counts_update(int32_t* counts, int32_t* tags, const int32_t* idx, int B,
+                             int32_t epoch, float* counts_out, void* stream) {
+  if (!counts || !tags || !idx || B < 0) { set_error("counts update: null buffer"); return 1; }
+  OAC_HIP_CHECK(launch_counts_update(counts, tags, idx, B, epoch, counts_out,
+                                     reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+int64_t oac_replay_priority_scratch_doubles(int64_t size) { return prio_scratch_doubles(size); }
+
+int oac_replay_priority_sample(const int32_t* counts, int64_t size, const double* u, int B,
+                               double* scratch, int32_t* idx_out, void* stream) {
+  if (size < 1 || size > 4096LL * 1024) { set_error("priority sample: size must be in [1, 4194304]"); return 1; }
+  if (B < 1) return 0;
+  OAC_HIP_CHECK(launch_priority_sample(counts, size, u, B, scratch, idx_out,
+                                       reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
 int oac_replay_gather(const float* replay, int64_t row_stride, const int32_t* idx, int B,
                       float* out, void* stream) {
   if (row_stride % 4) { set_error("row_stride must be a multiple of 4"); return 1; }

@@ -83,6 +83,17 @@ _SIGS = {
                                                  ctypes.c_void_p, ctypes.c_void_p]),
     "oac_replay_gather": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                          ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "oac_replay_insert": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                         ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p] + [ctypes.c_int] * 7 + [ctypes.c_void_p]),
+    "oac_replay_counts_update": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_int, ctypes.c_int32, ctypes.c_void_p,
+                                                ctypes.c_void_p]),
+    "oac_replay_priority_scratch_doubles": (ctypes.c_int64, [ctypes.c_int64]),
+    "oac_replay_priority_sample": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                                  ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p]),
     "oac_adam_polyak": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                        ctypes.c_float, ctypes.c_int, ctypes.c_double,

@@ -113,20 +113,56 @@ class ReplayBuffer(object):
             self._size = min(self._size + k, self._max_replay_buffer_size)
             done += k
 
+    def _insert(self, obs, act, rew, nobs, term):
+        """Ring insert of n transitions on the device (oac_replay_insert): the
+        reference's host dtypes -- float64 fields, uint8 terminals
+        (replay_buffer.py:40-45, 92-96) -- are copied once and packed into the
+        fp32 rows by a HIP kernel (f64 -> f32 rounding identical to the
+        reference's ptu.from_numpy(...).float() at sample time)."""
+        n = len(obs)
+        if n == 0:
+            return
+        N = self._max_replay_buffer_size
+        top = self._top
+        if n > N:   # sequential inserts of n > N rows leave the last N in place
+            k = n - N
+            top = (top + k) % N
+            obs, act, rew, nobs, term = obs[k:], act[k:], rew[k:], nobs[k:], term[k:]
+        m = len(obs)
+
+        def dev(x, dt, shape):
+            return torch.from_numpy(np.ascontiguousarray(np.asarray(x, dt).reshape(shape))).to(
+                self.device)
+        o = dev(obs, np.float64, (m, self.ob_dim))
+        a = dev(act, np.float64, (m, self.ac_dim))
+        r = dev(rew, np.float64, (m,))
+        no = dev(nobs, np.float64, (m, self.ob_dim))
+        t = dev(np.asarray(term).reshape(m).astype(np.uint8), np.uint8, (m,))
+        lay = self.rows
+        check(_lib.lib().oac_replay_insert(
+            ptr(self._storage), lay["row_stride"], N, top, m, ptr(o), ptr(a), ptr(r), ptr(no),
+            ptr(t), self.ob_dim, self.ac_dim, lay["off_obs"], lay["off_act"], lay["off_rew"],
+            lay["off_term"], lay["off_next_obs"], stream_ptr()))
+        self._on_insert(top, m)
+        self._top = (self._top + n) % N                     # _advance, :101-104
+        self._size = min(self._size + n, N)
+
+    def _on_insert(self, top, m):
+        """Hook: ring positions top .. top+m-1 (mod capacity) were just written."""
+
     def add_sample(self, observation, action, reward, next_observation, terminal,
                    env_info=None, **kwargs):
         """replay_buffer.py:88-99."""
         if hasattr(self._action_space, "n") and not hasattr(self._action_space, "low"):
             raise AssertionError("discrete action spaces are not supported")
-        self._write(self._rows_from([observation], [action], [reward], [next_observation],
-                                    [terminal]))
+        self._insert([observation], [action], [reward], [next_observation], [terminal])
 
     def add_path(self, path):
-        """replay_buffer.py:50-82, one host->device copy per path."""
+        """replay_buffer.py:50-82: one device insert per path."""
         if len(path["observations"]) == 0:
             return
-        self._write(self._rows_from(path["observations"], path["actions"], path["rewards"],
-                                    path["next_observations"], path["terminals"]))
+        self._insert(path["observations"], path["actions"], path["rewards"],
+                     path["next_observations"], path["terminals"])
 
     def add_paths(self, paths):
         for path in paths:
@@ -207,6 +243,79 @@ class ReplayBuffer(object):
                                ss["_next_obs"], ss["_terminals"])
         self._storage[:len(rows)].copy_(torch.from_numpy(rows))
         self._top, self._size = int(ss["_top"]), int(ss["_size"])
+
+
+class ReplayBufferCount(ReplayBuffer):
+    """ReplayBufferCount (replay_buffer.py:151-197): per-transition sample
+    counts on the device.  random_batch's batch carries ``counts`` (the
+    counts of the drawn rows BEFORE this draw, a device float32 [B, 1]; the
+    reference returns a float64 copy) and every distinct drawn row's count is
+    incremented once (numpy fancy-index ``+=``); ``priority_sample`` draws
+    with p = 1/(count+1) (np.random.choice) -- the uniforms are numpy's own
+    ``random_sample`` draws on the global stream, exactly the ones the
+    reference's choice() consumes, the inverse-cdf search runs on the device
+    (oac_replay_priority_sample)."""
+
+    def __init__(self, max_replay_buffer_size, ob_space, action_space, priority_sample=False,
+                 device=None, index_source="numpy", seed=None):
+        super().__init__(max_replay_buffer_size, ob_space, action_space, device=device,
+                         index_source=index_source, seed=seed)
+        N = self._max_replay_buffer_size
+        self._counts = torch.zeros(N, dtype=torch.int32, device=self.device)
+        self._tags = torch.full((N,), -1, dtype=torch.int32, device=self.device)
+        self._epoch = 0
+        self.priority_sample = bool(priority_sample)
+        self._scratch = None
+
+    def _on_insert(self, top, m):
+        """self._counts[self._top] = 0 for every inserted row (:177)."""
+        N = self._max_replay_buffer_size
+        first = min(m, N - top)
+        self._counts[top:top + first].zero_()
+        if m > first:
+            self._counts[:m - first].zero_()
+
+    def load_transitions(self, rows_fp32):
+        super().load_transitions(rows_fp32)
+        self._counts.zero_()
+
+    def _priority_indices(self, B):
+        L = _lib.lib()
+        if self._scratch is None:
+            n = int(L.oac_replay_priority_scratch_doubles(self._max_replay_buffer_size))
+            self._scratch = torch.empty(n, dtype=torch.float64, device=self.device)
+        u = torch.from_numpy(np.random.random_sample(B)).to(self.device)   # choice()'s draws
+        idx = torch.empty(B, dtype=torch.int32, device=self.device)
+        check(L.oac_replay_priority_sample(ptr(self._counts), self._size, ptr(u), int(B),
+                                           ptr(self._scratch), ptr(idx), stream_ptr()))
+        return idx
+
+    def random_batch(self, batch_size):
+        """replay_buffer.py:180-197."""
+        B = int(batch_size)
+        if self.priority_sample:
+            idx = self._priority_indices(B)
+        else:
+            idx = super().random_batch(B).indices
+        counts = torch.empty(B, dtype=torch.float32, device=self.device)
+        check(_lib.lib().oac_replay_counts_update(ptr(self._counts), ptr(self._tags), ptr(idx), B,
+                                                  self._epoch, ptr(counts), stream_ptr()))
+        self._epoch += 1
+        batch = DeviceBatch(self, idx)
+        batch["counts"] = counts.view(B, 1)
+        return batch
+
+    def get_snapshot(self):
+        ss = super().get_snapshot()
+        ss["_counts"] = self._counts.cpu().numpy().astype(np.float64).reshape(-1, 1)
+        return ss
+
+    def restore_from_snapshot(self, ss):
+        ss = dict(ss)
+        counts = ss.pop("_counts", None)
+        super().restore_from_snapshot(ss)
+        if counts is not None:
+            self._counts.copy_(torch.from_numpy(np.asarray(counts).reshape(-1).astype(np.int32)))
 
 
 class DeviceIndexStream:

@@ -75,7 +75,7 @@ from networks import FlattenMlp  # noqa: E402
 from trainer.policies import TanhGaussianPolicy  # noqa: E402
 from trainer.trainer import SACTrainer  # noqa: E402
 from trainer.particle_trainer_oac import ParticleTrainer as ParticleTrainerOAC  # noqa: E402
-from replay_buffer import ReplayBuffer  # noqa: E402
+from replay_buffer import ReplayBuffer, ReplayBufferCount  # noqa: E402
 import optimistic_exploration as oe  # noqa: E402
 
 
@@ -365,6 +365,58 @@ def gen_randint():
     return dict(kind="randint", n_cases=len(cases)), out
 
 
+# ------------------------------------------------- ReplayBufferCount
+def _path(rs, T, obs_dim, act_dim):
+    """One rollout path in the reference's layout (path_collector.py rollout)."""
+    return dict(observations=rs.standard_normal((T, obs_dim)) * 3.0,
+                actions=rs.uniform(-1, 1, (T, act_dim)),
+                rewards=rs.standard_normal((T, 1)) * 10.0,
+                next_observations=rs.standard_normal((T, obs_dim)) * 3.0,
+                terminals=(rs.uniform(0, 1, (T, 1)) < 0.1),
+                agent_infos=[{}] * T, env_infos=[{}] * T)
+
+
+def gen_replay_count(priority):
+    """ReplayBufferCount (replay_buffer.py:151-197) run by the reference:
+    add_paths that wrap the ring, random_batch with the counts bookkeeping
+    (and np.random.choice priority sampling), recording per call the indices
+    (recomputed from the saved global RNG state with the reference's own
+    numpy algorithm and checked against the returned rows), the batch's
+    counts and the counts array after the update."""
+    obs_dim, act_dim, N, B = 5, 2, 600, 64
+    rb = ReplayBufferCount(N, Box(-1, 1, (obs_dim,)), Box(-1, 1, (act_dim,)),
+                           priority_sample=priority)
+    rs = np.random.RandomState(21)
+    np.random.seed(33)
+    out, ops = {}, []
+    for k in range(12):
+        T = int(rs.randint(20, 160))
+        path = _path(rs, T, obs_dim, act_dim)
+        rb.add_paths([path])
+        for key in ("observations", "actions", "rewards", "next_observations", "terminals"):
+            out[f"op{k}/path/{key}"] = np.asarray(path[key])
+        st = np.random.get_state()
+        batch = rb.random_batch(B)
+        r2 = np.random.RandomState()
+        r2.set_state(st)
+        if priority:
+            u = r2.random_sample(B)
+            out[f"op{k}/u"] = u
+        out[f"op{k}/counts_batch"] = batch["counts"][:, 0].astype(np.int64)
+        out[f"op{k}/counts_after"] = rb._counts[:, 0].astype(np.int64).copy()
+        out[f"op{k}/obs"] = batch["observations"]
+        ops.append(T)
+    out["final/observations"] = rb._observations
+    out["final/actions"] = rb._actions
+    out["final/rewards"] = rb._rewards
+    out["final/terminals"] = rb._terminals
+    out["final/next_obs"] = rb._next_obs
+    out["final/top_size"] = np.array([rb._top, rb._size])
+    meta = dict(kind="replay_count", priority=priority, obs_dim=obs_dim, act_dim=act_dim, N=N,
+                B=B, path_lengths=ops, np_seed=33)
+    return meta, out
+
+
 def save(name, meta, out):
     import json
     out = dict(out)
@@ -376,6 +428,10 @@ def save(name, meta, out):
 
 def main():
     torch.set_num_threads(8)
+    if len(sys.argv) > 1 and sys.argv[1] == "replay_count":
+        save("replay_count", *gen_replay_count(False))
+        save("replay_count_priority", *gen_replay_count(True))
+        return
     save("randint", *gen_randint())
     save("sac_small", *gen_sac("sac_small", 376, 17, [32, 32], 32, 3, 1000, True))
     save("sac_stress", *gen_sac("sac_stress", 11, 3, [32, 32], 16, 3, 300, True,
@@ -393,6 +449,8 @@ def main():
     save("oac_expl_humanoid", *gen_oac_expl("oac_expl_humanoid", 376, 17, [256, 256], 16,
                                             4.66, 23.53))
     save("oac_expl_small", *gen_oac_expl("oac_expl_small", 11, 3, [32, 32], 16, 0.0, 5.0))
+    save("replay_count", *gen_replay_count(False))
+    save("replay_count_priority", *gen_replay_count(True))
 
 
 if __name__ == "__main__":
