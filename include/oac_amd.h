@@ -94,6 +94,7 @@ enum oac_ws_buffer {
   OAC_WS_ACT1, OAC_WS_ACT2, OAC_WS_LOGP1, OAC_WS_LOGP2,
   OAC_WS_Q1, OAC_WS_Q2, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_TQ2,
   OAC_WS_Y, OAC_WS_SQE1, OAC_WS_SQE2, OAC_WS_QNEW,
+  OAC_WS_COUNTS,                       /* [B] batch counts (ReplayBufferCount) for OAC_STEP_COUNTS */
   OAC_WS_COUNT_PUBLIC
 };
 
@@ -101,6 +102,9 @@ enum oac_ws_buffer {
 #define OAC_STEP_GATHER       1  /* gather the batch from the replay via idx_ring */
 #define OAC_STEP_DEVICE_EPS   2  /* draw eps1/eps2 with Philox (else caller wrote them) */
 #define OAC_STEP_USE_GRAPH    4  /* replay the captured hipGraph of the step */
+#define OAC_STEP_COUNTS       8  /* particle trainer with counts=True: the batch counts the
+                                    caller wrote into OAC_WS_COUNTS shape the quantile targets
+                                    (particle_trainer_oac.py:220-224) */
 
 int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out);
 int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_sac** out);

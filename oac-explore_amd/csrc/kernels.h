@@ -154,6 +154,7 @@ struct ParticleTargetArgs {
   float* dq;                            // [B, K] dL/dq (sort backward scatter)
   float* sqe;                           // [B, K] (sorted_q - y)^2 per sorted slot
   float* y;                             // [B, K] quantile targets (sorted slots)
+  const float* counts;                  // [B] batch counts (counts=True) or null
 };
 struct ParticleMinArgs {
   const float* qn; int B, K;            // [B, K] Q(obs, a~) with the post-step critic

@@ -47,6 +47,7 @@ void particle_layout_workspace(SacPlan& p) {
   set(OAC_WS_LOGP1, B, 1); set(OAC_WS_LOGP2, B, 1);
   for (int id : {OAC_WS_Q1, OAC_WS_QN1, OAC_WS_TQ1, OAC_WS_Y, OAC_WS_SQE1}) set(id, B, K);
   set(OAC_WS_QNEW, B, 1);
+  set(OAC_WS_COUNTS, B, 1);
   for (int id = X_H1P; id <= X_H2T; ++id) set(id, B, H);
   for (int id : {X_STD1, X_U1, X_STD2, X_U2, X_DA}) set(id, B, Da);
   set(X_DQ, B, K); set(X_GQ, B, K);
@@ -131,7 +132,7 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
   return 0;
 }
 
-static int pphase1(SacPlan& p, hipStream_t s) {
+static int pphase1(SacPlan& p, int flags, hipStream_t s) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -164,6 +165,7 @@ static int pphase1(SacPlan& p, hipStream_t s) {
     a.off_rew = c.off_rew; a.off_term = c.off_term; a.reward_scale = c.reward_scale;
     a.discount = c.discount; a.B = B; a.K = K;
     a.dq = p.W(X_DQ); a.sqe = p.W(OAC_WS_SQE1); a.y = p.W(OAC_WS_Y);
+    a.counts = (flags & OAC_STEP_COUNTS) ? p.W(OAC_WS_COUNTS) : nullptr;
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_particle_targets(a, s)));
     p.launches++;
   }
@@ -284,7 +286,7 @@ static int pphase2(SacPlan& p, hipStream_t s) {
 int particle_run_step(SacPlan& p, int flags, hipStream_t s) {
   p.launches = 0;
   if (pphase0(p, flags, s)) return 1;
-  if (pphase1(p, s)) return 1;
+  if (pphase1(p, flags, s)) return 1;
   {
     AdamArgs a = critic_adam(p, 0, nullptr);   // alpha is updated after the critic step
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
@@ -303,7 +305,7 @@ int particle_step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
   switch (phase) {
     case 0: return pphase0(p, flags, s);
     case 1:
-      if (pphase1(p, s)) return 1;
+      if (pphase1(p, flags, s)) return 1;
       if (p.S_q > 1) {
         AdamArgs a = critic_adam(p, 1, nullptr);
         OAC_HIP_CHECK(launch_adam(a, s));

@@ -257,10 +257,20 @@ __global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArg
   const float invB = 1.f / (float)p.B;
   const float sr = __fmul_rn(p.reward_scale, rew);
   const float gd = __fmul_rn(1.f - term, p.discount);
+  float y[kMaxHeads];
+  for (int i = 0; i < K; ++i) y[i] = __fadd_rn(sr, __fmul_rn(gd, t[i]));
+  // counts=True (particle_trainer_oac.py:220-224): a row drawn before (count
+  // > 0) gets the sorted predictions re-centred on the target mean,
+  //   y_i <- (sorted_q_i - mean_k sorted_q) + mean_k y
+  if (p.counts && p.counts[r] != 0.f) {
+    float sq = 0.f, sy = 0.f;
+    for (int i = 0; i < K; ++i) { sq += q[i]; sy += y[i]; }
+    const float mq = sq / (float)K, my = sy / (float)K;
+    for (int i = 0; i < K; ++i) y[i] = (q[i] - mq) + my;
+  }
   for (int i = 0; i < K; ++i) {
-    const float y = __fadd_rn(sr, __fmul_rn(gd, t[i]));
-    const float d = q[i] - y;
-    p.y[(long)r * K + i] = y;
+    const float d = q[i] - y[i];
+    p.y[(long)r * K + i] = y[i];
     p.sqe[(long)r * K + i] = d * d;
     p.dq[(long)r * K + qi[i]] = __fmul_rn(2.f * d, invB);
   }

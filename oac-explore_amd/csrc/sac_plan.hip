@@ -82,6 +82,7 @@ static void layout_workspace(SacPlan& p) {
   set(OAC_WS_LOGP1, B, 1); set(OAC_WS_LOGP2, B, 1);
   for (int id : {OAC_WS_Q1, OAC_WS_Q2, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_TQ2}) set(id, B, Q);
   for (int id : {OAC_WS_Y, OAC_WS_SQE1, OAC_WS_SQE2, OAC_WS_QNEW}) set(id, B, Q);
+  set(OAC_WS_COUNTS, B, 1);   // unused by SAC (the reference SACTrainer ignores counts)
   for (int id = W_H1P; id <= W_H2T2; ++id) set(id, B, H);
   for (int id : {W_STD1, W_U1, W_STD2, W_U2, W_DA1, W_DA2}) set(id, B, Da);
   for (int id : {W_DQ1, W_DQ2, W_GQ1, W_GQ2}) set(id, B, Q);

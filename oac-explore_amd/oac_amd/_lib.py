@@ -16,11 +16,12 @@ OAC_KIND_PARTICLE = 1
 OAC_STEP_GATHER = 1
 OAC_STEP_DEVICE_EPS = 2
 OAC_STEP_USE_GRAPH = 4
+OAC_STEP_COUNTS = 8
 
 # public workspace ids (enum oac_ws_buffer)
 WS = {name: i for i, name in enumerate([
     "batch", "eps1", "eps2", "head1", "head2", "act1", "act2", "logp1", "logp2",
-    "q1", "q2", "qn1", "qn2", "tq1", "tq2", "y", "sqe1", "sqe2", "qnew"])}
+    "q1", "q2", "qn1", "qn2", "tq1", "tq2", "y", "sqe1", "sqe2", "qnew", "counts"])}
 
 
 class SacConfig(ctypes.Structure):

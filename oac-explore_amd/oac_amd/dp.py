@@ -104,11 +104,16 @@ class _DataParallel:
         for _ in range(n_steps):
             dp_step(ex, self._all_reduce)
 
-    def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None, n_steps=1):
+    def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None, n_steps=1,
+             counts=None):
         def go(sp):
             f = flags
             if batch is not None:
                 self._pack_batch(plan, batch)
+            if counts is not None:
+                v = plan.views["counts"]
+                v.copy_(torch.as_tensor(counts).reshape(v.shape).to(torch.float32), non_blocking=True)
+                f |= _lib.OAC_STEP_COUNTS
             if idx is not None:
                 self._idx.copy_(idx)
             if eps1 is not None:
@@ -116,7 +121,7 @@ class _DataParallel:
                 plan.views["eps2"].copy_(torch.as_tensor(eps2).reshape(plan.views["eps2"].shape))
             else:
                 f |= _lib.OAC_STEP_DEVICE_EPS
-            static = batch is None and idx is None and eps1 is None   # ring path
+            static = batch is None and idx is None and eps1 is None and counts is None   # ring path
             key = (id(plan), f, n_steps)
             if not (self.capture and static):
                 self._steps(plan, f, n_steps, self.stream)

@@ -31,14 +31,14 @@ class ParticleTrainer(_ArenaTrainer):
                  std_soft_update_prob=0., train_bias=True, lb=0.1,
                  device=None, seed=0, use_graph=True, gemm_cfg=-1):
         unsupported = dict(share_layers=not share_layers, deterministic=deterministic,
-                           ensemble=ensemble, mellow_max=mellow_max, counts=counts,
+                           ensemble=ensemble, mellow_max=mellow_max,
                            global_opt=global_opt, std_soft_update=std_soft_update,
                            train_bias=not train_bias)
         bad = [k for k, v in unsupported.items() if v]
         if bad:
             raise NotImplementedError(
                 "oac_amd.ParticleTrainer implements the P-OAC recipe configuration "
-                "(share_layers=True, stochastic policy, no counts / mellow-max / global-opt / "
+                "(share_layers=True, stochastic policy, counts, no mellow-max / global-opt / "
                 f"std-soft-update, trainable bias); unsupported: {bad}")
         assert not counts or not std_soft_update   # particle_trainer_oac.py:97
         self.device = torch.device(device) if device is not None else torch.device(

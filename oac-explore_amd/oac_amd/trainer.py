@@ -226,11 +226,16 @@ class _ArenaTrainer(object):
         put(r["off_term"], 1, batch["terminals"])
         put(r["off_next_obs"], Do, batch["next_observations"])
 
-    def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None, n_steps=1):
+    def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None, n_steps=1,
+             counts=None):
         def go(sp):
             f = flags
             if batch is not None:
                 self._pack_batch(plan, batch)
+            if counts is not None:   # ReplayBufferCount's batch counts (counts=True trainers)
+                v = plan.views["counts"]
+                v.copy_(torch.as_tensor(counts).reshape(v.shape).to(torch.float32), non_blocking=True)
+                f |= _lib.OAC_STEP_COUNTS
             if idx is not None:
                 self._idx.copy_(idx)
             if eps1 is not None:
@@ -268,14 +273,24 @@ class _ArenaTrainer(object):
         device Philox stream)."""
         B = int(np.shape(batch["observations"])[0])
         plan = self._plan(B)
-        self._run(plan, 0, eps1, eps2, batch=batch)
+        self._run(plan, 0, eps1, eps2, batch=batch, counts=self._batch_counts(batch))
+
+    def _batch_counts(self, batch):
+        """batch['counts'] for trainers built with counts=True
+        (particle_trainer_oac.py:220); the SAC trainer ignores it."""
+        if not getattr(self, "counts", False):
+            return None
+        if batch.get("counts") is None:
+            raise KeyError("counts=True needs batch['counts'] (ReplayBufferCount)")
+        return batch["counts"]
 
     def train_device_batch(self, dbatch, eps1=None, eps2=None):
         B = dbatch.batch_size
         if self._idx is None or self._idx.numel() != B:
             self._idx = torch.zeros(B, dtype=torch.int32, device=self.device)
         plan = self._plan(B, replay=dbatch.storage, idx=self._idx)
-        self._run(plan, _lib.OAC_STEP_GATHER, eps1, eps2, idx=dbatch.indices)
+        self._run(plan, _lib.OAC_STEP_GATHER, eps1, eps2, idx=dbatch.indices,
+                  counts=self._batch_counts(dbatch))
 
     def train_from_ring(self, storage, ring, ring_slots, B, n_steps=1):
         """Fast path for a device-resident replay with a device index ring
@@ -284,6 +299,9 @@ class _ArenaTrainer(object):
         rl_algorithm.py's inner loop of num_trains_per_train_loop train()
         calls -- in one graph launch.  Diagnostics (on the first step after
         end_epoch in the reference) come from the last step of the call."""
+        if getattr(self, "counts", False):
+            raise NotImplementedError("counts=True trains from ReplayBufferCount batches "
+                                      "(train / train_from_torch), not from the index ring")
         plan = self._plan(B, replay=storage, idx=ring, ring_slots=ring_slots)
         self._run(plan, _lib.OAC_STEP_GATHER, n_steps=n_steps)
 

@@ -415,6 +415,10 @@ class ParticleOACOracle:
         tq = q_forward(nobs, pf2["a"], self.T)["q"].t()      # 198-201
         tq_sorted, _ = torch.sort(tq, dim=0)                 # 202
         y = self.reward_scale * rew.t() + (1.0 - term.t()) * self.discount * tq_sorted  # 207-208
+        if batch.get("counts") is not None:                  # counts=True, 220-224
+            cnt = _t(batch["counts"], dt).reshape(1, B)
+            factor = (cnt == 0).to(dt)
+            y = y * factor + (1 - factor) * (sorted_qs - sorted_qs.mean(dim=0) + y.mean(dim=0))
         losses = ((sorted_qs - y) ** 2).mean(dim=1)          # 247-251
         d_sorted = 2.0 * (sorted_qs - y) / B
         dq = torch.zeros_like(qs).scatter_(0, qs_idx, d_sorted).t()   # sort backward

@@ -251,7 +251,7 @@ def gen_sac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=7,
 # ------------------------------------------------------------- P-OAC runs
 def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=11,
              delta=0.95, q_min=0.0, q_max=500.0, discount=0.99, lr=3e-4, tau=5e-3,
-             idx_seed=1, eps_seed=2, pi_init_w=1e-3):
+             idx_seed=1, eps_seed=2, pi_init_w=1e-3, counts=False):
     pp, qp = _producers(obs_dim, act_dim, hidden, q_out=K)
     torch.manual_seed(0)
     tr = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Box(-1, 1, (act_dim,)),
@@ -259,8 +259,9 @@ def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=1
                             policy_lr=lr, qf_lr=lr, optimizer_class=Adam14,
                             soft_target_tau=tau, target_update_period=1,
                             use_automatic_entropy_tuning=True, deterministic=False,
-                            q_min=q_min, q_max=q_max, share_layers=True)
+                            q_min=q_min, q_max=q_max, share_layers=True, counts=counts)
     bias = np.linspace(q_min, q_max, K)
+    crs = np.random.RandomState(77)   # batch counts (ReplayBufferCount's 'counts' key)
     params = sac_params(obs_dim, act_dim, hidden, seed, q_out=K, q_last_bias=bias,
                         pi_init_w=pi_init_w)
     load_sd(tr.policy, params["policy"])
@@ -274,12 +275,17 @@ def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=1
                 steps=steps, n_replay=n_replay, seed=seed, delta=delta, q_min=q_min,
                 q_max=q_max, discount=discount, lr=lr, tau=tau, idx_seed=idx_seed,
                 eps_seed=eps_seed, delta_index=int(tr.delta_index), pi_init_w=pi_init_w,
-                target_entropy=-float(act_dim))
+                target_entropy=-float(act_dim), counts=counts)
     for s in range(steps):
         EPS_LOG.clear()
         batch, idx = _record_batch(rb, B)
+        batch = dict(batch)
+        if counts:   # about half the rows unvisited (factor 1), the rest 1..3 (:220-224)
+            c = crs.randint(0, 4, (B, 1)) * (crs.uniform(0, 1, (B, 1)) < 0.5)
+            batch["counts"] = c.astype(np.float64)
+            out[f"s{s}/counts"] = batch["counts"][:, 0]
         tr.end_epoch(s)
-        tr.train(dict(batch))
+        tr.train(batch)
         assert len(EPS_LOG) == 2
         out[f"s{s}/idx"] = idx.astype(np.int64)
         out[f"s{s}/eps1"] = EPS_LOG[0]   # drawn by policy(next_obs) (line 193)
@@ -428,6 +434,10 @@ def save(name, meta, out):
 
 def main():
     torch.set_num_threads(8)
+    if len(sys.argv) > 1 and sys.argv[1] == "poac_counts":
+        save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
+                                      pi_init_w=0.3, counts=True))
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "replay_count":
         save("replay_count", *gen_replay_count(False))
         save("replay_count_priority", *gen_replay_count(True))
@@ -451,6 +461,8 @@ def main():
     save("oac_expl_small", *gen_oac_expl("oac_expl_small", 11, 3, [32, 32], 16, 0.0, 5.0))
     save("replay_count", *gen_replay_count(False))
     save("replay_count_priority", *gen_replay_count(True))
+    save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
+                                  pi_init_w=0.3, counts=True))
 
 
 if __name__ == "__main__":

@@ -27,16 +27,18 @@ def particle_trainer_for(meta, **kw):
                            share_layers=True, **kw)
 
 
-@pytest.mark.parametrize("name", ["poac_small", "poac_ant"])
+@pytest.mark.parametrize("name", ["poac_small", "poac_ant", "poac_counts"])
 def test_particle_step_matches_reference_golden(name):
     meta, g = parity.load(name)
-    tr = particle_trainer_for(meta)
+    tr = particle_trainer_for(meta, counts=bool(meta.get("counts")))
     assert tr.delta_index == meta["delta_index"]
     errs = {}
     for s in range(meta["steps"]):
         tr.end_epoch(s)
-        tr.train_from_torch(batch_from(meta, g[f"s{s}/idx"]), eps1=g[f"s{s}/eps1"],
-                            eps2=g[f"s{s}/eps2"])
+        b = batch_from(meta, g[f"s{s}/idx"])
+        if meta.get("counts"):
+            b["counts"] = g[f"s{s}/counts"][:, None]
+        tr.train_from_torch(b, eps1=g[f"s{s}/eps1"], eps2=g[f"s{s}/eps2"])
         torch.cuda.synchronize()
         for grp, mod, order in (("policy", tr.policy, PARAM_ORDER_POLICY),
                                 ("qf", tr.qfs[0], PARAM_ORDER_Q)):

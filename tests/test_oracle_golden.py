@@ -78,7 +78,7 @@ def test_sac_oracle_matches_reference_golden(name):
 
 
 def test_poac_oracle_matches_reference_golden():
-    for name in ("poac_small", "poac_ant"):
+    for name in ("poac_small", "poac_ant", "poac_counts"):
         meta, g = parity.load(name)
         params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
                             q_out=meta["K"], q_last_bias=np.linspace(meta["q_min"], meta["q_max"],
@@ -89,7 +89,10 @@ def test_poac_oracle_matches_reference_golden():
                                    qf_lr=meta["lr"], tau=meta["tau"])
         errs = {}
         for s in range(meta["steps"]):
-            out = orc.step(build_batch(meta, g[f"s{s}/idx"]), g[f"s{s}/eps1"], g[f"s{s}/eps2"])
+            b = build_batch(meta, g[f"s{s}/idx"])
+            if meta.get("counts"):
+                b["counts"] = g[f"s{s}/counts"][:, None]
+            out = orc.step(b, g[f"s{s}/eps1"], g[f"s{s}/eps2"])
             for grp, order in (("policy", PARAM_ORDER_POLICY), ("qf", PARAM_ORDER_Q)):
                 for pn in order:
                     key = f"s{s}/grad/{grp}/{pn}"
