@@ -188,6 +188,15 @@ int oac_expl_create(int obs_dim, int act_dim, int hidden, const float* policy, c
                     const float* q2, float* workspace, void* step_state, uint64_t seed,
                     oac_expl** out);
 int oac_expl_destroy(oac_expl* h);
+/* vectorised rollouts: one handle for n_obs observations; the
+ * obs slot is then [n_obs, obs_dim + act_dim] (row stride obs_dim + act_dim,
+ * the caller writes the first obs_dim floats of each row), eps [n_obs,
+ * act_dim], outputs [n_obs, act_dim]; each row is computed exactly as a
+ * single-observation call.  oac_expl_create = oac_expl_create_batch(1, ...) */
+int64_t oac_expl_workspace_floats_batch(int n_obs, int obs_dim, int act_dim, int hidden);
+int oac_expl_create_batch(int n_obs, int obs_dim, int act_dim, int hidden, const float* policy,
+                          const float* q1, const float* q2, float* workspace, void* step_state,
+                          uint64_t seed, oac_expl** out);
 /* ob: device [obs_dim] fp32 (already in the workspace slot returned by
  * oac_expl_obs_slot, or any device pointer); eps: device [act_dim] or NULL
  * (Philox).  Writes action[act_dim]; optional mu_E / std / grad outputs. */

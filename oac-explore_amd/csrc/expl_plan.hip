@@ -1,4 +1,6 @@
-// OAC optimistic exploration action on MI355X (batch 1):
+// OAC optimistic exploration action on MI355X, for N observations at once
+// (N = 1: the reference's per-step call; N > 1: one launch sequence for the
+// observations of N parallel environments, each row exactly as alone):
 // get_optimistic_exploration_action_stochastic
 // (/root/reference/optimistic_exploration.py:14-109, trainer=None, two critics):
 //   mu_T, std = policy(ob);  a = tanh(mu_T)
@@ -20,7 +22,7 @@ namespace oac {
 static inline int64_t a64(int64_t x) { return (x + 63) & ~int64_t(63); }
 
 struct ExplPlan {
-  int Do, Da, H;
+  int Do, Da, H, N = 1;
   const float* pol; const float* q1; const float* q2;
   float* ws;
   StepState* state;
@@ -28,7 +30,7 @@ struct ExplPlan {
   oac_sac_layout L;
   // workspace offsets
   int64_t o_x, o_h1p, o_h2p, o_head, o_std, o_mut, o_h1q1, o_h1q2, o_h2q1, o_h2q2, o_q1, o_q2, o_w,
-      o_dh1, o_dh2, o_da1, o_da2, o_grad, o_mue, o_act, total;
+      o_dh1, o_dh2, o_da1, o_da2, o_grad, o_mue, o_act, o_cnt, total;
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   hipStream_t gstream = nullptr;
@@ -38,7 +40,8 @@ struct ExplPlan {
 
 static void expl_layout(ExplPlan& p) {
   int64_t o = 0;
-  auto take = [&](int64_t n) { int64_t r = o; o = a64(o + n); return r; };
+  const int64_t N = p.N;
+  auto take = [&](int64_t n) { int64_t r = o; o = a64(o + N * n); return r; };
   p.o_x = take(p.Do + p.Da);
   p.o_h1p = take(p.H); p.o_h2p = take(p.H); p.o_head = take(2 * p.Da);
   p.o_std = take(p.Da); p.o_mut = take(p.Da);
@@ -46,7 +49,8 @@ static void expl_layout(ExplPlan& p) {
   p.o_q1 = take(1); p.o_q2 = take(1); p.o_w = take(2);
   p.o_dh1 = take(p.H); p.o_dh2 = take(p.H); p.o_da1 = take(p.Da); p.o_da2 = take(p.Da);
   p.o_grad = take(p.Da); p.o_mue = take(p.Da); p.o_act = take(p.Da);
-  p.total = o;
+  p.o_cnt = o; o = a64(o + 2);   // Philox counter snapshot (8 bytes)
+  p.total = o + 64;              // tail pad: k-contiguous GEMM loads may read 7 floats past a row
 }
 
 static GemmTask e_task() {
@@ -56,11 +60,12 @@ static GemmTask e_task() {
   return t;
 }
 
-static GemmTask e_fwd(const float* x, int K, const float* W, long ldw, int N, float* y, int epi,
-                      const float* bias) {
+// rows of x: M observations, row stride ldx
+static GemmTask e_fwd(const float* x, long ldx, int M, int K, const float* W, long ldw, int N,
+                      float* y, int epi, const float* bias) {
   GemmTask t = e_task();
-  t.A = x; t.lda = K; t.a_kc = 1; t.B = W; t.ldb = ldw; t.b_kc = 1;
-  t.C = y; t.ldc = N; t.M = 1; t.N = N; t.K = K; t.epi = epi; t.bias = bias;
+  t.A = x; t.lda = ldx; t.a_kc = 1; t.B = W; t.ldb = ldw; t.b_kc = 1;
+  t.C = y; t.ldc = N; t.M = M; t.N = N; t.K = K; t.epi = epi; t.bias = bias;
   return t;
 }
 
@@ -71,22 +76,22 @@ static int e_run(GemmBatch& gb, hipStream_t s) {
 }
 
 static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta, hipStream_t s) {
-  const int Do = p.Do, Da = p.Da, H = p.H, Dq = Do + Da;
+  const int Do = p.Do, Da = p.Da, H = p.H, Dq = Do + Da, N = p.N;
   const oac_sac_layout& L = p.L;
   float* w = p.ws;
   {
     GemmBatch gb{};
-    gb.t[gb.ntasks++] = e_fwd(w + p.o_x, Do, p.pol + L.pol_fc0_w, Do, H, w + p.o_h1p, EPI_BIAS_RELU, p.pol + L.pol_fc0_b);
+    gb.t[gb.ntasks++] = e_fwd(w + p.o_x, Dq, N, Do, p.pol + L.pol_fc0_w, Do, H, w + p.o_h1p, EPI_BIAS_RELU, p.pol + L.pol_fc0_b);
     if (e_run(gb, s)) return 1;
   }
   {
     GemmBatch gb{};
-    gb.t[gb.ntasks++] = e_fwd(w + p.o_h1p, H, p.pol + L.pol_fc1_w, H, H, w + p.o_h2p, EPI_BIAS_RELU, p.pol + L.pol_fc1_b);
+    gb.t[gb.ntasks++] = e_fwd(w + p.o_h1p, H, N, H, p.pol + L.pol_fc1_w, H, H, w + p.o_h2p, EPI_BIAS_RELU, p.pol + L.pol_fc1_b);
     if (e_run(gb, s)) return 1;
   }
   {
     GemmBatch gb{};
-    gb.t[gb.ntasks++] = e_fwd(w + p.o_h2p, H, p.pol + L.pol_head_w, H, 2 * Da, w + p.o_head, EPI_BIAS, p.pol + L.pol_head_b);
+    gb.t[gb.ntasks++] = e_fwd(w + p.o_h2p, H, N, H, p.pol + L.pol_head_w, H, 2 * Da, w + p.o_head, EPI_BIAS, p.pol + L.pol_head_b);
     if (e_run(gb, s)) return 1;
   }
   OacArgs a;
@@ -94,27 +99,28 @@ static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta,
   a.head = w + p.o_head; a.xrow = w + p.o_x; a.stdv = w + p.o_std; a.mu_T = w + p.o_mut;
   a.q1 = w + p.o_q1; a.q2 = w + p.o_q2; a.w = w + p.o_w; a.da1 = w + p.o_da1; a.da2 = w + p.o_da2;
   a.eps = eps; a.grad = w + p.o_grad; a.mu_E = w + p.o_mue; a.action = w + p.o_act;
-  a.state = p.state; a.seed = p.seed; a.beta_UB = beta; a.sqrt_2delta = (float)std::sqrt(2.0 * (double)delta);
-  a.obs_dim = Do; a.act_dim = Da;
+  a.state = p.state; a.counter = reinterpret_cast<long long*>(w + p.o_cnt);
+  a.seed = p.seed; a.beta_UB = beta; a.sqrt_2delta = (float)std::sqrt(2.0 * (double)delta);
+  a.obs_dim = Do; a.act_dim = Da; a.n = N;
   OAC_HIP_CHECK(launch_oac_prep(a, s));
   const float* qs[2] = {p.q1, p.q2};
   const int64_t h1[2] = {p.o_h1q1, p.o_h1q2}, h2[2] = {p.o_h2q1, p.o_h2q2}, qo[2] = {p.o_q1, p.o_q2};
   {
     GemmBatch gb{};
     for (int i = 0; i < 2; ++i)
-      gb.t[gb.ntasks++] = e_fwd(w + p.o_x, Dq, qs[i] + L.q_fc0_w, Dq, H, w + h1[i], EPI_BIAS_RELU, qs[i] + L.q_fc0_b);
+      gb.t[gb.ntasks++] = e_fwd(w + p.o_x, Dq, N, Dq, qs[i] + L.q_fc0_w, Dq, H, w + h1[i], EPI_BIAS_RELU, qs[i] + L.q_fc0_b);
     if (e_run(gb, s)) return 1;
   }
   {
     GemmBatch gb{};
     for (int i = 0; i < 2; ++i)
-      gb.t[gb.ntasks++] = e_fwd(w + h1[i], H, qs[i] + L.q_fc1_w, H, H, w + h2[i], EPI_BIAS_RELU, qs[i] + L.q_fc1_b);
+      gb.t[gb.ntasks++] = e_fwd(w + h1[i], H, N, H, qs[i] + L.q_fc1_w, H, H, w + h2[i], EPI_BIAS_RELU, qs[i] + L.q_fc1_b);
     if (e_run(gb, s)) return 1;
   }
   {
     GemmBatch gb{};
     for (int i = 0; i < 2; ++i)
-      gb.t[gb.ntasks++] = e_fwd(w + h2[i], H, qs[i] + L.q_last_w, H, 1, w + qo[i], EPI_BIAS, qs[i] + L.q_last_b);
+      gb.t[gb.ntasks++] = e_fwd(w + h2[i], H, N, H, qs[i] + L.q_last_w, H, 1, w + qo[i], EPI_BIAS, qs[i] + L.q_last_b);
     if (e_run(gb, s)) return 1;
   }
   OAC_HIP_CHECK(launch_oac_seed(a, s));
@@ -123,10 +129,10 @@ static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta,
     GemmBatch gb{};
     for (int i = 0; i < 2; ++i) {
       GemmTask t = e_task();
-      t.a_mode = A_RANK1_MASK; t.a_s = w + p.o_w + i; t.a_v = qs[i] + L.q_last_w;
+      t.a_mode = A_RANK1_MASK; t.a_s = w + p.o_w + (long)i * N; t.a_v = qs[i] + L.q_last_w;
       t.a_mask = w + h2[i]; t.ld_mask = H; t.a_kc = 1;
       t.B = qs[i] + L.q_fc1_w; t.ldb = H; t.b_kc = 0;
-      t.C = w + dh[i]; t.ldc = H; t.M = 1; t.N = H; t.K = H;
+      t.C = w + dh[i]; t.ldc = H; t.M = N; t.N = H; t.K = H;
       t.epi = EPI_MASK; t.aux = w + h1[i]; t.ld_aux = H;
       gb.t[gb.ntasks++] = t;
     }
@@ -138,7 +144,7 @@ static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta,
       GemmTask t = e_task();
       t.A = w + dh[i]; t.lda = H; t.a_kc = 1;
       t.B = qs[i] + L.q_fc0_w + Do; t.ldb = Dq; t.b_kc = 0;
-      t.C = w + da[i]; t.ldc = Da; t.M = 1; t.N = Da; t.K = H; t.epi = EPI_STORE;
+      t.C = w + da[i]; t.ldc = Da; t.M = N; t.N = Da; t.K = H; t.epi = EPI_STORE;
       gb.t[gb.ntasks++] = t;
     }
     if (e_run(gb, s)) return 1;
@@ -157,24 +163,29 @@ struct oac_expl {
 
 extern "C" {
 
-int64_t oac_expl_workspace_floats(int obs_dim, int act_dim, int hidden) {
+int64_t oac_expl_workspace_floats_batch(int n_obs, int obs_dim, int act_dim, int hidden) {
   ExplPlan p;
-  p.Do = obs_dim; p.Da = act_dim; p.H = hidden;
+  p.Do = obs_dim; p.Da = act_dim; p.H = hidden; p.N = n_obs < 1 ? 1 : n_obs;
   expl_layout(p);
   return p.total;
 }
 
-int oac_expl_create(int obs_dim, int act_dim, int hidden, const float* policy, const float* q1,
-                    const float* q2, float* workspace, void* step_state, uint64_t seed,
-                    oac_expl** out) {
+int64_t oac_expl_workspace_floats(int obs_dim, int act_dim, int hidden) {
+  return oac_expl_workspace_floats_batch(1, obs_dim, act_dim, hidden);
+}
+
+int oac_expl_create_batch(int n_obs, int obs_dim, int act_dim, int hidden, const float* policy,
+                          const float* q1, const float* q2, float* workspace, void* step_state,
+                          uint64_t seed, oac_expl** out) {
   if (!policy || !q1 || !q2 || !workspace || !step_state || !out) {
     set_error("oac_expl_create: null pointer");
     return 1;
   }
   if (act_dim < 1 || act_dim > 63) { set_error("act_dim must be in [1, 63]"); return 1; }
+  if (n_obs < 1 || n_obs > 65536) { set_error("n_obs must be in [1, 65536]"); return 1; }
   oac_expl* h = new oac_expl();
   ExplPlan& p = h->p;
-  p.Do = obs_dim; p.Da = act_dim; p.H = hidden;
+  p.Do = obs_dim; p.Da = act_dim; p.H = hidden; p.N = n_obs;
   p.pol = policy; p.q1 = q1; p.q2 = q2; p.ws = workspace;
   p.state = reinterpret_cast<StepState*>(step_state); p.seed = seed;
   oac_sac_config c;
@@ -187,6 +198,13 @@ int oac_expl_create(int obs_dim, int act_dim, int hidden, const float* policy, c
   expl_layout(p);
   *out = h;
   return 0;
+}
+
+int oac_expl_create(int obs_dim, int act_dim, int hidden, const float* policy, const float* q1,
+                    const float* q2, float* workspace, void* step_state, uint64_t seed,
+                    oac_expl** out) {
+  return oac_expl_create_batch(1, obs_dim, act_dim, hidden, policy, q1, q2, workspace, step_state,
+                               seed, out);
 }
 
 int oac_expl_destroy(oac_expl* h) {
@@ -220,7 +238,7 @@ int oac_expl_action(oac_expl* h, const float* eps, float beta_UB, float delta, f
     p.gstream = s; p.g_eps = eps; p.g_beta = beta_UB; p.g_delta = delta;
   }
   OAC_HIP_CHECK(hipGraphLaunch(p.exec, s));
-  const size_t nb = sizeof(float) * p.Da;
+  const size_t nb = sizeof(float) * p.Da * p.N;
   if (action) OAC_HIP_CHECK(hipMemcpyAsync(action, p.ws + p.o_act, nb, hipMemcpyDeviceToDevice, s));
   if (mu_E) OAC_HIP_CHECK(hipMemcpyAsync(mu_E, p.ws + p.o_mue, nb, hipMemcpyDeviceToDevice, s));
   if (std_out) OAC_HIP_CHECK(hipMemcpyAsync(std_out, p.ws + p.o_std, nb, hipMemcpyDeviceToDevice, s));

@@ -98,19 +98,20 @@ struct PolicyHeadBwdArgs {
   float* dhead;         // [B, 2Da]
 };
 
-struct OacArgs {
-  const float* head;    // [2Da] policy head of the observation
-  float* xrow;          // [Do+Da] critic input row: ob | tanh(mu_T)
-  float* stdv; float* mu_T;
-  const float* q1; const float* q2;
-  float* w;             // [2] dQ_UB/dQ_i
-  const float* da1; const float* da2;
-  const float* eps;     // [Da] or null -> Philox
-  float* grad; float* mu_E; float* action;
+struct OacArgs {                        // N observations, one block per row
+  const float* head;    // [N, 2Da] policy heads of the observations
+  float* xrow;          // [N, Do+Da] critic input rows: ob | tanh(mu_T)
+  float* stdv; float* mu_T;               // [N, Da]
+  const float* q1; const float* q2;       // [N]
+  float* w;             // [2, N] dQ_UB/dQ_i
+  const float* da1; const float* da2;     // [N, Da]
+  const float* eps;     // [N, Da] or null -> Philox
+  float* grad; float* mu_E; float* action;   // [N, Da]
   StepState* state;
+  long long* counter;   // Philox counter snapshot of this call (prep writes, final reads)
   unsigned long long seed;
   float beta_UB, sqrt_2delta;
-  int obs_dim, act_dim;
+  int obs_dim, act_dim, n;
 };
 
 // ------------------------------------------------------------ replay/adam

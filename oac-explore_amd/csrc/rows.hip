@@ -116,30 +116,34 @@ __global__ void __launch_bounds__(256) policy_head_backward_kernel(PolicyHeadBwd
 }
 
 // --------------------------------------------------------------------------
-// OAC exploration (optimistic_exploration.py:14-109), batch 1.
+// OAC exploration (optimistic_exploration.py:14-109) for N observations
+// (one block per row; N = 1 is the reference's per-step call, N > 1 the
+// vectorised-rollout extension -- each row is computed exactly as alone).
 // prep: from the policy head (mean | ls_raw) of one observation:
 //   std = exp(clamp(ls_raw)); a = tanh(mu_T) written into the critic input row
-//   after the observation; the critic seeds w1, w2 = dQ_UB/dQ1, dQ_UB/dQ2 are
-//   computed by oac_seed_kernel once Q1, Q2 are known.
+//   after the observation; block 0 snapshots the Philox counter of the call.
+// seed: w1, w2 = dQ_UB/dQ1, dQ_UB/dQ2 once Q1, Q2 are known.
 // --------------------------------------------------------------------------
 __global__ void oac_prep_kernel(OacArgs p) {
-  const int j = threadIdx.x;
-  if (j >= p.act_dim) return;
-  const float mean = p.head[j];
-  const float ls = fminf(fmaxf(p.head[p.act_dim + j], -20.f), 2.f);
-  p.stdv[j] = expf(ls);
-  p.mu_T[j] = mean;
-  p.xrow[p.obs_dim + j] = tanhf(mean);
+  const int r = blockIdx.x, j = threadIdx.x, Da = p.act_dim;
+  if (r == 0 && j == 0) *p.counter = p.state->expl_counter;
+  if (j >= Da) return;
+  const float mean = p.head[(long)r * 2 * Da + j];
+  const float ls = fminf(fmaxf(p.head[(long)r * 2 * Da + Da + j], -20.f), 2.f);
+  p.stdv[(long)r * Da + j] = expf(ls);
+  p.mu_T[(long)r * Da + j] = mean;
+  p.xrow[(long)r * (p.obs_dim + Da) + p.obs_dim + j] = tanhf(mean);
 }
 
 __global__ void oac_seed_kernel(OacArgs p) {
-  if (threadIdx.x != 0) return;
+  const int r = blockIdx.x * 64 + threadIdx.x;
+  if (r >= p.n) return;
   // Q_UB = (Q1+Q2)/2 + beta*|Q1-Q2|/2 ; d|x|/dx = sign(x) (0 at 0)
-  const float d = p.q1[0] - p.q2[0];
+  const float d = p.q1[r] - p.q2[r];
   const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
   const float hb = p.beta_UB / 2.f;
-  p.w[0] = 0.5f + hb * sg;
-  p.w[1] = 0.5f - hb * sg;
+  p.w[r] = 0.5f + hb * sg;
+  p.w[p.n + r] = 0.5f - hb * sg;
 }
 
 // final: grad = (da1 + da2) * (1 - a^2); Sigma = std^2;
@@ -147,13 +151,14 @@ __global__ void oac_seed_kernel(OacArgs p) {
 //   mu_E = mu_T + mu_C;  action = tanh(eps*std + mu_E)
 __global__ void oac_final_kernel(OacArgs p) {
   __shared__ float red[64];
-  const int j = threadIdx.x;
+  const int r = blockIdx.x, j = threadIdx.x;
   const int Da = p.act_dim;
+  const long e = (long)r * Da + j;
   float g = 0.f, sig = 0.f;
   if (j < Da) {
-    const float a = p.xrow[p.obs_dim + j];
-    g = (p.da1[j] + p.da2[j]) * (1.f - a * a);
-    sig = p.stdv[j] * p.stdv[j];
+    const float a = p.xrow[(long)r * (p.obs_dim + Da) + p.obs_dim + j];
+    g = (p.da1[e] + p.da2[e]) * (1.f - a * a);
+    sig = p.stdv[e] * p.stdv[e];
     red[j] = g * g * sig;
   }
   __syncthreads();
@@ -166,16 +171,15 @@ __global__ void oac_final_kernel(OacArgs p) {
   if (j < Da) {
     const float denom = red[63];
     const float mu_C = (p.sqrt_2delta * (sig * g)) / denom;
-    const float mu_E = p.mu_T[j] + mu_C;
-    float e;
-    if (p.eps) e = p.eps[j];
-    else e = philox_normal(p.seed, (unsigned long long)p.state->expl_counter, 3u, (unsigned)j);
-    p.grad[j] = g;
-    p.mu_E[j] = mu_E;
-    p.action[j] = tanhf(add_rn(mul_rn(e, p.stdv[j]), mu_E));
+    const float mu_E = p.mu_T[e] + mu_C;
+    float ev;
+    if (p.eps) ev = p.eps[e];
+    else ev = philox_normal(p.seed, (unsigned long long)*p.counter, 3u, (unsigned)(r * Da + j));
+    p.grad[e] = g;
+    p.mu_E[e] = mu_E;
+    p.action[e] = tanhf(add_rn(mul_rn(ev, p.stdv[e]), mu_E));
   }
-  __syncthreads();
-  if (j == 0 && !p.eps) p.state->expl_counter += 1;
+  if (r == 0 && j == 0 && !p.eps) p.state->expl_counter = *p.counter + 1;
 }
 
 }  // namespace oac
@@ -202,15 +206,15 @@ hipError_t launch_policy_head_backward(const PolicyHeadBwdArgs& a, hipStream_t s
   return hipGetLastError();
 }
 hipError_t launch_oac_prep(const OacArgs& a, hipStream_t s) {
-  OAC_LAUNCH(oac_prep_kernel, dim3(1), dim3(64), 0, s, a);
+  OAC_LAUNCH(oac_prep_kernel, dim3(a.n), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_oac_seed(const OacArgs& a, hipStream_t s) {
-  OAC_LAUNCH(oac_seed_kernel, dim3(1), dim3(64), 0, s, a);
+  OAC_LAUNCH(oac_seed_kernel, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_oac_final(const OacArgs& a, hipStream_t s) {
-  OAC_LAUNCH(oac_final_kernel, dim3(1), dim3(64), 0, s, a);
+  OAC_LAUNCH(oac_final_kernel, dim3(a.n), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

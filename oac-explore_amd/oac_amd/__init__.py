@@ -11,6 +11,7 @@ from ._lib import lib, LIB_PATH  # noqa: F401
 from .trainer import SACTrainer, row_layout  # noqa: F401
 from .particle_trainer import ParticleTrainer  # noqa: F401
 from .replay_buffer import ReplayBuffer, ReplayBufferCount, DeviceBatch, DeviceIndexStream  # noqa: F401
-from .optimistic_exploration import get_optimistic_exploration_action  # noqa: F401
+from .optimistic_exploration import (get_optimistic_exploration_action,  # noqa: F401
+                                     get_optimistic_exploration_actions)
 from .producers import get_policy_producer, get_q_producer  # noqa: F401
 from .networks import MakeDeterministic  # noqa: F401

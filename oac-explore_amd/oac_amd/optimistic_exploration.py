@@ -3,7 +3,9 @@
 computed by liboac_amd's batch-1 kernel sequence (csrc/expl_plan.hip).
 
 Same signature and return value as the reference: ``(action float32[Da], {})``
-for a 1-D observation.  ``policy`` must be the policy of an oac_amd trainer
+for a 1-D observation.  ``get_optimistic_exploration_actions`` is the
+vectorised-rollout extension: N observations [N, Do] in one launch
+sequence, each row exactly as a single call.  ``policy`` must be the policy of an oac_amd trainer
 (its parameters live in the trainer's HBM arena, which the kernels read in
 place); there is no torch/CPU fallback.
 """
@@ -42,14 +44,35 @@ def get_optimistic_exploration_action(ob_np, policy=None, qfs=None, trainer=None
     t = _owner(policy, qfs, trainer)
     if hyper_params.get("share_layers", False):
         raise NotImplementedError("share_layers OAC shift: use oac_amd.ParticleTrainer")
-    h, ws, slot, out = t._expl_handle()
+    a, info = _actions(t, np.asarray(ob_np)[None, :], hyper_params,
+                       None if eps is None else np.asarray(eps, np.float32)[None, :], return_info)
+    return a[0], {k: v[0] for k, v in info.items()}
+
+
+def get_optimistic_exploration_actions(obs_np, policy=None, qfs=None, trainer=None,
+                                       hyper_params=None, eps=None, return_info=False):
+    """Vectorised get_optimistic_exploration_action: ``obs_np`` [N, Do] (one
+    row per parallel environment) -> (actions float32 [N, Da], info).  The
+    Philox draws of a call use one counter value (row r takes elements
+    r*Da .. r*Da+Da-1 of the stream); ``eps`` [N, Da] replaces them."""
+    assert np.ndim(obs_np) == 2
+    t = _owner(policy, qfs, trainer)
+    if hyper_params.get("share_layers", False):
+        raise NotImplementedError("share_layers OAC shift: use oac_amd.ParticleTrainer")
+    return _actions(t, np.asarray(obs_np), hyper_params,
+                    None if eps is None else np.asarray(eps, np.float32), return_info)
+
+
+def _actions(t, obs, hyper_params, eps, return_info):
+    n = obs.shape[0]
+    h, ws, slot, out = t._expl_handle(n)
 
     def go(sp):
-        slot.copy_(torch.as_tensor(np.asarray(ob_np)).to(torch.float32), non_blocking=False)
+        slot.copy_(torch.as_tensor(obs).to(torch.float32), non_blocking=False)
         e = None
         if eps is not None:
             e = out[3]
-            e.copy_(torch.as_tensor(np.asarray(eps, np.float32)))
+            e.copy_(torch.as_tensor(eps).reshape(e.shape))
         check(_lib.lib().oac_expl_action(h, ptr(e), float(hyper_params["beta_UB"]),
                                          float(hyper_params["delta"]), ptr(out[0]), ptr(out[1]),
                                          ptr(out[2]), None, sp))

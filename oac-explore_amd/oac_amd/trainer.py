@@ -205,8 +205,8 @@ class _ArenaTrainer(object):
             L = _lib.lib()
             for p in self._plans.values():
                 L.oac_sac_destroy(p.handle)
-            if self._expl is not None:
-                L.oac_expl_destroy(self._expl[0])
+            for e in (self._expl or {}).values():
+                L.oac_expl_destroy(e[0])
         except Exception:
             pass
 
@@ -463,20 +463,25 @@ class SACTrainer(_ArenaTrainer):
         self.step_state[0] = self._n_train_steps_total
 
     # ------------------------------------------------------------ exploration
-    def _expl_handle(self):
+    def _expl_handle(self, n=1):
+        """Exploration plan for n observations per call (cached per n):
+        (handle, workspace, obs slot view [n, obs_dim], outputs [4, n, act_dim])."""
         if self._expl is None:
+            self._expl = {}
+        if n not in self._expl:
             L = _lib.lib()
-            n = L.oac_expl_workspace_floats(self.obs_dim, self.act_dim, self.hidden)
-            ws = torch.zeros(int(n), dtype=torch.float32, device=self.device)
-            out = torch.zeros(4, self.act_dim, dtype=torch.float32, device=self.device)
+            nf = L.oac_expl_workspace_floats_batch(n, self.obs_dim, self.act_dim, self.hidden)
+            ws = torch.zeros(int(nf), dtype=torch.float32, device=self.device)
+            out = torch.zeros(4, n, self.act_dim, dtype=torch.float32, device=self.device)
             h = ctypes.c_void_p()
             p = self.params
-            check(L.oac_expl_create(self.obs_dim, self.act_dim, self.hidden, ptr(p),
-                                    ctypes.c_void_p(p.data_ptr() + 4 * self.layout.q1_base),
-                                    ctypes.c_void_p(p.data_ptr() + 4 * self.layout.q2_base),
-                                    ptr(ws), ptr(self.step_state), ctypes.c_uint64(self.seed + 1),
-                                    ctypes.byref(h)))
+            check(L.oac_expl_create_batch(n, self.obs_dim, self.act_dim, self.hidden, ptr(p),
+                                          ctypes.c_void_p(p.data_ptr() + 4 * self.layout.q1_base),
+                                          ctypes.c_void_p(p.data_ptr() + 4 * self.layout.q2_base),
+                                          ptr(ws), ptr(self.step_state),
+                                          ctypes.c_uint64(self.seed + 1), ctypes.byref(h)))
             slot_addr = L.oac_expl_obs_slot(h)
-            slot = ws[(slot_addr - ws.data_ptr()) // 4:][:self.obs_dim]
-            self._expl = (h, ws, slot, out)
-        return self._expl
+            off = (slot_addr - ws.data_ptr()) // 4
+            rows = ws[off:off + n * (self.obs_dim + self.act_dim)].view(n, self.obs_dim + self.act_dim)
+            self._expl[n] = (h, ws, rows[:, :self.obs_dim], out)
+        return self._expl[n]

@@ -157,3 +157,33 @@ def test_oac_exploration_matches_reference_golden(name):
         assert parity.rel_err(info["std"], g["std"][i]) <= 1e-5
         assert parity.rel_err(info["mu_E"], g["mu_E"][i]) <= parity.TOL
         assert parity.rel_err(a, g["action"][i]) <= parity.TOL
+
+
+@pytest.mark.parametrize("name", ["oac_expl_humanoid", "oac_expl_small"])
+def test_batched_oac_exploration_equals_single_calls(name):
+    """Vectorised rollouts: all n_obs observations in one call match the
+    reference golden and are bitwise the single-observation calls."""
+    from oac_amd import get_optimistic_exploration_action, get_optimistic_exploration_actions
+    meta, g = parity.load(name)
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                        pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"])
+    m = dict(obs_dim=meta["obs_dim"], act_dim=meta["act_dim"], hidden=meta["hidden"],
+             discount=0.99, reward_scale=1.0, lr=3e-4, tau=5e-3, auto_alpha=True, log_alpha0=0.0,
+             seed=meta["seed"], pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"])
+    tr = sac_trainer_for(m, params=params)
+    hp = dict(beta_UB=meta["beta_UB"], delta=meta["delta"], share_layers=False)
+    A, info = get_optimistic_exploration_actions(g["obs"], policy=tr.policy, qfs=tr.qfs,
+                                                 hyper_params=hp, eps=g["eps"], return_info=True)
+    assert A.shape == (meta["n_obs"], meta["act_dim"]) and A.dtype == np.float32
+    for i in range(meta["n_obs"]):
+        assert parity.rel_err(A[i], g["action"][i]) <= parity.TOL
+        assert parity.rel_err(info["mu_E"][i], g["mu_E"][i]) <= parity.TOL
+        a, _ = get_optimistic_exploration_action(g["obs"][i], policy=tr.policy, qfs=tr.qfs,
+                                                 hyper_params=hp, eps=g["eps"][i])
+        np.testing.assert_array_equal(a, A[i])
+    # Philox path: finite, in (-1, 1), distinct rows, counter advanced once per call
+    c0 = int(tr.step_state[2].item())
+    A2, _ = get_optimistic_exploration_actions(g["obs"], policy=tr.policy, qfs=tr.qfs,
+                                               hyper_params=hp)
+    assert np.isfinite(A2).all() and np.abs(A2).max() < 1
+    assert int(tr.step_state[2].item()) == c0 + 1
