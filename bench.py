@@ -173,6 +173,32 @@ def cpu_baseline(args):
                        f"{args.cpu_threads} thread(s))")
 
 
+def exploration_timing(tr, obs_dim, reps=200):
+    """get_optimistic_exploration_action latency (one observation, the
+    reference's per-env-step call; beta_UB 4.66, delta 23.53) and the
+    vectorised throughput at 64 observations per call -- host wall time per
+    call including the H2D observation copy and the D2H action copy."""
+    from oac_amd import get_optimistic_exploration_action, get_optimistic_exploration_actions
+    hp = dict(beta_UB=4.66, delta=23.53, share_layers=False)
+    rs = np.random.RandomState(0)
+    ob = rs.standard_normal(obs_dim)
+    obs64 = rs.standard_normal((64, obs_dim))
+    for _ in range(20):
+        get_optimistic_exploration_action(ob, policy=tr.policy, qfs=tr.qfs, hyper_params=hp)
+        get_optimistic_exploration_actions(obs64, policy=tr.policy, qfs=tr.qfs, hyper_params=hp)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        get_optimistic_exploration_action(ob, policy=tr.policy, qfs=tr.qfs, hyper_params=hp)
+    t1 = time.perf_counter()
+    for _ in range(reps):
+        get_optimistic_exploration_actions(obs64, policy=tr.policy, qfs=tr.qfs, hyper_params=hp)
+    t2 = time.perf_counter()
+    return {"us_per_call_1obs": round(1e6 * (t1 - t0) / reps, 1),
+            "actions_per_s_64obs": round(64 * reps / (t2 - t1), 1),
+            "beta_UB": 4.66, "delta": 23.53}
+
+
 def load_traffic(B):
     path = os.path.join(ROOT, "profiles", "pmc_gemm_traffic.json")
     try:
@@ -270,6 +296,8 @@ def main():
             out["gather_GBps"] = round(GATHER_BYTES_PER_SAMPLE * B / (ga["avg_us"] * 1e-6) / 1e9, 1)
         if ad["launches"]:
             out["adam_GBps"] = round(ADAM_BYTES_PER_STEP * args.timing_steps / (ad["ms"] * 1e-3) / 1e9, 1)
+        if world == 1:
+            out["exploration"] = exploration_timing(tr, args.obs_dim)
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
