@@ -15,7 +15,7 @@ import torch
 
 from . import _lib
 from .networks import ArenaFlattenMlp, ArenaTanhGaussianPolicy
-from .trainer import AdamStateView, _ArenaTrainer, _dims_from_state, _twin_views
+from .trainer import AdamStateView, _ArenaTrainer, _dims_from_state, _twin_views, _plain_stats
 
 
 class ParticleTrainer(_ArenaTrainer):
@@ -169,7 +169,7 @@ class ParticleTrainer(_ArenaTrainer):
     def get_snapshot(self):
         data = dict(policy_state_dict=self.policy.state_dict(),
                     policy_optim_state_dict=self.policy_optimizer.state_dict(),
-                    eval_statistics=self.eval_statistics,
+                    eval_statistics=_plain_stats(self.eval_statistics),
                     _n_train_steps_total=self._n_train_steps_total,
                     _need_to_update_eval_statistics=self._need_to_update_eval_statistics)
         if self.use_automatic_entropy_tuning:

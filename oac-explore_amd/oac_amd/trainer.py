@@ -68,6 +68,16 @@ def _twin_views(arena, other, params):
     return out
 
 
+def _plain_stats(st):
+    """eval_statistics with numpy scalars as Python floats (same values, same
+    key order): the checkpoint then loads with torch.load(weights_only=True)."""
+    from collections import OrderedDict
+    if st is None:
+        return st
+    return OrderedDict((k, float(v) if isinstance(v, (np.generic, float, int)) else v)
+                       for k, v in st.items())
+
+
 class AdamStateView:
     """torch.optim.Adam-compatible ``state_dict`` over the m / v arenas.  The
     update itself is fused into the step kernels; ``step``/``zero_grad`` are
@@ -437,7 +447,7 @@ class SACTrainer(_ArenaTrainer):
             qf2_state_dict=self.qf2.state_dict(),
             qf2_optim_state_dict=self.qf2_optimizer.state_dict(),
             target_qf2_state_dict=self.target_qf2.state_dict(),
-            eval_statistics=self.eval_statistics,
+            eval_statistics=_plain_stats(self.eval_statistics),
             _n_train_steps_total=self._n_train_steps_total,
             _need_to_update_eval_statistics=self._need_to_update_eval_statistics,
         )

@@ -423,6 +423,59 @@ def gen_replay_count(priority):
     return meta, out
 
 
+# ------------------------------------------------------------ checkpoint
+def _plain(x):
+    """A snapshot in types torch.load(weights_only=True) accepts."""
+    if isinstance(x, dict):
+        return {k: _plain(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_plain(v) for v in x)
+    if isinstance(x, torch.Tensor):
+        return x.detach().clone()
+    if isinstance(x, np.generic):
+        return x.item()
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(x.copy())
+    return x
+
+
+def gen_sac_snapshot(path, obs_dim=11, act_dim=3, hidden=(32, 32), B=16, seed=7):
+    """The reference SACTrainer's checkpoint (trainer/trainer.py:299-317,
+    restored by :319-369) after two steps, and the third step it then takes:
+    its batch indices, eps draws and the post-step parameters."""
+    pp, qp = _producers(obs_dim, act_dim, list(hidden))
+    torch.manual_seed(0)
+    tr = SACTrainer(pp, qp, action_space=Box(-1, 1, (act_dim,)), discount=0.99, reward_scale=1.0,
+                    policy_lr=3e-4, qf_lr=3e-4, optimizer_class=Adam14, soft_target_tau=5e-3,
+                    target_update_period=1, use_automatic_entropy_tuning=True)
+    params = sac_params(obs_dim, act_dim, list(hidden), seed, pi_init_w=0.2, q_init_w=0.1)
+    load_sd(tr.policy, params["policy"])
+    for k in ("qf1", "qf2", "target_qf1", "target_qf2"):
+        load_sd(getattr(tr, k), params[k])
+    rb, _ = _fill_buffer(obs_dim, act_dim, 300)
+    np.random.seed(3)
+    torch.manual_seed(4)
+    for s in range(2):
+        batch, _ = _record_batch(rb, B)
+        tr.end_epoch(s)
+        tr.train(dict(batch))
+    snap = _plain(tr.get_snapshot())
+    EPS_LOG.clear()
+    batch, idx = _record_batch(rb, B)
+    tr.end_epoch(2)
+    tr.train(dict(batch))
+    post = {g: {k: v.detach().clone() for k, v in getattr(tr, g).state_dict().items()}
+            for g in ("policy", "qf1", "qf2", "target_qf1", "target_qf2")}
+    fixture = dict(meta=dict(obs_dim=obs_dim, act_dim=act_dim, hidden=list(hidden), B=B, seed=seed,
+                             pi_init_w=0.2, q_init_w=0.1, n_replay=300, lr=3e-4, tau=5e-3),
+                   snapshot=snap, step3=dict(idx=torch.from_numpy(idx.astype(np.int64)),
+                                             eps1=torch.from_numpy(EPS_LOG[0]),
+                                             eps2=torch.from_numpy(EPS_LOG[1]), post=post,
+                                             log_alpha=tr.log_alpha.detach().clone()))
+    torch.save(fixture, path)
+    print(f"{os.path.basename(path)}: {os.path.getsize(path) / 1e3:.0f} KB")
+
+
 def save(name, meta, out):
     import json
     out = dict(out)
@@ -434,6 +487,9 @@ def save(name, meta, out):
 
 def main():
     torch.set_num_threads(8)
+    if len(sys.argv) > 1 and sys.argv[1] == "sac_snapshot":
+        gen_sac_snapshot(os.path.join(HERE, "sac_snapshot.pt"))
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "poac_counts":
         save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
                                       pi_init_w=0.3, counts=True))
@@ -463,6 +519,7 @@ def main():
     save("replay_count_priority", *gen_replay_count(True))
     save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
                                   pi_init_w=0.3, counts=True))
+    gen_sac_snapshot(os.path.join(HERE, "sac_snapshot.pt"))
 
 
 if __name__ == "__main__":
