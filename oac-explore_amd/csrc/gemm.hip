@@ -341,18 +341,14 @@ __global__ void __launch_bounds__(256) gemm_grouped_kernel(const GemmBatch batch
 // LDS-tiled kernel for the large-batch stages (cfg 1); cfg 0 is the
 // latency-optimised register-direct kernel of gemm_small.hip.
 using CfgLarge = GemmCfg<64, 64, 32, 2, 2, 1>;
-using CfgL2 = GemmCfg<128, 128, 16, 2, 2, 1>;
-using CfgL3 = GemmCfg<128, 128, 32, 2, 2, 1>;
-using CfgL4 = GemmCfg<128, 64, 32, 2, 2, 1>;
 
-int gemm_tile_m(int cfg) {
-  switch (cfg) { case 0: return 32; case 2: return CfgL2::kBM; case 3: return CfgL3::kBM;
-                 case 4: return CfgL4::kBM; default: return CfgLarge::kBM; }
-}
-int gemm_tile_n(int cfg) {
-  switch (cfg) { case 0: return 32; case 2: return CfgL2::kBN; case 3: return CfgL3::kBN;
-                 case 4: return CfgL4::kBN; default: return CfgLarge::kBN; }
-}
+// cfg 2: the register-direct kernel of gemm_big.hip (128 x 128 workgroup tiles)
+int gemm_big_tile_m();
+int gemm_big_tile_n();
+hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s);
+
+int gemm_tile_m(int cfg) { return cfg == 0 ? 32 : cfg == 2 ? gemm_big_tile_m() : CfgLarge::kBM; }
+int gemm_tile_n(int cfg) { return cfg == 0 ? 32 : cfg == 2 ? gemm_big_tile_n() : CfgLarge::kBN; }
 
 void gemm_small_finalize(GemmBatch& b);
 hipError_t gemm_small_launch(const GemmBatch& b, hipStream_t s);
@@ -381,12 +377,8 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   for (int i = 0; i < b.ntasks; ++i)               // dual products / head backward: small kernel
     if (b.t[i].K2 > 0 || b.t[i].epi == EPI_HEAD_BWD || b.t[i].epi == EPI_BIAS_RELU_DOT)
       return hipErrorInvalidValue;
-  switch (cfg) {
-    case 2: OAC_LAUNCH(gemm_grouped_kernel<CfgL2>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-    case 3: OAC_LAUNCH(gemm_grouped_kernel<CfgL3>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-    case 4: OAC_LAUNCH(gemm_grouped_kernel<CfgL4>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-    default: OAC_LAUNCH(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-  }
+  if (cfg == 2) return gemm_big_launch(b, s);
+  OAC_LAUNCH(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 

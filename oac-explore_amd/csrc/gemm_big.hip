@@ -1,0 +1,239 @@
+// Register-direct grouped fp32 GEMM for the forward products of the
+// large-batch stages (B >= 1024: BASELINE configs 2-4), gemm_cfg 2 (the
+// backward products stay on the LDS kernel, plan_common.h launch_cfg).
+//
+// The LDS-staged 64x64 kernel (gemm.hip) reached ~21 % of the fp32 MFMA peak
+// at B=4096: one barrier per 32-deep K block, dword staging loads and one
+// 32x32 accumulator per wave.  Here every wave owns a (32 WM) x (32 WN) output
+// block -- WM x WN accumulators of v_mfma_f32_32x32x2_f32 -- and feeds the
+// MFMAs straight from L2 into VGPRs (gemm_operand.h: a k-contiguous operand is
+// one 16-byte load per lane per 4 MFMAs), so per 8-deep k-group a lane issues
+// WM + WN loads for 4 WM WN MFMAs, with no LDS and no barrier: the waves of
+// a workgroup run independently and the next group's loads are in flight
+// while the current group's MFMAs issue (register double buffer).  Four
+// waves (2 x 2) form a (64 WM) x (64 WN) workgroup tile so neighbouring waves
+// share operand lines in L1/L2.  Split-K (the dW tasks, K = batch) writes
+// slabs exactly like the other kernels; every epilogue reads the accumulator
+// registers directly.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "oac_common.h"
+#include "kernels.h"
+#include "gemm_operand.h"
+#include "adam_common.h"
+
+namespace oac {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+template <int AK, int BK, int WM, int WN>
+struct Frag {
+  float ax[WM][4], ay[WM][4], bx[WN][4], by[WN][4];
+};
+
+template <int AK, int BK, int WM, int WN>
+__device__ __forceinline__ void frag_load(const Lane (&la)[WM], const Lane (&lb)[WN], int g, int half,
+                                          int kmax, Frag<AK, BK, WM, WN>& f) {
+  const int kb = 8 * g + 4 * half;
+#pragma unroll
+  for (int i = 0; i < WM; ++i) load4<AK>(la[i], kb, kmax, f.ax[i], f.ay[i]);
+#pragma unroll
+  for (int j = 0; j < WN; ++j) load4<BK>(lb[j], kb, kmax, f.bx[j], f.by[j]);
+}
+
+template <int AK, int BK, int WM, int WN>
+__device__ __forceinline__ void frag_mma(const Lane (&la)[WM], const Lane (&lb)[WN], int g, int half,
+                                         int k_lo, int k_hi, const Frag<AK, BK, WM, WN>& f,
+                                         floatx16 (&acc)[WM][WN]) {
+  const int kb = 8 * g + 4 * half;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float a[WM], b[WN];
+#pragma unroll
+    for (int i = 0; i < WM; ++i)   // k < k_lo: a continuation pass's first group (A side only)
+      a[i] = kb + c >= k_lo ? fix1<AK>(la[i], kb + c, k_hi, f.ax[i][c], f.ay[i][c]) : 0.f;
+#pragma unroll
+    for (int j = 0; j < WN; ++j) b[j] = fix1<BK>(lb[j], kb + c, k_hi, f.bx[j][c], f.by[j][c]);
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// acc += A[mw.., k_lo..k_hi) . B[k_lo..k_hi), nw..] over this wave's block
+template <int AK, int BK, int WM, int WN, int PF = 2>
+__device__ __forceinline__ void rd_loop(const GemmTask& t, const float* A, long lda, const float* Bp,
+                                        long ldb, int M, int Nlanes, bool ones, int mw, int nw,
+                                        int k_lo, int k_hi, floatx16 (&acc)[WM][WN]) {
+  const int lane = threadIdx.x & 63;
+  const int l32 = lane & 31, half = lane >> 5;
+  const bool ar1 = (AK == OP_KC_R1 || AK == OP_MN_R1);
+  Lane la[WM], lb[WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+    la[i] = lane_init<AK>(mw + 32 * i + l32, M, false, ar1 ? t.a_mask : A, ar1 ? t.ld_mask : lda,
+                          t.a_s, t.a_v);
+#pragma unroll
+  for (int j = 0; j < WN; ++j)
+    lb[j] = lane_init<BK>(nw + 32 * j + l32, Nlanes, ones, Bp, ldb, nullptr, nullptr);
+  const int g_lo = k_lo >> 3, g_hi = (k_hi + 7) >> 3, kmax = k_hi - 1;
+  if (g_lo >= g_hi) return;
+  // PF k-groups in flight: group g + PF is requested as soon as group g's
+  // fragments are consumed
+  Frag<AK, BK, WM, WN> f[PF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q)
+    if (g_lo + q < g_hi) frag_load<AK, BK, WM, WN>(la, lb, g_lo + q, half, kmax, f[q]);
+#pragma unroll 1
+  for (int g = g_lo; g < g_hi; g += PF) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      if (g + q < g_hi) {
+        frag_mma<AK, BK, WM, WN>(la, lb, g + q, half, k_lo, k_hi, f[q], acc);
+        if (g + q + PF < g_hi) frag_load<AK, BK, WM, WN>(la, lb, g + q + PF, half, kmax, f[q]);
+      }
+    }
+  }
+}
+
+// element (m, n) of an accumulator register: lane l, register r of a 32x32 block
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+template <int WM, int WN>
+__device__ __forceinline__ void rd_epilogue(const GemmTask& t, int mw, int nw,
+                                            const floatx16 (&acc)[WM][WN], bool second) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int n = nw + 32 * j + (lane & 31);
+    if (n >= t.N) continue;
+    float bias = 0.f;
+    if (t.epi == EPI_BIAS || t.epi == EPI_BIAS_RELU || t.epi == EPI_BIAS_RANK_RELU) bias = t.bias[n];
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = mw + 32 * i + acc_row(r, lane);
+        if (m >= t.M) continue;
+        const float v = acc[i][j][r];
+        const long o = (long)m * t.ldc + n;
+        switch (t.epi) {
+          case EPI_STORE: t.C[o] = v; break;
+          case EPI_GRAD:
+            if (t.b_ones && n == t.N - 1) t.bias_grad[m] = v;
+            else t.C[o] = v;
+            break;
+          case EPI_BIAS: t.C[o] = v + bias; break;
+          case EPI_BIAS_RELU: t.C[o] = fmaxf(v + bias, 0.f); break;
+          case EPI_BIAS_RANK_RELU:   // pass 1: C = X W^T + b ; pass 2 (acc += U V^T): C2 = relu(. + b)
+            if (!second) t.C[o] = v + bias;
+            else t.C2[(long)m * t.ldc2 + n] = fmaxf(v + bias, 0.f);
+            break;
+          case EPI_ADD_RELU: t.C[o] = fmaxf(v + t.aux[(long)m * t.ld_aux + n], 0.f); break;
+          case EPI_MASK: t.C[o] = t.aux[(long)m * t.ld_aux + n] > 0.f ? v : 0.f; break;
+          default: break;
+        }
+      }
+  }
+}
+
+template <int WM, int WN>
+__global__ void __launch_bounds__(256)
+gemm_big_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
+                const GemmBatch batch) {
+  const int bid = blockIdx.x;
+  if (batch.publish && bid == 0 && threadIdx.x == 0)
+    publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
+  if (bid >= total_tiles) return;
+  int ti = 0;   // task from the preloaded tile starts
+  ti = bid >= tb1 ? 1 : ti; ti = bid >= tb2 ? 2 : ti; ti = bid >= tb3 ? 3 : ti;
+  ti = bid >= tb4 ? 4 : ti; ti = bid >= tb5 ? 5 : ti; ti = bid >= tb6 ? 6 : ti;
+  ti = bid >= tb7 ? 7 : ti;
+  ti = __builtin_amdgcn_readfirstlane(ti);
+  GemmTask t = batch.t[ti];
+  int local = bid - t.tile_begin;
+  int k_lo = 0, k_hi = t.K;
+  if (t.ksplit > 1) {
+    const int split = local % t.ksplit;
+    local /= t.ksplit;
+    k_lo = split * t.kchunk;
+    k_hi = min(t.K, k_lo + t.kchunk);
+    t.C += (long)split * t.slab_stride;
+    t.bias_grad += (long)split * t.slab_stride;
+  }
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int m0 = (local / t.tiles_n) * (64 * WM);
+  const int n0 = (local % t.tiles_n) * (64 * WN);
+  const int mw = m0 + (wave >> 1) * 32 * WM;
+  const int nw = n0 + (wave & 1) * 32 * WN;
+  if (mw >= t.M || nw >= t.N) return;   // wave-uniform: no barriers in this kernel
+  floatx16 acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // forward products only (both operands k-contiguous; plan_common.h launch_cfg)
+  rd_loop<OP_KC, OP_KC, WM, WN>(t, t.A, t.lda, t.B, t.ldb, t.M, t.b_ones ? t.N - 1 : t.N,
+                                t.b_ones != 0, mw, nw, k_lo, k_hi, acc);
+  rd_epilogue<WM, WN>(t, mw, nw, acc, false);
+  if (t.epi == EPI_BIAS_RANK_RELU) {
+    // + U V^T: U / V continue A / B along k (the batch actions follow the
+    // observations in a replay row, the action columns follow the observation
+    // columns in W0; checked at launch), so the same accumulators run on over
+    // k in [K, K + R) -- the critic's 393-wide layer 0 with the obs-only
+    // projection P snapshotted on the way
+    rd_loop<OP_KC, OP_KC, WM, WN>(t, t.A, t.lda, t.B, t.ldb, t.M, t.N, false, mw, nw, t.K, t.K + t.R, acc);
+    rd_epilogue<WM, WN>(t, mw, nw, acc, true);
+  }
+}
+
+// wave block (32 WM) x (32 WN), default 64 x 32 (workgroup 128 x 64): at
+// B=4096, 1,828 steps/s against 1,827 for 32 x 64, 1,775 for 64 x 64 and 1,741
+// for 32 x 32; 3 k-groups in flight instead of 2 changed nothing (+-1 %).
+// OAC_BIG_TILE="WM,WN" selects another instantiation (tuning experiments)
+static int big_wm() {
+  static int v = [] { const char* e = getenv("OAC_BIG_TILE"); return e ? atoi(e) : 2; }();
+  return v;
+}
+static int big_wn() {
+  static int v = [] {
+    const char* e = getenv("OAC_BIG_TILE");
+    const char* c = e ? strchr(e, ',') : nullptr;
+    return c ? atoi(c + 1) : 1;
+  }();
+  return v;
+}
+int gemm_big_tile_m() { return 64 * big_wm(); }
+int gemm_big_tile_n() { return 64 * big_wn(); }
+
+hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s) {
+  if (b.total_tiles <= 0) return hipSuccess;
+  for (int i = 0; i < b.ntasks; ++i) {
+    const GemmTask& t = b.t[i];
+    if (t.K2 > 0 || t.epi == EPI_HEAD_BWD || t.epi == EPI_BIAS_RELU_DOT || b.fuse_adam ||
+        !t.a_kc || !t.b_kc || t.a_mode != A_PLAIN)
+      return hipErrorInvalidValue;   // forward (k-contiguous) products only
+    if (t.epi == EPI_BIAS_RANK_RELU &&
+        (!t.C2 || t.ksplit > 1 || t.U != t.A + t.K || t.ldu != t.lda || t.V != t.B + t.K ||
+         t.ldv != t.ldb))
+      return hipErrorInvalidValue;
+  }
+  int tb[8];
+  for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
+#define OAC_BIG(WM_, WN_) \
+  if (big_wm() == WM_ && big_wn() == WN_) { \
+    OAC_LAUNCH((gemm_big_kernel<WM_, WN_>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, \
+               tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
+    return hipGetLastError(); }
+  OAC_BIG(2, 2) OAC_BIG(1, 2) OAC_BIG(2, 1) OAC_BIG(1, 1)
+#undef OAC_BIG
+  return hipErrorInvalidValue;
+}
+
+}  // namespace oac

@@ -148,13 +148,25 @@ static inline void read_tuning(PlanBase& p) {
   }
 }
 
+// gemm_cfg 2 (register-direct kernel, gemm_big.hip) wins on the forward
+// products (both operands k-contiguous, N >= 64: B=4096 layer 0 115 -> 80 us,
+// layer 1 64 -> 40 us) and loses on dX / dW (n- or m-contiguous operands, one
+// dword load per k) and narrow outputs; those launches run on the LDS kernel
+static inline int launch_cfg(int cfg, const GemmBatch& gb) {
+  if (cfg != 2) return cfg;
+  for (int i = 0; i < gb.ntasks; ++i)
+    if (!gb.t[i].a_kc || !gb.t[i].b_kc || gb.t[i].a_mode != A_PLAIN || gb.t[i].N < 64) return 1;
+  return 2;
+}
+
 static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {
-  gemm_batch_finalize(gb, p.cfg);
+  const int cfg = launch_cfg(p.cfg, gb);
+  gemm_batch_finalize(gb, cfg);
   if (p.launches < 64 && p.tune_nw[p.launches] > 0) {
     gb.force_nw = p.tune_nw[p.launches];
     gb.force_gpw = p.tune_gpw[p.launches];
   }
-  TIMED(p, K_GEMM, s, OAC_HIP_CHECK(gemm_batch_launch(gb, p.cfg, s)));
+  TIMED(p, K_GEMM, s, OAC_HIP_CHECK(gemm_batch_launch(gb, cfg, s)));
   p.launches++;
   return 0;
 }

@@ -494,7 +494,7 @@ static int validate(const oac_sac_config* c) {
 
 static void plan_splits(SacPlan& p) {
   const oac_sac_config& c = p.c;
-  p.cfg = c.gemm_cfg >= 0 ? c.gemm_cfg : (c.batch >= 1024 ? 1 : 0);
+  p.cfg = c.gemm_cfg >= 0 ? c.gemm_cfg : (c.batch >= 1024 ? 2 : 0);
   const int tm = gemm_tile_m(p.cfg), tn = gemm_tile_n(p.cfg);
   auto tiles = [&](int M, int N) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
   const int H = c.hidden, Dq = c.obs_dim + c.act_dim, Do = c.obs_dim, Da = c.act_dim;
