@@ -214,10 +214,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N-rank path on a 1-GPU box: OAC_BENCH_BACKEND=gloo and
+    # OAC_BENCH_SAME_DEVICE=1 put every rank on cuda:0 (RCCL refuses that)
+    if os.environ.get("OAC_BENCH_SAME_DEVICE") == "1":
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("OAC_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     B = args.batch
