@@ -16,6 +16,8 @@
  *   oac_sac_step_phase    the same step split at the data-parallel exchange points
  *   oac_particle_*        ParticleTrainer.train_from_torch, share_layers=True
  *                         (trainer/particle_trainer_oac.py:169-363)
+ *   OAC_KIND_GAUSS        GaussianTrainer.train_from_torch (g-oac), share_layers=True
+ *                         (trainer/gaussian_trainer.py:177-437)
  *   oac_expl_action       get_optimistic_exploration_action (stochastic branch)
  *                         (optimistic_exploration.py:7-11, 14-109)
  *   oac_replay_sample_indices   np.random.randint(0, size, B) (replay_buffer.py:107)
@@ -36,10 +38,11 @@ extern "C" {
 #define OAC_ABI_VERSION 1
 
 /* ---------------------------------------------------------------- config */
-enum oac_kind { OAC_KIND_SAC = 0, OAC_KIND_PARTICLE = 1 };
+enum oac_kind { OAC_KIND_SAC = 0, OAC_KIND_PARTICLE = 1, OAC_KIND_GAUSS = 2 };
 
 typedef struct oac_sac_config {
-  int kind;              /* OAC_KIND_SAC (twin critics, q_out=1) or OAC_KIND_PARTICLE */
+  int kind;              /* OAC_KIND_SAC (twin critics, q_out=1), OAC_KIND_PARTICLE or
+                            OAC_KIND_GAUSS (one critic, q_out=2: mean | log std) */
   int obs_dim, act_dim;
   int hidden;            /* width of both hidden layers (reference: [M]*N, N=2) */
   int q_out;             /* 1 for SAC/OAC; K heads for the shared-layer particle critic */
@@ -54,6 +57,10 @@ typedef struct oac_sac_config {
   uint64_t seed;         /* Philox key for the policy noise */
   int gemm_cfg;          /* -1 auto, 0 small tiles + split-K, 1 large tiles */
   int world_size;        /* data-parallel ranks (alpha / gradient averaging) */
+  /* OAC_KIND_GAUSS only (gaussian_trainer.py:65-72, main.py:219-233, 549-554) */
+  float std_bound;       /* standard_bound = norm.ppf(delta) */
+  float std_init;        /* (q_max - q_min) / sqrt(12): upper clamp of the std target */
+  float std_soft_prob;   /* std_soft_update_prob; < 0: std_soft_update off */
 } oac_sac_config;
 
 /* Flat parameter arena layout (float offsets; every tensor 16-byte aligned).
@@ -62,8 +69,9 @@ typedef struct oac_sac_config {
  * last_fc.weight, rows Da..2Da-1 = last_fc_log_std.weight) and their biases
  * likewise.  Each critic block holds fc0.weight, fc0.bias, fc1.weight,
  * fc1.bias, last_fc.weight, last_fc.bias.  Arenas: params/grads/adam_m/adam_v
- * = [policy | critic 1 | critic 2] (one critic for PARTICLE);
- * targets = [target critic 1 | target critic 2]. */
+ * = [policy | critic 1 | critic 2] (one critic for PARTICLE; [policy |
+ * target_policy | critic] for GAUSS); targets = [target critic 1 | target
+ * critic 2]. */
 typedef struct oac_sac_layout {
   int64_t pol_fc0_w, pol_fc0_b, pol_fc1_w, pol_fc1_b, pol_head_w, pol_head_b, pol_size;
   int64_t q_fc0_w, q_fc0_b, q_fc1_w, q_fc1_b, q_last_w, q_last_b, q_size;
@@ -71,6 +79,8 @@ typedef struct oac_sac_layout {
   int64_t n_critics;
   int64_t params_total, targets_total;
   int64_t workspace_floats;
+  int64_t tpol_base;     /* GAUSS: target_policy block (params = [policy | target_policy |
+                            critic], one Adam group over both policies); else -1 */
 } oac_sac_layout;
 
 typedef struct oac_sac_buffers {
@@ -95,6 +105,7 @@ enum oac_ws_buffer {
   OAC_WS_Q1, OAC_WS_Q2, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_TQ2,
   OAC_WS_Y, OAC_WS_SQE1, OAC_WS_SQE2, OAC_WS_QNEW,
   OAC_WS_COUNTS,                       /* [B] batch counts (ReplayBufferCount) for OAC_STEP_COUNTS */
+  OAC_WS_HEAD3, OAC_WS_ACT3,           /* GAUSS: target_policy(obs) head [B, 2Da] and action */
   OAC_WS_COUNT_PUBLIC
 };
 
@@ -102,9 +113,10 @@ enum oac_ws_buffer {
 #define OAC_STEP_GATHER       1  /* gather the batch from the replay via idx_ring */
 #define OAC_STEP_DEVICE_EPS   2  /* draw eps1/eps2 with Philox (else caller wrote them) */
 #define OAC_STEP_USE_GRAPH    4  /* replay the captured hipGraph of the step */
-#define OAC_STEP_COUNTS       8  /* particle trainer with counts=True: the batch counts the
-                                    caller wrote into OAC_WS_COUNTS shape the quantile targets
-                                    (particle_trainer_oac.py:220-224) */
+#define OAC_STEP_COUNTS       8  /* particle / gaussian trainer with counts=True: the batch
+                                    counts the caller wrote into OAC_WS_COUNTS shape the
+                                    quantile targets (particle_trainer_oac.py:220-224) or the
+                                    std target (gaussian_trainer.py:238-242) */
 
 int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out);
 int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_sac** out);

@@ -1,0 +1,350 @@
+// g-oac Gaussian trainer step on MI355X: GaussianTrainer.train_from_torch
+// with share_layers=True and the deterministic policy -- the configuration of
+// reproduce_g-oac*.sh (--share_layers [--counts]; GaussianTrainer's default
+// deterministic=True is not overridden for g-oac, main.py:219-233).
+// One critic with two outputs (Q mean | log std), its target, the policy and
+// a separately trained target_policy (/root/reference/trainer/gaussian_trainer.py):
+//   Q(obs,a) [187] -> a' = tanh(mean_pi(next_obs)) [199-202]
+//   -> QT(next_obs,a') [204] -> q / std targets (counts, soft update, clamp)
+//      [207-237] -> Adam(Q, grad MSE(q) + MSE(std)) [227-237]
+//   -> a~ = tanh(mean_pi(obs)) [315-318] -> ub = Q_new(a~)_0 + z*exp(Q_new(a~)_1)
+//      [325-331] -> Adam(pi, -mean(ub)) [334-337]
+//   -> a~_T = tanh(mean_piT(obs)) [342-344] -> Adam(piT, -mean(Q_new(a~_T)_0)) [346-354]
+//   -> Polyak Q -> QT [359-362]
+// Both policy forwards on obs use pre-step policies and the post-step critic,
+// freshly evaluated (no saved-activation quirk here): the critic Adam
+// completes before either policy loss is formed.  The two policy losses are
+// independent (pi's step does not touch Q or piT), so their backward passes
+// share launches, and one Adam pass updates [policy | target_policy].
+#include <cstring>
+
+#include "../../include/oac_amd.h"
+#include "kernels.h"
+#include "oac_common.h"
+#include "plan_common.h"
+#include "sac_plan.h"
+
+namespace oac {
+
+enum GWs {
+  // public ids: HEAD1/ACT1 = pi(obs), HEAD2/ACT2 = pi(next_obs), HEAD3/ACT3 =
+  // target_policy(obs); Q1 = Q(obs,a) [B,2] raw, TQ1 = QT(next_obs,a') [B,2],
+  // QN1 = Q_new(obs,a~) [B,2], QN2 = Q_new(obs,a~_T) [B,2], Y / SQE1 [B,2]
+  // (q | std), QNEW = upper bound [B].
+  G_H1P = OAC_WS_COUNT_PUBLIC, G_H2P, G_H1P2, G_H2P2, G_H1TP, G_H2TP,
+  G_P, G_H1Q, G_H2Q, G_PT, G_H1T, G_H2T,
+  G_DQ, G_DH2Q, G_DH1Q,
+  G_PN, G_H1N, G_H2N, G_PN3, G_H1N3, G_H2N3, G_GQ, G_GQ3, G_DH2N, G_DH1N, G_DH2N3, G_DH1N3,
+  G_DA, G_DA3, G_DHEAD, G_DHEAD3, G_DH2P, G_DH1P, G_DH2TP, G_DH1TP,
+  G_COUNT
+};
+static_assert(G_COUNT <= WS_GSLAB_Q, "workspace ids");
+
+void gauss_layout_workspace(SacPlan& p) {
+  const oac_sac_config& c = p.c;
+  const int64_t B = c.batch, H = c.hidden, Da = c.act_dim;
+  for (int i = 0; i < kMaxWs; ++i) p.ws[i] = {0, 0, 0};
+  auto set = [&](int id, int64_t r, int64_t cl) { p.ws[id] = {0, r, cl}; };
+  set(OAC_WS_BATCH, B, c.row_stride);
+  for (int id : {OAC_WS_HEAD1, OAC_WS_HEAD2, OAC_WS_HEAD3}) set(id, B, 2 * Da);
+  for (int id : {OAC_WS_ACT1, OAC_WS_ACT2, OAC_WS_ACT3}) set(id, B, Da);
+  for (int id : {OAC_WS_Q1, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_Y, OAC_WS_SQE1}) set(id, B, 2);
+  set(OAC_WS_QNEW, B, 1);
+  set(OAC_WS_COUNTS, B, 1);
+  for (int id = G_H1P; id <= G_H2T; ++id) set(id, B, H);
+  for (int id : {G_DQ, G_GQ, G_GQ3}) set(id, B, 2);
+  for (int id : {G_DH2Q, G_DH1Q, G_PN, G_H1N, G_H2N, G_PN3, G_H1N3, G_H2N3, G_DH2N, G_DH1N,
+                 G_DH2N3, G_DH1N3, G_DH2P, G_DH1P, G_DH2TP, G_DH1TP})
+    set(id, B, H);
+  for (int id : {G_DA, G_DA3}) set(id, B, Da);
+  for (int id : {G_DHEAD, G_DHEAD3}) set(id, B, 2 * Da);
+  if (p.S_q > 1) set(WS_GSLAB_Q, p.S_q, q_group(p));
+  if (p.S_p > 1) set(WS_GSLAB_P, p.S_p, p_group(p));
+  int64_t off = 0;
+  for (int i = 0; i < kMaxWs; ++i) {
+    p.ws[i].off = off;
+    off = al64(off + p.ws[i].rows * p.ws[i].cols);
+  }
+  p.L.workspace_floats = off + 64;   // tail pad: GEMM k-contiguous loads may read 7 floats past a row
+}
+
+// ------------------------------------------------------------------ phases
+// forward of everything the pre-step parameters determine
+static int gphase0(SacPlan& p, int flags, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
+  const int Dq = Do + Da;
+  float* X = p.W(OAC_WS_BATCH);
+  const float* obs = X + c.off_obs;
+  const float* nobs = X + c.off_next_obs;
+  if (flags & OAC_STEP_GATHER) {
+    GatherArgs g;
+    std::memset(&g, 0, sizeof(g));
+    g.replay = p.b.replay; g.row_stride = RS; g.idx = p.b.idx_ring; g.ring_slots = p.b.ring_slots;
+    g.out = X; g.B = B;
+    g.seed = c.seed; g.state = p.state();
+    TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_gather(g, s)));
+    p.launches++;
+  }
+  const float* pol = p.b.params;
+  const float* tpol = p.b.params + L.tpol_base;
+  const float* q = p.b.params + L.q1_base;
+  const float* tq = p.b.targets;
+  {
+    GemmBatch gb{};
+    add(gb, t_fwd(obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(G_H1P), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
+    gb.publish = p.state(); gb.pub_beta1 = c.beta1; gb.pub_beta2 = c.beta2;   // step's Adam constants
+    add(gb, t_fwd(nobs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(G_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
+    add(gb, t_fwd(obs, RS, B, Do, tpol + L.pol_fc0_w, Do, H, p.W(G_H1TP), H, EPI_BIAS_RELU, tpol + L.pol_fc0_b));
+    GemmTask t = t_fwd(obs, RS, B, Do, q + L.q_fc0_w, Dq, H, p.W(G_P), H, EPI_BIAS_RANK_RELU, q + L.q_fc0_b);
+    t.U = X + c.off_act; t.ldu = RS; t.V = q + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
+    t.C2 = p.W(G_H1Q); t.ldc2 = H;
+    add(gb, t);
+    add(gb, t_fwd(nobs, RS, B, Do, tq + L.q_fc0_w, Dq, H, p.W(G_PT), H, EPI_BIAS, tq + L.q_fc0_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_fwd(p.W(G_H1P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(G_H2P), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
+    add(gb, t_fwd(p.W(G_H1P2), H, B, H, pol + L.pol_fc1_w, H, H, p.W(G_H2P2), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
+    add(gb, t_fwd(p.W(G_H1TP), H, B, H, tpol + L.pol_fc1_w, H, H, p.W(G_H2TP), H, EPI_BIAS_RELU, tpol + L.pol_fc1_b));
+    add(gb, t_fwd(p.W(G_H1Q), H, B, H, q + L.q_fc1_w, H, H, p.W(G_H2Q), H, EPI_BIAS_RELU, q + L.q_fc1_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_fwd(p.W(G_H2P), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD1), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
+    add(gb, t_fwd(p.W(G_H2P2), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD2), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
+    add(gb, t_fwd(p.W(G_H2TP), H, B, H, tpol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD3), 2 * Da, EPI_BIAS, tpol + L.pol_head_b));
+    add(gb, t_fwd(p.W(G_H2Q), H, B, H, q + L.q_last_w, H, 2, p.W(OAC_WS_Q1), 2, EPI_BIAS, q + L.q_last_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    DetActionArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.head[0] = p.W(OAC_WS_HEAD1); a.act[0] = p.W(OAC_WS_ACT1);
+    a.head[1] = p.W(OAC_WS_HEAD2); a.act[1] = p.W(OAC_WS_ACT2);
+    a.head[2] = p.W(OAC_WS_HEAD3); a.act[2] = p.W(OAC_WS_ACT3);
+    a.nseg = 3; a.B = B; a.act_dim = Da;
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_det_action(a, s)));
+    p.launches++;
+  }
+  return 0;
+}
+
+// target critic, TD targets, critic gradients (into grad_q)
+static int gphase1(SacPlan& p, int flags, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
+  const int Dq = Do + Da;
+  float* X = p.W(OAC_WS_BATCH);
+  const float* q = p.b.params + L.q1_base;
+  const float* tq = p.b.targets;
+  {
+    GemmBatch gb{};
+    GemmTask t = t_fwd(p.W(OAC_WS_ACT2), Da, B, Da, tq + L.q_fc0_w + Do, Dq, H, p.W(G_H1T), H,
+                       EPI_ADD_RELU, nullptr);
+    t.aux = p.W(G_PT); t.ld_aux = H;
+    add(gb, t);
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_fwd(p.W(G_H1T), H, B, H, tq + L.q_fc1_w, H, H, p.W(G_H2T), H, EPI_BIAS_RELU, tq + L.q_fc1_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_fwd(p.W(G_H2T), H, B, H, tq + L.q_last_w, H, 2, p.W(OAC_WS_TQ1), 2, EPI_BIAS, tq + L.q_last_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GaussTargetArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.q = p.W(OAC_WS_Q1); a.tq = p.W(OAC_WS_TQ1); a.batch = X; a.ld_batch = RS;
+    a.off_rew = c.off_rew; a.off_term = c.off_term; a.reward_scale = c.reward_scale;
+    a.discount = c.discount; a.std_init = c.std_init; a.soft_prob = c.std_soft_prob;
+    a.counts = (flags & OAC_STEP_COUNTS) ? p.W(OAC_WS_COUNTS) : nullptr;
+    a.B = B; a.dq = p.W(G_DQ); a.y = p.W(OAC_WS_Y); a.sqe = p.W(OAC_WS_SQE1);
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_gauss_targets(a, s)));
+    p.launches++;
+  }
+  {
+    GemmBatch gb{};
+    float* gq = grad_q(p);
+    add(gb, t_dw(p.W(G_DQ), 2, 2, B, p.W(G_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
+                 q_group(p), p.sp_ql));
+    add(gb, t_dx(p.W(G_DQ), 2, B, 2, q + L.q_last_w, H, H, p.W(G_DH2Q), H, p.W(G_H2Q), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    float* gq = grad_q(p);
+    add(gb, t_dw(p.W(G_DH2Q), H, H, B, p.W(G_H1Q), H, H, gq + L.q_fc1_w, gq + L.q_fc1_b,
+                 q_group(p), p.sp_q1));
+    add(gb, t_dx(p.W(G_DH2Q), H, B, H, q + L.q_fc1_w, H, H, p.W(G_DH1Q), H, p.W(G_H1Q), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    float* gq = grad_q(p);
+    add(gb, t_dw(p.W(G_DH1Q), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_fc0_w, gq + L.q_fc0_b,
+                 q_group(p), p.sp_q0));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  return 0;
+}
+
+// critic Adam done: post-step critic on (obs, a~) and (obs, a~_T), the two
+// policy losses' gradients (into grad_p: policy block, target_policy block)
+static int gphase2(SacPlan& p, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
+  const int Dq = Do + Da;
+  float* X = p.W(OAC_WS_BATCH);
+  const float* pol = p.b.params;
+  const float* tpol = p.b.params + L.tpol_base;
+  const float* q = p.b.params + L.q1_base;
+  {
+    GemmBatch gb{};
+    for (int k = 0; k < 2; ++k) {
+      GemmTask t = t_fwd(X + c.off_obs, RS, B, Do, q + L.q_fc0_w, Dq, H, p.W(k ? G_PN3 : G_PN), H,
+                         EPI_BIAS_RANK_RELU, q + L.q_fc0_b);
+      t.U = p.W(k ? OAC_WS_ACT3 : OAC_WS_ACT1); t.ldu = Da; t.V = q + L.q_fc0_w + Do; t.ldv = Dq;
+      t.R = Da; t.C2 = p.W(k ? G_H1N3 : G_H1N); t.ldc2 = H;
+      add(gb, t);
+    }
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_fwd(p.W(G_H1N), H, B, H, q + L.q_fc1_w, H, H, p.W(G_H2N), H, EPI_BIAS_RELU, q + L.q_fc1_b));
+    add(gb, t_fwd(p.W(G_H1N3), H, B, H, q + L.q_fc1_w, H, H, p.W(G_H2N3), H, EPI_BIAS_RELU, q + L.q_fc1_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_fwd(p.W(G_H2N), H, B, H, q + L.q_last_w, H, 2, p.W(OAC_WS_QN1), 2, EPI_BIAS, q + L.q_last_b));
+    add(gb, t_fwd(p.W(G_H2N3), H, B, H, q + L.q_last_w, H, 2, p.W(OAC_WS_QN2), 2, EPI_BIAS, q + L.q_last_b));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GaussSeedArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.qn = p.W(OAC_WS_QN1); a.qt = p.W(OAC_WS_QN2); a.std_bound = c.std_bound; a.B = B;
+    a.g = p.W(G_GQ); a.gt = p.W(G_GQ3); a.ub = p.W(OAC_WS_QNEW);
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_gauss_seed(a, s)));
+    p.launches++;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_dx(p.W(G_GQ), 2, B, 2, q + L.q_last_w, H, H, p.W(G_DH2N), H, p.W(G_H2N), H));
+    add(gb, t_dx(p.W(G_GQ3), 2, B, 2, q + L.q_last_w, H, H, p.W(G_DH2N3), H, p.W(G_H2N3), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_dx(p.W(G_DH2N), H, B, H, q + L.q_fc1_w, H, H, p.W(G_DH1N), H, p.W(G_H1N), H));
+    add(gb, t_dx(p.W(G_DH2N3), H, B, H, q + L.q_fc1_w, H, H, p.W(G_DH1N3), H, p.W(G_H1N3), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_dx(p.W(G_DH1N), H, B, H, q + L.q_fc0_w + Do, Dq, Da, p.W(G_DA), Da, nullptr, 0));
+    add(gb, t_dx(p.W(G_DH1N3), H, B, H, q + L.q_fc0_w + Do, Dq, Da, p.W(G_DA3), Da, nullptr, 0));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    DetHeadBwdArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.da[0] = p.W(G_DA); a.act[0] = p.W(OAC_WS_ACT1); a.dhead[0] = p.W(G_DHEAD);
+    a.da[1] = p.W(G_DA3); a.act[1] = p.W(OAC_WS_ACT3); a.dhead[1] = p.W(G_DHEAD3);
+    a.nseg = 2; a.B = B; a.act_dim = Da;
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_det_head_backward(a, s)));
+    p.launches++;
+  }
+  const long pg = p_group(p);
+  float* gp = grad_p(p);
+  float* gtp = gp + L.tpol_base;
+  {
+    GemmBatch gb{};
+    add(gb, t_dw(p.W(G_DHEAD), 2 * Da, 2 * Da, B, p.W(G_H2P), H, H, gp + L.pol_head_w,
+                 gp + L.pol_head_b, pg, p.sp_ph));
+    add(gb, t_dx(p.W(G_DHEAD), 2 * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(G_DH2P), H, p.W(G_H2P), H));
+    add(gb, t_dw(p.W(G_DHEAD3), 2 * Da, 2 * Da, B, p.W(G_H2TP), H, H, gtp + L.pol_head_w,
+                 gtp + L.pol_head_b, pg, p.sp_ph));
+    add(gb, t_dx(p.W(G_DHEAD3), 2 * Da, B, 2 * Da, tpol + L.pol_head_w, H, H, p.W(G_DH2TP), H, p.W(G_H2TP), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_dw(p.W(G_DH2P), H, H, B, p.W(G_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b, pg, p.sp_p1));
+    add(gb, t_dx(p.W(G_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(G_DH1P), H, p.W(G_H1P), H));
+    add(gb, t_dw(p.W(G_DH2TP), H, H, B, p.W(G_H1TP), H, H, gtp + L.pol_fc1_w, gtp + L.pol_fc1_b, pg, p.sp_p1));
+    add(gb, t_dx(p.W(G_DH2TP), H, B, H, tpol + L.pol_fc1_w, H, H, p.W(G_DH1TP), H, p.W(G_H1TP), H));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  {
+    GemmBatch gb{};
+    add(gb, t_dw(p.W(G_DH1P), H, H, B, X + c.off_obs, RS, Do, gp + L.pol_fc0_w, gp + L.pol_fc0_b, pg, p.sp_p0));
+    add(gb, t_dw(p.W(G_DH1TP), H, H, B, X + c.off_obs, RS, Do, gtp + L.pol_fc0_w, gtp + L.pol_fc0_b, pg, p.sp_p0));
+    if (run_gemm(p, gb, s)) return 1;
+  }
+  return 0;
+}
+
+int gauss_run_step(SacPlan& p, int flags, hipStream_t s) {
+  p.launches = 0;
+  if (gphase0(p, flags, s)) return 1;
+  if (gphase1(p, flags, s)) return 1;
+  {
+    AdamArgs a = critic_adam(p, 0, nullptr);
+    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
+    p.launches++;
+  }
+  if (gphase2(p, s)) return 1;
+  {
+    AdamArgs a = policy_adam(p, 0, nullptr);
+    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
+    p.launches++;
+  }
+  return 0;
+}
+
+// data-parallel split (no whole-batch quantity besides the gradients: the
+// phase-0 exchange is empty)
+int gauss_step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
+  switch (phase) {
+    case 0: return gphase0(p, flags, s);
+    case 1:
+      if (gphase1(p, flags, s)) return 1;
+      if (p.S_q > 1) {
+        AdamArgs a = critic_adam(p, 1, nullptr);
+        OAC_HIP_CHECK(launch_adam(a, s));
+      }
+      return 0;
+    case 2: {
+      AdamArgs a = critic_adam(p, -1, nullptr);
+      OAC_HIP_CHECK(launch_adam(a, s));
+      if (gphase2(p, s)) return 1;
+      if (p.S_p > 1) {
+        AdamArgs b = policy_adam(p, 1, nullptr);
+        OAC_HIP_CHECK(launch_adam(b, s));
+      }
+      return 0;
+    }
+    case 3: {
+      AdamArgs a = policy_adam(p, -1, nullptr);
+      OAC_HIP_CHECK(launch_adam(a, s));
+      return 0;
+    }
+    default:
+      set_error("bad phase %d", phase);
+      return 1;
+  }
+}
+
+}  // namespace oac

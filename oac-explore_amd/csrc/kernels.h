@@ -168,6 +168,44 @@ struct ParticleMinArgs {
 hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s);
 hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s);
 
+// g-oac GaussianTrainer, share_layers=True (trainer/gaussian_trainer.py:177-437):
+// the critic has two outputs, column 0 = Q mean, column 1 = log std (the
+// FlattenMlp positive=[False, True] exp, networks.py:69-75, is applied here).
+struct DetActionArgs {                  // deterministic policy: a = tanh(mean) (policies.py:286-288)
+  const float* head[3];                 // [B, 2Da] heads (mean | raw log std)
+  float* act[3];                        // [B, Da]
+  int nseg, B, act_dim;
+};
+hipError_t launch_det_action(const DetActionArgs& a, hipStream_t s);
+
+struct GaussTargetArgs {
+  const float* q; const float* tq;      // [B, 2] Q(obs, a), Q_target(next_obs, a') raw outputs
+  const float* batch; long ld_batch; int off_rew, off_term;
+  float reward_scale, discount, std_init;
+  float soft_prob;                      // std_soft_update_prob, < 0: off
+  const float* counts;                  // [B] batch counts (counts=True) or null
+  int B;
+  float* dq;                            // [B, 2] dL/d(raw outputs) of q_loss + std_loss
+  float* y;                             // [B, 2] q_target | std_target
+  float* sqe;                           // [B, 2] squared errors
+};
+hipError_t launch_gauss_targets(const GaussTargetArgs& a, hipStream_t s);
+
+struct GaussSeedArgs {
+  const float* qn;                      // [B, 2] post-step Q(obs, tanh(mean_pi(obs)))
+  const float* qt;                      // [B, 2] post-step Q(obs, tanh(mean_target_pi(obs)))
+  float std_bound; int B;
+  float* g; float* gt;                  // [B, 2] seeds of -mean(upper bound), -mean(q)
+  float* ub;                            // [B] upper bound q + std_bound * std
+};
+hipError_t launch_gauss_seed(const GaussSeedArgs& a, hipStream_t s);
+
+struct DetHeadBwdArgs {                 // d tanh(mean): dmean = da (1 - a^2), d log std = 0
+  const float* da[2]; const float* act[2]; float* dhead[2];
+  int nseg, B, act_dim;
+};
+hipError_t launch_det_head_backward(const DetHeadBwdArgs& a, hipStream_t s);
+
 struct LogpSumArgs { const float* logp; int B; float target_entropy; AlphaState* alpha; };
 hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s);
 

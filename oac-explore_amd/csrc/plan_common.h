@@ -154,8 +154,19 @@ static inline void read_tuning(PlanBase& p) {
 // dword load per k) and narrow outputs; those launches run on the LDS kernel
 static inline int launch_cfg(int cfg, const GemmBatch& gb) {
   if (cfg != 2) return cfg;
-  for (int i = 0; i < gb.ntasks; ++i)
-    if (!gb.t[i].a_kc || !gb.t[i].b_kc || gb.t[i].a_mode != A_PLAIN || gb.t[i].N < 64) return 1;
+  for (int i = 0; i < gb.ntasks; ++i) {
+    const GemmTask& t = gb.t[i];
+    if (!t.a_kc || !t.b_kc || t.a_mode != A_PLAIN || t.N < 64 || t.K2 > 0 ||
+        t.epi == EPI_HEAD_BWD || t.epi == EPI_BIAS_RELU_DOT || gb.fuse_adam)
+      return 1;
+    // the big kernel runs the rank-R columns as a continuation of the same
+    // row (the action stored right after the observation); a separate action
+    // buffer (the policy's a~) goes to the LDS kernel
+    if (t.epi == EPI_BIAS_RANK_RELU &&
+        (!t.C2 || t.ksplit > 1 || t.U != t.A + t.K || t.ldu != t.lda || t.V != t.B + t.K ||
+         t.ldv != t.ldb))
+      return 1;
+  }
   return 2;
 }
 

@@ -328,4 +328,97 @@ hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// --------------------------------------------------------------------------
+// g-oac GaussianTrainer, share_layers=True (trainer/gaussian_trainer.py).
+// The critic's raw outputs are [mean | log std]; std = exp(log std) is the
+// FlattenMlp positive=[False, True] output (networks.py:69-75).
+// --------------------------------------------------------------------------
+
+// deterministic policy action a = tanh(mean) (policies.py:286-288); one
+// thread per (row, action dim), y-dimension = segment
+__global__ void __launch_bounds__(256) det_action_kernel(DetActionArgs p) {
+  const int Da = p.act_dim;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= p.B * Da) return;
+  const int r = idx / Da, j = idx % Da;
+  const int g = blockIdx.y;
+  p.act[g][idx] = tanhf(p.head[g][(long)r * 2 * Da + j]);
+}
+
+// TD targets and the critic gradient (gaussian_trainer.py:199-242 with the
+// share_layers branch 205-237):
+//   std_target = (1-d)*gamma*exp(tq1)   [soft update: p*next + (1-p)*std]
+//   counts=True: std_target <- std where count != 0 (factor, 238-242 / 219-223)
+//   q_target   = scale*r + (1-d)*gamma*tq0 ; std_target = clamp(., 0, std_init)
+//   loss = MSE(q0, q_target) + MSE(std, std_target)
+//   dL/dq0 = 2 (q0 - y_q) / B ;  dL/dq1 = 2 (std - y_s) / B * std  (exp backward)
+__global__ void __launch_bounds__(256) gauss_targets_kernel(GaussTargetArgs p) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= p.B) return;
+  const float q0 = p.q[2L * r], sd = expf(p.q[2L * r + 1]);
+  const float t0 = p.tq[2L * r], tsd = expf(p.tq[2L * r + 1]);
+  const float rew = p.batch[(long)r * p.ld_batch + p.off_rew];
+  const float term = p.batch[(long)r * p.ld_batch + p.off_term];
+  const float gd = __fmul_rn(1.f - term, p.discount);
+  float ys = __fmul_rn(gd, tsd);
+  if (p.soft_prob >= 0.f)
+    ys = __fadd_rn(__fmul_rn(p.soft_prob, ys), __fmul_rn(1.f - p.soft_prob, sd));
+  if (p.counts && p.counts[r] != 0.f) ys = sd;
+  ys = fminf(fmaxf(ys, 0.f), p.std_init);
+  const float yq = __fadd_rn(__fmul_rn(p.reward_scale, rew), __fmul_rn(gd, t0));
+  const float invB = 1.f / (float)p.B;
+  const float d0 = q0 - yq, d1 = sd - ys;
+  p.dq[2L * r] = __fmul_rn(2.f * d0, invB);
+  p.dq[2L * r + 1] = __fmul_rn(__fmul_rn(2.f * d1, invB), sd);
+  p.y[2L * r] = yq;
+  p.y[2L * r + 1] = ys;
+  p.sqe[2L * r] = d0 * d0;
+  p.sqe[2L * r + 1] = d1 * d1;
+}
+
+// Policy-loss seeds through the post-step critic (gaussian_trainer.py:323-336,
+// 338-350): policy: L = -mean(q0 + z*exp(q1)) -> [-1/B, -z/B * std];
+// target policy: L = -mean(q0) -> [-1/B, 0]
+__global__ void __launch_bounds__(256) gauss_seed_kernel(GaussSeedArgs p) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= p.B) return;
+  const float g0 = -(1.f / (float)p.B);
+  const float sd = expf(p.qn[2L * r + 1]);
+  p.ub[r] = __fadd_rn(p.qn[2L * r], __fmul_rn(p.std_bound, sd));
+  p.g[2L * r] = g0;
+  p.g[2L * r + 1] = __fmul_rn(__fmul_rn(g0, p.std_bound), sd);
+  p.gt[2L * r] = g0;
+  p.gt[2L * r + 1] = 0.f;
+}
+
+__global__ void __launch_bounds__(256) det_head_backward_kernel(DetHeadBwdArgs p) {
+  const int Da = p.act_dim;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= p.B * Da) return;
+  const int r = idx / Da, j = idx % Da;
+  const int g = blockIdx.y;
+  const float a = p.act[g][idx];
+  float* dh = p.dhead[g] + (long)r * 2 * Da;
+  dh[j] = __fmul_rn(p.da[g][idx], __fsub_rn(1.f, __fmul_rn(a, a)));
+  dh[Da + j] = 0.f;
+}
+
+hipError_t launch_det_action(const DetActionArgs& a, hipStream_t s) {
+  OAC_LAUNCH(det_action_kernel, dim3((a.B * a.act_dim + 255) / 256, a.nseg), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_gauss_targets(const GaussTargetArgs& a, hipStream_t s) {
+  OAC_LAUNCH(gauss_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_gauss_seed(const GaussSeedArgs& a, hipStream_t s) {
+  OAC_LAUNCH(gauss_seed_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_det_head_backward(const DetHeadBwdArgs& a, hipStream_t s) {
+  OAC_LAUNCH(det_head_backward_kernel, dim3((a.B * a.act_dim + 255) / 256, a.nseg), dim3(256), 0,
+             s, a);
+  return hipGetLastError();
+}
+
 }  // namespace oac

@@ -42,6 +42,9 @@ inline float* grad_q(SacPlan& p) {
 }
 inline float* grad_p(SacPlan& p) { return p.S_p > 1 ? p.W(WS_GSLAB_P) : p.b.grads; }
 inline long q_group(const SacPlan& p) { return (long)(p.L.n_critics * p.L.q_size); }
+// the policy Adam group: everything in front of the critic block (the policy,
+// plus the target_policy for GAUSS)
+inline long p_group(const SacPlan& p) { return (long)p.L.q1_base; }
 
 // critic update: reduce slabs, Adam (t = n_steps + 1), Polyak, snapshot t
 inline AdamArgs critic_adam(SacPlan& p, int reduce_only, AlphaState* commit) {
@@ -68,10 +71,10 @@ inline AdamArgs policy_adam(SacPlan& p, int reduce_only, AlphaState* commit) {
   const oac_sac_config& c = p.c;
   AdamArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.n = p.L.pol_size;
+  a.p = p.b.params; a.g = p.b.grads; a.m = p.b.adam_m; a.v = p.b.adam_v; a.n = p_group(p);
   a.gslab = reduce_only < 0 ? a.g : grad_p(p);
   a.S = reduce_only < 0 ? 1 : p.S_p;
-  a.slab_stride = p.L.pol_size;
+  a.slab_stride = p_group(p);
   a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
   a.state = p.state(); a.advance = 1; a.alpha = commit;
   a.gscale = reduce_only < 0 ? 1.f / (float)c.world_size : 1.f;
@@ -100,5 +103,10 @@ void particle_layout_workspace(SacPlan& p);
 int particle_run_step(SacPlan& p, int flags, hipStream_t s);
 int particle_step_phase(SacPlan& p, int phase, int flags, hipStream_t s);
 void particle_plan_splits(SacPlan& p);
+
+// g-oac gaussian trainer (gauss_plan.hip)
+void gauss_layout_workspace(SacPlan& p);
+int gauss_run_step(SacPlan& p, int flags, hipStream_t s);
+int gauss_step_phase(SacPlan& p, int phase, int flags, hipStream_t s);
 
 }  // namespace oac

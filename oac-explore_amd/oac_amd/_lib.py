@@ -12,6 +12,7 @@ LIB_PATH = os.path.join(HERE, "liboac_amd.so")
 
 OAC_KIND_SAC = 0
 OAC_KIND_PARTICLE = 1
+OAC_KIND_GAUSS = 2
 
 OAC_STEP_GATHER = 1
 OAC_STEP_DEVICE_EPS = 2
@@ -21,7 +22,8 @@ OAC_STEP_COUNTS = 8
 # public workspace ids (enum oac_ws_buffer)
 WS = {name: i for i, name in enumerate([
     "batch", "eps1", "eps2", "head1", "head2", "act1", "act2", "logp1", "logp2",
-    "q1", "q2", "qn1", "qn2", "tq1", "tq2", "y", "sqe1", "sqe2", "qnew", "counts"])}
+    "q1", "q2", "qn1", "qn2", "tq1", "tq2", "y", "sqe1", "sqe2", "qnew", "counts",
+    "head3", "act3"])}
 
 
 class SacConfig(ctypes.Structure):
@@ -36,6 +38,8 @@ class SacConfig(ctypes.Structure):
         ("off_obs", ctypes.c_int), ("off_act", ctypes.c_int), ("off_rew", ctypes.c_int),
         ("off_term", ctypes.c_int), ("off_next_obs", ctypes.c_int),
         ("seed", ctypes.c_uint64), ("gemm_cfg", ctypes.c_int), ("world_size", ctypes.c_int),
+        ("std_bound", ctypes.c_float), ("std_init", ctypes.c_float),
+        ("std_soft_prob", ctypes.c_float),
     ]
 
 
@@ -43,7 +47,8 @@ class SacLayout(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "pol_fc0_w", "pol_fc0_b", "pol_fc1_w", "pol_fc1_b", "pol_head_w", "pol_head_b", "pol_size",
         "q_fc0_w", "q_fc0_b", "q_fc1_w", "q_fc1_b", "q_last_w", "q_last_b", "q_size",
-        "q1_base", "q2_base", "n_critics", "params_total", "targets_total", "workspace_floats")]
+        "q1_base", "q2_base", "n_critics", "params_total", "targets_total", "workspace_floats",
+        "tpol_base")]
 
 
 class SacBuffers(ctypes.Structure):

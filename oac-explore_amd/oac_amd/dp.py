@@ -27,6 +27,7 @@ import torch.distributed as dist
 
 from . import _lib
 from ._lib import check
+from .gaussian_trainer import GaussianTrainer
 from .particle_trainer import ParticleTrainer
 from .trainer import SACTrainer
 
@@ -51,7 +52,7 @@ class _GpuExecutor:
         self.auto_alpha = trainer.use_automatic_entropy_tuning
         lay = trainer.layout
         self._crit = trainer.grads[lay.q1_base:lay.q1_base + lay.n_critics * lay.q_size]
-        self._pol = trainer.grads[:lay.pol_size]
+        self._pol = trainer.grads[:lay.q1_base]   # policy Adam group
 
     def phase(self, i):
         check(_lib.lib().oac_sac_step_phase(self.plan.handle, i, self.flags if i == 0 else 0,
@@ -150,3 +151,8 @@ class DataParallelSACTrainer(_DataParallel, SACTrainer):
 
 class DataParallelParticleTrainer(_DataParallel, ParticleTrainer):
     """ParticleTrainer (trainer/particle_trainer_oac.py) with the data-parallel step."""
+
+
+class DataParallelGaussianTrainer(_DataParallel, GaussianTrainer):
+    """GaussianTrainer (trainer/gaussian_trainer.py, g-oac) with the data-parallel
+    step (no alpha: the phase-0 exchange is skipped)."""

@@ -42,9 +42,10 @@ class ArenaFlattenMlp(nn.Module):
     """FlattenMlp (networks.py:154-161): relu hidden layers, identity output,
     inputs concatenated along dim 1."""
 
-    def __init__(self, arena, base, layout, obs_dim, act_dim, hidden, out_dim):
+    def __init__(self, arena, base, layout, obs_dim, act_dim, hidden, out_dim, positive=False):
         super().__init__()
         L = layout
+        self.positive = positive   # exp of the output (all, or per column), networks.py:69-75
         din = obs_dim + act_dim
         self.input_size, self.output_size = din, out_dim
         self.fc0 = _ArenaLinear(_view(arena, base + L.q_fc0_w, hidden, din),
@@ -60,7 +61,13 @@ class ArenaFlattenMlp(nn.Module):
         h = torch.cat(inputs, dim=1)
         for fc in self.fcs:
             h = F.relu(fc(h))
-        return self.last_fc(h)
+        out = self.last_fc(h)
+        if isinstance(self.positive, (list, tuple)):
+            out = torch.stack([torch.exp(out[:, i]) if v else out[:, i]
+                               for i, v in enumerate(self.positive)], dim=1)
+        elif self.positive:
+            out = torch.exp(out)
+        return out
 
 
 class ArenaTanhGaussianPolicy(nn.Module):

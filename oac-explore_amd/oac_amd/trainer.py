@@ -83,9 +83,12 @@ class AdamStateView:
     update itself is fused into the step kernels; ``step``/``zero_grad`` are
     no-ops kept for interface compatibility."""
 
-    def __init__(self, trainer, params, m_views, v_views, lr, betas, eps):
+    def __init__(self, trainer, params, m_views, v_views, lr, betas, eps, no_grad=()):
         self._t, self.params = trainer, params
         self.m, self.v = m_views, v_views
+        # parameters that never receive a gradient (torch Adam keeps no state
+        # for them; their m / v stay zero here, so the update is exactly 0)
+        self._no_grad = set(no_grad)
         self.param_groups = [dict(lr=lr, betas=betas, eps=eps, weight_decay=0, amsgrad=False,
                                   params=list(range(len(params))))]
 
@@ -100,7 +103,8 @@ class AdamStateView:
         state = {}
         if t > 0:
             for i, (m, v) in enumerate(zip(self.m, self.v)):
-                state[i] = dict(step=t, exp_avg=m, exp_avg_sq=v)
+                if i not in self._no_grad:
+                    state[i] = dict(step=t, exp_avg=m, exp_avg_sq=v)
         return dict(state=state, param_groups=[dict(g) for g in self.param_groups])
 
     def load_state_dict(self, sd):

@@ -18,6 +18,9 @@ It restates, with explicit forward and backward passes written out by hand
   activations / ReLU masks);
 * ``ParticleTrainer.train_from_torch`` /root/reference/trainer/particle_trainer_oac.py:169-363
   (shared-layer K-head critic);
+* ``GaussianTrainer.train_from_torch`` /root/reference/trainer/gaussian_trainer.py:177-437
+  (g-oac: shared-layer critic with outputs [Q | log std], deterministic
+  policy, separately trained target_policy);
 * ``get_optimistic_exploration_action_stochastic``
                                        /root/reference/optimistic_exploration.py:14-109
 * torch 1.4 ``optim.Adam.step`` (constructed at trainer/trainer.py:75-91) and
@@ -446,6 +449,101 @@ class ParticleOACOracle:
         self.last = dict(grads=dict(policy=gp, qf=gq, log_alpha=g_la), qf_losses=losses,
                          qf_loss=losses.sum(), policy_loss=policy_loss, alpha=alpha,
                          alpha_loss=alpha_loss, sorted_qs=sorted_qs, y=y)
+        return self.last
+
+
+class GaussianOACOracle:
+    """GaussianTrainer (gaussian_trainer.py) with share_layers=True and the
+    deterministic policy (the reproduce_g-oac*.sh configuration): critic Q
+    with raw outputs [mean | log std] (FlattenMlp positive=[False, True],
+    networks.py:69-75), target critic, policy and target_policy."""
+
+    def __init__(self, params, obs_dim, act_dim, delta=0.95, q_min=0.0, q_max=100.0,
+                 discount=0.99, reward_scale=1.0, policy_lr=3e-4, qf_lr=3e-4, tau=5e-3,
+                 target_update_period=1, std_soft_update_prob=None, dtype=torch.float32):
+        from scipy.stats import norm
+        self.dtype = dtype
+        self.Do, self.Da = obs_dim, act_dim
+        self.P = to_torch_params(params["policy"], dtype)
+        self.TP = to_torch_params(params["target_policy"], dtype)
+        self.Q = to_torch_params(params["qf1"], dtype)
+        self.T = to_torch_params(params["target_qf1"], dtype)
+        self.z = float(norm.ppf(delta, loc=0, scale=1))          # gaussian_trainer.py:69
+        self.std_init = (q_max - q_min) / np.sqrt(12)            # :72
+        self.discount, self.reward_scale, self.tau = discount, reward_scale, tau
+        self.period = target_update_period
+        self.soft = std_soft_update_prob
+        self.opt_p = Adam14(self.P, policy_lr)
+        self.opt_tp = Adam14(self.TP, policy_lr)
+        self.opt_q = Adam14(self.Q, qf_lr)
+        self.n_steps = 0
+
+    @staticmethod
+    def det_policy_backward(c, p, ga):
+        """Gradient of sum(ga * tanh(mean)) w.r.t. the policy params; the
+        log-std head gets none (it is not in the graph: zeros here)."""
+        a, hs = c["a"], c["hs"]
+        dmean = ga * (1 - a * a)
+        L = len(hs) - 1
+        g = {"last_fc.weight": dmean.t() @ hs[L], "last_fc.bias": dmean.sum(0),
+             "last_fc_log_std.weight": torch.zeros_like(p["last_fc_log_std.weight"]),
+             "last_fc_log_std.bias": torch.zeros_like(p["last_fc_log_std.bias"])}
+        dh = (dmean @ p["last_fc.weight"]) * (hs[L] > 0)
+        for i in range(L - 1, -1, -1):
+            g[f"fc{i}.weight"] = dh.t() @ hs[i]
+            g[f"fc{i}.bias"] = dh.sum(0)
+            if i > 0:
+                dh = (dh @ p[f"fc{i}.weight"]) * (hs[i] > 0)
+        return g
+
+    def step(self, batch):
+        dt = self.dtype
+        obs = _t(batch["observations"], dt)
+        act = _t(batch["actions"], dt)
+        rew = _t(batch["rewards"], dt)
+        term = _t(batch["terminals"], dt)
+        nobs = _t(batch["next_observations"], dt)
+        B = obs.shape[0]
+        c = q_forward(obs, act, self.Q)                              # :187
+        q_preds, std_preds = c["q"][:, :1], torch.exp(c["q"][:, 1:2])
+        pf2 = policy_forward(nobs, self.P, None, deterministic=True)  # :199-202
+        tq = q_forward(nobs, pf2["a"], self.T)["q"]                  # :204
+        tq0, tstd = tq[:, :1], torch.exp(tq[:, 1:2])
+        std_target = (1. - term) * self.discount * tstd              # :213
+        if self.soft is not None:                                    # :215-218
+            std_target = self.soft * std_target + (1 - self.soft) * std_preds
+        if batch.get("counts") is not None:                          # :220-224
+            cnt = _t(batch["counts"], dt).reshape(B, 1)
+            factor = (cnt == 0).to(dt)
+            std_target = std_target * factor + (1 - factor) * std_preds
+        q_target = self.reward_scale * rew + (1. - term) * self.discount * tq0   # :227-228
+        std_target = torch.clamp(std_target, 0, self.std_init)       # :229
+        q_loss = ((q_preds - q_target) ** 2).mean()                  # :231-234
+        std_loss = ((std_preds - std_target) ** 2).mean()
+        dq = torch.cat([2.0 * (q_preds - q_target) / B,
+                        2.0 * (std_preds - std_target) / B * std_preds], dim=1)
+        gq = q_param_grads(c, dq, self.Q)
+        self.opt_q.step(gq)                                          # :237
+        pf = policy_forward(obs, self.P, None, deterministic=True)   # :315-318 (pre-step pi)
+        cn = q_forward(obs, pf["a"], self.Q)                         # :325 (post-step Q)
+        qs, stds = cn["q"][:, :1], torch.exp(cn["q"][:, 1:2])
+        ub = qs + self.z * stds                                      # :331
+        g0 = -torch.ones_like(qs) / B
+        da = q_input_grad(cn, torch.cat([g0, g0 * self.z * stds], dim=1), self.Q)[:, self.Do:]
+        gp = self.det_policy_backward(pf, self.P, da)
+        self.opt_p.step(gp)                                          # :334-337
+        tpf = policy_forward(obs, self.TP, None, deterministic=True)  # :342-344
+        ct = q_forward(obs, tpf["a"], self.Q)                        # :346
+        dat = q_input_grad(ct, torch.cat([g0, torch.zeros_like(g0)], dim=1), self.Q)[:, self.Do:]
+        gtp = self.det_policy_backward(tpf, self.TP, dat)
+        self.opt_tp.step(gtp)                                        # :352-354
+        if self.n_steps % self.period == 0:                          # :358-362
+            polyak(self.T, self.Q, self.tau)
+        self.n_steps += 1
+        self.last = dict(grads=dict(policy=gp, target_policy=gtp, qf=gq), q_loss=q_loss,
+                         std_loss=std_loss, q_preds=q_preds, std_preds=std_preds,
+                         q_target=q_target, std_target=std_target, upper_bound=ub,
+                         target_head=tpf)
         return self.last
 
 

@@ -48,6 +48,18 @@ def sac_params(obs_dim, act_dim, hidden, seed, q_out=1, pi_init_w=1e-3,
     return dict(policy=pol, qf1=qf1, qf2=qf2, target_qf1=tq1, target_qf2=tq2)
 
 
+def goac_params(obs_dim, act_dim, hidden, seed, q_min, q_max, pi_init_w=1e-3, q_init_w=3e-3):
+    """g-oac (GaussianTrainer, share_layers): policy, target_policy, qf1
+    (outputs Q | log std, last bias [mean, log std] of the uniform prior on
+    [q_min, q_max], gaussian_trainer.py:70-92) and target_qf1 (fp32)."""
+    bias = [(q_max + q_min) / 2, np.log((q_max - q_min) / np.sqrt(12))]
+    d = sac_params(obs_dim, act_dim, hidden, seed, q_out=2, pi_init_w=pi_init_w,
+                   q_init_w=q_init_w, q_last_bias=bias)
+    rs = np.random.RandomState(seed + 1)
+    tp = mlp_params(rs, obs_dim, hidden, act_dim, pi_init_w, log_std_head=True)
+    return dict(policy=d["policy"], target_policy=tp, qf1=d["qf1"], target_qf1=d["target_qf1"])
+
+
 def synthetic_transitions(n, obs_dim, act_dim, seed=0, term_p=0.01):
     """BASELINE.md section 3 synthetic replay content (float64, like the
     reference's numpy store, replay_buffer.py:32-45)."""

@@ -31,7 +31,8 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))  # tests/
-from fixtures_lib import sac_params, synthetic_transitions, PARAM_ORDER_POLICY, PARAM_ORDER_Q  # noqa
+from fixtures_lib import (goac_params, sac_params, synthetic_transitions,  # noqa
+                          PARAM_ORDER_POLICY, PARAM_ORDER_Q)
 
 REF = "/root/reference"
 
@@ -75,6 +76,7 @@ from networks import FlattenMlp  # noqa: E402
 from trainer.policies import TanhGaussianPolicy  # noqa: E402
 from trainer.trainer import SACTrainer  # noqa: E402
 from trainer.particle_trainer_oac import ParticleTrainer as ParticleTrainerOAC  # noqa: E402
+from trainer.gaussian_trainer import GaussianTrainer  # noqa: E402
 from replay_buffer import ReplayBuffer, ReplayBufferCount  # noqa: E402
 import optimistic_exploration as oe  # noqa: E402
 
@@ -304,6 +306,70 @@ def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=1
     return meta, out
 
 
+# ------------------------------------------------------------- g-oac runs
+def gen_goac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=13, delta=0.95,
+             r_min=0.0, r_max=5.0, discount=0.99, lr=3e-4, tau=5e-3, idx_seed=1,
+             pi_init_w=1e-3, q_init_w=3e-3, counts=False, soft=None):
+    """GaussianTrainer (g-oac) as reproduce_g-oac*.sh builds it: share_layers,
+    deterministic policy (main.py:219-233), q_min/q_max = r_min/r_max / (1 -
+    discount); ``soft``: std_soft_update with that probability.  Parameters
+    with no gradient (the deterministic policies' log-std heads) are recorded
+    as zero gradients."""
+    pp, qp = _producers(obs_dim, act_dim, hidden, q_out=2)
+    q_min, q_max = r_min / (1 - discount), r_max / (1 - discount)
+    torch.manual_seed(0)
+    tr = GaussianTrainer(pp, qp, n_estimators=2, action_space=Box(-1, 1, (act_dim,)),
+                         discount=discount, reward_scale=1.0, delta=delta, policy_lr=lr,
+                         qf_lr=lr, optimizer_class=Adam14, soft_target_tau=tau,
+                         target_update_period=1, q_min=q_min, q_max=q_max, share_layers=True,
+                         counts=counts, std_soft_update=soft is not None,
+                         std_soft_update_prob=0.0 if soft is None else soft)
+    assert tr.deterministic
+    params = goac_params(obs_dim, act_dim, hidden, seed, q_min, q_max, pi_init_w=pi_init_w,
+                         q_init_w=q_init_w)
+    load_sd(tr.policy, params["policy"])
+    load_sd(tr.target_policy, params["target_policy"])
+    load_sd(tr.q, params["qf1"])
+    load_sd(tr.q_target, params["target_qf1"])
+    rb, _ = _fill_buffer(obs_dim, act_dim, n_replay)
+    crs = np.random.RandomState(77)
+    np.random.seed(idx_seed)
+    out = {}
+    meta = dict(kind="goac", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, B=B, steps=steps,
+                n_replay=n_replay, seed=seed, delta=delta, q_min=q_min, q_max=q_max,
+                discount=discount, lr=lr, tau=tau, idx_seed=idx_seed, pi_init_w=pi_init_w,
+                q_init_w=q_init_w, counts=counts, soft=soft,
+                standard_bound=float(tr.standard_bound), std_init=float(tr.std_init))
+    for s in range(steps):
+        EPS_LOG.clear()
+        batch, idx = _record_batch(rb, B)
+        batch = dict(batch)
+        if counts:
+            c = crs.randint(0, 4, (B, 1)) * (crs.uniform(0, 1, (B, 1)) < 0.5)
+            batch["counts"] = c.astype(np.float64)
+            out[f"s{s}/counts"] = batch["counts"][:, 0]
+        tr.end_epoch(s)
+        tr.train(batch)
+        assert len(EPS_LOG) == 0      # deterministic policies draw nothing
+        out[f"s{s}/idx"] = idx.astype(np.int64)
+        for k, v in tr.get_diagnostics().items():
+            out[f"s{s}/stat/{k}"] = np.array(v, np.float64)
+        for gname, opt, order in (("policy", tr.policy_optimizer, PARAM_ORDER_POLICY),
+                                  ("target_policy", tr.target_policy_optimizer,
+                                   PARAM_ORDER_POLICY),
+                                  ("qf", tr.q_optimizer, PARAM_ORDER_Q)):
+            mod = dict(policy=tr.policy, target_policy=tr.target_policy, qf=tr.q)[gname]
+            for pname, g in zip(order, opt.recorded[-1]):
+                if g is None:
+                    g = torch.zeros_like(mod.state_dict()[pname])
+                pack(out, f"s{s}/grad/{gname}/{pname}", g.numpy(), full)
+        for gname, mod in (("policy", tr.policy), ("target_policy", tr.target_policy),
+                           ("qf", tr.q), ("tf", tr.q_target)):
+            for pname, t in mod.state_dict().items():
+                pack(out, f"s{s}/post/{gname}/{pname}", t.numpy(), full)
+    return meta, out
+
+
 # ------------------------------------------------------- OAC exploration
 def gen_oac_expl(name, obs_dim, act_dim, hidden, n_obs, beta_UB, delta, seed=5,
                  pi_init_w=0.1, q_init_w=0.1, eps_seed=3):
@@ -494,6 +560,9 @@ def main():
         save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
                                       pi_init_w=0.3, counts=True))
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "goac":
+        gen_goac_all()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "replay_count":
         save("replay_count", *gen_replay_count(False))
         save("replay_count_priority", *gen_replay_count(True))
@@ -520,6 +589,19 @@ def main():
     save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
                                   pi_init_w=0.3, counts=True))
     gen_sac_snapshot(os.path.join(HERE, "sac_snapshot.pt"))
+    gen_goac_all()
+
+
+def gen_goac_all():
+    save("goac_small", *gen_goac("goac_small", 111, 8, [32, 32], 32, 3, 500, True,
+                                 pi_init_w=0.3, q_init_w=0.3))
+    save("goac_counts", *gen_goac("goac_counts", 111, 8, [32, 32], 32, 3, 500, True,
+                                  pi_init_w=0.3, q_init_w=0.3, counts=True))
+    save("goac_soft", *gen_goac("goac_soft", 11, 3, [16, 16], 16, 3, 200, True,
+                                pi_init_w=0.5, q_init_w=0.5, soft=0.3, r_min=-1.0, r_max=1.0,
+                                discount=0.9, tau=0.05, lr=1e-3))
+    save("goac_humanoid", *gen_goac("goac_humanoid", 376, 17, [256, 256], 256, 2, 20000, False,
+                                    counts=True))
 
 
 if __name__ == "__main__":

@@ -4,7 +4,8 @@ import numpy as np
 import pytest
 import torch
 
-from fixtures_lib import sac_params, synthetic_transitions, PARAM_ORDER_POLICY, PARAM_ORDER_Q
+from fixtures_lib import (goac_params, sac_params, synthetic_transitions, PARAM_ORDER_POLICY,
+                          PARAM_ORDER_Q)
 import parity
 from oracle import sac_oracle as so
 from oracle.mt_oracle import MT
@@ -110,6 +111,62 @@ def test_poac_oracle_matches_reference_golden():
         bad = {k: v for k, v in errs.items()
                if v > (parity.TOL if k.startswith("s0/") else 1e-4)}
         assert not bad, (name, sorted(bad.items(), key=lambda kv: -kv[1])[:10])
+
+
+GOAC_FIXTURES = ["goac_small", "goac_counts", "goac_soft", "goac_humanoid"]
+GOAC_STATS = ("QF mean", "QF std", "QF Loss", "STD Loss", "Q Target Mean", "Q STD Target Mean",
+              "Policy Loss", "Policy mu Mean", "Policy log std Mean")
+
+
+def make_goac_oracle(meta, dtype=torch.float32):
+    params = goac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                         meta["q_min"], meta["q_max"], pi_init_w=meta["pi_init_w"],
+                         q_init_w=meta["q_init_w"])
+    return so.GaussianOACOracle(params, meta["obs_dim"], meta["act_dim"], delta=meta["delta"],
+                                q_min=meta["q_min"], q_max=meta["q_max"],
+                                discount=meta["discount"], policy_lr=meta["lr"],
+                                qf_lr=meta["lr"], tau=meta["tau"],
+                                std_soft_update_prob=meta["soft"], dtype=dtype)
+
+
+def goac_errors(meta, g, orc):
+    errs = {}
+    for s in range(meta["steps"]):
+        b = build_batch(meta, g[f"s{s}/idx"])
+        if meta["counts"]:
+            b["counts"] = g[f"s{s}/counts"][:, None]
+        out = orc.step(b)
+        for grp in ("policy", "target_policy", "qf"):
+            for pn in (PARAM_ORDER_Q if grp == "qf" else PARAM_ORDER_POLICY):
+                key = f"s{s}/grad/{grp}/{pn}"
+                errs[key] = parity.compare(g, key, out["grads"][grp][pn].numpy())
+        for grp, params_ in (("policy", orc.P), ("target_policy", orc.TP), ("qf", orc.Q),
+                             ("tf", orc.T)):
+            for pn, t in params_.items():
+                key = f"s{s}/post/{grp}/{pn}"
+                gk = f"s{s}/grad/{grp}/{pn}" if s == 0 and grp != "tf" else None
+                errs[key], _ = parity.compare_post(g, key, gk, t.numpy(), meta["lr"])
+        Da = meta["act_dim"]
+        th = out["target_head"]
+        st = {"QF mean": out["q_preds"].mean(), "QF std": out["std_preds"].mean(),
+              "QF Loss": out["q_loss"], "STD Loss": out["std_loss"],
+              "Q Target Mean": out["q_target"].mean(),
+              "Q STD Target Mean": out["std_target"].mean(),
+              "Policy Loss": out["upper_bound"].mean(), "Policy mu Mean": th["mean"].mean(),
+              "Policy log std Mean": th["log_std"].mean()}
+        for k in GOAC_STATS:
+            errs[f"s{s}/stat/{k}"] = parity.stat_err(float(st[k]), g, f"s{s}/stat/{k}")
+    return errs
+
+
+@pytest.mark.parametrize("name", GOAC_FIXTURES)
+def test_goac_oracle_matches_reference_golden(name):
+    """GaussianTrainer (g-oac) restatement vs the reference's own run."""
+    meta, g = parity.load(name)
+    errs = goac_errors(meta, g, make_goac_oracle(meta))
+    noise = goac_errors(meta, g, make_goac_oracle(meta, torch.float64))
+    bad = {k: (v, noise[k]) for k, v in errs.items() if v > parity.gate(k, noise[k])}
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
 
 
 @pytest.mark.parametrize("name", ["oac_expl_humanoid", "oac_expl_small"])
