@@ -173,6 +173,40 @@ def cpu_baseline(args):
                        f"{args.cpu_threads} thread(s))")
 
 
+def goac_cpu_baseline(args, steps=200):
+    """The oracle's CPU restatement of the g-oac step (GaussianOACOracle),
+    same dims / batch, on a bounded sample of steps."""
+    sys.path.insert(0, ROOT)
+    from oracle import sac_oracle as so
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from fixtures_lib import goac_params
+    torch.set_num_threads(args.cpu_threads)
+    Do, Da, H, B = args.obs_dim, args.act_dim, args.hidden, args.batch
+    n = 20_000
+    rs = np.random.RandomState(0)
+    data = dict(observations=rs.standard_normal((n, Do)), actions=rs.uniform(-1, 1, (n, Da)),
+                rewards=rs.standard_normal((n, 1)),
+                terminals=(rs.uniform(0, 1, (n, 1)) < 0.01).astype(np.uint8),
+                next_observations=rs.standard_normal((n, Do)))
+    rep = so.NumpyReplay(data)
+    orc = so.GaussianOACOracle(goac_params(Do, Da, [H, H], 0, 0.0, 500.0), Do, Da, q_max=500.0)
+    irs = np.random.RandomState(1)
+
+    def step():
+        _, b = rep.random_batch(B, irs)
+        orc.step(so.NumpyReplay.to_torch(b))
+    for _ in range(3):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    dt = time.perf_counter() - t0
+    return dict(value=round(steps / dt, 2), unit="grad-steps/s", cores=args.cpu_threads,
+                kind="port",
+                sample=f"{steps} oracle g-oac steps (Humanoid dims, 2x256, B={B}, "
+                       f"torch CPU fp32, {args.cpu_threads} thread(s))")
+
+
 def exploration_timing(tr, obs_dim, reps=200):
     """get_optimistic_exploration_action latency (one observation, the
     reference's per-env-step call; beta_UB 4.66, delta 23.53) and the
@@ -197,6 +231,40 @@ def exploration_timing(tr, obs_dim, reps=200):
     return {"us_per_call_1obs": round(1e6 * (t1 - t0) / reps, 1),
             "actions_per_s_64obs": round(64 * reps / (t2 - t1), 1),
             "beta_UB": 4.66, "delta": 23.53}
+
+
+def goac_timing(args, device, rb, steps=640, warmup=64, n=64):
+    """g-oac GaussianTrainer (trainer/gaussian_trainer.py, share_layers critic,
+    deterministic policy) on the same replay and dims:
+    gradient steps/s from the device index ring, n steps per graph launch."""
+    import oac_amd
+    from oac_amd import DeviceIndexStream, GaussianTrainer
+    torch.manual_seed(0)
+    hid = [args.hidden, args.hidden]
+    pp = oac_amd.get_policy_producer(args.obs_dim, args.act_dim, hid, device=device)
+    qp = oac_amd.get_q_producer(args.obs_dim, args.act_dim, hid, output_size=2, device=device)
+    tr = GaussianTrainer(pp, qp, action_space=Space(args.act_dim), discount=0.99,
+                         policy_lr=3e-4, qf_lr=3e-4, soft_target_tau=5e-3, q_min=0.0,
+                         q_max=500.0, share_layers=True, device=device, gemm_cfg=args.gemm_cfg)
+    stream = DeviceIndexStream(rb, args.batch, chunk=64, seed=11)
+    step = step_fn(tr, rb, stream, args.batch, n)
+    for _ in range(warmup // n):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps // n):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    assert torch.isfinite(tr.params).all().item(), "non-finite g-oac parameters"
+    return {"steps_per_s": round(steps / el, 1), "ms_per_step": round(1e3 * el / steps, 4),
+            "batch": args.batch, "steps": steps, "steps_per_launch": n,
+            "launches_per_step": int(_launches(tr))}
+
+
+def _launches(tr):
+    from oac_amd import _lib
+    return _lib.lib().oac_sac_launch_count(tr._last_plan.handle)
 
 
 def load_traffic(B):
@@ -306,6 +374,9 @@ def main():
             out["adam_GBps"] = round(ADAM_BYTES_PER_STEP * args.timing_steps / (ad["ms"] * 1e-3) / 1e9, 1)
         if world == 1:
             out["exploration"] = exploration_timing(tr, args.obs_dim)
+            out["goac"] = goac_timing(args, device, rb)
+            if not args.no_cpu_baseline:
+                out["goac"]["cpu_baseline"] = goac_cpu_baseline(args)
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

@@ -55,7 +55,9 @@ class _GpuExecutor:
         self._pol = trainer.grads[:lay.q1_base]   # policy Adam group
 
     def phase(self, i):
-        check(_lib.lib().oac_sac_step_phase(self.plan.handle, i, self.flags if i == 0 else 0,
+        # every phase sees the step flags: phase 0 gathers / draws, phase 1
+        # reads OAC_STEP_COUNTS (particle / gaussian targets)
+        check(_lib.lib().oac_sac_step_phase(self.plan.handle, i, self.flags,
                                             _lib.stream_ptr(self.stream)))
 
     def alpha_sum(self):

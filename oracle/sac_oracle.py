@@ -497,14 +497,37 @@ class GaussianOACOracle:
         return g
 
     def step(self, batch):
+        self.phase0(batch)
+        self.phase1()
+        self.phase2()
+        return self.phase3()
+
+    @staticmethod
+    def _flat(grads, order):
+        return torch.cat([grads[k].reshape(-1) for k in order])
+
+    @staticmethod
+    def _unflat(flat, like, order):
+        out, o = {}, 0
+        for k in order:
+            n = like[k].numel()
+            out[k] = flat[o:o + n].view(like[k].shape)
+            o += n
+        return out
+
+    # data-parallel split (oac_amd.dp.dp_step): the only cross-rank quantities
+    # are the critic and the policy gradients (local batch means; the Adam
+    # passes divide the all-reduced sums by the world size)
+    def phase0(self, batch):
         dt = self.dtype
-        obs = _t(batch["observations"], dt)
+        S = self.S = {}
+        obs = S["obs"] = _t(batch["observations"], dt)
         act = _t(batch["actions"], dt)
         rew = _t(batch["rewards"], dt)
         term = _t(batch["terminals"], dt)
         nobs = _t(batch["next_observations"], dt)
-        B = obs.shape[0]
-        c = q_forward(obs, act, self.Q)                              # :187
+        B = S["B"] = obs.shape[0]
+        c = S["c"] = q_forward(obs, act, self.Q)                     # :187
         q_preds, std_preds = c["q"][:, :1], torch.exp(c["q"][:, 1:2])
         pf2 = policy_forward(nobs, self.P, None, deterministic=True)  # :199-202
         tq = q_forward(nobs, pf2["a"], self.T)["q"]                  # :204
@@ -518,32 +541,53 @@ class GaussianOACOracle:
             std_target = std_target * factor + (1 - factor) * std_preds
         q_target = self.reward_scale * rew + (1. - term) * self.discount * tq0   # :227-228
         std_target = torch.clamp(std_target, 0, self.std_init)       # :229
-        q_loss = ((q_preds - q_target) ** 2).mean()                  # :231-234
-        std_loss = ((std_preds - std_target) ** 2).mean()
-        dq = torch.cat([2.0 * (q_preds - q_target) / B,
-                        2.0 * (std_preds - std_target) / B * std_preds], dim=1)
-        gq = q_param_grads(c, dq, self.Q)
-        self.opt_q.step(gq)                                          # :237
-        pf = policy_forward(obs, self.P, None, deterministic=True)   # :315-318 (pre-step pi)
+        S.update(q_preds=q_preds, std_preds=std_preds, q_target=q_target, std_target=std_target,
+                 q_loss=((q_preds - q_target) ** 2).mean(),          # :231-234
+                 std_loss=((std_preds - std_target) ** 2).mean())
+        # both policy forwards on obs use the pre-step policies      :315-318, :342-344
+        S["pf"] = policy_forward(obs, self.P, None, deterministic=True)
+        S["tpf"] = policy_forward(obs, self.TP, None, deterministic=True)
+
+    def phase1(self, world=1):
+        S = self.S
+        B = S["B"]
+        dq = torch.cat([2.0 * (S["q_preds"] - S["q_target"]) / B,
+                        2.0 * (S["std_preds"] - S["std_target"]) / B * S["std_preds"]], dim=1)
+        S["gq"] = q_param_grads(S["c"], dq, self.Q)
+        self.crit_flat = self._flat(S["gq"], list(self.Q))
+
+    def phase2(self, world=1):
+        S = self.S
+        B, obs = S["B"], S["obs"]
+        gq = self._unflat(self.crit_flat, self.Q, list(self.Q))
+        self.opt_q.step({k: v / world for k, v in gq.items()})     # :237
+        pf, tpf = S["pf"], S["tpf"]
         cn = q_forward(obs, pf["a"], self.Q)                         # :325 (post-step Q)
         qs, stds = cn["q"][:, :1], torch.exp(cn["q"][:, 1:2])
-        ub = qs + self.z * stds                                      # :331
+        S["ub"] = qs + self.z * stds                                 # :331
         g0 = -torch.ones_like(qs) / B
         da = q_input_grad(cn, torch.cat([g0, g0 * self.z * stds], dim=1), self.Q)[:, self.Do:]
-        gp = self.det_policy_backward(pf, self.P, da)
-        self.opt_p.step(gp)                                          # :334-337
-        tpf = policy_forward(obs, self.TP, None, deterministic=True)  # :342-344
+        S["gp"] = self.det_policy_backward(pf, self.P, da)
         ct = q_forward(obs, tpf["a"], self.Q)                        # :346
         dat = q_input_grad(ct, torch.cat([g0, torch.zeros_like(g0)], dim=1), self.Q)[:, self.Do:]
-        gtp = self.det_policy_backward(tpf, self.TP, dat)
-        self.opt_tp.step(gtp)                                        # :352-354
+        S["gtp"] = self.det_policy_backward(tpf, self.TP, dat)
+        self.pol_flat = torch.cat([self._flat(S["gp"], list(self.P)),
+                                   self._flat(S["gtp"], list(self.TP))])
+
+    def phase3(self, world=1):
+        S = self.S
+        n = self._flat(S["gp"], list(self.P)).numel()
+        gp = self._unflat(self.pol_flat[:n], self.P, list(self.P))
+        gtp = self._unflat(self.pol_flat[n:], self.TP, list(self.TP))
+        self.opt_p.step({k: v / world for k, v in gp.items()})      # :334-337
+        self.opt_tp.step({k: v / world for k, v in gtp.items()})    # :352-354
         if self.n_steps % self.period == 0:                          # :358-362
             polyak(self.T, self.Q, self.tau)
         self.n_steps += 1
-        self.last = dict(grads=dict(policy=gp, target_policy=gtp, qf=gq), q_loss=q_loss,
-                         std_loss=std_loss, q_preds=q_preds, std_preds=std_preds,
-                         q_target=q_target, std_target=std_target, upper_bound=ub,
-                         target_head=tpf)
+        self.last = dict(grads=dict(policy=S["gp"], target_policy=S["gtp"], qf=S["gq"]),
+                         q_loss=S["q_loss"], std_loss=S["std_loss"], q_preds=S["q_preds"],
+                         std_preds=S["std_preds"], q_target=S["q_target"],
+                         std_target=S["std_target"], upper_bound=S["ub"], target_head=S["tpf"])
         return self.last
 
 

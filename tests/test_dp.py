@@ -107,3 +107,84 @@ def test_dp_two_ranks_equals_single_process_on_global_batch(auto_alpha):
                       for t in d.values()] + [ref.log_alpha]).numpy()
     assert parity.rel_err(got, want) < 1e-6
     assert np.max(np.abs(got - want)) < 1e-5
+
+
+# ---------------------------------------------------------------- g-oac
+class GaussOracleExecutor:
+    """GaussianOACOracle phases behind the dp_step executor interface (no
+    alpha: the phase-0 exchange is skipped, like the GPU executor's)."""
+    auto_alpha = False
+
+    def __init__(self, orc, batch, world):
+        self.o, self.b, self.w = orc, batch, world
+
+    def phase(self, i):
+        if i == 0:
+            self.o.phase0(self.b)
+        else:
+            getattr(self.o, f"phase{i}")(self.w)
+
+    def critic_grads(self):
+        return self.o.crit_flat
+
+    def policy_grads(self):
+        return self.o.pol_flat
+
+
+def _goac_make():
+    from fixtures_lib import goac_params
+    from oracle import sac_oracle as so
+    p = goac_params(Do, Da, H, 3, 0.0, 100.0, pi_init_w=0.2, q_init_w=0.1)
+    return so.GaussianOACOracle(p, Do, Da, q_min=0.0, q_max=100.0, policy_lr=1e-3, qf_lr=1e-3)
+
+
+def _goac_inputs(world):
+    out = []
+    for s, (batch, _, _) in enumerate(_inputs(world)):
+        rs = np.random.RandomState(100 + s)
+        n = BL * world
+        b = dict(batch, counts=(rs.randint(0, 3, (n, 1)) * (rs.uniform(0, 1, (n, 1)) < 0.5)))
+        out.append(b)
+    return out
+
+
+def _goac_flat(orc):
+    return torch.cat([t.reshape(-1) for d in (orc.P, orc.TP, orc.Q, orc.T)
+                      for t in d.values()]).numpy()
+
+
+def _goac_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oac_amd.dp import dp_step
+    orc = _goac_make()
+    for batch in _goac_inputs(world):
+        sl = slice(rank * BL, (rank + 1) * BL)
+        ex = GaussOracleExecutor(orc, {k: v[sl] for k, v in batch.items()}, world)
+        dp_step(ex, lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM))
+    if rank == 0:
+        out.put(_goac_flat(orc))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_goac_dp_two_ranks_equals_single_process_on_global_batch():
+    """g-oac (GaussianTrainer) data-parallel step over gloo, counts=True."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_goac_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ref = _goac_make()
+    for batch in _goac_inputs(world):
+        ref.step(batch)
+    want = _goac_flat(ref)
+    assert parity.rel_err(got, want) < 1e-6
+    assert np.max(np.abs(got - want)) < 1e-5

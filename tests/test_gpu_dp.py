@@ -32,8 +32,31 @@ def _inputs(world):
     return out
 
 
-def _trainer(dp):
+def _trainer(dp, kind="sac"):
     from gpu_helpers import producers, Space
+    if kind == "goac":
+        from fixtures_lib import goac_params
+        from oac_amd import GaussianTrainer
+        from oac_amd.dp import DataParallelGaussianTrainer
+        from test_gpu_goac import goac_producers
+        pp, qp = goac_producers(goac_params(Do, Da, [H, H], 3, 0.0, 100.0, pi_init_w=0.2,
+                                            q_init_w=0.1))
+        cls = DataParallelGaussianTrainer if dp else GaussianTrainer
+        return cls(pp, qp, action_space=Space(Da), discount=0.99, policy_lr=1e-3, qf_lr=1e-3,
+                   soft_target_tau=5e-3, q_min=0.0, q_max=100.0, share_layers=True, counts=True)
+    if kind == "poac":
+        from oac_amd import ParticleTrainer
+        from oac_amd.dp import DataParallelParticleTrainer
+        K = 5
+        pp, qp = producers(sac_params(Do, Da, [H, H], 3, q_out=K, pi_init_w=0.2,
+                                      q_last_bias=np.linspace(0.0, 50.0, K)),
+                           q_keys=("qf1", "qf2", "target_qf1", "target_qf2", "qf1",
+                                   "target_qf1"))
+        cls = DataParallelParticleTrainer if dp else ParticleTrainer
+        return cls(pp, qp, n_estimators=K, action_space=Space(Da), discount=0.99,
+                   policy_lr=1e-3, qf_lr=1e-3, soft_target_tau=5e-3,
+                   use_automatic_entropy_tuning=True, deterministic=False, q_min=0.0,
+                   q_max=50.0, share_layers=True, counts=True)
     from oac_amd import SACTrainer
     from oac_amd.dp import DataParallelSACTrainer
     pp, qp = producers(sac_params(Do, Da, [H, H], 3, pi_init_w=0.2, q_init_w=0.1))
@@ -42,7 +65,15 @@ def _trainer(dp):
                qf_lr=1e-3, soft_target_tau=5e-3, use_automatic_entropy_tuning=True)
 
 
-def _worker(rank, world, port, q):
+def _with_counts(batch, step):
+    b = dict(batch)
+    rs = np.random.RandomState(100 + step)
+    n = len(b["rewards"])
+    b["counts"] = (rs.randint(0, 3, (n, 1)) * (rs.uniform(0, 1, (n, 1)) < 0.5)).astype(np.float64)
+    return b
+
+
+def _worker(rank, world, port, q, kind="sac"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
@@ -51,9 +82,14 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    tr = _trainer(True)
-    for batch, e1, e2 in _inputs(world):
+    tr = _trainer(True, kind)
+    for step, (batch, e1, e2) in enumerate(_inputs(world)):
         sl = slice(rank * BL, (rank + 1) * BL)
+        if kind == "goac":
+            tr.train_from_torch({k: v[sl] for k, v in _with_counts(batch, step).items()})
+            continue
+        if kind == "poac":
+            batch = _with_counts(batch, step)
         tr.train_from_torch({k: v[sl] for k, v in batch.items()}, eps1=e1[sl], eps2=e2[sl])
     torch.cuda.synchronize()
     if rank == 0:
@@ -62,7 +98,8 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_dp_trainer_two_ranks_equals_single_gpu_on_global_batch():
+@pytest.mark.parametrize("kind", ["sac", "goac", "poac"])
+def test_dp_trainer_two_ranks_equals_single_gpu_on_global_batch(kind):
     world = 2
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -70,16 +107,21 @@ def test_dp_trainer_two_ranks_equals_single_gpu_on_global_batch():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
     got = q.get()
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
-    tr = _trainer(False)
-    for batch, e1, e2 in _inputs(world):
-        tr.train_from_torch(batch, eps1=e1, eps2=e2)
+    tr = _trainer(False, kind)
+    for step, (batch, e1, e2) in enumerate(_inputs(world)):
+        if kind == "goac":
+            tr.train_from_torch(_with_counts(batch, step))
+        elif kind == "poac":
+            tr.train_from_torch(_with_counts(batch, step), eps1=e1, eps2=e2)
+        else:
+            tr.train_from_torch(batch, eps1=e1, eps2=e2)
     want = torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy()
     assert parity.rel_err(got, want) < 1e-6, parity.rel_err(got, want)
 
