@@ -18,6 +18,8 @@
  *                         (trainer/particle_trainer_oac.py:169-363)
  *   OAC_KIND_GAUSS        GaussianTrainer.train_from_torch (g-oac), share_layers=True
  *                         (trainer/gaussian_trainer.py:177-437)
+ *   OAC_KIND_PARTICLE_UB  ParticleTrainer.train_from_torch, share_layers=True
+ *                         (trainer/particle_trainer.py:175-432; the p-oac recipes)
  *   oac_expl_action       get_optimistic_exploration_action (stochastic branch)
  *                         (optimistic_exploration.py:7-11, 14-109)
  *   oac_replay_sample_indices   np.random.randint(0, size, B) (replay_buffer.py:107)
@@ -38,10 +40,17 @@ extern "C" {
 #define OAC_ABI_VERSION 1
 
 /* ---------------------------------------------------------------- config */
-enum oac_kind { OAC_KIND_SAC = 0, OAC_KIND_PARTICLE = 1, OAC_KIND_GAUSS = 2 };
+enum oac_kind {
+  OAC_KIND_SAC = 0,          /* SACTrainer (OAC / SAC)                         */
+  OAC_KIND_PARTICLE = 1,     /* particle_trainer_oac.ParticleTrainer (p-oac + OAC exploration) */
+  OAC_KIND_GAUSS = 2,        /* gaussian_trainer.GaussianTrainer (g-oac)       */
+  OAC_KIND_PARTICLE_UB = 3   /* particle_trainer.ParticleTrainer (p-oac recipes: deterministic
+                                policy, upper-bound quantile loss, target_policy) */
+};
 
 typedef struct oac_sac_config {
-  int kind;              /* OAC_KIND_SAC (twin critics, q_out=1), OAC_KIND_PARTICLE or
+  int kind;              /* OAC_KIND_SAC (twin critics, q_out=1); OAC_KIND_PARTICLE and
+                            OAC_KIND_PARTICLE_UB (one critic, q_out = K particles);
                             OAC_KIND_GAUSS (one critic, q_out=2: mean | log std) */
   int obs_dim, act_dim;
   int hidden;            /* width of both hidden layers (reference: [M]*N, N=2) */
@@ -57,10 +66,16 @@ typedef struct oac_sac_config {
   uint64_t seed;         /* Philox key for the policy noise */
   int gemm_cfg;          /* -1 auto, 0 small tiles + split-K, 1 large tiles */
   int world_size;        /* data-parallel ranks (alpha / gradient averaging) */
-  /* OAC_KIND_GAUSS only (gaussian_trainer.py:65-72, main.py:219-233, 549-554) */
+  /* OAC_KIND_GAUSS (gaussian_trainer.py:65-72, main.py:219-233, 549-554) */
   float std_bound;       /* standard_bound = norm.ppf(delta) */
   float std_init;        /* (q_max - q_min) / sqrt(12): upper clamp of the std target */
-  float std_soft_prob;   /* std_soft_update_prob; < 0: std_soft_update off */
+  int std_soft_update;   /* GAUSS, PARTICLE_UB: std_soft_update with probability std_soft_prob */
+  float std_soft_prob;   /* std_soft_update_prob */
+  /* OAC_KIND_GAUSS / OAC_KIND_PARTICLE_UB */
+  int mean_update;       /* next actions from target_policy instead of policy */
+  /* OAC_KIND_PARTICLE_UB (particle_trainer.py:61-69, 255-264) */
+  int delta_index;       /* sorted particle the policy maximises */
+  float rescale_spread;  /* rescale_targets_around_mean: q_max - q_min; <= 0: off */
 } oac_sac_config;
 
 /* Flat parameter arena layout (float offsets; every tensor 16-byte aligned).
@@ -70,7 +85,7 @@ typedef struct oac_sac_config {
  * likewise.  Each critic block holds fc0.weight, fc0.bias, fc1.weight,
  * fc1.bias, last_fc.weight, last_fc.bias.  Arenas: params/grads/adam_m/adam_v
  * = [policy | critic 1 | critic 2] (one critic for PARTICLE; [policy |
- * target_policy | critic] for GAUSS); targets = [target critic 1 | target
+ * target_policy | critic] for GAUSS and PARTICLE_UB); targets = [target critic 1 | target
  * critic 2]. */
 typedef struct oac_sac_layout {
   int64_t pol_fc0_w, pol_fc0_b, pol_fc1_w, pol_fc1_b, pol_head_w, pol_head_b, pol_size;
@@ -79,8 +94,8 @@ typedef struct oac_sac_layout {
   int64_t n_critics;
   int64_t params_total, targets_total;
   int64_t workspace_floats;
-  int64_t tpol_base;     /* GAUSS: target_policy block (params = [policy | target_policy |
-                            critic], one Adam group over both policies); else -1 */
+  int64_t tpol_base;     /* GAUSS, PARTICLE_UB: target_policy block (params = [policy |
+                            target_policy | critic], one Adam group over both policies); else -1 */
 } oac_sac_layout;
 
 typedef struct oac_sac_buffers {
@@ -105,7 +120,7 @@ enum oac_ws_buffer {
   OAC_WS_Q1, OAC_WS_Q2, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_TQ2,
   OAC_WS_Y, OAC_WS_SQE1, OAC_WS_SQE2, OAC_WS_QNEW,
   OAC_WS_COUNTS,                       /* [B] batch counts (ReplayBufferCount) for OAC_STEP_COUNTS */
-  OAC_WS_HEAD3, OAC_WS_ACT3,           /* GAUSS: target_policy(obs) head [B, 2Da] and action */
+  OAC_WS_HEAD3, OAC_WS_ACT3,           /* GAUSS, PARTICLE_UB: target_policy(obs) head and action */
   OAC_WS_COUNT_PUBLIC
 };
 
@@ -115,8 +130,9 @@ enum oac_ws_buffer {
 #define OAC_STEP_USE_GRAPH    4  /* replay the captured hipGraph of the step */
 #define OAC_STEP_COUNTS       8  /* particle / gaussian trainer with counts=True: the batch
                                     counts the caller wrote into OAC_WS_COUNTS shape the
-                                    quantile targets (particle_trainer_oac.py:220-224) or the
-                                    std target (gaussian_trainer.py:238-242) */
+                                    quantile targets (particle_trainer_oac.py:220-224,
+                                    particle_trainer.py:236-241) or the std target
+                                    (gaussian_trainer.py:238-242) */
 
 int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out);
 int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_sac** out);

@@ -1,21 +1,34 @@
-// g-oac Gaussian trainer step on MI355X: GaussianTrainer.train_from_torch
-// with share_layers=True and the deterministic policy -- the configuration of
-// reproduce_g-oac*.sh (--share_layers [--counts]; GaussianTrainer's default
-// deterministic=True is not overridden for g-oac, main.py:219-233).
-// One critic with two outputs (Q mean | log std), its target, the policy and
-// a separately trained target_policy (/root/reference/trainer/gaussian_trainer.py):
-//   Q(obs,a) [187] -> a' = tanh(mean_pi(next_obs)) [199-202]
-//   -> QT(next_obs,a') [204] -> q / std targets (counts, soft update, clamp)
-//      [207-237] -> Adam(Q, grad MSE(q) + MSE(std)) [227-237]
-//   -> a~ = tanh(mean_pi(obs)) [315-318] -> ub = Q_new(a~)_0 + z*exp(Q_new(a~)_1)
-//      [325-331] -> Adam(pi, -mean(ub)) [334-337]
-//   -> a~_T = tanh(mean_piT(obs)) [342-344] -> Adam(piT, -mean(Q_new(a~_T)_0)) [346-354]
-//   -> Polyak Q -> QT [359-362]
+// Deterministic-policy trainers with a separately trained target_policy, on
+// MI355X: one critic with K outputs, its target, the policy and the
+// target_policy (params = [policy | target_policy | critic], one Adam group
+// over both policies).  Two reference trainers share this launch sequence and
+// differ only in their row kernels:
+//
+// * g-oac GaussianTrainer, share_layers=True (OAC_KIND_GAUSS, K = 2 outputs
+//   Q | log std; /root/reference/trainer/gaussian_trainer.py) -- the
+//   configuration of reproduce_g-oac*.sh (GaussianTrainer's default
+//   deterministic=True is not overridden for g-oac, main.py:219-233):
+//     Q(obs,a) [187] -> a' = tanh(mean_pi(next_obs)) [199-202]
+//     -> QT(next_obs,a') [204] -> q / std targets (counts, soft update, clamp)
+//        [207-237] -> Adam(Q, grad MSE(q) + MSE(std)) [227-237]
+//     -> a~ = tanh(mean_pi(obs)) [315-318] -> ub = Q_new(a~)_0 + z*exp(Q_new(a~)_1)
+//        [325-331] -> Adam(pi, -mean(ub)) [334-337]
+//     -> a~_T = tanh(mean_piT(obs)) [342-344] -> Adam(piT, -mean(Q_new(a~_T)_0))
+//        [346-354] -> Polyak Q -> QT [359-362]
+// * p-oac ParticleTrainer, share_layers=True (OAC_KIND_PARTICLE_UB, K
+//   particles; /root/reference/trainer/particle_trainer.py) -- what main.py
+//   builds for --alg p-oac without --beta_UB (main.py:198-204, 364, 488-490),
+//   i.e. every reproduce_p-oac*.sh recipe: sorted-particle TD targets (counts,
+//   soft update, rescale) with the loss averaged over particles [190-270], the
+//   policy maximising the delta_index-th sorted particle of Q_new [317-330],
+//   the target policy the particle mean [339-348], Polyak [353-357].
+//
+// mean_update: next actions come from the target policy (both trainers).
 // Both policy forwards on obs use pre-step policies and the post-step critic,
-// freshly evaluated (no saved-activation quirk here): the critic Adam
-// completes before either policy loss is formed.  The two policy losses are
-// independent (pi's step does not touch Q or piT), so their backward passes
-// share launches, and one Adam pass updates [policy | target_policy].
+// freshly evaluated (no saved-activation quirk): the critic Adam completes
+// before either policy loss is formed.  The two policy losses are independent
+// (pi's step touches neither Q nor piT), so their backward passes share
+// launches, and one Adam pass updates [policy | target_policy].
 #include <cstring>
 
 #include "../../include/oac_amd.h"
@@ -27,10 +40,11 @@
 namespace oac {
 
 enum GWs {
-  // public ids: HEAD1/ACT1 = pi(obs), HEAD2/ACT2 = pi(next_obs), HEAD3/ACT3 =
-  // target_policy(obs); Q1 = Q(obs,a) [B,2] raw, TQ1 = QT(next_obs,a') [B,2],
-  // QN1 = Q_new(obs,a~) [B,2], QN2 = Q_new(obs,a~_T) [B,2], Y / SQE1 [B,2]
-  // (q | std), QNEW = upper bound [B].
+  // public ids: HEAD1/ACT1 = pi(obs), HEAD2/ACT2 = next-action policy
+  // (pi or, mean_update, piT) on next_obs, HEAD3/ACT3 = target_policy(obs);
+  // Q1 = Q(obs,a) [B,K] raw, TQ1 = QT(next_obs,a') [B,K], QN1 = Q_new(obs,a~),
+  // QN2 = Q_new(obs,a~_T) [B,K]; Y / SQE1 [B,K] (GAUSS: q | std; PARTICLE_UB:
+  // sorted slots), QNEW = upper bound [B].
   G_H1P = OAC_WS_COUNT_PUBLIC, G_H2P, G_H1P2, G_H2P2, G_H1TP, G_H2TP,
   G_P, G_H1Q, G_H2Q, G_PT, G_H1T, G_H2T,
   G_DQ, G_DH2Q, G_DH1Q,
@@ -40,19 +54,19 @@ enum GWs {
 };
 static_assert(G_COUNT <= WS_GSLAB_Q, "workspace ids");
 
-void gauss_layout_workspace(SacPlan& p) {
+void det_layout_workspace(SacPlan& p) {
   const oac_sac_config& c = p.c;
-  const int64_t B = c.batch, H = c.hidden, Da = c.act_dim;
+  const int64_t B = c.batch, H = c.hidden, Da = c.act_dim, K = c.q_out;
   for (int i = 0; i < kMaxWs; ++i) p.ws[i] = {0, 0, 0};
   auto set = [&](int id, int64_t r, int64_t cl) { p.ws[id] = {0, r, cl}; };
   set(OAC_WS_BATCH, B, c.row_stride);
   for (int id : {OAC_WS_HEAD1, OAC_WS_HEAD2, OAC_WS_HEAD3}) set(id, B, 2 * Da);
   for (int id : {OAC_WS_ACT1, OAC_WS_ACT2, OAC_WS_ACT3}) set(id, B, Da);
-  for (int id : {OAC_WS_Q1, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_Y, OAC_WS_SQE1}) set(id, B, 2);
+  for (int id : {OAC_WS_Q1, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_Y, OAC_WS_SQE1}) set(id, B, K);
   set(OAC_WS_QNEW, B, 1);
   set(OAC_WS_COUNTS, B, 1);
   for (int id = G_H1P; id <= G_H2T; ++id) set(id, B, H);
-  for (int id : {G_DQ, G_GQ, G_GQ3}) set(id, B, 2);
+  for (int id : {G_DQ, G_GQ, G_GQ3}) set(id, B, K);
   for (int id : {G_DH2Q, G_DH1Q, G_PN, G_H1N, G_H2N, G_PN3, G_H1N3, G_H2N3, G_DH2N, G_DH1N,
                  G_DH2N3, G_DH1N3, G_DH2P, G_DH1P, G_DH2TP, G_DH1TP})
     set(id, B, H);
@@ -70,7 +84,7 @@ void gauss_layout_workspace(SacPlan& p) {
 
 // ------------------------------------------------------------------ phases
 // forward of everything the pre-step parameters determine
-static int gphase0(SacPlan& p, int flags, hipStream_t s) {
+static int dphase0(SacPlan& p, int flags, hipStream_t s) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -87,15 +101,17 @@ static int gphase0(SacPlan& p, int flags, hipStream_t s) {
     TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_gather(g, s)));
     p.launches++;
   }
+  const int K = c.q_out;
   const float* pol = p.b.params;
   const float* tpol = p.b.params + L.tpol_base;
+  const float* npol = c.mean_update ? tpol : pol;   // the policy acting on next_obs
   const float* q = p.b.params + L.q1_base;
   const float* tq = p.b.targets;
   {
     GemmBatch gb{};
     add(gb, t_fwd(obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(G_H1P), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
     gb.publish = p.state(); gb.pub_beta1 = c.beta1; gb.pub_beta2 = c.beta2;   // step's Adam constants
-    add(gb, t_fwd(nobs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(G_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
+    add(gb, t_fwd(nobs, RS, B, Do, npol + L.pol_fc0_w, Do, H, p.W(G_H1P2), H, EPI_BIAS_RELU, npol + L.pol_fc0_b));
     add(gb, t_fwd(obs, RS, B, Do, tpol + L.pol_fc0_w, Do, H, p.W(G_H1TP), H, EPI_BIAS_RELU, tpol + L.pol_fc0_b));
     GemmTask t = t_fwd(obs, RS, B, Do, q + L.q_fc0_w, Dq, H, p.W(G_P), H, EPI_BIAS_RANK_RELU, q + L.q_fc0_b);
     t.U = X + c.off_act; t.ldu = RS; t.V = q + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
@@ -107,7 +123,7 @@ static int gphase0(SacPlan& p, int flags, hipStream_t s) {
   {
     GemmBatch gb{};
     add(gb, t_fwd(p.W(G_H1P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(G_H2P), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
-    add(gb, t_fwd(p.W(G_H1P2), H, B, H, pol + L.pol_fc1_w, H, H, p.W(G_H2P2), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
+    add(gb, t_fwd(p.W(G_H1P2), H, B, H, npol + L.pol_fc1_w, H, H, p.W(G_H2P2), H, EPI_BIAS_RELU, npol + L.pol_fc1_b));
     add(gb, t_fwd(p.W(G_H1TP), H, B, H, tpol + L.pol_fc1_w, H, H, p.W(G_H2TP), H, EPI_BIAS_RELU, tpol + L.pol_fc1_b));
     add(gb, t_fwd(p.W(G_H1Q), H, B, H, q + L.q_fc1_w, H, H, p.W(G_H2Q), H, EPI_BIAS_RELU, q + L.q_fc1_b));
     if (run_gemm(p, gb, s)) return 1;
@@ -115,9 +131,9 @@ static int gphase0(SacPlan& p, int flags, hipStream_t s) {
   {
     GemmBatch gb{};
     add(gb, t_fwd(p.W(G_H2P), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD1), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
-    add(gb, t_fwd(p.W(G_H2P2), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD2), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
+    add(gb, t_fwd(p.W(G_H2P2), H, B, H, npol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD2), 2 * Da, EPI_BIAS, npol + L.pol_head_b));
     add(gb, t_fwd(p.W(G_H2TP), H, B, H, tpol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD3), 2 * Da, EPI_BIAS, tpol + L.pol_head_b));
-    add(gb, t_fwd(p.W(G_H2Q), H, B, H, q + L.q_last_w, H, 2, p.W(OAC_WS_Q1), 2, EPI_BIAS, q + L.q_last_b));
+    add(gb, t_fwd(p.W(G_H2Q), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_Q1), K, EPI_BIAS, q + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
@@ -134,11 +150,11 @@ static int gphase0(SacPlan& p, int flags, hipStream_t s) {
 }
 
 // target critic, TD targets, critic gradients (into grad_q)
-static int gphase1(SacPlan& p, int flags, hipStream_t s) {
+static int dphase1(SacPlan& p, int flags, hipStream_t s) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
-  const int Dq = Do + Da;
+  const int Dq = Do + Da, K = c.q_out;
   float* X = p.W(OAC_WS_BATCH);
   const float* q = p.b.params + L.q1_base;
   const float* tq = p.b.targets;
@@ -157,26 +173,40 @@ static int gphase1(SacPlan& p, int flags, hipStream_t s) {
   }
   {
     GemmBatch gb{};
-    add(gb, t_fwd(p.W(G_H2T), H, B, H, tq + L.q_last_w, H, 2, p.W(OAC_WS_TQ1), 2, EPI_BIAS, tq + L.q_last_b));
+    add(gb, t_fwd(p.W(G_H2T), H, B, H, tq + L.q_last_w, H, K, p.W(OAC_WS_TQ1), K, EPI_BIAS, tq + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {
+  const float* counts = (flags & OAC_STEP_COUNTS) ? p.W(OAC_WS_COUNTS) : nullptr;
+  if (c.kind == OAC_KIND_GAUSS) {
     GaussTargetArgs a;
     std::memset(&a, 0, sizeof(a));
     a.q = p.W(OAC_WS_Q1); a.tq = p.W(OAC_WS_TQ1); a.batch = X; a.ld_batch = RS;
     a.off_rew = c.off_rew; a.off_term = c.off_term; a.reward_scale = c.reward_scale;
-    a.discount = c.discount; a.std_init = c.std_init; a.soft_prob = c.std_soft_prob;
-    a.counts = (flags & OAC_STEP_COUNTS) ? p.W(OAC_WS_COUNTS) : nullptr;
+    a.discount = c.discount; a.std_init = c.std_init;
+    a.soft_prob = c.std_soft_update ? c.std_soft_prob : -1.f;
+    a.counts = counts;
     a.B = B; a.dq = p.W(G_DQ); a.y = p.W(OAC_WS_Y); a.sqe = p.W(OAC_WS_SQE1);
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_gauss_targets(a, s)));
+    p.launches++;
+  } else {
+    ParticleTargetArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.q = p.W(OAC_WS_Q1); a.tq = p.W(OAC_WS_TQ1); a.batch = X; a.ld_batch = RS;
+    a.off_rew = c.off_rew; a.off_term = c.off_term; a.reward_scale = c.reward_scale;
+    a.discount = c.discount; a.B = B; a.K = K;
+    a.dq = p.W(G_DQ); a.sqe = p.W(OAC_WS_SQE1); a.y = p.W(OAC_WS_Y); a.counts = counts;
+    a.loss_scale = 1.f / (float)K;                       // qf_loss /= num_particles
+    a.soft_prob = c.std_soft_update ? c.std_soft_prob : -1.f;
+    a.rescale_spread = c.rescale_spread;
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_particle_targets(a, s)));
     p.launches++;
   }
   {
     GemmBatch gb{};
     float* gq = grad_q(p);
-    add(gb, t_dw(p.W(G_DQ), 2, 2, B, p.W(G_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
+    add(gb, t_dw(p.W(G_DQ), K, K, B, p.W(G_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
                  q_group(p), p.sp_ql));
-    add(gb, t_dx(p.W(G_DQ), 2, B, 2, q + L.q_last_w, H, H, p.W(G_DH2Q), H, p.W(G_H2Q), H));
+    add(gb, t_dx(p.W(G_DQ), K, B, K, q + L.q_last_w, H, H, p.W(G_DH2Q), H, p.W(G_H2Q), H));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
@@ -199,11 +229,11 @@ static int gphase1(SacPlan& p, int flags, hipStream_t s) {
 
 // critic Adam done: post-step critic on (obs, a~) and (obs, a~_T), the two
 // policy losses' gradients (into grad_p: policy block, target_policy block)
-static int gphase2(SacPlan& p, hipStream_t s) {
+static int dphase2(SacPlan& p, hipStream_t s) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
-  const int Dq = Do + Da;
+  const int Dq = Do + Da, K = c.q_out;
   float* X = p.W(OAC_WS_BATCH);
   const float* pol = p.b.params;
   const float* tpol = p.b.params + L.tpol_base;
@@ -227,22 +257,30 @@ static int gphase2(SacPlan& p, hipStream_t s) {
   }
   {
     GemmBatch gb{};
-    add(gb, t_fwd(p.W(G_H2N), H, B, H, q + L.q_last_w, H, 2, p.W(OAC_WS_QN1), 2, EPI_BIAS, q + L.q_last_b));
-    add(gb, t_fwd(p.W(G_H2N3), H, B, H, q + L.q_last_w, H, 2, p.W(OAC_WS_QN2), 2, EPI_BIAS, q + L.q_last_b));
+    add(gb, t_fwd(p.W(G_H2N), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_QN1), K, EPI_BIAS, q + L.q_last_b));
+    add(gb, t_fwd(p.W(G_H2N3), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_QN2), K, EPI_BIAS, q + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {
+  if (c.kind == OAC_KIND_GAUSS) {
     GaussSeedArgs a;
     std::memset(&a, 0, sizeof(a));
     a.qn = p.W(OAC_WS_QN1); a.qt = p.W(OAC_WS_QN2); a.std_bound = c.std_bound; a.B = B;
     a.g = p.W(G_GQ); a.gt = p.W(G_GQ3); a.ub = p.W(OAC_WS_QNEW);
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_gauss_seed(a, s)));
     p.launches++;
+  } else {
+    ParticleUbSeedArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.qn = p.W(OAC_WS_QN1); a.qt = p.W(OAC_WS_QN2); a.B = B; a.K = K;
+    a.delta_index = c.delta_index;
+    a.g = p.W(G_GQ); a.gt = p.W(G_GQ3); a.ub = p.W(OAC_WS_QNEW);
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_particle_ub_seed(a, s)));
+    p.launches++;
   }
   {
     GemmBatch gb{};
-    add(gb, t_dx(p.W(G_GQ), 2, B, 2, q + L.q_last_w, H, H, p.W(G_DH2N), H, p.W(G_H2N), H));
-    add(gb, t_dx(p.W(G_GQ3), 2, B, 2, q + L.q_last_w, H, H, p.W(G_DH2N3), H, p.W(G_H2N3), H));
+    add(gb, t_dx(p.W(G_GQ), K, B, K, q + L.q_last_w, H, H, p.W(G_DH2N), H, p.W(G_H2N), H));
+    add(gb, t_dx(p.W(G_GQ3), K, B, K, q + L.q_last_w, H, H, p.W(G_DH2N3), H, p.W(G_H2N3), H));
     if (run_gemm(p, gb, s)) return 1;
   }
   {
@@ -296,16 +334,16 @@ static int gphase2(SacPlan& p, hipStream_t s) {
   return 0;
 }
 
-int gauss_run_step(SacPlan& p, int flags, hipStream_t s) {
+int det_run_step(SacPlan& p, int flags, hipStream_t s) {
   p.launches = 0;
-  if (gphase0(p, flags, s)) return 1;
-  if (gphase1(p, flags, s)) return 1;
+  if (dphase0(p, flags, s)) return 1;
+  if (dphase1(p, flags, s)) return 1;
   {
     AdamArgs a = critic_adam(p, 0, nullptr);
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
   }
-  if (gphase2(p, s)) return 1;
+  if (dphase2(p, s)) return 1;
   {
     AdamArgs a = policy_adam(p, 0, nullptr);
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
@@ -316,11 +354,11 @@ int gauss_run_step(SacPlan& p, int flags, hipStream_t s) {
 
 // data-parallel split (no whole-batch quantity besides the gradients: the
 // phase-0 exchange is empty)
-int gauss_step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
+int det_step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
   switch (phase) {
-    case 0: return gphase0(p, flags, s);
+    case 0: return dphase0(p, flags, s);
     case 1:
-      if (gphase1(p, flags, s)) return 1;
+      if (dphase1(p, flags, s)) return 1;
       if (p.S_q > 1) {
         AdamArgs a = critic_adam(p, 1, nullptr);
         OAC_HIP_CHECK(launch_adam(a, s));
@@ -329,7 +367,7 @@ int gauss_step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
     case 2: {
       AdamArgs a = critic_adam(p, -1, nullptr);
       OAC_HIP_CHECK(launch_adam(a, s));
-      if (gphase2(p, s)) return 1;
+      if (dphase2(p, s)) return 1;
       if (p.S_p > 1) {
         AdamArgs b = policy_adam(p, 1, nullptr);
         OAC_HIP_CHECK(launch_adam(b, s));

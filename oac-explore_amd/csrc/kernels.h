@@ -156,6 +156,11 @@ struct ParticleTargetArgs {
   float* sqe;                           // [B, K] (sorted_q - y)^2 per sorted slot
   float* y;                             // [B, K] quantile targets (sorted slots)
   const float* counts;                  // [B] batch counts (counts=True) or null
+  // particle_trainer.py (OAC_KIND_PARTICLE_UB) only; 1 / -1 / 0 keep the
+  // particle_trainer_oac.py behaviour
+  float loss_scale;                     // 1/K: qf_loss /= num_particles (:269)
+  float soft_prob;                      // std_soft_update_prob (:222-231), < 0: off
+  float rescale_spread;                 // rescale_targets_around_mean (:254-262), <= 0: off
 };
 struct ParticleMinArgs {
   const float* qn; int B, K;            // [B, K] Q(obs, a~) with the post-step critic
@@ -199,6 +204,16 @@ struct GaussSeedArgs {
   float* ub;                            // [B] upper bound q + std_bound * std
 };
 hipError_t launch_gauss_seed(const GaussSeedArgs& a, hipStream_t s);
+
+struct ParticleUbSeedArgs {            // particle_trainer.py:317-330, :339-348
+  const float* qn;                      // [B, K] post-step Q(obs, tanh(mean_pi(obs)))
+  const float* qt;                      // [B, K] post-step Q(obs, tanh(mean_target_pi(obs)))
+  int B, K, delta_index;
+  float* g;                             // [B, K] -1/B at the delta_index-th sorted head
+  float* gt;                            // [B, K] -1/(B K) on every head (mean over particles)
+  float* ub;                            // [B] upper bound sorted_k[delta_index]
+};
+hipError_t launch_particle_ub_seed(const ParticleUbSeedArgs& a, hipStream_t s);
 
 struct DetHeadBwdArgs {                 // d tanh(mean): dmean = da (1 - a^2), d log std = 0
   const float* da[2]; const float* act[2]; float* dhead[2];

@@ -166,6 +166,7 @@ static int pphase1(SacPlan& p, int flags, hipStream_t s) {
     a.discount = c.discount; a.B = B; a.K = K;
     a.dq = p.W(X_DQ); a.sqe = p.W(OAC_WS_SQE1); a.y = p.W(OAC_WS_Y);
     a.counts = (flags & OAC_STEP_COUNTS) ? p.W(OAC_WS_COUNTS) : nullptr;
+    a.loss_scale = 1.f; a.soft_prob = -1.f; a.rescale_spread = 0.f;   // particle_trainer_oac.py
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_particle_targets(a, s)));
     p.launches++;
   }

@@ -266,17 +266,40 @@ __global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArg
   // counts=True (particle_trainer_oac.py:220-224): a row drawn before (count
   // > 0) gets the sorted predictions re-centred on the target mean,
   //   y_i <- (sorted_q_i - mean_k sorted_q) + mean_k y
+  // std_soft_update (particle_trainer.py:222-231): current sorted predictions
+  // re-centred on the next-value mean, mixed with the next values
+  if (p.soft_prob >= 0.f) {
+    float sq = 0.f, sy = 0.f;
+    for (int i = 0; i < K; ++i) { sq += q[i]; sy += y[i]; }
+    const float mq = sq / (float)K, my = sy / (float)K;
+    const float w = 1.f - p.soft_prob;
+    for (int i = 0; i < K; ++i)
+      y[i] = __fadd_rn(__fmul_rn(p.soft_prob, y[i]), __fmul_rn(w, (q[i] - mq) + my));
+  }
   if (p.counts && p.counts[r] != 0.f) {
     float sq = 0.f, sy = 0.f;
     for (int i = 0; i < K; ++i) { sq += q[i]; sy += y[i]; }
     const float mq = sq / (float)K, my = sy / (float)K;
     for (int i = 0; i < K; ++i) y[i] = (q[i] - mq) + my;
   }
+  // rescale_targets_around_mean (particle_trainer.py:254-262): a target spread
+  // wider than q_max - q_min is shrunk around its mean to that width
+  if (p.rescale_spread > 0.f) {
+    const float range = y[K - 1] - y[0];
+    if (range > p.rescale_spread) {
+      float sy = 0.f;
+      for (int i = 0; i < K; ++i) sy += y[i];
+      const float my = sy / (float)K;
+      const float f = p.rescale_spread / (range + 1e-6f);
+      for (int i = 0; i < K; ++i) y[i] = __fadd_rn(__fmul_rn(y[i] - my, f), my);
+    }
+  }
+  const float g2 = p.loss_scale > 0.f ? __fmul_rn(2.f, p.loss_scale) : 2.f;
   for (int i = 0; i < K; ++i) {
     const float d = q[i] - y[i];
     p.y[(long)r * K + i] = y[i];
     p.sqe[(long)r * K + i] = d * d;
-    p.dq[(long)r * K + qi[i]] = __fmul_rn(2.f * d, invB);
+    p.dq[(long)r * K + qi[i]] = __fmul_rn(g2 * d, invB);
   }
 }
 
@@ -391,6 +414,26 @@ __global__ void __launch_bounds__(256) gauss_seed_kernel(GaussSeedArgs p) {
   p.gt[2L * r + 1] = 0.f;
 }
 
+// particle_trainer.py policy losses through the post-step critic: the
+// policy maximises the delta_index-th sorted particle (:317-330; gradient to
+// the head sort placed there), the target policy the particle mean (:339-348)
+__global__ void __launch_bounds__(256) particle_ub_seed_kernel(ParticleUbSeedArgs p) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= p.B) return;
+  const int K = p.K;
+  float v[kMaxHeads];
+  int ix[kMaxHeads];
+  for (int i = 0; i < K; ++i) { v[i] = p.qn[(long)r * K + i]; ix[i] = i; }
+  sort_k(v, ix, K);
+  const float g0 = -(1.f / (float)p.B);
+  const int sel = ix[p.delta_index];
+  for (int i = 0; i < K; ++i) {
+    p.g[(long)r * K + i] = (i == sel) ? g0 : 0.f;
+    p.gt[(long)r * K + i] = g0 / (float)K;
+  }
+  p.ub[r] = v[p.delta_index];
+}
+
 __global__ void __launch_bounds__(256) det_head_backward_kernel(DetHeadBwdArgs p) {
   const int Da = p.act_dim;
   const int idx = blockIdx.x * 256 + threadIdx.x;
@@ -413,6 +456,10 @@ hipError_t launch_gauss_targets(const GaussTargetArgs& a, hipStream_t s) {
 }
 hipError_t launch_gauss_seed(const GaussSeedArgs& a, hipStream_t s) {
   OAC_LAUNCH(gauss_seed_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+hipError_t launch_particle_ub_seed(const ParticleUbSeedArgs& a, hipStream_t s) {
+  OAC_LAUNCH(particle_ub_seed_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_det_head_backward(const DetHeadBwdArgs& a, hipStream_t s) {

@@ -104,9 +104,13 @@ int particle_run_step(SacPlan& p, int flags, hipStream_t s);
 int particle_step_phase(SacPlan& p, int phase, int flags, hipStream_t s);
 void particle_plan_splits(SacPlan& p);
 
-// g-oac gaussian trainer (gauss_plan.hip)
-void gauss_layout_workspace(SacPlan& p);
-int gauss_run_step(SacPlan& p, int flags, hipStream_t s);
-int gauss_step_phase(SacPlan& p, int phase, int flags, hipStream_t s);
+// deterministic-policy trainers with a target_policy: g-oac GaussianTrainer and
+// the p-oac ParticleTrainer of particle_trainer.py (det_plan.hip)
+inline bool has_target_policy(int kind) {
+  return kind == OAC_KIND_GAUSS || kind == OAC_KIND_PARTICLE_UB;
+}
+void det_layout_workspace(SacPlan& p);
+int det_run_step(SacPlan& p, int flags, hipStream_t s);
+int det_step_phase(SacPlan& p, int phase, int flags, hipStream_t s);
 
 }  // namespace oac

@@ -55,8 +55,8 @@ static void compute_layout(const oac_sac_config& c, oac_sac_layout& L) {
   L.n_critics = (c.kind == OAC_KIND_SAC) ? 2 : 1;
   // GAUSS: the target_policy block follows the policy, so both policies form
   // one Adam group (same lr, same step) in front of the critic
-  L.tpol_base = (c.kind == OAC_KIND_GAUSS) ? L.pol_size : -1;
-  L.q1_base = (c.kind == OAC_KIND_GAUSS) ? 2 * L.pol_size : L.pol_size;
+  L.tpol_base = has_target_policy(c.kind) ? L.pol_size : -1;
+  L.q1_base = has_target_policy(c.kind) ? 2 * L.pol_size : L.pol_size;
   L.q2_base = (L.n_critics == 2) ? L.q1_base + L.q_size : -1;
   L.params_total = L.q1_base + L.n_critics * L.q_size;
   L.targets_total = L.n_critics * L.q_size;
@@ -473,8 +473,14 @@ int oac_abi_version(void) { return OAC_ABI_VERSION; }
 
 static int validate(const oac_sac_config* c) {
   if (!c) { set_error("null config"); return 1; }
-  if (c->kind != OAC_KIND_SAC && c->kind != OAC_KIND_PARTICLE && c->kind != OAC_KIND_GAUSS) {
+  if (c->kind != OAC_KIND_SAC && c->kind != OAC_KIND_PARTICLE && c->kind != OAC_KIND_GAUSS &&
+      c->kind != OAC_KIND_PARTICLE_UB) {
     set_error("bad kind %d", c->kind);
+    return 1;
+  }
+  if (c->kind == OAC_KIND_PARTICLE_UB &&
+      (c->q_out < 2 || c->q_out > 16 || c->delta_index < 0 || c->delta_index >= c->q_out)) {
+    set_error("particle critic: 2 <= q_out <= 16 particles, 0 <= delta_index < q_out");
     return 1;
   }
   if (c->kind == OAC_KIND_GAUSS && c->q_out != 2) {
@@ -526,7 +532,7 @@ int oac_sac_query_layout(const oac_sac_config* cfg, oac_sac_layout* out) {
   compute_layout(p.c, p.L);
   plan_splits(p);
   if (p.c.kind == OAC_KIND_PARTICLE) particle_layout_workspace(p);
-  else if (p.c.kind == OAC_KIND_GAUSS) gauss_layout_workspace(p);
+  else if (has_target_policy(p.c.kind)) det_layout_workspace(p);
   else layout_workspace(p);
   *out = p.L;
   return 0;
@@ -541,7 +547,7 @@ int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_s
   compute_layout(p.c, p.L);
   plan_splits(p);
   if (p.c.kind == OAC_KIND_PARTICLE) particle_layout_workspace(p);
-  else if (p.c.kind == OAC_KIND_GAUSS) gauss_layout_workspace(p);
+  else if (has_target_policy(p.c.kind)) det_layout_workspace(p);
   else layout_workspace(p);
   p.b = *bufs;
   read_tuning(p);
@@ -567,7 +573,7 @@ int oac_sac_step_n(oac_sac* h, int flags, int n_steps, void* stream) {
   auto steps = [&](int f) {
     for (int i = 0; i < n_steps; ++i) {
       const int rc = p.c.kind == OAC_KIND_PARTICLE ? particle_run_step(p, f, s)
-                     : p.c.kind == OAC_KIND_GAUSS  ? gauss_run_step(p, f, s)
+                     : has_target_policy(p.c.kind) ? det_run_step(p, f, s)
                                                    : run_step(p, f, s, i, n_steps);
       if (rc) return rc;
     }
@@ -603,7 +609,7 @@ int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
   SacPlan& p = h->plan;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (p.c.kind == OAC_KIND_PARTICLE) return particle_step_phase(p, phase, flags, s);
-  if (p.c.kind == OAC_KIND_GAUSS) return gauss_step_phase(p, phase, flags, s);
+  if (has_target_policy(p.c.kind)) return det_step_phase(p, phase, flags, s);
   switch (phase) {
     case 0: return phase0(p, flags, s);
     case 1:

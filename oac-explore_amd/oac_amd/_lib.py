@@ -13,6 +13,7 @@ LIB_PATH = os.path.join(HERE, "liboac_amd.so")
 OAC_KIND_SAC = 0
 OAC_KIND_PARTICLE = 1
 OAC_KIND_GAUSS = 2
+OAC_KIND_PARTICLE_UB = 3
 
 OAC_STEP_GATHER = 1
 OAC_STEP_DEVICE_EPS = 2
@@ -39,7 +40,9 @@ class SacConfig(ctypes.Structure):
         ("off_term", ctypes.c_int), ("off_next_obs", ctypes.c_int),
         ("seed", ctypes.c_uint64), ("gemm_cfg", ctypes.c_int), ("world_size", ctypes.c_int),
         ("std_bound", ctypes.c_float), ("std_init", ctypes.c_float),
-        ("std_soft_prob", ctypes.c_float),
+        ("std_soft_update", ctypes.c_int), ("std_soft_prob", ctypes.c_float),
+        ("mean_update", ctypes.c_int), ("delta_index", ctypes.c_int),
+        ("rescale_spread", ctypes.c_float),
     ]
 
 

@@ -29,6 +29,7 @@ from . import _lib
 from ._lib import check
 from .gaussian_trainer import GaussianTrainer
 from .particle_trainer import ParticleTrainer
+from .particle_trainer_oac import ParticleTrainer as ParticleTrainerOAC
 from .trainer import SACTrainer
 
 
@@ -151,8 +152,13 @@ class DataParallelSACTrainer(_DataParallel, SACTrainer):
     """SACTrainer (trainer/trainer.py) with the data-parallel step."""
 
 
-class DataParallelParticleTrainer(_DataParallel, ParticleTrainer):
+class DataParallelParticleTrainerOAC(_DataParallel, ParticleTrainerOAC):
     """ParticleTrainer (trainer/particle_trainer_oac.py) with the data-parallel step."""
+
+
+class DataParallelParticleTrainer(_DataParallel, ParticleTrainer):
+    """ParticleTrainer (trainer/particle_trainer.py, the p-oac recipes) with the
+    data-parallel step (no alpha: the phase-0 exchange is skipped)."""
 
 
 class DataParallelGaussianTrainer(_DataParallel, GaussianTrainer):

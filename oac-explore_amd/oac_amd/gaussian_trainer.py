@@ -4,12 +4,12 @@ builds for ``--alg g-oac``, main.py:219-233), in the configuration every
 reproduce_g-oac*.sh recipe runs: ``--share_layers`` (one critic with two
 outputs, Q mean | log std, exp'd by ``positive=[False, True]``), the
 deterministic policy (GaussianTrainer's default, not overridden for g-oac),
-optionally ``--counts`` / ``std_soft_update``.  The step runs in liboac_amd
-(csrc/gauss_plan.hip); the interface is the reference's: constructor kwargs,
-``train`` / ``train_from_torch``, ``predict``, ``obj_func``,
-``get_diagnostics``, ``end_epoch``, ``networks``, ``get_snapshot`` /
-``restore_from_snapshot``, ``q`` / ``q_target`` / ``target_policy`` /
-``qfs`` / ``tfs``.
+optionally ``--counts`` / ``std_soft_update`` / ``--mean_update``.  The step
+runs in liboac_amd (csrc/det_plan.hip); the interface is the reference's:
+constructor kwargs, ``train`` / ``train_from_torch``, ``predict``,
+``obj_func``, ``get_diagnostics``, ``end_epoch``, ``networks``,
+``get_snapshot`` / ``restore_from_snapshot``, ``q`` / ``q_target`` /
+``target_policy`` / ``qfs`` / ``tfs``.
 """
 from collections import OrderedDict
 
@@ -18,15 +18,13 @@ import torch
 from scipy.stats import norm
 
 from . import _lib
-from .networks import ArenaFlattenMlp, ArenaTanhGaussianPolicy
-from .trainer import AdamStateView, _ArenaTrainer, _dims_from_state, _twin_views, _plain_stats
-
-_LOG_STD_HEAD = ("last_fc_log_std.weight", "last_fc_log_std.bias")
+from .tp_trainer import _TargetPolicyTrainer
 
 
-class GaussianTrainer(_ArenaTrainer):
+class GaussianTrainer(_TargetPolicyTrainer):
     _kind = _lib.OAC_KIND_GAUSS
     _q_out = 2
+    _positive = [False, True]
 
     def __init__(self, policy_producer, q_producer, n_estimators=2, action_space=None,
                  discount=0.99, reward_scale=1.0, delta=0.95, policy_lr=1e-3, qf_lr=3e-4,
@@ -39,24 +37,19 @@ class GaussianTrainer(_ArenaTrainer):
                  rescale_targets_around_mean=False,
                  device=None, seed=0, use_graph=True, gemm_cfg=-1):
         unsupported = dict(share_layers=not share_layers, deterministic=not deterministic,
-                           ensemble=ensemble, global_opt=global_opt, mean_update=mean_update,
-                           use_target_policy=use_target_policy, train_bias=not train_bias)
+                           ensemble=ensemble, global_opt=global_opt,
+                           use_target_policy=use_target_policy,
+                           train_bias=not train_bias)
         bad = [k for k, v in unsupported.items() if v]
         if bad:
             raise NotImplementedError(
                 "oac_amd.GaussianTrainer implements the g-oac recipe configuration "
-                "(share_layers=True, deterministic policy, counts / std_soft_update, "
-                f"trainable bias, no ensemble / global-opt / mean-update); unsupported: {bad}")
+                "(share_layers=True, deterministic policy, counts / std_soft_update / "
+                f"mean_update, trainable bias, no ensemble / global-opt); unsupported: {bad}")
         assert not counts or not std_soft_update   # gaussian_trainer.py:88
-        self.device = torch.device(device) if device is not None else torch.device(
-            "cuda", torch.cuda.current_device())
-        # SACTrainer.__init__ bookkeeping (the entropy term is unused by this step)
-        self.use_automatic_entropy_tuning = False
-        self.target_entropy = 0.0
-        self.soft_target_tau, self.target_update_period = soft_target_tau, target_update_period
-        self.deterministic, self.discount, self.reward_scale = deterministic, discount, reward_scale
-        self.policy_lr, self.qf_lr, self.std_lr = policy_lr, qf_lr, std_lr
-        self.use_graph, self.seed, self._gemm_cfg = use_graph, int(seed), gemm_cfg
+        self._common_init(device, soft_target_tau, target_update_period, deterministic,
+                          discount, reward_scale, policy_lr, qf_lr, use_graph, seed, gemm_cfg)
+        self.std_lr = std_lr
         # gaussian_trainer.py:65-86
         self.action_space = action_space
         self.q_min, self.q_max, self.delta = q_min, q_max, delta
@@ -83,48 +76,14 @@ class GaussianTrainer(_ArenaTrainer):
         ref_q = q_producer(bias=qb, positive=[False, True], train_bias=train_bias)
         ref_qt = q_producer(bias=qb, positive=[False, True], train_bias=train_bias)
         ref_tp = policy_producer()
-        pol_sd = {k: v.detach() for k, v in ref_pol.state_dict().items()}
-        Do, Da, H, K = _dims_from_state(pol_sd, ref_q.state_dict())
-        if K != 2:
-            raise ValueError("share_layers: q_producer must build a critic with 2 outputs")
-        lay = self._alloc(Do, Da, H, self.device)
-        self.policy = ArenaTanhGaussianPolicy(self.params, 0, lay, Do, Da, H)
-        self.target_policy = ArenaTanhGaussianPolicy(self.params, lay.tpol_base, lay, Do, Da, H)
-        self.q = ArenaFlattenMlp(self.params, lay.q1_base, lay, Do, Da, H, 2,
-                                 positive=[False, True])
-        self.q_target = ArenaFlattenMlp(self.targets, 0, lay, Do, Da, H, 2, positive=[False, True])
-        self.policy.load_state_dict(pol_sd)
-        self.target_policy.load_state_dict({k: v.detach() for k, v in ref_tp.state_dict().items()})
-        self.q.load_state_dict({k: v.detach() for k, v in ref_q.state_dict().items()})
-        self.q_target.load_state_dict({k: v.detach() for k, v in ref_qt.state_dict().items()})
-        self.policy.oac_trainer = self
-        self.qfs, self.tfs = [self.q], [self.q_target]
-        tw = lambda other, mod: _twin_views(self.params, other, list(mod.parameters()))
-        names = [n for n, _ in self.policy.named_parameters()]
-        no_grad = [i for i, n in enumerate(names) if n in _LOG_STD_HEAD]   # deterministic policy
-
-        def popt(mod):
-            return AdamStateView(self, list(mod.parameters()), tw(self.adam_m, mod),
-                                 tw(self.adam_v, mod), policy_lr, (0.9, 0.999), 1e-8,
-                                 no_grad=no_grad)
-        self.policy_optimizer = popt(self.policy)
-        self.target_policy_optimizer = popt(self.target_policy)
-        self.q_optimizer = AdamStateView(self, list(self.q.parameters()), tw(self.adam_m, self.q),
-                                         tw(self.adam_v, self.q), qf_lr, (0.9, 0.999), 1e-8)
-        self.qf_optimizers = [self.q_optimizer]
-        # SACTrainer's alpha (snapshot keys only; g-oac does not tune it)
-        self.alpha_optimizer = AdamStateView(self, [self.log_alpha], [self.alpha_state[1:2]],
-                                             [self.alpha_state[2:3]], policy_lr, (0.9, 0.999),
-                                             1e-8)
-        self.eval_statistics = OrderedDict()
-        self._n_train_steps_total = 0
-        self._need_to_update_eval_statistics = True
+        self._build(ref_pol, ref_q, ref_qt, ref_tp, policy_lr, qf_lr)
+        self.q, self.q_target = self.qfs[0], self.tfs[0]
+        self.q_optimizer = self.qf_optimizers[0]
 
     def _make_cfg(self, batch):
         c = super()._make_cfg(batch)
         c.std_bound = self.standard_bound
         c.std_init = float(self.std_init)
-        c.std_soft_prob = float(self.std_soft_update_prob) if self.std_soft_update else -1.0
         return c
 
     # ------------------------------------------------------------ diagnostics
@@ -138,39 +97,23 @@ class GaussianTrainer(_ArenaTrainer):
         q_preds = v["q1"][:, :1]
         std_preds = np.exp(v["q1"][:, 1:2])
         st = OrderedDict()
-
-        def stats(name, arr):
-            st[name + " Mean"] = np.mean(arr)
-            st[name + " Std"] = np.std(arr)
-            st[name + " Max"] = np.max(arr)
-            st[name + " Min"] = np.min(arr)
         st["QF mean"] = np.mean(q_preds)
         st["QF std"] = np.mean(std_preds)
         st["QF Loss"] = np.float32(np.mean(v["sqe1"][:, 0]))
-        stats("Q Predictions", q_preds)
-        stats("Q Target", v["y"][:, :1])
+        self._stats(st, "Q Predictions", q_preds)
+        self._stats(st, "Q Target", v["y"][:, :1])
         st["STD Loss"] = np.float32(np.mean(v["sqe1"][:, 1]))
-        stats("Q STD Predictions", std_preds)
-        stats("Q STD Target", v["y"][:, 1:2])
+        self._stats(st, "Q STD Predictions", std_preds)
+        self._stats(st, "Q STD Target", v["y"][:, 1:2])
         st["Policy Loss"] = np.mean(v["qnew"])
-        stats("Policy mu", v["head3"][:, :Da])
-        stats("Policy log std", np.clip(v["head3"][:, Da:], -20, 2))
+        self._stats(st, "Policy mu", v["head3"][:, :Da])
+        self._stats(st, "Policy log std", np.clip(v["head3"][:, Da:], -20, 2))
         self.eval_statistics = st
-
-    def get_diagnostics(self):
-        return self.eval_statistics
-
-    def end_epoch(self, epoch):
-        self._need_to_update_eval_statistics = True
 
     # ------------------------------------------------------------ misc API
     def _qs(self, obs, action):
-        obs = torch.as_tensor(np.asarray(obs) if not torch.is_tensor(obs) else obs,
-                              dtype=torch.float32, device=self.device)
-        action = torch.as_tensor(np.asarray(action) if not torch.is_tensor(action) else action,
-                                 dtype=torch.float32, device=self.device)
         with torch.no_grad():
-            out = self.q(obs, action)
+            out = self.q(self._tensor(obs), self._tensor(action))
         return out[:, 0].unsqueeze(-1), out[:, 1].unsqueeze(-1)
 
     def predict(self, obs, action, std=True):
@@ -185,38 +128,3 @@ class GaussianTrainer(_ArenaTrainer):
         """gaussian_trainer.py:519-529."""
         qs, stds = self._qs(states, actions)
         return qs + self.standard_bound * stds if upper_bound else qs
-
-    @property
-    def networks(self):
-        return [self.policy] + self.qfs + self.tfs + [self.target_policy]
-
-    def get_snapshot(self):
-        """gaussian_trainer.py:452-482 (keys)."""
-        return dict(policy_state_dict=self.policy.state_dict(),
-                    policy_optim_state_dict=self.policy_optimizer.state_dict(),
-                    log_alpha=self.log_alpha,
-                    alpha_optim_state_dict=self.alpha_optimizer.state_dict(),
-                    eval_statistics=_plain_stats(self.eval_statistics),
-                    _n_train_steps_total=self._n_train_steps_total,
-                    _need_to_update_eval_statistics=self._need_to_update_eval_statistics,
-                    qfs_state_dicts=[self.q.state_dict()],
-                    qfs_optims_state_dicts=[self.q_optimizer.state_dict()],
-                    target_qfs_state_dicts=[self.q_target.state_dict()],
-                    target_policy_state_dict=self.target_policy.state_dict(),
-                    target_policy_opt_state_dict=self.target_policy_optimizer.state_dict())
-
-    def restore_from_snapshot(self, ss):
-        """gaussian_trainer.py:484-517."""
-        self.policy.load_state_dict(ss["policy_state_dict"])
-        self.policy_optimizer.load_state_dict(ss["policy_optim_state_dict"])
-        self.q.load_state_dict(ss["qfs_state_dicts"][0])
-        self.q_optimizer.load_state_dict(ss["qfs_optims_state_dicts"][0])
-        self.q_target.load_state_dict(ss["target_qfs_state_dicts"][0])
-        self.log_alpha.copy_(torch.as_tensor(ss["log_alpha"]).reshape(1))
-        self.alpha_optimizer.load_state_dict(ss["alpha_optim_state_dict"])
-        self.eval_statistics = ss["eval_statistics"]
-        self._n_train_steps_total = int(ss["_n_train_steps_total"])
-        self._need_to_update_eval_statistics = ss["_need_to_update_eval_statistics"]
-        self.target_policy.load_state_dict(ss["target_policy_state_dict"])
-        self.target_policy_optimizer.load_state_dict(ss["target_policy_opt_state_dict"])
-        self.step_state[0] = self._n_train_steps_total

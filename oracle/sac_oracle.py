@@ -21,6 +21,9 @@ It restates, with explicit forward and backward passes written out by hand
 * ``GaussianTrainer.train_from_torch`` /root/reference/trainer/gaussian_trainer.py:177-437
   (g-oac: shared-layer critic with outputs [Q | log std], deterministic
   policy, separately trained target_policy);
+* ``ParticleTrainer.train_from_torch`` /root/reference/trainer/particle_trainer.py:175-432
+  (the p-oac recipes: K-particle critic, deterministic policy, upper-bound
+  quantile policy loss, target_policy);
 * ``get_optimistic_exploration_action_stochastic``
                                        /root/reference/optimistic_exploration.py:14-109
 * torch 1.4 ``optim.Adam.step`` (constructed at trainer/trainer.py:75-91) and
@@ -452,6 +455,25 @@ class ParticleOACOracle:
         return self.last
 
 
+def det_policy_backward(c, p, ga):
+    """Gradient of sum(ga * tanh(mean)) w.r.t. the params of a deterministic
+    TanhGaussianPolicy (policies.py:286-288); the log-std head is not in the
+    graph (zeros here; torch Adam skips it, which leaves it unchanged too)."""
+    a, hs = c["a"], c["hs"]
+    dmean = ga * (1 - a * a)
+    L = len(hs) - 1
+    g = {"last_fc.weight": dmean.t() @ hs[L], "last_fc.bias": dmean.sum(0),
+         "last_fc_log_std.weight": torch.zeros_like(p["last_fc_log_std.weight"]),
+         "last_fc_log_std.bias": torch.zeros_like(p["last_fc_log_std.bias"])}
+    dh = (dmean @ p["last_fc.weight"]) * (hs[L] > 0)
+    for i in range(L - 1, -1, -1):
+        g[f"fc{i}.weight"] = dh.t() @ hs[i]
+        g[f"fc{i}.bias"] = dh.sum(0)
+        if i > 0:
+            dh = (dh @ p[f"fc{i}.weight"]) * (hs[i] > 0)
+    return g
+
+
 class GaussianOACOracle:
     """GaussianTrainer (gaussian_trainer.py) with share_layers=True and the
     deterministic policy (the reproduce_g-oac*.sh configuration): critic Q
@@ -460,8 +482,10 @@ class GaussianOACOracle:
 
     def __init__(self, params, obs_dim, act_dim, delta=0.95, q_min=0.0, q_max=100.0,
                  discount=0.99, reward_scale=1.0, policy_lr=3e-4, qf_lr=3e-4, tau=5e-3,
-                 target_update_period=1, std_soft_update_prob=None, dtype=torch.float32):
+                 target_update_period=1, std_soft_update_prob=None, mean_update=False,
+                 dtype=torch.float32):
         from scipy.stats import norm
+        self.mean_update = mean_update
         self.dtype = dtype
         self.Do, self.Da = obs_dim, act_dim
         self.P = to_torch_params(params["policy"], dtype)
@@ -477,24 +501,6 @@ class GaussianOACOracle:
         self.opt_tp = Adam14(self.TP, policy_lr)
         self.opt_q = Adam14(self.Q, qf_lr)
         self.n_steps = 0
-
-    @staticmethod
-    def det_policy_backward(c, p, ga):
-        """Gradient of sum(ga * tanh(mean)) w.r.t. the policy params; the
-        log-std head gets none (it is not in the graph: zeros here)."""
-        a, hs = c["a"], c["hs"]
-        dmean = ga * (1 - a * a)
-        L = len(hs) - 1
-        g = {"last_fc.weight": dmean.t() @ hs[L], "last_fc.bias": dmean.sum(0),
-             "last_fc_log_std.weight": torch.zeros_like(p["last_fc_log_std.weight"]),
-             "last_fc_log_std.bias": torch.zeros_like(p["last_fc_log_std.bias"])}
-        dh = (dmean @ p["last_fc.weight"]) * (hs[L] > 0)
-        for i in range(L - 1, -1, -1):
-            g[f"fc{i}.weight"] = dh.t() @ hs[i]
-            g[f"fc{i}.bias"] = dh.sum(0)
-            if i > 0:
-                dh = (dh @ p[f"fc{i}.weight"]) * (hs[i] > 0)
-        return g
 
     def step(self, batch):
         self.phase0(batch)
@@ -529,7 +535,8 @@ class GaussianOACOracle:
         B = S["B"] = obs.shape[0]
         c = S["c"] = q_forward(obs, act, self.Q)                     # :187
         q_preds, std_preds = c["q"][:, :1], torch.exp(c["q"][:, 1:2])
-        pf2 = policy_forward(nobs, self.P, None, deterministic=True)  # :199-202
+        pf2 = policy_forward(nobs, self.TP if self.mean_update else self.P, None,
+                             deterministic=True)                      # :192-202
         tq = q_forward(nobs, pf2["a"], self.T)["q"]                  # :204
         tq0, tstd = tq[:, :1], torch.exp(tq[:, 1:2])
         std_target = (1. - term) * self.discount * tstd              # :213
@@ -567,10 +574,10 @@ class GaussianOACOracle:
         S["ub"] = qs + self.z * stds                                 # :331
         g0 = -torch.ones_like(qs) / B
         da = q_input_grad(cn, torch.cat([g0, g0 * self.z * stds], dim=1), self.Q)[:, self.Do:]
-        S["gp"] = self.det_policy_backward(pf, self.P, da)
+        S["gp"] = det_policy_backward(pf, self.P, da)
         ct = q_forward(obs, tpf["a"], self.Q)                        # :346
         dat = q_input_grad(ct, torch.cat([g0, torch.zeros_like(g0)], dim=1), self.Q)[:, self.Do:]
-        S["gtp"] = self.det_policy_backward(tpf, self.TP, dat)
+        S["gtp"] = det_policy_backward(tpf, self.TP, dat)
         self.pol_flat = torch.cat([self._flat(S["gp"], list(self.P)),
                                    self._flat(S["gtp"], list(self.TP))])
 
@@ -588,6 +595,110 @@ class GaussianOACOracle:
                          q_loss=S["q_loss"], std_loss=S["std_loss"], q_preds=S["q_preds"],
                          std_preds=S["std_preds"], q_target=S["q_target"],
                          std_target=S["std_target"], upper_bound=S["ub"], target_head=S["tpf"])
+        return self.last
+
+
+class ParticleUBOracle(GaussianOACOracle):
+    """ParticleTrainer (trainer/particle_trainer.py, the p-oac recipes) with
+    share_layers=True and the deterministic policy: critic Q with K particle
+    outputs, sorted-particle TD targets (counts, std_soft_update,
+    rescale_targets_around_mean) with the loss averaged over particles, the
+    policy maximising sorted particle ``delta_index``, the target policy the
+    particle mean.  Same phase split as GaussianOACOracle."""
+
+    def __init__(self, params, obs_dim, act_dim, K, delta_index, q_min=0.0, q_max=100.0,
+                 discount=0.99, reward_scale=1.0, policy_lr=1e-3, qf_lr=1e-3, tau=5e-3,
+                 target_update_period=1, std_soft_update_prob=None, mean_update=False,
+                 rescale=False, dtype=torch.float32):
+        super().__init__(params, obs_dim, act_dim, q_min=q_min, q_max=q_max, discount=discount,
+                         reward_scale=reward_scale, policy_lr=policy_lr, qf_lr=qf_lr, tau=tau,
+                         target_update_period=target_update_period,
+                         std_soft_update_prob=std_soft_update_prob, mean_update=mean_update,
+                         dtype=dtype)
+        self.K, self.delta_index = K, delta_index
+        self.spread = (q_max - q_min) if rescale else None
+
+    def phase0(self, batch):
+        dt = self.dtype
+        S = self.S = {}
+        obs = S["obs"] = _t(batch["observations"], dt)
+        act = _t(batch["actions"], dt)
+        rew = _t(batch["rewards"], dt)
+        term = _t(batch["terminals"], dt)
+        nobs = _t(batch["next_observations"], dt)
+        B = S["B"] = obs.shape[0]
+        c = S["c"] = q_forward(obs, act, self.Q)                     # :190-195
+        qs = c["q"].t()                                              # [K, B]
+        sorted_qs, qs_idx = torch.sort(qs, dim=0)                    # :196
+        pf2 = policy_forward(nobs, self.TP if self.mean_update else self.P, None,
+                             deterministic=True)                      # :197-207
+        tq = q_forward(nobs, pf2["a"], self.T)["q"].t()              # :211-214
+        tq_sorted, _ = torch.sort(tq, dim=0)                         # :215
+        y = self.reward_scale * rew.t() + (1. - term.t()) * self.discount * tq_sorted   # :219-220
+        if self.soft is not None:                                    # :222-231
+            cur_mean = torch.mean(sorted_qs, dim=0)
+            nxt_mean = torch.mean(y, dim=0)
+            y = self.soft * y + (1 - self.soft) * (sorted_qs - cur_mean + nxt_mean)
+        if batch.get("counts") is not None:                          # :233-238
+            cnt = _t(batch["counts"], dt).reshape(1, B)
+            factor = (cnt == 0).to(dt)
+            y = y * factor + (1 - factor) * (sorted_qs - torch.mean(sorted_qs, dim=0)
+                                             + torch.mean(y, dim=0))
+        if self.spread is not None:                                  # :254-262
+            q_range = y[-1] - y[0]
+            factor = torch.ones_like(q_range)
+            factor[q_range > self.spread] = 0
+            q_mean = torch.mean(y, dim=0)
+            y = factor * y + (1 - factor) * ((y - q_mean) * (self.spread / (q_range + 1e-6))
+                                             + q_mean)
+        losses = ((sorted_qs - y) ** 2).mean(dim=1)                  # :264-268
+        d_sorted = 2.0 * (sorted_qs - y) / B / self.K                # qf_loss /= K, :269
+        S["dq"] = torch.zeros_like(qs).scatter_(0, qs_idx, d_sorted).t()
+        S.update(sorted_qs=sorted_qs, y=y, tq=tq, qf_losses=losses, qf_loss=losses.sum() / self.K)
+        S["pf"] = policy_forward(obs, self.P, None, deterministic=True)     # :309-311
+        S["tpf"] = policy_forward(obs, self.TP, None, deterministic=True)   # :335-337
+
+    def phase1(self, world=1):
+        S = self.S
+        S["gq"] = q_param_grads(S["c"], S["dq"], self.Q)
+        self.crit_flat = self._flat(S["gq"], list(self.Q))
+
+    def phase2(self, world=1):
+        S = self.S
+        B, obs = S["B"], S["obs"]
+        gq = self._unflat(self.crit_flat, self.Q, list(self.Q))
+        self.opt_q.step({k: v / world for k, v in gq.items()})     # :270-272
+        pf, tpf = S["pf"], S["tpf"]
+        cn = q_forward(obs, pf["a"], self.Q)                         # :317 (post-step Q)
+        pq = cn["q"].t()
+        sq, sidx = torch.sort(pq, dim=0)                             # :322
+        S["ub"] = sq[self.delta_index]                               # :323
+        g0 = -torch.ones_like(S["ub"]) / B
+        gsel = torch.zeros_like(pq).scatter_(0, sidx[self.delta_index:self.delta_index + 1],
+                                             g0[None]).t()
+        da = q_input_grad(cn, gsel, self.Q)[:, self.Do:]
+        S["gp"] = det_policy_backward(pf, self.P, da)
+        ct = q_forward(obs, tpf["a"], self.Q)                        # :339
+        gt = (g0 / self.K)[:, None].expand(B, self.K)                # mean over particles :343
+        dat = q_input_grad(ct, gt, self.Q)[:, self.Do:]
+        S["gtp"] = det_policy_backward(tpf, self.TP, dat)
+        self.pol_flat = torch.cat([self._flat(S["gp"], list(self.P)),
+                                   self._flat(S["gtp"], list(self.TP))])
+
+    def phase3(self, world=1):
+        S = self.S
+        n = self._flat(S["gp"], list(self.P)).numel()
+        gp = self._unflat(self.pol_flat[:n], self.P, list(self.P))
+        gtp = self._unflat(self.pol_flat[n:], self.TP, list(self.TP))
+        self.opt_p.step({k: v / world for k, v in gp.items()})      # :329-330
+        self.opt_tp.step({k: v / world for k, v in gtp.items()})    # :345-347
+        if self.n_steps % self.period == 0:                          # :352-357
+            polyak(self.T, self.Q, self.tau)
+        self.n_steps += 1
+        self.last = dict(grads=dict(policy=S["gp"], target_policy=S["gtp"], qf=S["gq"]),
+                         qf_losses=S["qf_losses"], qf_loss=S["qf_loss"],
+                         sorted_qs=S["sorted_qs"], y=S["y"], tq=S["tq"], upper_bound=S["ub"],
+                         target_head=S["tpf"])
         return self.last
 
 

@@ -60,6 +60,19 @@ def goac_params(obs_dim, act_dim, hidden, seed, q_min, q_max, pi_init_w=1e-3, q_
     return dict(policy=d["policy"], target_policy=tp, qf1=d["qf1"], target_qf1=d["target_qf1"])
 
 
+def ptrain_params(obs_dim, act_dim, hidden, seed, K, q_min, q_max, pi_init_w=1e-3,
+                  q_init_w=3e-3):
+    """p-oac ParticleTrainer (particle_trainer.py, share_layers): policy,
+    target_policy, qf1 (K particles, last bias linspace(q_min, q_max, K)) and
+    target_qf1 = qf1 (the constructor copies it, soft_update tau=1, :100-102)."""
+    d = sac_params(obs_dim, act_dim, hidden, seed, q_out=K, pi_init_w=pi_init_w,
+                   q_init_w=q_init_w, q_last_bias=np.linspace(q_min, q_max, K))
+    rs = np.random.RandomState(seed + 1)
+    tp = mlp_params(rs, obs_dim, hidden, act_dim, pi_init_w, log_std_head=True)
+    return dict(policy=d["policy"], target_policy=tp, qf1=d["qf1"],
+                target_qf1={k: v.copy() for k, v in d["qf1"].items()})
+
+
 def synthetic_transitions(n, obs_dim, act_dim, seed=0, term_p=0.01):
     """BASELINE.md section 3 synthetic replay content (float64, like the
     reference's numpy store, replay_buffer.py:32-45)."""

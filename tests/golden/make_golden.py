@@ -31,7 +31,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))  # tests/
-from fixtures_lib import (goac_params, sac_params, synthetic_transitions,  # noqa
+from fixtures_lib import (goac_params, ptrain_params, sac_params, synthetic_transitions,  # noqa
                           PARAM_ORDER_POLICY, PARAM_ORDER_Q)
 
 REF = "/root/reference"
@@ -77,6 +77,7 @@ from trainer.policies import TanhGaussianPolicy  # noqa: E402
 from trainer.trainer import SACTrainer  # noqa: E402
 from trainer.particle_trainer_oac import ParticleTrainer as ParticleTrainerOAC  # noqa: E402
 from trainer.gaussian_trainer import GaussianTrainer  # noqa: E402
+from trainer.particle_trainer import ParticleTrainer  # noqa: E402
 from replay_buffer import ReplayBuffer, ReplayBufferCount  # noqa: E402
 import optimistic_exploration as oe  # noqa: E402
 
@@ -370,6 +371,88 @@ def gen_goac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=13, 
     return meta, out
 
 
+# ------------------------------------------------- p-oac (particle_trainer)
+def gen_ptrain(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=17, delta=0.95,
+               r_min=0.0, r_max=5.0, discount=0.99, lr=3e-4, tau=5e-3, idx_seed=1,
+               pi_init_w=1e-3, q_init_w=3e-3, counts=False, soft=None, mean_update=False,
+               rescale=False, q_range=None):
+    """ParticleTrainer (trainer/particle_trainer.py) as main.py builds it for
+    --alg p-oac without --beta_UB (main.py:198-218): share_layers,
+    deterministic policy, q_min/q_max = r_min/r_max / (1 - discount) (or
+    ``q_range``).  Parameters with no gradient (the deterministic policies'
+    log-std heads) are recorded as zero gradients."""
+    pp, qp = _producers(obs_dim, act_dim, hidden, q_out=K)
+    q_min, q_max = q_range if q_range else (r_min / (1 - discount), r_max / (1 - discount))
+    torch.manual_seed(0)
+    tr = ParticleTrainer(pp, qp, n_estimators=K, action_space=Box(-1, 1, (act_dim,)),
+                         discount=discount, reward_scale=1.0, delta=delta, policy_lr=lr,
+                         qf_lr=lr, optimizer_class=Adam14, soft_target_tau=tau,
+                         target_update_period=1, deterministic=True, q_min=q_min, q_max=q_max,
+                         share_layers=True, counts=counts, mean_update=mean_update,
+                         std_soft_update=soft is not None,
+                         std_soft_update_prob=0.0 if soft is None else soft,
+                         rescale_targets_around_mean=rescale)
+    params = ptrain_params(obs_dim, act_dim, hidden, seed, K, q_min, q_max, pi_init_w=pi_init_w,
+                           q_init_w=q_init_w)
+    load_sd(tr.policy, params["policy"])
+    load_sd(tr.target_policy, params["target_policy"])
+    load_sd(tr.qfs[0], params["qf1"])
+    load_sd(tr.tfs[0], params["target_qf1"])
+    rb, _ = _fill_buffer(obs_dim, act_dim, n_replay)
+    crs = np.random.RandomState(77)
+    np.random.seed(idx_seed)
+    out = {}
+    meta = dict(kind="ptrain", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, K=K, B=B,
+                steps=steps, n_replay=n_replay, seed=seed, delta=delta, q_min=q_min,
+                q_max=q_max, discount=discount, lr=lr, tau=tau, idx_seed=idx_seed,
+                pi_init_w=pi_init_w, q_init_w=q_init_w, counts=counts, soft=soft,
+                mean_update=mean_update, rescale=rescale, delta_index=int(tr.delta_index))
+    for s in range(steps):
+        EPS_LOG.clear()
+        batch, idx = _record_batch(rb, B)
+        batch = dict(batch)
+        if counts:
+            c = crs.randint(0, 4, (B, 1)) * (crs.uniform(0, 1, (B, 1)) < 0.5)
+            batch["counts"] = c.astype(np.float64)
+            out[f"s{s}/counts"] = batch["counts"][:, 0]
+        tr.end_epoch(s)
+        tr.train(batch)
+        assert len(EPS_LOG) == 0      # deterministic policies draw nothing
+        out[f"s{s}/idx"] = idx.astype(np.int64)
+        for k, v in tr.get_diagnostics().items():
+            out[f"s{s}/stat/{k}"] = np.array(v, np.float64)
+        for gname, opt, mod, order in (
+                ("policy", tr.policy_optimizer, tr.policy, PARAM_ORDER_POLICY),
+                ("target_policy", tr.target_policy_optimizer, tr.target_policy,
+                 PARAM_ORDER_POLICY),
+                ("qf", tr.qf_optimizers[0], tr.qfs[0], PARAM_ORDER_Q)):
+            for pname, g in zip(order, opt.recorded[-1]):
+                if g is None:
+                    g = torch.zeros_like(mod.state_dict()[pname])
+                pack(out, f"s{s}/grad/{gname}/{pname}", g.numpy(), full)
+        for gname, mod in (("policy", tr.policy), ("target_policy", tr.target_policy),
+                           ("qf", tr.qfs[0]), ("tf", tr.tfs[0])):
+            for pname, t in mod.state_dict().items():
+                pack(out, f"s{s}/post/{gname}/{pname}", t.numpy(), full)
+    return meta, out
+
+
+def gen_ptrain_all():
+    save("ptrain_small", *gen_ptrain("ptrain_small", 111, 8, [32, 32], 10, 32, 3, 500, True,
+                                     pi_init_w=0.3, q_init_w=0.3))
+    save("ptrain_counts", *gen_ptrain("ptrain_counts", 111, 8, [32, 32], 10, 32, 3, 500, True,
+                                      pi_init_w=0.3, q_init_w=0.3, counts=True))
+    save("ptrain_soft_rescale", *gen_ptrain("ptrain_soft_rescale", 11, 3, [16, 16], 5, 16, 3,
+                                            200, True, pi_init_w=0.5, q_init_w=0.5, soft=0.3,
+                                            rescale=True, q_range=(0.0, 1.0), lr=1e-3,
+                                            tau=0.05, delta=0.75))
+    save("ptrain_mean_update", *gen_ptrain("ptrain_mean_update", 11, 3, [16, 16], 10, 16, 3, 200,
+                                           True, pi_init_w=0.5, q_init_w=0.5, mean_update=True,
+                                           lr=1e-3))
+    save("ptrain_humanoid", *gen_ptrain("ptrain_humanoid", 376, 17, [256, 256], 10, 256, 2,
+                                        20000, False, counts=True))
+
+
 # ------------------------------------------------------- OAC exploration
 def gen_oac_expl(name, obs_dim, act_dim, hidden, n_obs, beta_UB, delta, seed=5,
                  pi_init_w=0.1, q_init_w=0.1, eps_seed=3):
@@ -560,6 +643,9 @@ def main():
         save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
                                       pi_init_w=0.3, counts=True))
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "ptrain":
+        gen_ptrain_all()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "goac":
         gen_goac_all()
         return
@@ -590,6 +676,7 @@ def main():
                                   pi_init_w=0.3, counts=True))
     gen_sac_snapshot(os.path.join(HERE, "sac_snapshot.pt"))
     gen_goac_all()
+    gen_ptrain_all()
 
 
 def gen_goac_all():

@@ -44,9 +44,20 @@ def _trainer(dp, kind="sac"):
         cls = DataParallelGaussianTrainer if dp else GaussianTrainer
         return cls(pp, qp, action_space=Space(Da), discount=0.99, policy_lr=1e-3, qf_lr=1e-3,
                    soft_target_tau=5e-3, q_min=0.0, q_max=100.0, share_layers=True, counts=True)
-    if kind == "poac":
+    if kind == "ptrain":
+        from fixtures_lib import ptrain_params
         from oac_amd import ParticleTrainer
         from oac_amd.dp import DataParallelParticleTrainer
+        from test_gpu_ptrain import ptrain_producers
+        pp, qp = ptrain_producers(ptrain_params(Do, Da, [H, H], 3, 5, 0.0, 50.0, pi_init_w=0.2,
+                                                q_init_w=0.1))
+        cls = DataParallelParticleTrainer if dp else ParticleTrainer
+        return cls(pp, qp, n_estimators=5, action_space=Space(Da), discount=0.99,
+                   policy_lr=1e-3, qf_lr=1e-3, soft_target_tau=5e-3, q_min=0.0, q_max=50.0,
+                   share_layers=True, counts=True)
+    if kind == "poac":
+        from oac_amd import ParticleTrainerOAC as ParticleTrainer
+        from oac_amd.dp import DataParallelParticleTrainerOAC as DataParallelParticleTrainer
         K = 5
         pp, qp = producers(sac_params(Do, Da, [H, H], 3, q_out=K, pi_init_w=0.2,
                                       q_last_bias=np.linspace(0.0, 50.0, K)),
@@ -85,7 +96,7 @@ def _worker(rank, world, port, q, kind="sac"):
     tr = _trainer(True, kind)
     for step, (batch, e1, e2) in enumerate(_inputs(world)):
         sl = slice(rank * BL, (rank + 1) * BL)
-        if kind == "goac":
+        if kind in ("goac", "ptrain"):
             tr.train_from_torch({k: v[sl] for k, v in _with_counts(batch, step).items()})
             continue
         if kind == "poac":
@@ -98,7 +109,7 @@ def _worker(rank, world, port, q, kind="sac"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["sac", "goac", "poac"])
+@pytest.mark.parametrize("kind", ["sac", "goac", "poac", "ptrain"])
 def test_dp_trainer_two_ranks_equals_single_gpu_on_global_batch(kind):
     world = 2
     s = socket.socket()
@@ -116,7 +127,7 @@ def test_dp_trainer_two_ranks_equals_single_gpu_on_global_batch(kind):
         assert p.exitcode == 0
     tr = _trainer(False, kind)
     for step, (batch, e1, e2) in enumerate(_inputs(world)):
-        if kind == "goac":
+        if kind in ("goac", "ptrain"):
             tr.train_from_torch(_with_counts(batch, step))
         elif kind == "poac":
             tr.train_from_torch(_with_counts(batch, step), eps1=e1, eps2=e2)

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 
 def particle_trainer_for(meta, **kw):
-    from oac_amd import ParticleTrainer
+    from oac_amd import ParticleTrainerOAC as ParticleTrainer
     K = meta["K"]
     params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"], q_out=K,
                         q_last_bias=np.linspace(meta["q_min"], meta["q_max"], K),

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 import torch
 
-from fixtures_lib import (goac_params, sac_params, synthetic_transitions, PARAM_ORDER_POLICY,
+from fixtures_lib import (goac_params, ptrain_params, sac_params, synthetic_transitions, PARAM_ORDER_POLICY,
                           PARAM_ORDER_Q)
 import parity
 from oracle import sac_oracle as so
@@ -165,6 +165,61 @@ def test_goac_oracle_matches_reference_golden(name):
     meta, g = parity.load(name)
     errs = goac_errors(meta, g, make_goac_oracle(meta))
     noise = goac_errors(meta, g, make_goac_oracle(meta, torch.float64))
+    bad = {k: (v, noise[k]) for k, v in errs.items() if v > parity.gate(k, noise[k])}
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
+
+
+PTRAIN_FIXTURES = ["ptrain_small", "ptrain_counts", "ptrain_soft_rescale", "ptrain_mean_update",
+                   "ptrain_humanoid"]
+
+
+def make_ptrain_oracle(meta, dtype=torch.float32):
+    params = ptrain_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                           meta["K"], meta["q_min"], meta["q_max"], pi_init_w=meta["pi_init_w"],
+                           q_init_w=meta["q_init_w"])
+    return so.ParticleUBOracle(params, meta["obs_dim"], meta["act_dim"], meta["K"],
+                               meta["delta_index"], q_min=meta["q_min"], q_max=meta["q_max"],
+                               discount=meta["discount"], policy_lr=meta["lr"], qf_lr=meta["lr"],
+                               tau=meta["tau"], std_soft_update_prob=meta["soft"],
+                               mean_update=meta["mean_update"], rescale=meta["rescale"],
+                               dtype=dtype)
+
+
+def ptrain_errors(meta, g, orc):
+    errs = {}
+    for s in range(meta["steps"]):
+        b = build_batch(meta, g[f"s{s}/idx"])
+        if meta["counts"]:
+            b["counts"] = g[f"s{s}/counts"][:, None]
+        out = orc.step(b)
+        for grp in ("policy", "target_policy", "qf"):
+            for pn in (PARAM_ORDER_Q if grp == "qf" else PARAM_ORDER_POLICY):
+                key = f"s{s}/grad/{grp}/{pn}"
+                errs[key] = parity.compare(g, key, out["grads"][grp][pn].numpy())
+        for grp, params_ in (("policy", orc.P), ("target_policy", orc.TP), ("qf", orc.Q),
+                             ("tf", orc.T)):
+            for pn, t in params_.items():
+                key = f"s{s}/post/{grp}/{pn}"
+                gk = f"s{s}/grad/{grp}/{pn}" if s == 0 and grp != "tf" else None
+                errs[key], _ = parity.compare_post(g, key, gk, t.numpy(), meta["lr"])
+        th = out["target_head"]
+        st = {"Q Loss": out["qf_loss"], "Policy Loss": out["upper_bound"].mean(),
+              "Policy mu Mean": th["mean"].mean(), "Policy log std Mean": th["log_std"].mean(),
+              "QF mean": out["sorted_qs"].mean()}
+        for i in range(meta["K"]):
+            st[f"QF{i} Loss"] = out["qf_losses"][i]
+        for k, v in st.items():
+            errs[f"s{s}/stat/{k}"] = parity.stat_err(float(v), g, f"s{s}/stat/{k}")
+    return errs
+
+
+@pytest.mark.parametrize("name", PTRAIN_FIXTURES)
+def test_ptrain_oracle_matches_reference_golden(name):
+    """p-oac ParticleTrainer (particle_trainer.py) restatement vs the
+    reference's own run."""
+    meta, g = parity.load(name)
+    errs = ptrain_errors(meta, g, make_ptrain_oracle(meta))
+    noise = ptrain_errors(meta, g, make_ptrain_oracle(meta, torch.float64))
     bad = {k: (v, noise[k]) for k, v in errs.items() if v > parity.gate(k, noise[k])}
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
 
