@@ -150,7 +150,7 @@ static int dphase0(SacPlan& p, int flags, hipStream_t s) {
 }
 
 // target critic, TD targets, critic gradients (into grad_q)
-static int dphase1(SacPlan& p, int flags, hipStream_t s) {
+static int dphase1(SacPlan& p, int flags, hipStream_t s, bool fused) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -222,6 +222,11 @@ static int dphase1(SacPlan& p, int flags, hipStream_t s) {
     float* gq = grad_q(p);
     add(gb, t_dw(p.W(G_DH1Q), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_fc0_w, gq + L.q_fc0_b,
                  q_group(p), p.sp_q0));
+    if (fused) {   // critic Adam + Polyak in the epilogue (other layers: tail blocks)
+      const long off[1] = {(long)L.q_fc1_w};
+      const long n[1] = {(long)(L.q_size - L.q_fc1_w)};
+      fuse_adam(gb, critic_adam(p, 0, nullptr), 1, off, n);
+    }
     if (run_gemm(p, gb, s)) return 1;
   }
   return 0;
@@ -229,7 +234,7 @@ static int dphase1(SacPlan& p, int flags, hipStream_t s) {
 
 // critic Adam done: post-step critic on (obs, a~) and (obs, a~_T), the two
 // policy losses' gradients (into grad_p: policy block, target_policy block)
-static int dphase2(SacPlan& p, hipStream_t s) {
+static int dphase2(SacPlan& p, hipStream_t s, bool fused) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -329,6 +334,11 @@ static int dphase2(SacPlan& p, hipStream_t s) {
     GemmBatch gb{};
     add(gb, t_dw(p.W(G_DH1P), H, H, B, X + c.off_obs, RS, Do, gp + L.pol_fc0_w, gp + L.pol_fc0_b, pg, p.sp_p0));
     add(gb, t_dw(p.W(G_DH1TP), H, H, B, X + c.off_obs, RS, Do, gtp + L.pol_fc0_w, gtp + L.pol_fc0_b, pg, p.sp_p0));
+    if (fused) {   // [policy | target_policy] Adam in the epilogue; advances the step
+      const long off[2] = {(long)L.pol_fc1_w, (long)(L.tpol_base + L.pol_fc1_w)};
+      const long n[2] = {(long)(L.pol_size - L.pol_fc1_w), (long)(L.pol_size - L.pol_fc1_w)};
+      fuse_adam(gb, policy_adam(p, 0, nullptr), 2, off, n);
+    }
     if (run_gemm(p, gb, s)) return 1;
   }
   return 0;
@@ -336,15 +346,16 @@ static int dphase2(SacPlan& p, hipStream_t s) {
 
 int det_run_step(SacPlan& p, int flags, hipStream_t s) {
   p.launches = 0;
+  const bool fused = can_fuse_adam(p);
   if (dphase0(p, flags, s)) return 1;
-  if (dphase1(p, flags, s)) return 1;
-  {
+  if (dphase1(p, flags, s, fused)) return 1;
+  if (!fused) {
     AdamArgs a = critic_adam(p, 0, nullptr);
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
   }
-  if (dphase2(p, s)) return 1;
-  {
+  if (dphase2(p, s, fused)) return 1;
+  if (!fused) {
     AdamArgs a = policy_adam(p, 0, nullptr);
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
@@ -358,7 +369,7 @@ int det_step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
   switch (phase) {
     case 0: return dphase0(p, flags, s);
     case 1:
-      if (dphase1(p, flags, s)) return 1;
+      if (dphase1(p, flags, s, false)) return 1;
       if (p.S_q > 1) {
         AdamArgs a = critic_adam(p, 1, nullptr);
         OAC_HIP_CHECK(launch_adam(a, s));
@@ -367,7 +378,7 @@ int det_step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
     case 2: {
       AdamArgs a = critic_adam(p, -1, nullptr);
       OAC_HIP_CHECK(launch_adam(a, s));
-      if (dphase2(p, s)) return 1;
+      if (dphase2(p, s, false)) return 1;
       if (p.S_p > 1) {
         AdamArgs b = policy_adam(p, 1, nullptr);
         OAC_HIP_CHECK(launch_adam(b, s));

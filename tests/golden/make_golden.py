@@ -625,6 +625,65 @@ def gen_sac_snapshot(path, obs_dim=11, act_dim=3, hidden=(32, 32), B=16, seed=7)
     print(f"{os.path.basename(path)}: {os.path.getsize(path) / 1e3:.0f} KB")
 
 
+def gen_det_snapshot(path, kind, obs_dim=11, act_dim=3, hidden=(32, 32), B=16, seed=9):
+    """A checkpoint of the reference's GaussianTrainer (kind 'goac') or
+    particle_trainer.ParticleTrainer (kind 'ptrain', K=5) after two counts=True
+    steps -- built as main.py builds them (use_automatic_entropy_tuning from
+    --entropy_tuning, default on, so the snapshot carries log_alpha and the
+    unused alpha optimizer; gaussian_trainer.py:452-482,
+    particle_trainer.py:449-478) -- and the third step it then takes."""
+    K = 2 if kind == "goac" else 5
+    pp, qp = _producers(obs_dim, act_dim, list(hidden), q_out=K)
+    torch.manual_seed(0)
+    common = dict(action_space=Box(-1, 1, (act_dim,)), discount=0.99, reward_scale=1.0,
+                  delta=0.95, policy_lr=3e-4, qf_lr=3e-4, optimizer_class=Adam14,
+                  soft_target_tau=5e-3, target_update_period=1,
+                  use_automatic_entropy_tuning=True, q_min=0.0, q_max=100.0,
+                  share_layers=True, counts=True)
+    if kind == "goac":
+        tr = GaussianTrainer(pp, qp, n_estimators=2, **common)
+        params = goac_params(obs_dim, act_dim, list(hidden), seed, 0.0, 100.0, pi_init_w=0.2,
+                             q_init_w=0.1)
+        qf, tf = tr.q, tr.q_target
+    else:
+        tr = ParticleTrainer(pp, qp, n_estimators=K, deterministic=True, **common)
+        params = ptrain_params(obs_dim, act_dim, list(hidden), seed, K, 0.0, 100.0,
+                               pi_init_w=0.2, q_init_w=0.1)
+        qf, tf = tr.qfs[0], tr.tfs[0]
+    load_sd(tr.policy, params["policy"])
+    load_sd(tr.target_policy, params["target_policy"])
+    load_sd(qf, params["qf1"])
+    load_sd(tf, params["target_qf1"])
+    rb, _ = _fill_buffer(obs_dim, act_dim, 300)
+    crs = np.random.RandomState(5)
+    np.random.seed(3)
+
+    def batch_with_counts():
+        batch, idx = _record_batch(rb, B)
+        batch = dict(batch)
+        batch["counts"] = (crs.randint(0, 3, (B, 1)) * (crs.uniform(0, 1, (B, 1)) < 0.5)
+                           ).astype(np.float64)
+        return batch, idx
+    for s in range(2):
+        batch, _ = batch_with_counts()
+        tr.end_epoch(s)
+        tr.train(batch)
+    snap = _plain(tr.get_snapshot())
+    batch, idx = batch_with_counts()
+    tr.end_epoch(2)
+    tr.train(dict(batch))
+    mods = dict(policy=tr.policy, target_policy=tr.target_policy, qf=qf, tf=tf)
+    post = {g: {k: v.detach().clone() for k, v in m.state_dict().items()} for g, m in mods.items()}
+    fixture = dict(meta=dict(kind=kind, obs_dim=obs_dim, act_dim=act_dim, hidden=list(hidden), B=B,
+                             K=K, seed=seed, pi_init_w=0.2, q_init_w=0.1, n_replay=300, lr=3e-4,
+                             tau=5e-3, q_min=0.0, q_max=100.0, delta=0.95, discount=0.99),
+                   snapshot=snap,
+                   step3=dict(idx=torch.from_numpy(idx.astype(np.int64)),
+                              counts=torch.from_numpy(batch["counts"]), post=post))
+    torch.save(fixture, path)
+    print(f"{os.path.basename(path)}: {os.path.getsize(path) / 1e3:.0f} KB")
+
+
 def save(name, meta, out):
     import json
     out = dict(out)
@@ -642,6 +701,10 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "poac_counts":
         save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
                                       pi_init_w=0.3, counts=True))
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "det_snapshot":
+        gen_det_snapshot(os.path.join(HERE, "goac_snapshot.pt"), "goac")
+        gen_det_snapshot(os.path.join(HERE, "ptrain_snapshot.pt"), "ptrain")
         return
     if len(sys.argv) > 1 and sys.argv[1] == "ptrain":
         gen_ptrain_all()
@@ -677,6 +740,8 @@ def main():
     gen_sac_snapshot(os.path.join(HERE, "sac_snapshot.pt"))
     gen_goac_all()
     gen_ptrain_all()
+    gen_det_snapshot(os.path.join(HERE, "goac_snapshot.pt"), "goac")
+    gen_det_snapshot(os.path.join(HERE, "ptrain_snapshot.pt"), "ptrain")
 
 
 def gen_goac_all():
