@@ -2,7 +2,6 @@
 // bookkeeping, split-K sizing, GEMM task constructors, HIP-event timing.
 #pragma once
 #include <cstdio>
-#include <cstdlib>
 #include <cstring>
 #include <utility>
 #include <vector>
@@ -153,6 +152,15 @@ static inline void read_tuning(PlanBase& p) {
 // layer 1 64 -> 40 us) and loses on dX / dW (n- or m-contiguous operands, one
 // dword load per k) and narrow outputs; those launches run on the LDS kernel
 static inline int launch_cfg(int cfg, const GemmBatch& gb) {
+  if (cfg == 0) return 0;
+  // narrow products at large batch (width-1 critic heads, dL/da with N = act
+  // dim): a 64-wide LDS tile computes 1-17 useful columns over 8 barriered K
+  // blocks; the small-batch kernel's 32x32 tiles with K split over waves
+  // finish them in a fraction of the time
+  bool narrow = !gb.fuse_adam;
+  for (int i = 0; i < gb.ntasks && narrow; ++i)
+    narrow = gb.t[i].N <= 32 && gb.t[i].ksplit <= 1 && gb.t[i].K2 == 0;
+  if (narrow) return 0;
   if (cfg != 2) return cfg;
   for (int i = 0; i < gb.ntasks; ++i) {
     const GemmTask& t = gb.t[i];

@@ -222,7 +222,11 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
     HeadArgs a;
     std::memset(&a, 0, sizeof(a));
     a.wh = pol + L.pol_head_w; a.bh = pol + L.pol_head_b; a.ld_wa = Dq;
-    a.B = B; a.H = H; a.Da = Da; a.col_chunks = std::max(1, (H + 63) / 64);   // 64 columns each
+    a.B = B; a.H = H; a.Da = Da;
+    // 64 hidden columns per workgroup at small batch (more workgroups in
+    // flight); at large batch the fewest chunks the per-wave prefetch allows
+    // (each chunk recomputes the row block's heads)
+    a.col_chunks = std::max(1, (H + (B >= 1024 ? 127 : 63)) / (B >= 1024 ? 128 : 64));
     HeadSeg& s0 = a.seg[0];   // policy(obs; eps1) -> Q1/Q2(obs, a~)
     s0.h2 = p.W(W_H2P); s0.eps = p.E1(); s0.head = p.W(OAC_WS_HEAD1);
     s0.act = p.W(OAC_WS_ACT1); s0.stdv = p.W(W_STD1); s0.u = p.W(W_U1); s0.logp = p.W(OAC_WS_LOGP1);
