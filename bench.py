@@ -45,6 +45,9 @@ def parse():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--replay", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the exploration and g-oac legs (profiling runs: keeps the "
+                         "per-kernel statistics to the headline step)")
     ap.add_argument("--cpu-steps", type=int, default=1200)
     ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--timing-steps", type=int, default=50)
@@ -356,7 +359,10 @@ def main():
             "samples_per_s": round(value * B, 1),
             "steps_per_launch": n,
             "roofline": {"bound": "mfma",
-                         "kernel": "gemm_small_kernel" if B < 1024 else "gemm_grouped_kernel",
+                         # B >= 1024: per-launch choice among gemm_big_kernel (forward),
+                         # gemm_grouped_kernel (backward) and gemm_small_kernel (narrow)
+                         "kernel": "gemm_small_kernel" if B < 1024 else
+                                   "gemm launches (gemm_big/gemm_grouped/gemm_small)",
                          "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
                          "traffic": traffic,
@@ -372,7 +378,7 @@ def main():
             out["gather_GBps"] = round(GATHER_BYTES_PER_SAMPLE * B / (ga["avg_us"] * 1e-6) / 1e9, 1)
         if ad["launches"]:
             out["adam_GBps"] = round(ADAM_BYTES_PER_STEP * args.timing_steps / (ad["ms"] * 1e-3) / 1e9, 1)
-        if world == 1:
+        if world == 1 and not args.no_extras:
             out["exploration"] = exploration_timing(tr, args.obs_dim)
             out["goac"] = goac_timing(args, device, rb)
             if not args.no_cpu_baseline:

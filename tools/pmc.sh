@@ -9,7 +9,7 @@ R=$PWD
 cd /tmp && export TMPDIR=/tmp
 run() {
   timeout -s KILL 90 rocprofv3 --pmc $2 --kernel-trace --output-format csv -d $R/gpurun_out/pmc_${TAG}_$1 \
-    -- python3 $R/bench.py --steps 32 --warmup 16 --no-cpu-baseline --timing-steps 4 --steps-per-launch 1 "${@:3}" \
+    -- python3 $R/bench.py --steps 32 --warmup 16 --no-cpu-baseline --no-extras --timing-steps 4 --steps-per-launch 1 "${@:3}" \
     > $R/gpurun_out/pmc_${TAG}_$1.log 2>&1
 }
 run fetch FETCH_SIZE "$@"
