@@ -81,7 +81,7 @@ class Space:
 
 def build(args, rank, world, device):
     import oac_amd
-    from oac_amd import DeviceIndexStream, ReplayBuffer, SACTrainer
+    from oac_amd import DeviceIndexStream, ReplayBufferCount, SACTrainer
     torch.manual_seed(0)   # identical init on every rank
     hid = [args.hidden, args.hidden]
     pp = oac_amd.get_policy_producer(args.obs_dim, args.act_dim, hid, device=device)
@@ -95,7 +95,9 @@ def build(args, rank, world, device):
         tr = DataParallelSACTrainer(pp, qp, **kw)
     else:
         tr = SACTrainer(pp, qp, **kw)
-    rb = ReplayBuffer(args.replay, args.obs_dim, args.act_dim, device=device)
+    # ReplayBufferCount (per-row counts for the counts=True recipe legs; the
+    # SAC step ignores them)
+    rb = ReplayBufferCount(args.replay, args.obs_dim, args.act_dim, device=device)
     rb.load_transitions(synthetic_rows(args.replay, rb.rows, args.obs_dim, args.act_dim,
                                        device, seed=rank))
     stream = DeviceIndexStream(rb, args.batch, chunk=64, seed=1 + rank)
@@ -176,13 +178,14 @@ def cpu_baseline(args):
                        f"{args.cpu_threads} thread(s))")
 
 
-def goac_cpu_baseline(args, steps=200):
-    """The oracle's CPU restatement of the g-oac step (GaussianOACOracle),
-    same dims / batch, on a bounded sample of steps."""
+def recipe_cpu_baseline(kind, args, steps=200):
+    """The oracle's CPU restatement of the g-oac / p-oac recipe step
+    (GaussianOACOracle / ParticleUBOracle, counts=True), same dims / batch,
+    on a bounded sample of steps."""
     sys.path.insert(0, ROOT)
     from oracle import sac_oracle as so
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from fixtures_lib import goac_params
+    from fixtures_lib import goac_params, ptrain_params
     torch.set_num_threads(args.cpu_threads)
     Do, Da, H, B = args.obs_dim, args.act_dim, args.hidden, args.batch
     n = 20_000
@@ -192,12 +195,21 @@ def goac_cpu_baseline(args, steps=200):
                 terminals=(rs.uniform(0, 1, (n, 1)) < 0.01).astype(np.uint8),
                 next_observations=rs.standard_normal((n, Do)))
     rep = so.NumpyReplay(data)
-    orc = so.GaussianOACOracle(goac_params(Do, Da, [H, H], 0, 0.0, 500.0), Do, Da, q_max=500.0)
+    if kind == "goac":
+        orc = so.GaussianOACOracle(goac_params(Do, Da, [H, H], 0, 0.0, 500.0), Do, Da,
+                                   q_max=500.0)
+    else:
+        orc = so.ParticleUBOracle(ptrain_params(Do, Da, [H, H], 0, 10, 0.0, 500.0), Do, Da, 10,
+                                  8, q_max=500.0)
     irs = np.random.RandomState(1)
+    counts = np.zeros(n)
 
     def step():
-        _, b = rep.random_batch(B, irs)
-        orc.step(so.NumpyReplay.to_torch(b))
+        idx, b = rep.random_batch(B, irs)
+        b = so.NumpyReplay.to_torch(b)
+        b["counts"] = counts[idx][:, None].copy()
+        np.add.at(counts, np.unique(idx), 1)
+        orc.step(b)
     for _ in range(3):
         step()
     t0 = time.perf_counter()
@@ -206,7 +218,7 @@ def goac_cpu_baseline(args, steps=200):
     dt = time.perf_counter() - t0
     return dict(value=round(steps / dt, 2), unit="grad-steps/s", cores=args.cpu_threads,
                 kind="port",
-                sample=f"{steps} oracle g-oac steps (Humanoid dims, 2x256, B={B}, "
+                sample=f"{steps} oracle {kind} steps (Humanoid dims, 2x256, B={B}, counts, "
                        f"torch CPU fp32, {args.cpu_threads} thread(s))")
 
 
@@ -236,21 +248,33 @@ def exploration_timing(tr, obs_dim, reps=200):
             "beta_UB": 4.66, "delta": 23.53}
 
 
-def goac_timing(args, device, rb, steps=640, warmup=64, n=64):
-    """g-oac GaussianTrainer (trainer/gaussian_trainer.py, share_layers critic,
-    deterministic policy) on the same replay and dims:
-    gradient steps/s from the device index ring, n steps per graph launch."""
+def recipe_timing(kind, args, device, rb, steps=640, warmup=64, n=64):
+    """SURVEY 8f row 3 trainers in their Humanoid recipe configuration, on the
+    same replay and dims, gradient steps/s from the device index ring (n steps
+    per graph launch; counts read and bumped inside the step):
+      goac: GaussianTrainer, reproduce_g-oac.sh (--share_layers --counts,
+            deterministic policy, r_max 5 -> q_max 500);
+      poac: particle_trainer.ParticleTrainer, reproduce_p-oac_humanoid_counts.sh
+            (--n_estimators 10 --share_layers --counts, deterministic policy)."""
     import oac_amd
-    from oac_amd import DeviceIndexStream, GaussianTrainer
+    from oac_amd import DeviceIndexStream, GaussianTrainer, ParticleTrainer
     torch.manual_seed(0)
     hid = [args.hidden, args.hidden]
+    K = 2 if kind == "goac" else 10
     pp = oac_amd.get_policy_producer(args.obs_dim, args.act_dim, hid, device=device)
-    qp = oac_amd.get_q_producer(args.obs_dim, args.act_dim, hid, output_size=2, device=device)
-    tr = GaussianTrainer(pp, qp, action_space=Space(args.act_dim), discount=0.99,
-                         policy_lr=3e-4, qf_lr=3e-4, soft_target_tau=5e-3, q_min=0.0,
-                         q_max=500.0, share_layers=True, device=device, gemm_cfg=args.gemm_cfg)
+    qp = oac_amd.get_q_producer(args.obs_dim, args.act_dim, hid, output_size=K, device=device)
+    kw = dict(action_space=Space(args.act_dim), discount=0.99, policy_lr=3e-4, qf_lr=3e-4,
+              soft_target_tau=5e-3, q_min=0.0, q_max=500.0, share_layers=True, counts=True,
+              device=device, gemm_cfg=args.gemm_cfg)
+    tr = GaussianTrainer(pp, qp, **kw) if kind == "goac" else \
+        ParticleTrainer(pp, qp, n_estimators=K, delta=0.95, **kw)
     stream = DeviceIndexStream(rb, args.batch, chunk=64, seed=11)
-    step = step_fn(tr, rb, stream, args.batch, n)
+    cs = rb.device_count_state()
+
+    def step():
+        stream.before_step(n)
+        tr.train_from_ring(rb._storage, stream.ring, stream.slots, args.batch, n_steps=n,
+                           count_state=cs)
     for _ in range(warmup // n):
         step()
     torch.cuda.synchronize()
@@ -259,9 +283,9 @@ def goac_timing(args, device, rb, steps=640, warmup=64, n=64):
         step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    assert torch.isfinite(tr.params).all().item(), "non-finite g-oac parameters"
+    assert torch.isfinite(tr.params).all().item(), f"non-finite {kind} parameters"
     return {"steps_per_s": round(steps / el, 1), "ms_per_step": round(1e3 * el / steps, 4),
-            "batch": args.batch, "steps": steps, "steps_per_launch": n,
+            "batch": args.batch, "K": K, "counts": True, "steps": steps, "steps_per_launch": n,
             "launches_per_step": int(_launches(tr))}
 
 
@@ -380,9 +404,10 @@ def main():
             out["adam_GBps"] = round(ADAM_BYTES_PER_STEP * args.timing_steps / (ad["ms"] * 1e-3) / 1e9, 1)
         if world == 1 and not args.no_extras:
             out["exploration"] = exploration_timing(tr, args.obs_dim)
-            out["goac"] = goac_timing(args, device, rb)
-            if not args.no_cpu_baseline:
-                out["goac"]["cpu_baseline"] = goac_cpu_baseline(args)
+            for kind in ("goac", "poac"):
+                out[kind] = recipe_timing(kind, args, device, rb)
+                if not args.no_cpu_baseline:
+                    out[kind]["cpu_baseline"] = recipe_cpu_baseline(kind, args)
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)

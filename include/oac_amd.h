@@ -108,6 +108,12 @@ typedef struct oac_sac_buffers {
   int64_t replay_rows;
   const int32_t* idx_ring; /* [ring_slots * batch] sampled indices */
   int ring_slots;
+  /* ReplayBufferCount state for the ring path of counts=True trainers (may be
+   * NULL): per-row sample counts and dedupe tags [replay_rows], and a device
+   * epoch counter (one value per draw).  With OAC_STEP_GATHER | OAC_STEP_COUNTS
+   * each step reads its batch counts and bumps the drawn rows on the device
+   * (replay_buffer.py:186-197), so the counts recipes run from the ring. */
+  int32_t* counts; int32_t* count_tags; int32_t* count_epoch;
 } oac_sac_buffers;
 
 typedef struct oac_sac oac_sac;

@@ -140,6 +140,12 @@ struct ReplayInsertArgs {
   int obs_dim, act_dim, off_obs, off_act, off_rew, off_term, off_next_obs;
 };
 hipError_t launch_replay_insert(const ReplayInsertArgs& a, hipStream_t s);
+struct CountsStepArgs {
+  int* counts; int* tags; int* epoch;   // ReplayBufferCount device state
+  const int* idx; int ring_slots; const StepState* state; int B;
+  float* out;                           // [B] the step's batch counts
+};
+hipError_t launch_counts_step(const CountsStepArgs& a, hipStream_t s);
 hipError_t launch_counts_update(int* counts, int* tags, const int* idx, int B, int epoch,
                                 float* counts_out, hipStream_t s);
 long prio_scratch_doubles(long size);

@@ -84,6 +84,13 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
     TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_gather(g, s)));
     p.launches++;
   }
+  if ((flags & (OAC_STEP_GATHER | OAC_STEP_COUNTS)) == (OAC_STEP_GATHER | OAC_STEP_COUNTS) &&
+      p.b.counts) {   // ring path of a counts=True trainer: this draw's counts on the device
+    CountsStepArgs ca{p.b.counts, p.b.count_tags, p.b.count_epoch, p.b.idx_ring, p.b.ring_slots,
+                      p.state(), c.batch, p.W(OAC_WS_COUNTS)};
+    TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_counts_step(ca, s)));
+    p.launches++;
+  }
   const float* pol = p.b.params;
   const float* q = p.b.params + L.q1_base;
   const float* tq = p.b.targets;

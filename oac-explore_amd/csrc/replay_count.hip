@@ -75,6 +75,32 @@ hipError_t launch_counts_update(int* counts, int* tags, const int* idx, int B, i
   return hipGetLastError();
 }
 
+// Ring path of the counts=True trainers: one workgroup per step reads the
+// batch counts (before the draw's update) and then bumps every distinct drawn
+// row, so every read precedes every bump without a launch boundary; the tag
+// epoch is a device counter advanced by the same workgroup (the step's graph
+// carries no host value).  The step's indices are ring slot batch_counter %
+// ring_slots, as in gather_kernel.
+__global__ void __launch_bounds__(1024) counts_step_kernel(CountsStepArgs a) {
+  const long long bc = a.state ? a.state->batch_counter : 0;
+  const int* idx = a.ring_slots > 0 ? a.idx + (bc % a.ring_slots) * (long long)a.B : a.idx;
+  const int e = *a.epoch;
+  for (int i = threadIdx.x; i < a.B; i += blockDim.x) a.out[i] = (float)a.counts[idx[i]];
+  __syncthreads();
+  for (int i = threadIdx.x; i < a.B; i += blockDim.x) {
+    const int j = idx[i];
+    if (atomicExch(a.tags + j, e) != e) a.counts[j] += 1;   // first occurrence only
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *a.epoch = e + 1;
+}
+
+hipError_t launch_counts_step(const CountsStepArgs& a, hipStream_t s) {
+  if (a.B <= 0) return hipSuccess;
+  OAC_LAUNCH(counts_step_kernel, dim3(1), dim3(1024), 0, s, a);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------- priority sampling
 // Two-level inclusive scan of w_j = 1/(c_j + 1) in fp64: 1024 threads x 4
 // elements per block (kScanBlock), block totals scanned by one block (up to

@@ -62,6 +62,8 @@ class SacBuffers(ctypes.Structure):
         ("workspace", ctypes.c_void_p), ("replay", ctypes.c_void_p),
         ("replay_rows", ctypes.c_int64), ("idx_ring", ctypes.c_void_p),
         ("ring_slots", ctypes.c_int),
+        ("counts", ctypes.c_void_p), ("count_tags", ctypes.c_void_p),
+        ("count_epoch", ctypes.c_void_p),
     ]
 
 

@@ -264,6 +264,9 @@ class ReplayBufferCount(ReplayBuffer):
         self._counts = torch.zeros(N, dtype=torch.int32, device=self.device)
         self._tags = torch.full((N,), -1, dtype=torch.int32, device=self.device)
         self._epoch = 0
+        # dedupe epoch of the device ring path (train_from_ring with counts):
+        # a device counter, disjoint from the host path's epochs 0, 1, 2, ...
+        self._epoch_dev = torch.full((1,), 1 << 30, dtype=torch.int32, device=self.device)
         self.priority_sample = bool(priority_sample)
         self._scratch = None
 
@@ -304,6 +307,15 @@ class ReplayBufferCount(ReplayBuffer):
         batch = DeviceBatch(self, idx)
         batch["counts"] = counts.view(B, 1)
         return batch
+
+    def device_count_state(self):
+        """(counts, tags, epoch) device tensors for trainer.train_from_ring:
+        the ring path's steps read / bump these counts like random_batch
+        (uniform draws only: priority sampling draws from numpy's stream)."""
+        if self.priority_sample:
+            raise NotImplementedError("priority_sample draws on the host (np.random.choice); "
+                                      "train with random_batch batches")
+        return (self._counts, self._tags, self._epoch_dev)
 
     def get_snapshot(self):
         ss = super().get_snapshot()

@@ -181,9 +181,10 @@ class _ArenaTrainer(object):
         c.world_size = 1
         return c
 
-    def _plan(self, B, replay=None, idx=None, ring_slots=0):
+    def _plan(self, B, replay=None, idx=None, ring_slots=0, count_state=None):
         key = (B, None if replay is None else replay.data_ptr(),
-               None if idx is None else idx.data_ptr(), ring_slots)
+               None if idx is None else idx.data_ptr(), ring_slots,
+               None if count_state is None else count_state[0].data_ptr())
         p = self._plans.get(key)
         if p is not None:
             return p
@@ -202,6 +203,8 @@ class _ArenaTrainer(object):
         bufs.replay_rows = replay.shape[0] if replay is not None else 0
         bufs.idx_ring = idx.data_ptr() if idx is not None else None
         bufs.ring_slots = ring_slots
+        if count_state is not None:   # ReplayBufferCount device state (ring path, counts=True)
+            bufs.counts, bufs.count_tags, bufs.count_epoch = (t.data_ptr() for t in count_state)
         h = ctypes.c_void_p()
         check(L.oac_sac_create(ctypes.byref(cfg), ctypes.byref(bufs), ctypes.byref(h)))
         views = {}
@@ -306,18 +309,29 @@ class _ArenaTrainer(object):
         self._run(plan, _lib.OAC_STEP_GATHER, eps1, eps2, idx=dbatch.indices,
                   counts=self._batch_counts(dbatch))
 
-    def train_from_ring(self, storage, ring, ring_slots, B, n_steps=1):
+    def train_from_ring(self, storage, ring, ring_slots, B, n_steps=1, count_state=None):
         """Fast path for a device-resident replay with a device index ring
         (indices drawn by the device MT19937 stream, see ReplayBuffer):
         n_steps consecutive gradient steps, each on its own minibatch --
         rl_algorithm.py's inner loop of num_trains_per_train_loop train()
         calls -- in one graph launch.  Diagnostics (on the first step after
-        end_epoch in the reference) come from the last step of the call."""
+        end_epoch in the reference) come from the last step of the call.
+        counts=True trainers pass ``count_state`` =
+        ReplayBufferCount.device_count_state(): each step then reads and bumps
+        the drawn rows' counts on the device, exactly as random_batch does."""
+        flags = _lib.OAC_STEP_GATHER
         if getattr(self, "counts", False):
-            raise NotImplementedError("counts=True trains from ReplayBufferCount batches "
-                                      "(train / train_from_torch), not from the index ring")
-        plan = self._plan(B, replay=storage, idx=ring, ring_slots=ring_slots)
-        self._run(plan, _lib.OAC_STEP_GATHER, n_steps=n_steps)
+            if count_state is None:
+                raise ValueError("counts=True: pass count_state="
+                                 "ReplayBufferCount.device_count_state()")
+            if self._kind == _lib.OAC_KIND_SAC:
+                raise NotImplementedError("SACTrainer has no counts targets")
+            flags |= _lib.OAC_STEP_COUNTS
+        else:
+            count_state = None
+        plan = self._plan(B, replay=storage, idx=ring, ring_slots=ring_slots,
+                          count_state=count_state)
+        self._run(plan, flags, n_steps=n_steps)
 
 class SACTrainer(_ArenaTrainer):
     """SACTrainer (trainer/trainer.py:14) on liboac_amd."""

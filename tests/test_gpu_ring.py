@@ -47,3 +47,76 @@ def test_ring_steps_independent_of_call_split():
     assert np.isfinite(a).all()
     np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(a, c)
+
+
+# ------------------------------------------- counts=True trainers on the ring
+def _counts_trainer(kind):
+    from fixtures_lib import goac_params, ptrain_params
+    from gpu_helpers import producers, Space
+    if kind == "goac":
+        from oac_amd import GaussianTrainer
+        from test_gpu_goac import goac_producers
+        pp, qp = goac_producers(goac_params(Do, Da, [H, H], 3, 0.0, 100.0, pi_init_w=0.2,
+                                            q_init_w=0.1))
+        return GaussianTrainer(pp, qp, action_space=Space(Da), policy_lr=1e-3, qf_lr=1e-3,
+                               soft_target_tau=5e-3, q_min=0.0, q_max=100.0, share_layers=True,
+                               counts=True)
+    if kind == "ptrain":
+        from oac_amd import ParticleTrainer
+        from test_gpu_ptrain import ptrain_producers
+        pp, qp = ptrain_producers(ptrain_params(Do, Da, [H, H], 3, 5, 0.0, 50.0, pi_init_w=0.2,
+                                                q_init_w=0.1))
+        return ParticleTrainer(pp, qp, n_estimators=5, action_space=Space(Da), policy_lr=1e-3,
+                               qf_lr=1e-3, soft_target_tau=5e-3, q_min=0.0, q_max=50.0,
+                               share_layers=True, counts=True)
+    from oac_amd import ParticleTrainerOAC
+    K = 5
+    pp, qp = producers(sac_params(Do, Da, [H, H], 3, q_out=K, pi_init_w=0.2,
+                                  q_last_bias=np.linspace(0.0, 50.0, K)),
+                       q_keys=("qf1", "qf2", "target_qf1", "target_qf2", "qf1", "target_qf1"))
+    return ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Space(Da), policy_lr=1e-3,
+                              qf_lr=1e-3, soft_target_tau=5e-3, use_automatic_entropy_tuning=True,
+                              deterministic=False, q_min=0.0, q_max=50.0, share_layers=True,
+                              counts=True)
+
+
+def _count_buffer():
+    from oac_amd import ReplayBufferCount
+    from gpu_helpers import Space
+    rb = ReplayBufferCount(300, Space(Do), Space(Da), device="cuda:0", index_source="device")
+    data = synthetic_transitions(300, Do, Da, seed=1)
+    rb.load_transitions(torch.from_numpy(rb._rows_from(
+        data["observations"], data["actions"], data["rewards"], data["next_observations"],
+        data["terminals"])).cuda())
+    return rb
+
+
+@pytest.mark.parametrize("kind", ["goac", "ptrain", "poac"])
+def test_counts_ring_equals_random_batch_path(kind):
+    """counts=True trainers from the device index ring (counts read and bumped
+    inside the step's graph) equal the ReplayBufferCount.random_batch path
+    (host-driven draw + counts update, then train) on the same index stream:
+    parameters bitwise, counts array equal.  A small buffer (300 rows, B=32)
+    so rows repeat within and across batches."""
+    from oac_amd import DeviceIndexStream
+    steps, seed = 16, 4
+    # host path
+    rb_a = _count_buffer()
+    rb_a.seed_device_stream(seed)
+    tr_a = _counts_trainer(kind)
+    for _ in range(steps):
+        tr_a.train(rb_a.random_batch(B))
+    # ring path: two graph launches of 8 steps
+    rb_b = _count_buffer()
+    st = DeviceIndexStream(rb_b, B, chunk=8, seed=seed)
+    tr_b = _counts_trainer(kind)
+    for _ in range(2):
+        st.before_step(8)
+        tr_b.train_from_ring(rb_b._storage, st.ring, st.slots, B, n_steps=8,
+                             count_state=rb_b.device_count_state())
+    torch.cuda.synchronize()
+    assert torch.equal(rb_a._counts, rb_b._counts)
+    assert int(rb_a._counts.sum()) > 0
+    for name in ("params", "targets", "adam_m", "adam_v"):
+        np.testing.assert_array_equal(getattr(tr_a, name).cpu().numpy(),
+                                      getattr(tr_b, name).cpu().numpy())
