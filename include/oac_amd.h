@@ -237,6 +237,15 @@ int oac_expl_create_batch(int n_obs, int obs_dim, int act_dim, int hidden, const
 float* oac_expl_obs_slot(oac_expl* h);
 int oac_expl_action(oac_expl* h, const float* eps, float beta_UB, float delta, float* action,
                     float* mu_E, float* std_out, float* grad_out, void* stream);
+/* the handle's device result block [3][n_obs][act_dim]: action | mu_E | std
+ * (valid after the call's work on `stream` completes) */
+const float* oac_expl_outputs(oac_expl* h);
+/* optional pinned host staging: host_obs [n_obs, obs_dim + act_dim] (the
+ * first obs_dim floats of each row are the observation) is uploaded and the
+ * result block downloaded into host_out [3][n_obs][act_dim] inside the call's
+ * graph, so a call is one graph replay + one stream synchronisation (NULLs
+ * switch it off) */
+int oac_expl_set_host_io(oac_expl* h, const float* host_obs, float* host_out);
 
 /* ---------------------------------------------------------------- errors */
 const char* oac_last_error(void);

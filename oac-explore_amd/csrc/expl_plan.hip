@@ -8,8 +8,11 @@
 //   mu_C = sqrt(2 delta) Sigma g / (sqrt(g^T Sigma g) + 1e-5), Sigma = std^2
 //   action = tanh(mu_E + std * eps),  mu_E = mu_T + mu_C
 // The critics and policy are read in place from the trainer's parameter arena,
-// so the action always uses the current weights.  The launch sequence is
-// captured into a hipGraph (one replay per environment step).
+// so the action always uses the current weights.  The whole computation is one
+// launch (expl_fused.hip, a workgroup per observation), captured into a
+// hipGraph together with -- when the caller registers pinned host buffers --
+// the observation upload and the result download, so a call is one graph
+// replay and one stream synchronisation.
 #include <cmath>
 #include <cstring>
 
@@ -28,9 +31,13 @@ struct ExplPlan {
   StepState* state;
   unsigned long long seed;
   oac_sac_layout L;
-  // workspace offsets
-  int64_t o_x, o_h1p, o_h2p, o_head, o_std, o_mut, o_h1q1, o_h1q2, o_h2q1, o_h2q2, o_q1, o_q2, o_w,
-      o_dh1, o_dh2, o_da1, o_da2, o_grad, o_mue, o_act, o_cnt, total;
+  // workspace offsets (floats): observation rows [N, Do + Da], outputs
+  // [3][N][Da] (action | mu_E | std), dQ_UB/dmu_T [N, Da], ticket word
+  int64_t o_x, o_out, o_grad, o_cnt, total;
+  // optional pinned host staging (oac_expl_set_host_io): uploads / downloads
+  // captured into the graph
+  const float* host_obs = nullptr; float* host_out = nullptr;
+  long long* stage_clock = nullptr;   // instrumentation: per-stage wall clock of row 0
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   hipStream_t gstream = nullptr;
@@ -41,115 +48,38 @@ struct ExplPlan {
 static void expl_layout(ExplPlan& p) {
   int64_t o = 0;
   const int64_t N = p.N;
-  auto take = [&](int64_t n) { int64_t r = o; o = a64(o + N * n); return r; };
-  p.o_x = take(p.Do + p.Da);
-  p.o_h1p = take(p.H); p.o_h2p = take(p.H); p.o_head = take(2 * p.Da);
-  p.o_std = take(p.Da); p.o_mut = take(p.Da);
-  p.o_h1q1 = take(p.H); p.o_h1q2 = take(p.H); p.o_h2q1 = take(p.H); p.o_h2q2 = take(p.H);
-  p.o_q1 = take(1); p.o_q2 = take(1); p.o_w = take(2);
-  p.o_dh1 = take(p.H); p.o_dh2 = take(p.H); p.o_da1 = take(p.Da); p.o_da2 = take(p.Da);
-  p.o_grad = take(p.Da); p.o_mue = take(p.Da); p.o_act = take(p.Da);
-  p.o_cnt = o; o = a64(o + 2);   // Philox counter snapshot (8 bytes)
-  p.total = o + 64;              // tail pad: k-contiguous GEMM loads may read 7 floats past a row
-}
-
-static GemmTask e_task() {
-  GemmTask t;
-  std::memset(&t, 0, sizeof(t));
-  t.ksplit = 1;
-  return t;
-}
-
-// rows of x: M observations, row stride ldx
-static GemmTask e_fwd(const float* x, long ldx, int M, int K, const float* W, long ldw, int N,
-                      float* y, int epi, const float* bias) {
-  GemmTask t = e_task();
-  t.A = x; t.lda = ldx; t.a_kc = 1; t.B = W; t.ldb = ldw; t.b_kc = 1;
-  t.C = y; t.ldc = N; t.M = M; t.N = N; t.K = K; t.epi = epi; t.bias = bias;
-  return t;
-}
-
-static int e_run(GemmBatch& gb, hipStream_t s) {
-  gemm_batch_finalize(gb, 0);
-  OAC_HIP_CHECK(gemm_batch_launch(gb, 0, s));
-  return 0;
+  auto take = [&](int64_t n) { int64_t r = o; o = a64(o + n); return r; };
+  p.o_x = take(N * (p.Do + p.Da));
+  p.o_out = take(3 * N * p.Da);
+  p.o_grad = take(N * p.Da);
+  p.o_cnt = take(2);
+  p.total = o + 64;
 }
 
 static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta, hipStream_t s) {
-  const int Do = p.Do, Da = p.Da, H = p.H, Dq = Do + Da, N = p.N;
+  const int Do = p.Do, Da = p.Da, N = p.N;
   const oac_sac_layout& L = p.L;
   float* w = p.ws;
-  {
-    GemmBatch gb{};
-    gb.t[gb.ntasks++] = e_fwd(w + p.o_x, Dq, N, Do, p.pol + L.pol_fc0_w, Do, H, w + p.o_h1p, EPI_BIAS_RELU, p.pol + L.pol_fc0_b);
-    if (e_run(gb, s)) return 1;
-  }
-  {
-    GemmBatch gb{};
-    gb.t[gb.ntasks++] = e_fwd(w + p.o_h1p, H, N, H, p.pol + L.pol_fc1_w, H, H, w + p.o_h2p, EPI_BIAS_RELU, p.pol + L.pol_fc1_b);
-    if (e_run(gb, s)) return 1;
-  }
-  {
-    GemmBatch gb{};
-    gb.t[gb.ntasks++] = e_fwd(w + p.o_h2p, H, N, H, p.pol + L.pol_head_w, H, 2 * Da, w + p.o_head, EPI_BIAS, p.pol + L.pol_head_b);
-    if (e_run(gb, s)) return 1;
-  }
-  OacArgs a;
+  if (p.host_obs)   // rows [N, Do + Da]: the caller's pinned copy of the observations
+    OAC_HIP_CHECK(hipMemcpyAsync(w + p.o_x, p.host_obs, sizeof(float) * N * (Do + Da),
+                                 hipMemcpyHostToDevice, s));
+  ExplFusedArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.head = w + p.o_head; a.xrow = w + p.o_x; a.stdv = w + p.o_std; a.mu_T = w + p.o_mut;
-  a.q1 = w + p.o_q1; a.q2 = w + p.o_q2; a.w = w + p.o_w; a.da1 = w + p.o_da1; a.da2 = w + p.o_da2;
-  a.eps = eps; a.grad = w + p.o_grad; a.mu_E = w + p.o_mue; a.action = w + p.o_act;
-  a.state = p.state; a.counter = reinterpret_cast<long long*>(w + p.o_cnt);
+  a.obs = w + p.o_x; a.ld_obs = Do + Da;
+  a.pol = p.pol; a.q[0] = p.q1; a.q[1] = p.q2;
+  a.p_fc0_w = L.pol_fc0_w; a.p_fc0_b = L.pol_fc0_b; a.p_fc1_w = L.pol_fc1_w;
+  a.p_fc1_b = L.pol_fc1_b; a.p_head_w = L.pol_head_w; a.p_head_b = L.pol_head_b;
+  a.q_fc0_w = L.q_fc0_w; a.q_fc0_b = L.q_fc0_b; a.q_fc1_w = L.q_fc1_w; a.q_fc1_b = L.q_fc1_b;
+  a.q_last_w = L.q_last_w; a.q_last_b = L.q_last_b;
+  a.Do = Do; a.Da = Da; a.H = p.H; a.n = N;
+  a.eps = eps; a.out = w + p.o_out; a.grad = w + p.o_grad;
+  a.state = p.state; a.ticket = reinterpret_cast<unsigned*>(w + p.o_cnt);
   a.seed = p.seed; a.beta_UB = beta; a.sqrt_2delta = (float)std::sqrt(2.0 * (double)delta);
-  a.obs_dim = Do; a.act_dim = Da; a.n = N;
-  OAC_HIP_CHECK(launch_oac_prep(a, s));
-  const float* qs[2] = {p.q1, p.q2};
-  const int64_t h1[2] = {p.o_h1q1, p.o_h1q2}, h2[2] = {p.o_h2q1, p.o_h2q2}, qo[2] = {p.o_q1, p.o_q2};
-  {
-    GemmBatch gb{};
-    for (int i = 0; i < 2; ++i)
-      gb.t[gb.ntasks++] = e_fwd(w + p.o_x, Dq, N, Dq, qs[i] + L.q_fc0_w, Dq, H, w + h1[i], EPI_BIAS_RELU, qs[i] + L.q_fc0_b);
-    if (e_run(gb, s)) return 1;
-  }
-  {
-    GemmBatch gb{};
-    for (int i = 0; i < 2; ++i)
-      gb.t[gb.ntasks++] = e_fwd(w + h1[i], H, N, H, qs[i] + L.q_fc1_w, H, H, w + h2[i], EPI_BIAS_RELU, qs[i] + L.q_fc1_b);
-    if (e_run(gb, s)) return 1;
-  }
-  {
-    GemmBatch gb{};
-    for (int i = 0; i < 2; ++i)
-      gb.t[gb.ntasks++] = e_fwd(w + h2[i], H, N, H, qs[i] + L.q_last_w, H, 1, w + qo[i], EPI_BIAS, qs[i] + L.q_last_b);
-    if (e_run(gb, s)) return 1;
-  }
-  OAC_HIP_CHECK(launch_oac_seed(a, s));
-  const int64_t dh[2] = {p.o_dh1, p.o_dh2}, da[2] = {p.o_da1, p.o_da2};
-  {  // dQ_i/dh1 = (w_i * wl_i * [h2 > 0]) . W1_i  masked by h1 > 0
-    GemmBatch gb{};
-    for (int i = 0; i < 2; ++i) {
-      GemmTask t = e_task();
-      t.a_mode = A_RANK1_MASK; t.a_s = w + p.o_w + (long)i * N; t.a_v = qs[i] + L.q_last_w;
-      t.a_mask = w + h2[i]; t.ld_mask = H; t.a_kc = 1;
-      t.B = qs[i] + L.q_fc1_w; t.ldb = H; t.b_kc = 0;
-      t.C = w + dh[i]; t.ldc = H; t.M = N; t.N = H; t.K = H;
-      t.epi = EPI_MASK; t.aux = w + h1[i]; t.ld_aux = H;
-      gb.t[gb.ntasks++] = t;
-    }
-    if (e_run(gb, s)) return 1;
-  }
-  {  // dQ_i/da = dh1_i . W0_i[:, Do:]
-    GemmBatch gb{};
-    for (int i = 0; i < 2; ++i) {
-      GemmTask t = e_task();
-      t.A = w + dh[i]; t.lda = H; t.a_kc = 1;
-      t.B = qs[i] + L.q_fc0_w + Do; t.ldb = Dq; t.b_kc = 0;
-      t.C = w + da[i]; t.ldc = Da; t.M = N; t.N = Da; t.K = H; t.epi = EPI_STORE;
-      gb.t[gb.ntasks++] = t;
-    }
-    if (e_run(gb, s)) return 1;
-  }
-  OAC_HIP_CHECK(launch_oac_final(a, s));
+  a.stage_clock = p.stage_clock;
+  OAC_HIP_CHECK(launch_expl_fused(a, s));
+  if (p.host_out)
+    OAC_HIP_CHECK(hipMemcpyAsync(p.host_out, w + p.o_out, sizeof(float) * 3 * N * Da,
+                                 hipMemcpyDeviceToHost, s));
   return 0;
 }
 
@@ -183,6 +113,10 @@ int oac_expl_create_batch(int n_obs, int obs_dim, int act_dim, int hidden, const
   }
   if (act_dim < 1 || act_dim > 63) { set_error("act_dim must be in [1, 63]"); return 1; }
   if (n_obs < 1 || n_obs > 65536) { set_error("n_obs must be in [1, 65536]"); return 1; }
+  if (expl_fused_lds_bytes(obs_dim, act_dim, hidden) > 64 * 1024) {
+    set_error("exploration: obs_dim + 8 * hidden too large for one workgroup's LDS");
+    return 1;
+  }
   oac_expl* h = new oac_expl();
   ExplPlan& p = h->p;
   p.Do = obs_dim; p.Da = act_dim; p.H = hidden; p.N = n_obs;
@@ -239,10 +173,32 @@ int oac_expl_action(oac_expl* h, const float* eps, float beta_UB, float delta, f
   }
   OAC_HIP_CHECK(hipGraphLaunch(p.exec, s));
   const size_t nb = sizeof(float) * p.Da * p.N;
-  if (action) OAC_HIP_CHECK(hipMemcpyAsync(action, p.ws + p.o_act, nb, hipMemcpyDeviceToDevice, s));
-  if (mu_E) OAC_HIP_CHECK(hipMemcpyAsync(mu_E, p.ws + p.o_mue, nb, hipMemcpyDeviceToDevice, s));
-  if (std_out) OAC_HIP_CHECK(hipMemcpyAsync(std_out, p.ws + p.o_std, nb, hipMemcpyDeviceToDevice, s));
+  const float* o = p.ws + p.o_out;
+  if (action) OAC_HIP_CHECK(hipMemcpyAsync(action, o, nb, hipMemcpyDeviceToDevice, s));
+  if (mu_E) OAC_HIP_CHECK(hipMemcpyAsync(mu_E, o + p.Da * p.N, nb, hipMemcpyDeviceToDevice, s));
+  if (std_out) OAC_HIP_CHECK(hipMemcpyAsync(std_out, o + 2 * p.Da * p.N, nb, hipMemcpyDeviceToDevice, s));
   if (grad_out) OAC_HIP_CHECK(hipMemcpyAsync(grad_out, p.ws + p.o_grad, nb, hipMemcpyDeviceToDevice, s));
+  return 0;
+}
+
+// instrumentation hook (tools/expl_latency.py; not in include/oac_amd.h):
+// device buffer of >= 16 int64 stage stamps of row 0's workgroup, or NULL
+int oac_expl_debug_stage_clock(oac_expl* h, long long* dev_buf) {
+  if (!h) return 1;
+  h->p.stage_clock = dev_buf;
+  if (h->p.exec) { (void)hipGraphExecDestroy(h->p.exec); h->p.exec = nullptr; }
+  if (h->p.graph) { (void)hipGraphDestroy(h->p.graph); h->p.graph = nullptr; }
+  return 0;
+}
+
+const float* oac_expl_outputs(oac_expl* h) { return h ? h->p.ws + h->p.o_out : nullptr; }
+
+int oac_expl_set_host_io(oac_expl* h, const float* host_obs, float* host_out) {
+  if (!h) { set_error("null handle"); return 1; }
+  ExplPlan& p = h->p;
+  p.host_obs = host_obs; p.host_out = host_out;
+  if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }   // re-capture
+  if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
   return 0;
 }
 

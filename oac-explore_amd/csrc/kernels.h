@@ -98,21 +98,23 @@ struct PolicyHeadBwdArgs {
   float* dhead;         // [B, 2Da]
 };
 
-struct OacArgs {                        // N observations, one block per row
-  const float* head;    // [N, 2Da] policy heads of the observations
-  float* xrow;          // [N, Do+Da] critic input rows: ob | tanh(mu_T)
-  float* stdv; float* mu_T;               // [N, Da]
-  const float* q1; const float* q2;       // [N]
-  float* w;             // [2, N] dQ_UB/dQ_i
-  const float* da1; const float* da2;     // [N, Da]
-  const float* eps;     // [N, Da] or null -> Philox
-  float* grad; float* mu_E; float* action;   // [N, Da]
-  StepState* state;
-  long long* counter;   // Philox counter snapshot of this call (prep writes, final reads)
+
+struct ExplFusedArgs {                  // expl_fused.hip: one workgroup per observation
+  const float* obs; long ld_obs;        // [N, ld_obs] observation rows
+  const float* pol; const float* q[2];  // parameter blocks (oac_sac_layout offsets below)
+  long p_fc0_w, p_fc0_b, p_fc1_w, p_fc1_b, p_head_w, p_head_b;
+  long q_fc0_w, q_fc0_b, q_fc1_w, q_fc1_b, q_last_w, q_last_b;
+  int Do, Da, H, n;
+  const float* eps;                     // [N, Da] or null -> Philox (counter expl_counter)
+  float* out;                           // [3][N][Da]: action | mu_E | std
+  float* grad;                          // [N, Da] dQ_UB/dmu_T or null
+  StepState* state; unsigned* ticket;   // ticket: zeroed device word (re-armed by the kernel)
   unsigned long long seed;
   float beta_UB, sqrt_2delta;
-  int obs_dim, act_dim, n;
+  long long* stage_clock;               // instrumentation (tools/expl_latency.py) or null
 };
+size_t expl_fused_lds_bytes(int Do, int Da, int H);
+hipError_t launch_expl_fused(const ExplFusedArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ replay/adam
 struct GatherArgs {
@@ -241,9 +243,6 @@ hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s);
 hipError_t launch_policy_head_backward(const PolicyHeadBwdArgs& a, hipStream_t s);
 hipError_t launch_gather(const GatherArgs& a, hipStream_t s);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s);
-hipError_t launch_oac_prep(const OacArgs& a, hipStream_t s);
-hipError_t launch_oac_seed(const OacArgs& a, hipStream_t s);
-hipError_t launch_oac_final(const OacArgs& a, hipStream_t s);
 hipError_t launch_mt_randint(unsigned* mt_state, unsigned long long size, int count, int* out,
                              hipStream_t s);
 

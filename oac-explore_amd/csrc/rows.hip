@@ -115,73 +115,6 @@ __global__ void __launch_bounds__(256) policy_head_backward_kernel(PolicyHeadBwd
   p.dhead[(long)r * 2 * Da + Da + j] = dls;
 }
 
-// --------------------------------------------------------------------------
-// OAC exploration (optimistic_exploration.py:14-109) for N observations
-// (one block per row; N = 1 is the reference's per-step call, N > 1 the
-// vectorised-rollout extension -- each row is computed exactly as alone).
-// prep: from the policy head (mean | ls_raw) of one observation:
-//   std = exp(clamp(ls_raw)); a = tanh(mu_T) written into the critic input row
-//   after the observation; block 0 snapshots the Philox counter of the call.
-// seed: w1, w2 = dQ_UB/dQ1, dQ_UB/dQ2 once Q1, Q2 are known.
-// --------------------------------------------------------------------------
-__global__ void oac_prep_kernel(OacArgs p) {
-  const int r = blockIdx.x, j = threadIdx.x, Da = p.act_dim;
-  if (r == 0 && j == 0) *p.counter = p.state->expl_counter;
-  if (j >= Da) return;
-  const float mean = p.head[(long)r * 2 * Da + j];
-  const float ls = fminf(fmaxf(p.head[(long)r * 2 * Da + Da + j], -20.f), 2.f);
-  p.stdv[(long)r * Da + j] = expf(ls);
-  p.mu_T[(long)r * Da + j] = mean;
-  p.xrow[(long)r * (p.obs_dim + Da) + p.obs_dim + j] = tanhf(mean);
-}
-
-__global__ void oac_seed_kernel(OacArgs p) {
-  const int r = blockIdx.x * 64 + threadIdx.x;
-  if (r >= p.n) return;
-  // Q_UB = (Q1+Q2)/2 + beta*|Q1-Q2|/2 ; d|x|/dx = sign(x) (0 at 0)
-  const float d = p.q1[r] - p.q2[r];
-  const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-  const float hb = p.beta_UB / 2.f;
-  p.w[r] = 0.5f + hb * sg;
-  p.w[p.n + r] = 0.5f - hb * sg;
-}
-
-// final: grad = (da1 + da2) * (1 - a^2); Sigma = std^2;
-//   denom = sqrt(sum(grad^2 Sigma)) + 1e-5; mu_C = sqrt(2 delta) Sigma grad / denom;
-//   mu_E = mu_T + mu_C;  action = tanh(eps*std + mu_E)
-__global__ void oac_final_kernel(OacArgs p) {
-  __shared__ float red[64];
-  const int r = blockIdx.x, j = threadIdx.x;
-  const int Da = p.act_dim;
-  const long e = (long)r * Da + j;
-  float g = 0.f, sig = 0.f;
-  if (j < Da) {
-    const float a = p.xrow[(long)r * (p.obs_dim + Da) + p.obs_dim + j];
-    g = (p.da1[e] + p.da2[e]) * (1.f - a * a);
-    sig = p.stdv[e] * p.stdv[e];
-    red[j] = g * g * sig;
-  }
-  __syncthreads();
-  if (j == 0) {
-    float s = 0.f;
-    for (int i = 0; i < Da; ++i) s += red[i];
-    red[63] = sqrtf(s) + 10e-6f;
-  }
-  __syncthreads();
-  if (j < Da) {
-    const float denom = red[63];
-    const float mu_C = (p.sqrt_2delta * (sig * g)) / denom;
-    const float mu_E = p.mu_T[e] + mu_C;
-    float ev;
-    if (p.eps) ev = p.eps[e];
-    else ev = philox_normal(p.seed, (unsigned long long)*p.counter, 3u, (unsigned)(r * Da + j));
-    p.grad[e] = g;
-    p.mu_E[e] = mu_E;
-    p.action[e] = tanhf(add_rn(mul_rn(ev, p.stdv[e]), mu_E));
-  }
-  if (r == 0 && j == 0 && !p.eps) p.state->expl_counter = *p.counter + 1;
-}
-
 }  // namespace oac
 
 namespace oac {
@@ -203,18 +136,6 @@ hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s) {
 hipError_t launch_policy_head_backward(const PolicyHeadBwdArgs& a, hipStream_t s) {
   OAC_LAUNCH(policy_head_backward_kernel, dim3((a.B * a.act_dim + 255) / 256), dim3(256),
                      0, s, a);
-  return hipGetLastError();
-}
-hipError_t launch_oac_prep(const OacArgs& a, hipStream_t s) {
-  OAC_LAUNCH(oac_prep_kernel, dim3(a.n), dim3(64), 0, s, a);
-  return hipGetLastError();
-}
-hipError_t launch_oac_seed(const OacArgs& a, hipStream_t s) {
-  OAC_LAUNCH(oac_seed_kernel, dim3((a.n + 63) / 64), dim3(64), 0, s, a);
-  return hipGetLastError();
-}
-hipError_t launch_oac_final(const OacArgs& a, hipStream_t s) {
-  OAC_LAUNCH(oac_final_kernel, dim3(a.n), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

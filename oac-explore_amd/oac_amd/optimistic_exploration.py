@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import check, ptr
+from ._lib import check, ptr, stream_ptr
 
 
 def _owner(policy, qfs, trainer):
@@ -64,20 +64,24 @@ def get_optimistic_exploration_actions(obs_np, policy=None, qfs=None, trainer=No
 
 
 def _actions(t, obs, hyper_params, eps, return_info):
+    """One graph replay: the observations go through pinned host staging
+    (uploaded and the results downloaded inside the graph, oac_expl_set_host_io),
+    then one synchronisation of the trainer's stream."""
     n = obs.shape[0]
-    h, ws, slot, out = t._expl_handle(n)
-
-    def go(sp):
-        slot.copy_(torch.as_tensor(obs).to(torch.float32), non_blocking=False)
-        e = None
-        if eps is not None:
-            e = out[3]
-            e.copy_(torch.as_tensor(eps).reshape(e.shape))
-        check(_lib.lib().oac_expl_action(h, ptr(e), float(hyper_params["beta_UB"]),
-                                         float(hyper_params["delta"]), ptr(out[0]), ptr(out[1]),
-                                         ptr(out[2]), None, sp))
-        return out[:3].cpu().numpy()
-    res = t._on_stream(go)
+    e = t._expl_handle(n)
+    e.obs_np[:, :t.obs_dim] = obs                 # float64 observations -> fp32 rows
+    s = t.stream
+    s.wait_stream(torch.cuda.current_stream(t.device))   # parameter writes on torch's stream
+    ed = None
+    if eps is not None:
+        with torch.cuda.stream(s):
+            e.eps.copy_(torch.from_numpy(np.ascontiguousarray(eps, np.float32)).reshape(e.eps.shape))
+        ed = e.eps
+    check(_lib.lib().oac_expl_action(e.handle, ptr(ed), float(hyper_params["beta_UB"]),
+                                     float(hyper_params["delta"]), None, None, None, None,
+                                     stream_ptr(s)))
+    s.synchronize()
+    res = e.out_np
     info = {}
     if return_info:
         info = dict(mu_E=res[1].copy(), std=res[2].copy())

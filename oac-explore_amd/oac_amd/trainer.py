@@ -118,6 +118,16 @@ class AdamStateView:
                 v.zero_()
 
 
+class _ExplHandle:
+    def __init__(self, handle, ws, eps, obs_pin, out_pin):
+        self.handle, self.ws, self.eps = handle, ws, eps
+        self.obs_pin, self.out_pin = obs_pin, out_pin      # keep the pinned pages alive
+        self.obs_np, self.out_np = obs_pin.numpy(), out_pin.numpy()
+
+    def __getitem__(self, i):   # (handle, ...) unpacking of older callers
+        return (self.handle, self.ws)[i]
+
+
 class _Plan:
     def __init__(self, handle, ws, views, key):
         self.handle, self.ws, self.views, self.key = handle, ws, views, key
@@ -223,7 +233,7 @@ class _ArenaTrainer(object):
             for p in self._plans.values():
                 L.oac_sac_destroy(p.handle)
             for e in (self._expl or {}).values():
-                L.oac_expl_destroy(e[0])
+                L.oac_expl_destroy(e.handle)
         except Exception:
             pass
 
@@ -492,15 +502,18 @@ class SACTrainer(_ArenaTrainer):
 
     # ------------------------------------------------------------ exploration
     def _expl_handle(self, n=1):
-        """Exploration plan for n observations per call (cached per n):
-        (handle, workspace, obs slot view [n, obs_dim], outputs [4, n, act_dim])."""
+        """Exploration plan for n observations per call (cached per n): the
+        liboac_amd handle, its workspace, a device eps slot [n, act_dim]
+        (parity runs), and pinned host staging -- observation rows
+        [n, obs_dim + act_dim] and results [3, n, act_dim] (action | mu_E |
+        std) -- that the call's graph uploads / downloads itself."""
         if self._expl is None:
             self._expl = {}
         if n not in self._expl:
             L = _lib.lib()
             nf = L.oac_expl_workspace_floats_batch(n, self.obs_dim, self.act_dim, self.hidden)
             ws = torch.zeros(int(nf), dtype=torch.float32, device=self.device)
-            out = torch.zeros(4, n, self.act_dim, dtype=torch.float32, device=self.device)
+            eps = torch.zeros(n, self.act_dim, dtype=torch.float32, device=self.device)
             h = ctypes.c_void_p()
             p = self.params
             check(L.oac_expl_create_batch(n, self.obs_dim, self.act_dim, self.hidden, ptr(p),
@@ -508,8 +521,10 @@ class SACTrainer(_ArenaTrainer):
                                           ctypes.c_void_p(p.data_ptr() + 4 * self.layout.q2_base),
                                           ptr(ws), ptr(self.step_state),
                                           ctypes.c_uint64(self.seed + 1), ctypes.byref(h)))
-            slot_addr = L.oac_expl_obs_slot(h)
-            off = (slot_addr - ws.data_ptr()) // 4
-            rows = ws[off:off + n * (self.obs_dim + self.act_dim)].view(n, self.obs_dim + self.act_dim)
-            self._expl[n] = (h, ws, rows[:, :self.obs_dim], out)
+            obs_pin = torch.zeros(n, self.obs_dim + self.act_dim, dtype=torch.float32,
+                                  pin_memory=True)
+            out_pin = torch.zeros(3, n, self.act_dim, dtype=torch.float32, pin_memory=True)
+            check(L.oac_expl_set_host_io(h, ctypes.c_void_p(obs_pin.data_ptr()),
+                                         ctypes.c_void_p(out_pin.data_ptr())))
+            self._expl[n] = _ExplHandle(h, ws, eps, obs_pin, out_pin)
         return self._expl[n]

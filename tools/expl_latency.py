@@ -1,0 +1,76 @@
+"""Break down the host-side latency of one get_optimistic_exploration_action
+call (Humanoid dims, one observation): the full call, and its pieces (H2D obs
+copy, graph replay + sync, D2H action copy).  usage: python tools/expl_latency.py"""
+import os
+import sys
+import ctypes
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oac-explore_amd"))
+import oac_amd  # noqa: E402
+from oac_amd import _lib  # noqa: E402
+from oac_amd._lib import check, stream_ptr  # noqa: E402
+
+
+class Space:
+    def __init__(self, n):
+        self.shape = (n,)
+
+
+def bench(fn, reps=500):
+    for _ in range(50):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    return 1e6 * (time.perf_counter() - t0) / reps
+
+
+def main():
+    Do, Da, H = 376, 17, [256, 256]
+    dev = torch.device("cuda", 0)
+    pp = oac_amd.get_policy_producer(Do, Da, H, device=dev)
+    qp = oac_amd.get_q_producer(Do, Da, H, device=dev)
+    tr = oac_amd.SACTrainer(pp, qp, action_space=Space(Da), device=dev)
+    hp = dict(beta_UB=4.66, delta=23.53, share_layers=False)
+    ob = np.random.RandomState(0).standard_normal(Do)
+    full = bench(lambda: oac_amd.get_optimistic_exploration_action(ob, policy=tr.policy,
+                                                                   qfs=tr.qfs, hyper_params=hp))
+    e = tr._expl_handle(1)
+    L = _lib.lib()
+    s = tr.stream
+
+    def launch():
+        check(L.oac_expl_action(e.handle, None, 4.66, 23.53, None, None, None, None,
+                                stream_ptr(s)))
+        s.synchronize()
+    t_launch = bench(launch)
+    check(L.oac_expl_set_host_io(e.handle, None, None))   # device-only graph
+    t_kernel = bench(launch)
+    check(L.oac_expl_set_host_io(e.handle, e.obs_pin.data_ptr(), e.out_pin.data_ptr()))
+    clk = torch.zeros(16, dtype=torch.int64, device=dev)
+    fn = L.oac_expl_debug_stage_clock
+    fn.argtypes, fn.restype = [ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int
+    fn(e.handle, ctypes.c_void_p(clk.data_ptr()))
+    for _ in range(20):
+        launch()
+    c = clk.cpu().numpy()
+    names = ["load", "pol L0", "pol L1", "head+tanh", "Q L0", "Q L1+last+seed", "dh2/dh1",
+             "da", "final"]
+    print({n: round((c[i + 1] - c[i]) / 100.0, 2) for i, n in enumerate(names[:-1])},
+          "(us, 100 MHz wall clock)")
+    print("head matvec+sync", (c[9] - c[2]) / 100.0, "tanh+sync", (c[3] - c[9]) / 100.0,
+          "Q1 L0", (c[10] - c[3]) / 100.0, "Q2 L0+sync", (c[4] - c[10]) / 100.0)
+    fn(e.handle, None)
+    print({"full_call_us": round(full, 1), "graph_with_host_io_sync_us": round(t_launch, 1),
+           "graph_device_only_sync_us": round(t_kernel, 1)})
+
+
+if __name__ == "__main__":
+    main()
