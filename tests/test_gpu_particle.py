@@ -70,3 +70,37 @@ def test_particle_stats_keys_match_reference_order():
     tr.train_from_torch(batch_from(meta, g["s0/idx"]), eps1=g["s0/eps1"], eps2=g["s0/eps2"])
     keys = [k[len("s0/stat/"):] for k in g if k.startswith("s0/stat/")]
     assert list(tr.get_diagnostics().keys()) == keys
+
+
+@pytest.mark.parametrize("B", [1024, 4096])
+def test_particle_large_batch_matches_oracle(B):
+    """BASELINE configs[4] (particle_trainer_oac K=10, Ant-v2 dims, batch
+    4096) on the large-batch kernels (register-direct forward, LDS backward,
+    narrow products on the small-tile kernel): one step against the fp32 CPU
+    oracle on the same inputs and eps (1e-5 on every gradient tensor)."""
+    from oracle import sac_oracle as so
+    from gpu_helpers import batch_from
+    meta = dict(obs_dim=111, act_dim=8, hidden=[256, 256], K=10, seed=11, q_min=0.0,
+                q_max=500.0, pi_init_w=1e-3, lr=3e-4, tau=5e-3, discount=0.99, delta=0.95,
+                n_replay=20000)
+    K = meta["K"]
+    params = sac_params(111, 8, [256, 256], meta["seed"], q_out=K,
+                        q_last_bias=np.linspace(0.0, 500.0, K), pi_init_w=1e-3)
+    tr = particle_trainer_for(meta)
+    rs = np.random.RandomState(B)
+    b = batch_from(meta, rs.randint(0, meta["n_replay"], B))
+    e1 = rs.standard_normal((B, 8)).astype(np.float32)
+    e2 = rs.standard_normal((B, 8)).astype(np.float32)
+    tr.train_from_torch(b, eps1=e1, eps2=e2)
+    torch.cuda.synchronize()
+    out = so.ParticleOACOracle(params, 111, 8, K, policy_lr=3e-4, qf_lr=3e-4).step(b, e1, e2)
+    worst = {}
+    for grp, mod, order in (("policy", tr.policy, PARAM_ORDER_POLICY),
+                            ("qf", tr.qfs[0], PARAM_ORDER_Q)):
+        gv = module_tensors(tr, mod, tr.grads)
+        for pn in order:
+            worst[f"{grp}/{pn}"] = parity.rel_err(gv[pn].cpu().numpy(),
+                                                  out["grads"][grp][pn].numpy())
+    bad = {k: v for k, v in worst.items() if v > 1e-5}
+    print(B, sorted(worst.items(), key=lambda kv: -kv[1])[:3])
+    assert not bad, bad
