@@ -149,19 +149,42 @@ namespace oac {
 //   sorted_qs = sort_K(Q(obs, a));  tq_sorted = sort_K(TQ(next_obs, a'))
 //   y_i = scale*r + (1-d)*gamma*tq_sorted_i                      (207-208)
 //   qf_loss = sum_i MSE(sorted_qs_i, y_i)   (NOT divided by K)   (247-251)
-// The per-sample sort over K (<= 16) is an in-register stable insertion
-// sort; the gradient is scattered back through the sort permutation.
+// The per-sample sort over K (<= 16) is a 16-wide bitonic network on
+// (value, head index) pairs -- every array index static, so the rows stay in
+// registers (an insertion sort's data-dependent indexing put them in scratch:
+// 11.6 us for 256 rows) -- ordering ties by head index, i.e. a stable sort;
+// the gradient is scattered back through the sort permutation.
 // --------------------------------------------------------------------------
 constexpr int kMaxHeads = 16;
 
-__device__ __forceinline__ void sort_k(float (&v)[kMaxHeads], int (&ix)[kMaxHeads], int K) {
-  for (int i = 1; i < K; ++i) {
-    const float x = v[i];
-    const int xi = ix[i];
-    int j = i - 1;
-    while (j >= 0 && v[j] > x) { v[j + 1] = v[j]; ix[j + 1] = ix[j]; --j; }
-    v[j + 1] = x;
-    ix[j + 1] = xi;
+__device__ __forceinline__ void cas_kv(float& va, int& ia, float& vb, int& ib, bool up) {
+  const bool gt = va > vb || (va == vb && ia > ib);
+  if (gt == up) {
+    const float tv = va; va = vb; vb = tv;
+    const int ti = ia; ia = ib; ib = ti;
+  }
+}
+
+// ascending sort of (v, ix); entries K..15 must hold +inf (and indices >= K)
+__device__ __forceinline__ void sort16(float (&v)[kMaxHeads], int (&ix)[kMaxHeads]) {
+#pragma unroll
+  for (int k = 2; k <= kMaxHeads; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+      for (int i = 0; i < kMaxHeads; ++i) {
+        const int l = i ^ j;
+        if (l > i) cas_kv(v[i], ix[i], v[l], ix[l], (i & k) == 0);
+      }
+}
+
+// row r's K values (padded with +inf) and their head indices
+__device__ __forceinline__ void load_row16(const float* src, int K, float (&v)[kMaxHeads],
+                                           int (&ix)[kMaxHeads]) {
+#pragma unroll
+  for (int i = 0; i < kMaxHeads; ++i) {
+    v[i] = i < K ? src[i] : __builtin_huge_valf();
+    ix[i] = i;
   }
 }
 
@@ -169,58 +192,70 @@ __global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArg
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= p.B) return;
   const int K = p.K;
+  const float fK = (float)K;
   float q[kMaxHeads], t[kMaxHeads];
   int qi[kMaxHeads], tix[kMaxHeads];
-  for (int i = 0; i < K; ++i) {
-    q[i] = p.q[(long)r * K + i]; qi[i] = i;
-    t[i] = p.tq[(long)r * K + i]; tix[i] = i;
-  }
-  sort_k(q, qi, K);
-  sort_k(t, tix, K);
+  load_row16(p.q + (long)r * K, K, q, qi);
+  load_row16(p.tq + (long)r * K, K, t, tix);
+  sort16(q, qi);
+  sort16(t, tix);
   const float rew = p.batch[(long)r * p.ld_batch + p.off_rew];
   const float term = p.batch[(long)r * p.ld_batch + p.off_term];
   const float invB = 1.f / (float)p.B;
   const float sr = __fmul_rn(p.reward_scale, rew);
   const float gd = __fmul_rn(1.f - term, p.discount);
   float y[kMaxHeads];
-  for (int i = 0; i < K; ++i) y[i] = __fadd_rn(sr, __fmul_rn(gd, t[i]));
-  // counts=True (particle_trainer_oac.py:220-224): a row drawn before (count
-  // > 0) gets the sorted predictions re-centred on the target mean,
-  //   y_i <- (sorted_q_i - mean_k sorted_q) + mean_k y
+#pragma unroll
+  for (int i = 0; i < kMaxHeads; ++i) y[i] = __fadd_rn(sr, __fmul_rn(gd, t[i]));
+  // sums over the K valid slots, in slot order
+  auto mean_k = [&](const float (&a)[kMaxHeads]) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < kMaxHeads; ++i) if (i < K) s += a[i];
+    return s / fK;
+  };
   // std_soft_update (particle_trainer.py:222-231): current sorted predictions
   // re-centred on the next-value mean, mixed with the next values
   if (p.soft_prob >= 0.f) {
-    float sq = 0.f, sy = 0.f;
-    for (int i = 0; i < K; ++i) { sq += q[i]; sy += y[i]; }
-    const float mq = sq / (float)K, my = sy / (float)K;
+    const float mq = mean_k(q), my = mean_k(y);
     const float w = 1.f - p.soft_prob;
-    for (int i = 0; i < K; ++i)
-      y[i] = __fadd_rn(__fmul_rn(p.soft_prob, y[i]), __fmul_rn(w, (q[i] - mq) + my));
+#pragma unroll
+    for (int i = 0; i < kMaxHeads; ++i)
+      if (i < K) y[i] = __fadd_rn(__fmul_rn(p.soft_prob, y[i]), __fmul_rn(w, (q[i] - mq) + my));
   }
+  // counts=True (particle_trainer_oac.py:220-224, particle_trainer.py:236-241):
+  // a row drawn before (count > 0) gets the sorted predictions re-centred on
+  // the target mean, y_i <- (sorted_q_i - mean_k sorted_q) + mean_k y
   if (p.counts && p.counts[r] != 0.f) {
-    float sq = 0.f, sy = 0.f;
-    for (int i = 0; i < K; ++i) { sq += q[i]; sy += y[i]; }
-    const float mq = sq / (float)K, my = sy / (float)K;
-    for (int i = 0; i < K; ++i) y[i] = (q[i] - mq) + my;
+    const float mq = mean_k(q), my = mean_k(y);
+#pragma unroll
+    for (int i = 0; i < kMaxHeads; ++i)
+      if (i < K) y[i] = (q[i] - mq) + my;
   }
   // rescale_targets_around_mean (particle_trainer.py:254-262): a target spread
   // wider than q_max - q_min is shrunk around its mean to that width
   if (p.rescale_spread > 0.f) {
-    const float range = y[K - 1] - y[0];
+    float ylast = y[0];
+#pragma unroll
+    for (int i = 1; i < kMaxHeads; ++i) if (i == K - 1) ylast = y[i];
+    const float range = ylast - y[0];
     if (range > p.rescale_spread) {
-      float sy = 0.f;
-      for (int i = 0; i < K; ++i) sy += y[i];
-      const float my = sy / (float)K;
+      const float my = mean_k(y);
       const float f = p.rescale_spread / (range + 1e-6f);
-      for (int i = 0; i < K; ++i) y[i] = __fadd_rn(__fmul_rn(y[i] - my, f), my);
+#pragma unroll
+      for (int i = 0; i < kMaxHeads; ++i)
+        if (i < K) y[i] = __fadd_rn(__fmul_rn(y[i] - my, f), my);
     }
   }
   const float g2 = p.loss_scale > 0.f ? __fmul_rn(2.f, p.loss_scale) : 2.f;
-  for (int i = 0; i < K; ++i) {
-    const float d = q[i] - y[i];
-    p.y[(long)r * K + i] = y[i];
-    p.sqe[(long)r * K + i] = d * d;
-    p.dq[(long)r * K + qi[i]] = __fmul_rn(g2 * d, invB);
+#pragma unroll
+  for (int i = 0; i < kMaxHeads; ++i) {
+    if (i < K) {
+      const float d = q[i] - y[i];
+      p.y[(long)r * K + i] = y[i];
+      p.sqe[(long)r * K + i] = d * d;
+      p.dq[(long)r * K + qi[i]] = __fmul_rn(g2 * d, invB);
+    }
   }
 }
 
@@ -344,15 +379,22 @@ __global__ void __launch_bounds__(256) particle_ub_seed_kernel(ParticleUbSeedArg
   const int K = p.K;
   float v[kMaxHeads];
   int ix[kMaxHeads];
-  for (int i = 0; i < K; ++i) { v[i] = p.qn[(long)r * K + i]; ix[i] = i; }
-  sort_k(v, ix, K);
+  load_row16(p.qn + (long)r * K, K, v, ix);
+  sort16(v, ix);
   const float g0 = -(1.f / (float)p.B);
-  const int sel = ix[p.delta_index];
-  for (int i = 0; i < K; ++i) {
-    p.g[(long)r * K + i] = (i == sel) ? g0 : 0.f;
-    p.gt[(long)r * K + i] = g0 / (float)K;
+  int sel = ix[0];
+  float ub = v[0];
+#pragma unroll
+  for (int i = 1; i < kMaxHeads; ++i)
+    if (i == p.delta_index) { sel = ix[i]; ub = v[i]; }
+#pragma unroll
+  for (int i = 0; i < kMaxHeads; ++i) {
+    if (i < K) {
+      p.g[(long)r * K + i] = (i == sel) ? g0 : 0.f;
+      p.gt[(long)r * K + i] = g0 / (float)K;
+    }
   }
-  p.ub[r] = v[p.delta_index];
+  p.ub[r] = ub;
 }
 
 __global__ void __launch_bounds__(256) det_head_backward_kernel(DetHeadBwdArgs p) {
