@@ -108,8 +108,7 @@ static int dphase0(SacPlan& p, int flags, hipStream_t s) {
     TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_counts_step(ca, s)));
     p.launches++;
   }
-  const int K = c.q_out;
-  const float* pol = p.b.params;
+    const float* pol = p.b.params;
   const float* tpol = p.b.params + L.tpol_base;
   const float* npol = c.mean_update ? tpol : pol;   // the policy acting on next_obs
   const float* q = p.b.params + L.q1_base;
@@ -135,22 +134,24 @@ static int dphase0(SacPlan& p, int flags, hipStream_t s) {
     add(gb, t_fwd(p.W(G_H1Q), H, B, H, q + L.q_fc1_w, H, H, p.W(G_H2Q), H, EPI_BIAS_RELU, q + L.q_fc1_b));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {
-    GemmBatch gb{};
-    add(gb, t_fwd(p.W(G_H2P), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD1), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
-    add(gb, t_fwd(p.W(G_H2P2), H, B, H, npol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD2), 2 * Da, EPI_BIAS, npol + L.pol_head_b));
-    add(gb, t_fwd(p.W(G_H2TP), H, B, H, tpol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD3), 2 * Da, EPI_BIAS, tpol + L.pol_head_b));
-    add(gb, t_fwd(p.W(G_H2Q), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_Q1), K, EPI_BIAS, q + L.q_last_b));
-    if (run_gemm(p, gb, s)) return 1;
-  }
-  {
-    DetActionArgs a;
+  {  // the three heads, a = tanh(mean), and the target critic's action
+     // columns on next_obs (h1 = relu(P + a'. W0[:, Do:]), one launch (head.hip)
+    HeadArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.head[0] = p.W(OAC_WS_HEAD1); a.act[0] = p.W(OAC_WS_ACT1);
-    a.head[1] = p.W(OAC_WS_HEAD2); a.act[1] = p.W(OAC_WS_ACT2);
-    a.head[2] = p.W(OAC_WS_HEAD3); a.act[2] = p.W(OAC_WS_ACT3);
-    a.nseg = 3; a.B = B; a.act_dim = Da;
-    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_det_action(a, s)));
+    a.ld_wa = Dq; a.det = 1;
+    a.B = B; a.H = H; a.Da = Da;
+    a.col_chunks = std::max(1, (H + (B >= 1024 ? 127 : 63)) / (B >= 1024 ? 128 : 64));
+    HeadSeg& s0 = a.seg[0];   // policy(obs) -> a~ (post-step critic, phase 2)
+    s0.h2 = p.W(G_H2P); s0.wh = pol + L.pol_head_w; s0.bh = pol + L.pol_head_b;
+    s0.head = p.W(OAC_WS_HEAD1); s0.act = p.W(OAC_WS_ACT1);
+    HeadSeg& s1 = a.seg[1];   // next-action policy(next_obs) -> QT(next_obs, a')
+    s1.h2 = p.W(G_H2P2); s1.wh = npol + L.pol_head_w; s1.bh = npol + L.pol_head_b;
+    s1.head = p.W(OAC_WS_HEAD2); s1.act = p.W(OAC_WS_ACT2);
+    s1.n_nets = 1; s1.wa[0] = tq + L.q_fc0_w + Do; s1.pre[0] = p.W(G_PT); s1.h1[0] = p.W(G_H1T);
+    HeadSeg& s2 = a.seg[2];   // target_policy(obs) -> a~_T (phase 2)
+    s2.h2 = p.W(G_H2TP); s2.wh = tpol + L.pol_head_w; s2.bh = tpol + L.pol_head_b;
+    s2.head = p.W(OAC_WS_HEAD3); s2.act = p.W(OAC_WS_ACT3);
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head(a, 3, s)));
     p.launches++;
   }
   return 0;
@@ -165,17 +166,10 @@ static int dphase1(SacPlan& p, int flags, hipStream_t s, bool fused) {
   float* X = p.W(OAC_WS_BATCH);
   const float* q = p.b.params + L.q1_base;
   const float* tq = p.b.targets;
-  {
-    GemmBatch gb{};
-    GemmTask t = t_fwd(p.W(OAC_WS_ACT2), Da, B, Da, tq + L.q_fc0_w + Do, Dq, H, p.W(G_H1T), H,
-                       EPI_ADD_RELU, nullptr);
-    t.aux = p.W(G_PT); t.ld_aux = H;
-    add(gb, t);
-    if (run_gemm(p, gb, s)) return 1;
-  }
-  {
+  {  // target critic layer 1, and the critic's outputs Q(obs, a)
     GemmBatch gb{};
     add(gb, t_fwd(p.W(G_H1T), H, B, H, tq + L.q_fc1_w, H, H, p.W(G_H2T), H, EPI_BIAS_RELU, tq + L.q_fc1_b));
+    add(gb, t_fwd(p.W(G_H2Q), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_Q1), K, EPI_BIAS, q + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
   {

@@ -51,6 +51,8 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
   constexpr int kRed = kHeadWaves * 4 * 4 * 64;   // waves x col tiles x regs x lanes
   __shared__ __attribute__((aligned(16))) float lds[kRed];
   const HeadSeg& sg = a.seg[blockIdx.y];
+  const float* wh = sg.wh ? sg.wh : a.wh;
+  const float* bh = sg.bh ? sg.bh : a.bh;
   const int rb = blockIdx.x / a.col_chunks;
   const int chunk = blockIdx.x % a.col_chunks;
   const int m0 = rb * kRows;
@@ -67,12 +69,12 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
   const int pairs = sg.n_nets * tiles;
   const int ksteps = (Da + 3) >> 2;              // <= 8 (Da <= 32)
   const int srow = threadIdx.x >> 5, sj = threadIdx.x & 31;   // step 2: row, action dim
-  const float eps_pf = sg.eps[(long)min(m0 + srow, B - 1) * Da + min(sj, Da - 1)];
+  const float eps_pf = a.det ? 0.f : sg.eps[(long)min(m0 + srow, B - 1) * Da + min(sj, Da - 1)];
   float bh_pf[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int e = threadIdx.x + i * 64 * kHeadWaves;          // head element (see step 1)
-    bh_pf[i] = a.bh[min(((e >> 8) << 4) + (e & 15), D2 - 1)];
+    bh_pf[i] = bh[min(((e >> 8) << 4) + (e & 15), D2 - 1)];
   }
   constexpr int kPairs = 2;                      // pairs per wave prefetched
   float bw_pf[kPairs][8], pre_pf[kPairs][4];
@@ -103,7 +105,7 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
     const float* arow = sg.h2 + (long)min(m0 + l16, B - 1) * H;
     const float* brow[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) brow[t] = a.wh + (long)min(t * 16 + l16, D2 - 1) * H;
+    for (int t = 0; t < 4; ++t) brow[t] = wh + (long)min(t * 16 + l16, D2 - 1) * H;
     const int chunks = (H + 15) >> 4;
     constexpr int kC = 2;                         // k-chunks in flight per wave
 #pragma unroll 1
@@ -178,13 +180,18 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
     if (m < B && j < Da) {
       const long e = (long)m * Da + j;
       float sd, u;
-      l = tanh_gauss_sample(hs[row * 65 + j], hs[row * 65 + Da + j], eps_pf, act, sd, u);
-      if (chunk == 0) { sg.act[e] = act; sg.stdv[e] = sd; sg.u[e] = u; }
+      if (a.det) {
+        act = tanhf(hs[row * 65 + j]);
+        if (chunk == 0) sg.act[e] = act;
+      } else {
+        l = tanh_gauss_sample(hs[row * 65 + j], hs[row * 65 + Da + j], eps_pf, act, sd, u);
+        if (chunk == 0) { sg.act[e] = act; sg.stdv[e] = sd; sg.u[e] = u; }
+      }
     }
     as[row * 33 + j] = act;   // 0 beyond Da / B
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) l += __shfl_xor(l, o, 32);
-    if (j == 0 && m < B && chunk == 0) sg.logp[m] = l;
+    if (j == 0 && m < B && chunk == 0 && !a.det) sg.logp[m] = l;
   }
   __syncthreads();
   STAGE(3);
@@ -216,7 +223,8 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
 }
 
 hipError_t launch_policy_head(const HeadArgs& a, int nseg, hipStream_t s) {
-  if (a.Da < 1 || 2 * a.Da > 64 || a.col_chunks < 1 || nseg < 1 || nseg > 2)
+  if (a.Da < 1 || 2 * a.Da > 64 || a.col_chunks < 1 || nseg < 1 || nseg > 3 ||
+      (nseg > 2 && !a.det))
     return hipErrorInvalidValue;
   for (int i = 0; i < nseg; ++i)
     if (a.seg[i].n_nets < 0 || a.seg[i].n_nets > 2) return hipErrorInvalidValue;

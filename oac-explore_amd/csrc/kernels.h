@@ -46,7 +46,9 @@ struct PolicySampleSeg {
 // fused policy head + sample + critics' action columns (head.hip)
 struct HeadSeg {
   const float* h2;        // [B, H] policy hidden layer 2
-  const float* eps;       // [B, Da]
+  const float* wh; const float* bh;   // this segment's stacked heads [2*Da, H], [2*Da]
+                                      // (null: HeadArgs.wh / bh)
+  const float* eps;       // [B, Da] (unused with HeadArgs.det)
   float* head; float* act; float* stdv; float* u; float* logp;   // per-row outputs
   int n_nets;             // critics fed with this batch's actions (0..2)
   const float* wa[2];     // W0[:, Do:] of each critic (row n at wa + n*ld_wa)
@@ -54,8 +56,10 @@ struct HeadSeg {
   float* h1[2];           // [B, H] relu(pre + a . wa^T)
 };
 struct HeadArgs {
-  HeadSeg seg[2];
+  HeadSeg seg[3];
   const float* wh; const float* bh;   // stacked heads [2*Da, H], [2*Da]
+  int det;                            // deterministic policies: a = tanh(mean) (policies.py:286-288);
+                                      // stdv / u / logp / eps unused
   long ld_wa;
   int B, H, Da;
   int col_chunks;                     // workgroups per 32-row block
@@ -184,12 +188,6 @@ hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s);
 // g-oac GaussianTrainer, share_layers=True (trainer/gaussian_trainer.py:177-437):
 // the critic has two outputs, column 0 = Q mean, column 1 = log std (the
 // FlattenMlp positive=[False, True] exp, networks.py:69-75, is applied here).
-struct DetActionArgs {                  // deterministic policy: a = tanh(mean) (policies.py:286-288)
-  const float* head[3];                 // [B, 2Da] heads (mean | raw log std)
-  float* act[3];                        // [B, Da]
-  int nseg, B, act_dim;
-};
-hipError_t launch_det_action(const DetActionArgs& a, hipStream_t s);
 
 struct GaussTargetArgs {
   const float* q; const float* tq;      // [B, 2] Q(obs, a), Q_target(next_obs, a') raw outputs

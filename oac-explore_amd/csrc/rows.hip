@@ -313,17 +313,6 @@ hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s) {
 // FlattenMlp positive=[False, True] output (networks.py:69-75).
 // --------------------------------------------------------------------------
 
-// deterministic policy action a = tanh(mean) (policies.py:286-288); one
-// thread per (row, action dim), y-dimension = segment
-__global__ void __launch_bounds__(256) det_action_kernel(DetActionArgs p) {
-  const int Da = p.act_dim;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= p.B * Da) return;
-  const int r = idx / Da, j = idx % Da;
-  const int g = blockIdx.y;
-  p.act[g][idx] = tanhf(p.head[g][(long)r * 2 * Da + j]);
-}
-
 // TD targets and the critic gradient (gaussian_trainer.py:199-242 with the
 // share_layers branch 205-237):
 //   std_target = (1-d)*gamma*exp(tq1)   [soft update: p*next + (1-p)*std]
@@ -409,10 +398,6 @@ __global__ void __launch_bounds__(256) det_head_backward_kernel(DetHeadBwdArgs p
   dh[Da + j] = 0.f;
 }
 
-hipError_t launch_det_action(const DetActionArgs& a, hipStream_t s) {
-  OAC_LAUNCH(det_action_kernel, dim3((a.B * a.act_dim + 255) / 256, a.nseg), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
 hipError_t launch_gauss_targets(const GaussTargetArgs& a, hipStream_t s) {
   OAC_LAUNCH(gauss_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
