@@ -231,6 +231,12 @@ int64_t oac_expl_workspace_floats_batch(int n_obs, int obs_dim, int act_dim, int
 int oac_expl_create_batch(int n_obs, int obs_dim, int act_dim, int hidden, const float* policy,
                           const float* q1, const float* q2, float* workspace, void* step_state,
                           uint64_t seed, oac_expl** out);
+/* one critic with K heads (share_layers, K in [2, 16]): Q_UB = mean_k Q_k + beta_UB std_k Q_k
+ * (unbiased std; optimistic_exploration.py:48-58, the except branch taken when qfs has
+ * one shared-layer critic); q points at its block in a K-head critic layout */
+int oac_expl_create_shared(int n_obs, int obs_dim, int act_dim, int hidden, int K,
+                           const float* policy, const float* q, float* workspace,
+                           void* step_state, uint64_t seed, oac_expl** out);
 /* ob: device [obs_dim] fp32 (already in the workspace slot returned by
  * oac_expl_obs_slot, or any device pointer); eps: device [act_dim] or NULL
  * (Philox).  Writes action[act_dim]; optional mu_E / std / grad outputs. */

@@ -142,19 +142,22 @@ __global__ void __launch_bounds__(1024) oac_expl_fused_kernel(ExplFusedArgs a) {
 
   // ---- critics on [ob | a]
   XSTAGE(3);
-  for (int i = 0; i < 2; ++i) {
+  const int nq = a.nq, KQ = a.K;
+  float* qk = da + 64;                     // share_layers: K head values, then their seeds
+  float* wk = qk + 16;
+  for (int i = 0; i < nq; ++i) {
     const float* q = a.q[i];
     matvec(q + a.q_fc0_w, Dq, q + a.q_fc0_b, x, Dq, H, qh1 + i * H, true);
     if (i == 0) XSTAGE(10);
   }
   __syncthreads();
   XSTAGE(4);
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < nq; ++i) {
     const float* q = a.q[i];
     matvec(q + a.q_fc1_w, H, q + a.q_fc1_b, qh1 + i * H, H, H, qh2 + i * H, true);
   }
   __syncthreads();
-  {
+  if (nq == 2) {
     const int wave = t >> 6, lane = t & 63;
     if (wave < 2) {
       const float* q = a.q[wave];
@@ -163,23 +166,43 @@ __global__ void __launch_bounds__(1024) oac_expl_fused_kernel(ExplFusedArgs a) {
       s = wave_sum(s);
       if (lane == 0) misc[wave] = s + q[a.q_last_b];
     }
+  } else {
+    matvec(a.q[0] + a.q_last_w, H, a.q[0] + a.q_last_b, qh2, H, KQ, qk, false);
   }
   __syncthreads();
-  if (t == 0) {   // Q_UB seeds: d|x|/dx = sign(x) (0 at 0)
-    const float d = misc[0] - misc[1];
-    const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-    const float hb = a.beta_UB / 2.f;
-    misc[2] = 0.5f + hb * sg;
-    misc[3] = 0.5f - hb * sg;
+  if (t == 0) {
+    if (nq == 2) {   // Q_UB = (Q1+Q2)/2 + beta |Q1-Q2|/2: d|x|/dx = sign(x) (0 at 0)
+      const float d = misc[0] - misc[1];
+      const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+      const float hb = a.beta_UB / 2.f;
+      misc[2] = 0.5f + hb * sg;
+      misc[3] = 0.5f - hb * sg;
+    } else {         // Q_UB = mean_k q + beta std_k q (unbiased): dQ_UB/dq_k =
+                     // 1/K + beta (q_k - mean) / ((K-1) std)
+      float sm = 0.f;
+      for (int k = 0; k < KQ; ++k) sm += qk[k];
+      const float mu = sm / (float)KQ;
+      float ss = 0.f;
+      for (int k = 0; k < KQ; ++k) ss += (qk[k] - mu) * (qk[k] - mu);
+      const float sd = sqrtf(ss / (float)(KQ - 1));
+      for (int k = 0; k < KQ; ++k)
+        wk[k] = 1.f / (float)KQ + a.beta_UB * ((qk[k] - mu) / ((float)(KQ - 1) * sd));
+    }
   }
   __syncthreads();
 
   XSTAGE(5);
-  // ---- dQ_UB/da: dh2_i[n] = w_i wl_i[n] [qh2_i[n] > 0] (kept in qh2),
+  // ---- dQ_UB/da: dh2_i[n] = [qh2_i[n] > 0] sum_k w_ik Wl_i[k, n] (kept in qh2),
   //      dh1_i[k] = [qh1_i[k] > 0] sum_n dh2_i[n] W1_i[n, k], da_i = dh1_i . W0_i[:, Do:]
-  for (int e = t; e < 2 * H; e += blockDim.x) {
+  for (int e = t; e < nq * H; e += blockDim.x) {
     const int i = e / H, n = e - i * H;
-    const float sv = misc[2 + i] * a.q[i][a.q_last_w + n];
+    float sv;
+    if (nq == 2) {
+      sv = misc[2 + i] * a.q[i][a.q_last_w + n];
+    } else {
+      sv = 0.f;
+      for (int k = 0; k < KQ; ++k) sv = fmaf(wk[k], a.q[0][a.q_last_w + (long)k * H + n], sv);
+    }
     qh2[e] = qh2[e] > 0.f ? sv : 0.f;
   }
   __syncthreads();
@@ -190,7 +213,7 @@ __global__ void __launch_bounds__(1024) oac_expl_fused_kernel(ExplFusedArgs a) {
     float* part = misc + 72;                // [P][H] partials
     const int P = blockDim.x / H >= 1 ? (int)blockDim.x / H : 1;
     const int rows = (H + P - 1) / P;
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < nq; ++i) {
       const float* W1 = a.q[i] + a.q_fc1_w;
       const float* g = qh2 + i * H;
       for (int e = t; e < P * H; e += blockDim.x) {
@@ -219,7 +242,7 @@ __global__ void __launch_bounds__(1024) oac_expl_fused_kernel(ExplFusedArgs a) {
   XSTAGE(6);
   {
     const int lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
-    for (int o = wave; o < 2 * Da; o += nw) {
+    for (int o = wave; o < nq * Da; o += nw) {
       const int i = o / Da, j = o - i * Da;
       const float* W0 = a.q[i] + a.q_fc0_w + Do + j;
       float s = 0.f;
@@ -236,7 +259,7 @@ __global__ void __launch_bounds__(1024) oac_expl_fused_kernel(ExplFusedArgs a) {
   float* red = misc + 8;
   if (t < Da) {
     const float act = x[Do + t];
-    g = (da[t] + da[64 + t]) * (1.f - act * act);
+    g = (nq == 2 ? da[t] + da[64 + t] : da[t]) * (1.f - act * act);
     sd = expf(fminf(fmaxf(head[Da + t], -20.f), 2.f));
     sig = sd * sd;
     mean = head[t];

@@ -26,6 +26,7 @@ static inline int64_t a64(int64_t x) { return (x + 63) & ~int64_t(63); }
 
 struct ExplPlan {
   int Do, Da, H, N = 1;
+  int K = 1;   // critic heads: 1 with twin critics (q1, q2); K with one shared-layer critic (q2 null)
   const float* pol; const float* q1; const float* q2;
   float* ws;
   StepState* state;
@@ -72,6 +73,7 @@ static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta,
   a.q_fc0_w = L.q_fc0_w; a.q_fc0_b = L.q_fc0_b; a.q_fc1_w = L.q_fc1_w; a.q_fc1_b = L.q_fc1_b;
   a.q_last_w = L.q_last_w; a.q_last_b = L.q_last_b;
   a.Do = Do; a.Da = Da; a.H = p.H; a.n = N;
+  a.nq = p.q2 ? 2 : 1; a.K = p.K;
   a.eps = eps; a.out = w + p.o_out; a.grad = w + p.o_grad;
   a.state = p.state; a.ticket = reinterpret_cast<unsigned*>(w + p.o_cnt);
   a.seed = p.seed; a.beta_UB = beta; a.sqrt_2delta = (float)std::sqrt(2.0 * (double)delta);
@@ -131,6 +133,28 @@ int oac_expl_create_batch(int n_obs, int obs_dim, int act_dim, int hidden, const
   if (oac_sac_query_layout(&c, &p.L)) { delete h; return 1; }
   expl_layout(p);
   *out = h;
+  return 0;
+}
+
+int oac_expl_create_shared(int n_obs, int obs_dim, int act_dim, int hidden, int K,
+                           const float* policy, const float* q, float* workspace,
+                           void* step_state, uint64_t seed, oac_expl** out) {
+  if (!q) { set_error("oac_expl_create_shared: null critic"); return 1; }
+  if (K < 2 || K > 16) { set_error("shared-layer critic: 2 <= K <= 16 heads"); return 1; }
+  // the twin-critic constructor with the second critic absent, then the heads
+  if (oac_expl_create_batch(n_obs, obs_dim, act_dim, hidden, policy, q, q, workspace, step_state,
+                            seed, out))
+    return 1;
+  ExplPlan& p = (*out)->p;
+  p.q2 = nullptr;
+  p.K = K;
+  oac_sac_config c;
+  std::memset(&c, 0, sizeof(c));
+  c.kind = OAC_KIND_PARTICLE; c.obs_dim = obs_dim; c.act_dim = act_dim; c.hidden = hidden;
+  c.q_out = K; c.batch = 1; c.row_stride = ((2 * obs_dim + act_dim + 2 + 3) / 4) * 4;
+  c.off_obs = 0; c.off_act = obs_dim; c.off_rew = obs_dim + act_dim; c.off_term = c.off_rew + 1;
+  c.off_next_obs = c.off_term + 1; c.gemm_cfg = 0; c.world_size = 1;
+  if (oac_sac_query_layout(&c, &p.L)) { oac_expl_destroy(*out); *out = nullptr; return 1; }
   return 0;
 }
 

@@ -109,6 +109,9 @@ struct ExplFusedArgs {                  // expl_fused.hip: one workgroup per obs
   long p_fc0_w, p_fc0_b, p_fc1_w, p_fc1_b, p_head_w, p_head_b;
   long q_fc0_w, q_fc0_b, q_fc1_w, q_fc1_b, q_last_w, q_last_b;
   int Do, Da, H, n;
+  int nq, K;                            // nq = 2, K = 1: twin critics (Q_UB = mean + beta |Q1-Q2|/2);
+                                        // nq = 1, K > 1: one critic with K heads (share_layers:
+                                        // Q_UB = mean_k + beta std_k, optimistic_exploration.py:48-58)
   const float* eps;                     // [N, Da] or null -> Philox (counter expl_counter)
   float* out;                           // [3][N][Da]: action | mu_E | std
   float* grad;                          // [N, Da] dQ_UB/dmu_T or null

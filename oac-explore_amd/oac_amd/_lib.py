@@ -121,6 +121,10 @@ _SIGS = {
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
                                              ctypes.POINTER(ctypes.c_void_p)]),
+    "oac_expl_create_shared": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                              ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "oac_expl_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "oac_expl_obs_slot": (ctypes.c_void_p, [ctypes.c_void_p]),
     "oac_expl_action": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,

@@ -1,6 +1,8 @@
 """Drop-in ``get_optimistic_exploration_action``
 (/root/reference/optimistic_exploration.py:7-11) -- the OAC action shift,
-computed by liboac_amd's batch-1 kernel sequence (csrc/expl_plan.hip).
+computed by liboac_amd in one launch (csrc/expl_plan.hip, expl_fused.hip), for
+twin critics (SACTrainer) or one shared-layer critic with K heads
+(ParticleTrainerOAC, share_layers: Q_UB = mean_k + beta_UB std_k).
 
 Same signature and return value as the reference: ``(action float32[Da], {})``
 for a 1-D observation.  ``get_optimistic_exploration_actions`` is the
@@ -16,15 +18,27 @@ from . import _lib
 from ._lib import check, ptr, stream_ptr
 
 
-def _owner(policy, qfs, trainer):
+def _owner(policy, qfs, trainer, hyper_params):
+    """The oac_amd trainer whose arena holds ``policy`` and ``qfs``.  Twin
+    critics take the try branch of optimistic_exploration.py:40-46 whatever
+    share_layers says; one shared-layer critic with K heads takes the except
+    branch (:47-56), which only works with share_layers=True."""
     t = getattr(policy, "oac_trainer", None)
     if t is None:
         raise TypeError("get_optimistic_exploration_action: policy is not an oac_amd policy "
-                        "(build the trainer with oac_amd.SACTrainer)")
-    if qfs is not None and (len(qfs) != 2 or qfs[0] is not t.qf1 or qfs[1] is not t.qf2):
-        raise NotImplementedError("oac_amd implements the two-critic (trainer.qfs) OAC shift")
-    if trainer is not None and trainer is not t:
-        raise NotImplementedError("trainer_UB must be the trainer that owns the policy")
+                        "(build the trainer with oac_amd.SACTrainer / ParticleTrainerOAC)")
+    if qfs is not None and (len(qfs) != len(t.qfs) or any(a is not b for a, b in zip(qfs, t.qfs))):
+        raise NotImplementedError("qfs must be the critics of the trainer that owns the policy")
+    twin = t.layout.q2_base >= 0
+    if trainer is not None:
+        if trainer is not t:
+            raise NotImplementedError("trainer_UB must be the trainer that owns the policy")
+        if not twin:
+            raise NotImplementedError("trainer_UB with a particle trainer (sorted-particle upper "
+                                      "bound, particle_trainer_oac.py:147-167) is not implemented")
+    if not twin and not hyper_params.get("share_layers", False):
+        raise ValueError("one critic with K heads needs hyper_params['share_layers'] = True "
+                         "(the reference's except branch fails without it)")
     return t
 
 
@@ -41,9 +55,7 @@ def get_optimistic_exploration_action(ob_np, policy=None, qfs=None, trainer=None
         raise NotImplementedError("the deterministic OAC variant is unreachable from rollout() "
                                   "(SURVEY 8a quirk Q7) and not implemented")
     assert np.ndim(ob_np) == 1
-    t = _owner(policy, qfs, trainer)
-    if hyper_params.get("share_layers", False):
-        raise NotImplementedError("share_layers OAC shift: use oac_amd.ParticleTrainer")
+    t = _owner(policy, qfs, trainer, hyper_params)
     a, info = _actions(t, np.asarray(ob_np)[None, :], hyper_params,
                        None if eps is None else np.asarray(eps, np.float32)[None, :], return_info)
     return a[0], {k: v[0] for k, v in info.items()}
@@ -56,9 +68,7 @@ def get_optimistic_exploration_actions(obs_np, policy=None, qfs=None, trainer=No
     Philox draws of a call use one counter value (row r takes elements
     r*Da .. r*Da+Da-1 of the stream); ``eps`` [N, Da] replaces them."""
     assert np.ndim(obs_np) == 2
-    t = _owner(policy, qfs, trainer)
-    if hyper_params.get("share_layers", False):
-        raise NotImplementedError("share_layers OAC shift: use oac_amd.ParticleTrainer")
+    t = _owner(policy, qfs, trainer, hyper_params)
     return _actions(t, np.asarray(obs_np), hyper_params,
                     None if eps is None else np.asarray(eps, np.float32), return_info)
 

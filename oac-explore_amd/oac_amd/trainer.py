@@ -343,6 +343,42 @@ class _ArenaTrainer(object):
                           count_state=count_state)
         self._run(plan, flags, n_steps=n_steps)
 
+    def _expl_handle(self, n=1):
+        """Exploration plan for n observations per call (cached per n): the
+        liboac_amd handle, its workspace, a device eps slot [n, act_dim]
+        (parity runs), and pinned host staging -- observation rows
+        [n, obs_dim + act_dim] and results [3, n, act_dim] (action | mu_E |
+        std) -- that the call's graph uploads / downloads itself."""
+        if self._expl is None:
+            self._expl = {}
+        if n not in self._expl:
+            L = _lib.lib()
+            nf = L.oac_expl_workspace_floats_batch(n, self.obs_dim, self.act_dim, self.hidden)
+            ws = torch.zeros(int(nf), dtype=torch.float32, device=self.device)
+            eps = torch.zeros(n, self.act_dim, dtype=torch.float32, device=self.device)
+            h = ctypes.c_void_p()
+            p = self.params
+            q1 = ctypes.c_void_p(p.data_ptr() + 4 * self.layout.q1_base)
+            if self.layout.q2_base >= 0:     # twin critics
+                check(L.oac_expl_create_batch(n, self.obs_dim, self.act_dim, self.hidden, ptr(p),
+                                              q1,
+                                              ctypes.c_void_p(p.data_ptr() + 4 * self.layout.q2_base),
+                                              ptr(ws), ptr(self.step_state),
+                                              ctypes.c_uint64(self.seed + 1), ctypes.byref(h)))
+            else:                            # one shared-layer critic with K heads
+                check(L.oac_expl_create_shared(n, self.obs_dim, self.act_dim, self.hidden,
+                                               self._q_out, ptr(p), q1, ptr(ws),
+                                               ptr(self.step_state),
+                                               ctypes.c_uint64(self.seed + 1), ctypes.byref(h)))
+            obs_pin = torch.zeros(n, self.obs_dim + self.act_dim, dtype=torch.float32,
+                                  pin_memory=True)
+            out_pin = torch.zeros(3, n, self.act_dim, dtype=torch.float32, pin_memory=True)
+            check(L.oac_expl_set_host_io(h, ctypes.c_void_p(obs_pin.data_ptr()),
+                                         ctypes.c_void_p(out_pin.data_ptr())))
+            self._expl[n] = _ExplHandle(h, ws, eps, obs_pin, out_pin)
+        return self._expl[n]
+
+
 class SACTrainer(_ArenaTrainer):
     """SACTrainer (trainer/trainer.py:14) on liboac_amd."""
 
@@ -501,30 +537,3 @@ class SACTrainer(_ArenaTrainer):
         self.step_state[0] = self._n_train_steps_total
 
     # ------------------------------------------------------------ exploration
-    def _expl_handle(self, n=1):
-        """Exploration plan for n observations per call (cached per n): the
-        liboac_amd handle, its workspace, a device eps slot [n, act_dim]
-        (parity runs), and pinned host staging -- observation rows
-        [n, obs_dim + act_dim] and results [3, n, act_dim] (action | mu_E |
-        std) -- that the call's graph uploads / downloads itself."""
-        if self._expl is None:
-            self._expl = {}
-        if n not in self._expl:
-            L = _lib.lib()
-            nf = L.oac_expl_workspace_floats_batch(n, self.obs_dim, self.act_dim, self.hidden)
-            ws = torch.zeros(int(nf), dtype=torch.float32, device=self.device)
-            eps = torch.zeros(n, self.act_dim, dtype=torch.float32, device=self.device)
-            h = ctypes.c_void_p()
-            p = self.params
-            check(L.oac_expl_create_batch(n, self.obs_dim, self.act_dim, self.hidden, ptr(p),
-                                          ctypes.c_void_p(p.data_ptr() + 4 * self.layout.q1_base),
-                                          ctypes.c_void_p(p.data_ptr() + 4 * self.layout.q2_base),
-                                          ptr(ws), ptr(self.step_state),
-                                          ctypes.c_uint64(self.seed + 1), ctypes.byref(h)))
-            obs_pin = torch.zeros(n, self.obs_dim + self.act_dim, dtype=torch.float32,
-                                  pin_memory=True)
-            out_pin = torch.zeros(3, n, self.act_dim, dtype=torch.float32, pin_memory=True)
-            check(L.oac_expl_set_host_io(h, ctypes.c_void_p(obs_pin.data_ptr()),
-                                         ctypes.c_void_p(out_pin.data_ptr())))
-            self._expl[n] = _ExplHandle(h, ws, eps, obs_pin, out_pin)
-        return self._expl[n]

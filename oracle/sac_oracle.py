@@ -727,3 +727,32 @@ def oac_exploration_action(ob_np, P, Q1, Q2, beta_UB, delta, eps_discard, eps,
     mu_E = mu_T + mu_C                                         # :87
     action = torch.tanh(_t(eps, dtype) * std + mu_E)           # TanhNormal(mu_E,std).sample() :92-94
     return dict(action=action, mu_E=mu_E, std=std, grad=grad, mu_T=mu_T)
+
+
+def oac_exploration_action_shared(ob_np, P, Q, beta_UB, delta, eps_discard, eps,
+                                  dtype=torch.float32):
+    """The same action with ONE shared-layer critic of K heads (share_layers=True,
+    qfs = [qf]): qfs[1] raises, so the except branch of
+    optimistic_exploration.py:47-56 takes mu_Q = mean_k Q_k, sigma_Q = std_k Q_k
+    (unbiased), Q_UB = mu_Q + beta_UB sigma_Q;
+    dQ_UB/dQ_k = 1/K + beta_UB (Q_k - mu_Q) / ((K-1) sigma_Q)."""
+    assert np.ndim(ob_np) == 1
+    ob = _t(np.asarray(ob_np), dtype)[None]
+    pf = policy_forward(ob, P, _t(eps_discard, dtype)[None])
+    mu_T, std = pf["mean"][0], pf["std"][0]
+    a = torch.tanh(mu_T)
+    c = q_forward(ob, a[None], Q)
+    q = c["q"][0]                                              # [K]
+    K = q.shape[0]
+    mu = q.mean()
+    sd = q.std()                                               # unbiased, like torch.std
+    w = 1.0 / K + beta_UB * (q - mu) / ((K - 1) * sd)
+    Do = ob.shape[1]
+    ga = q_input_grad(c, w[None], Q)[0, Do:]
+    grad = ga * (1 - a * a)
+    Sigma = torch.pow(std, 2)
+    denom = torch.sqrt(torch.sum(torch.mul(torch.pow(grad, 2), Sigma))) + 10e-6
+    mu_C = math.sqrt(2.0 * delta) * torch.mul(Sigma, grad) / denom
+    mu_E = mu_T + mu_C
+    action = torch.tanh(_t(eps, dtype) * std + mu_E)
+    return dict(action=action, mu_E=mu_E, std=std, grad=grad, mu_T=mu_T)

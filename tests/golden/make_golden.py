@@ -455,14 +455,23 @@ def gen_ptrain_all():
 
 # ------------------------------------------------------- OAC exploration
 def gen_oac_expl(name, obs_dim, act_dim, hidden, n_obs, beta_UB, delta, seed=5,
-                 pi_init_w=0.1, q_init_w=0.1, eps_seed=3):
-    pp, qp = _producers(obs_dim, act_dim, hidden)
+                 pi_init_w=0.1, q_init_w=0.1, eps_seed=3, K=None):
+    """K: one shared-layer critic with K heads (share_layers=True, the except
+    branch of optimistic_exploration.py:47-56) instead of twin critics."""
+    pp, qp = _producers(obs_dim, act_dim, hidden, q_out=K or 1)
     policy = pp()
-    qf1, qf2 = qp(), qp()
-    params = sac_params(obs_dim, act_dim, hidden, seed, pi_init_w=pi_init_w, q_init_w=q_init_w)
+    params = sac_params(obs_dim, act_dim, hidden, seed, pi_init_w=pi_init_w, q_init_w=q_init_w,
+                        q_out=K or 1,
+                        q_last_bias=None if K is None else np.linspace(0.0, 50.0, K))
     load_sd(policy, params["policy"])
+    qf1 = qp()
     load_sd(qf1, params["qf1"])
-    load_sd(qf2, params["qf2"])
+    if K is None:
+        qf2 = qp()
+        load_sd(qf2, params["qf2"])
+        qfs = [qf1, qf2]
+    else:
+        qfs = [qf1]
     rs = np.random.RandomState(seed + 100)
     obs = rs.standard_normal((n_obs, obs_dim))  # float64, like env observations
     captured = []
@@ -477,12 +486,12 @@ def gen_oac_expl(name, obs_dim, act_dim, hidden, n_obs, beta_UB, delta, seed=5,
     torch.manual_seed(eps_seed)
     out = {"obs": obs}
     acts, mu_e, stds, eps_d, eps_s = [], [], [], [], []
-    hp = dict(beta_UB=beta_UB, delta=delta, share_layers=False)
+    hp = dict(beta_UB=beta_UB, delta=delta, share_layers=K is not None)
     try:
         for i in range(n_obs):
             EPS_LOG.clear()
             captured.clear()
-            a, info = oe.get_optimistic_exploration_action(obs[i], policy=policy, qfs=[qf1, qf2],
+            a, info = oe.get_optimistic_exploration_action(obs[i], policy=policy, qfs=qfs,
                                                            trainer=None, hyper_params=hp)
             assert len(EPS_LOG) == 2 and len(captured) == 1
             eps_d.append(EPS_LOG[0])
@@ -495,7 +504,8 @@ def gen_oac_expl(name, obs_dim, act_dim, hidden, n_obs, beta_UB, delta, seed=5,
     out.update(action=np.stack(acts), mu_E=np.stack(mu_e), std=np.stack(stds),
                eps_discard=np.stack(eps_d), eps=np.stack(eps_s))
     meta = dict(kind="oac_expl", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, n_obs=n_obs,
-                beta_UB=beta_UB, delta=delta, seed=seed, pi_init_w=pi_init_w, q_init_w=q_init_w)
+                beta_UB=beta_UB, delta=delta, seed=seed, pi_init_w=pi_init_w, q_init_w=q_init_w,
+                K=K)
     return meta, out
 
 
@@ -702,6 +712,9 @@ def main():
         save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
                                       pi_init_w=0.3, counts=True))
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "oac_expl_shared":
+        gen_expl_shared()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "det_snapshot":
         gen_det_snapshot(os.path.join(HERE, "goac_snapshot.pt"), "goac")
         gen_det_snapshot(os.path.join(HERE, "ptrain_snapshot.pt"), "ptrain")
@@ -742,6 +755,14 @@ def main():
     gen_ptrain_all()
     gen_det_snapshot(os.path.join(HERE, "goac_snapshot.pt"), "goac")
     gen_det_snapshot(os.path.join(HERE, "ptrain_snapshot.pt"), "ptrain")
+    gen_expl_shared()
+
+
+def gen_expl_shared():
+    save("oac_expl_shared_ant", *gen_oac_expl("oac_expl_shared_ant", 111, 8, [256, 256], 16,
+                                              4.66, 23.53, K=10, q_init_w=0.3))
+    save("oac_expl_shared_small", *gen_oac_expl("oac_expl_shared_small", 11, 3, [32, 32], 16,
+                                                2.0, 5.0, K=4, q_init_w=0.5))
 
 
 def gen_goac_all():

@@ -187,3 +187,36 @@ def test_batched_oac_exploration_equals_single_calls(name):
                                                hyper_params=hp)
     assert np.isfinite(A2).all() and np.abs(A2).max() < 1
     assert int(tr.step_state[2].item()) == c0 + 1
+
+
+@pytest.mark.parametrize("name", ["oac_expl_shared_ant", "oac_expl_shared_small"])
+def test_oac_exploration_shared_matches_reference_golden(name):
+    """One shared-layer critic with K heads (ParticleTrainerOAC, share_layers):
+    single calls against the reference golden, the batched call bitwise equal
+    to the single calls."""
+    from oac_amd import (ParticleTrainerOAC, get_optimistic_exploration_action,
+                         get_optimistic_exploration_actions)
+    from gpu_helpers import Space, producers
+    meta, g = parity.load(name)
+    K = meta["K"]
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                        pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"], q_out=K,
+                        q_last_bias=np.linspace(0.0, 50.0, K))
+    pp, qp = producers(params, q_keys=("qf1", "qf2", "target_qf1", "target_qf2", "qf1",
+                                       "target_qf1"))
+    tr = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Space(meta["act_dim"]),
+                            deterministic=False, q_min=0.0, q_max=50.0, share_layers=True)
+    hp = dict(beta_UB=meta["beta_UB"], delta=meta["delta"], share_layers=True)
+    A, _ = get_optimistic_exploration_actions(g["obs"], policy=tr.policy, qfs=tr.qfs,
+                                              hyper_params=hp, eps=g["eps"])
+    for i in range(meta["n_obs"]):
+        a, info = get_optimistic_exploration_action(g["obs"][i], policy=tr.policy, qfs=tr.qfs,
+                                                    hyper_params=hp, eps=g["eps"][i],
+                                                    return_info=True)
+        assert parity.rel_err(info["std"], g["std"][i]) <= 1e-5
+        assert parity.rel_err(info["mu_E"], g["mu_E"][i]) <= parity.TOL
+        assert parity.rel_err(a, g["action"][i]) <= parity.TOL
+        np.testing.assert_array_equal(a, A[i])
+    with pytest.raises(ValueError):
+        get_optimistic_exploration_action(g["obs"][0], policy=tr.policy, qfs=tr.qfs,
+                                          hyper_params=dict(hp, share_layers=False))
