@@ -31,6 +31,7 @@ FLOP_PER_SAMPLE = 4_377_600        # algorithmic GEMM FLOPs per sampl
 GATHER_BYTES_PER_SAMPLE = 3_081 + 4
 ADAM_BYTES_PER_STEP = 18_142_244
 PEAK_FP32_TFLOPS = 157.3           # MI355X fp32 MFMA dense peak (MI355X_MICROARCH.md)
+LAUNCH_FLOOR_US = 5.2      # grouped-GEMM launch floor in a graph chain (tools/micro, r01)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -394,6 +395,15 @@ def main():
                          "avg_launch_us": round(gk["avg_us"], 3)},
             "step_roofline_frac": round(FLOP_PER_SAMPLE * B * value / world / 1e12
                                         / PEAK_FP32_TFLOPS, 5),
+            # the bound that actually applies at B=256: a dependent chain of
+            # launches, each costing at least the measured floor of a grouped
+            # GEMM launch in a hipGraph chain (tools/micro/floor_micro.hip:
+            # 5.2 us for 256 tiles of 32x32, K=256)
+            "latency_floor": {"launches_per_step": int(_launches(tr)),
+                              "floor_us_per_launch": LAUNCH_FLOOR_US,
+                              "floor_us_per_step": round(LAUNCH_FLOOR_US * _launches(tr), 2),
+                              "frac": round(LAUNCH_FLOOR_US * _launches(tr)
+                                            / (1e3 * ms_per_step), 4)},
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv
                             for kk, vv in v.items()} for k, v in kt.items()},
         }

@@ -76,6 +76,9 @@ typedef struct oac_sac_config {
   /* OAC_KIND_PARTICLE_UB (particle_trainer.py:61-69, 255-264) */
   int delta_index;       /* sorted particle the policy maximises */
   float rescale_spread;  /* rescale_targets_around_mean: q_max - q_min; <= 0: off */
+  /* PARTICLE, PARTICLE_UB, GAUSS: train_bias=False (networks.py:59-60: the critic's
+   * last_fc.bias has requires_grad=False, so it is never updated) */
+  int freeze_q_bias;
 } oac_sac_config;
 
 /* Flat parameter arena layout (float offsets; every tensor 16-byte aligned).

@@ -205,8 +205,12 @@ static int dphase1(SacPlan& p, int flags, hipStream_t s, bool fused) {
   {
     GemmBatch gb{};
     float* gq = grad_q(p);
-    add(gb, t_dw(p.W(G_DQ), K, K, B, p.W(G_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
-                 q_group(p), p.sp_ql));
+    GemmTask tl = t_dw(p.W(G_DQ), K, K, B, p.W(G_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
+                 q_group(p), p.sp_ql);
+    // train_bias=False: no ones column, the frozen bias keeps a zero gradient
+    // (Adam then leaves it, and its moments, exactly unchanged)
+    if (c.freeze_q_bias) { tl.N = H; tl.b_ones = 0; tl.bias_grad = nullptr; }
+    add(gb, tl);
     add(gb, t_dx(p.W(G_DQ), K, B, K, q + L.q_last_w, H, H, p.W(G_DH2Q), H, p.W(G_H2Q), H));
     if (run_gemm(p, gb, s)) return 1;
   }

@@ -180,8 +180,12 @@ static int pphase1(SacPlan& p, int flags, hipStream_t s) {
   {  // last layer: dW_last slab and dh2 = (dq . W_last) * [h2 > 0]
     GemmBatch gb{};
     float* gq = grad_q(p);
-    add(gb, t_dw(p.W(X_DQ), K, K, B, p.W(X_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
-                 q_group(p), p.sp_ql));
+    GemmTask tl = t_dw(p.W(X_DQ), K, K, B, p.W(X_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
+                 q_group(p), p.sp_ql);
+    // train_bias=False: no ones column, the frozen bias keeps a zero gradient
+    // (Adam then leaves it, and its moments, exactly unchanged)
+    if (c.freeze_q_bias) { tl.N = H; tl.b_ones = 0; tl.bias_grad = nullptr; }
+    add(gb, tl);
     add(gb, t_dx(p.W(X_DQ), K, B, K, q + L.q_last_w, H, H, p.W(X_DH2Q), H, p.W(X_H2Q), H));
     if (run_gemm(p, gb, s)) return 1;
   }

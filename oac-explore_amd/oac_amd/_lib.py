@@ -42,7 +42,7 @@ class SacConfig(ctypes.Structure):
         ("std_bound", ctypes.c_float), ("std_init", ctypes.c_float),
         ("std_soft_update", ctypes.c_int), ("std_soft_prob", ctypes.c_float),
         ("mean_update", ctypes.c_int), ("delta_index", ctypes.c_int),
-        ("rescale_spread", ctypes.c_float),
+        ("rescale_spread", ctypes.c_float), ("freeze_q_bias", ctypes.c_int),
     ]
 
 

@@ -38,17 +38,17 @@ class GaussianTrainer(_TargetPolicyTrainer):
                  device=None, seed=0, use_graph=True, gemm_cfg=-1):
         unsupported = dict(share_layers=not share_layers, deterministic=not deterministic,
                            ensemble=ensemble, global_opt=global_opt,
-                           use_target_policy=use_target_policy,
-                           train_bias=not train_bias)
+                           use_target_policy=use_target_policy)
         bad = [k for k, v in unsupported.items() if v]
         if bad:
             raise NotImplementedError(
                 "oac_amd.GaussianTrainer implements the g-oac recipe configuration "
                 "(share_layers=True, deterministic policy, counts / std_soft_update / "
-                f"mean_update, trainable bias, no ensemble / global-opt); unsupported: {bad}")
+                f"mean_update, no ensemble / global-opt); unsupported: {bad}")
         assert not counts or not std_soft_update   # gaussian_trainer.py:88
         self._common_init(device, soft_target_tau, target_update_period, deterministic,
                           discount, reward_scale, policy_lr, qf_lr, use_graph, seed, gemm_cfg)
+        self.train_bias = train_bias
         self.std_lr = std_lr
         # gaussian_trainer.py:65-86
         self.action_space = action_space

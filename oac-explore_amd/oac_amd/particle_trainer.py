@@ -37,17 +37,18 @@ class ParticleTrainer(_TargetPolicyTrainer):
                  device=None, seed=0, use_graph=True, gemm_cfg=-1):
         unsupported = dict(share_layers=not share_layers, deterministic=not deterministic,
                            ensemble=ensemble, global_opt=global_opt,
-                           use_target_policy=use_target_policy, train_bias=not train_bias)
+                           use_target_policy=use_target_policy)
         bad = [k for k, v in unsupported.items() if v]
         if bad:
             raise NotImplementedError(
                 "oac_amd.ParticleTrainer implements the p-oac recipe configuration "
                 "(share_layers=True, deterministic policy, counts / std_soft_update / "
-                "mean_update / rescale_targets_around_mean, trainable bias, no ensemble / "
+                "mean_update / rescale_targets_around_mean / train_bias, no ensemble / "
                 f"global-opt / DDPG target network); unsupported: {bad}")
         assert not counts or not std_soft_update   # particle_trainer.py:92
         self._common_init(device, soft_target_tau, target_update_period, deterministic,
                           discount, reward_scale, policy_lr, qf_lr, use_graph, seed, gemm_cfg)
+        self.train_bias = train_bias
         # quantile bookkeeping, particle_trainer.py:61-69 (delta_index uses p - 1
         # when the quantile grid steps over delta)
         quantiles = [i * 1. / (n_estimators - 1) for i in range(n_estimators)]

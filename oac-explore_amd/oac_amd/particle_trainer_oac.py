@@ -36,15 +36,15 @@ class ParticleTrainer(_ArenaTrainer):
                  device=None, seed=0, use_graph=True, gemm_cfg=-1):
         unsupported = dict(share_layers=not share_layers, deterministic=deterministic,
                            ensemble=ensemble, mellow_max=mellow_max,
-                           global_opt=global_opt, std_soft_update=std_soft_update,
-                           train_bias=not train_bias)
+                           global_opt=global_opt, std_soft_update=std_soft_update)
         bad = [k for k, v in unsupported.items() if v]
         if bad:
             raise NotImplementedError(
                 "oac_amd.ParticleTrainerOAC implements the P-OAC configuration "
                 "(share_layers=True, stochastic policy, counts, no mellow-max / global-opt / "
-                f"std-soft-update, trainable bias); unsupported: {bad}")
+                f"std-soft-update); unsupported: {bad}")
         assert not counts or not std_soft_update   # particle_trainer_oac.py:97
+        self.train_bias = train_bias
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
         self.use_automatic_entropy_tuning = use_automatic_entropy_tuning
@@ -104,14 +104,23 @@ class ParticleTrainer(_ArenaTrainer):
                                               tw(self.adam_m, self.policy),
                                               tw(self.adam_v, self.policy), policy_lr,
                                               (0.9, 0.999), 1e-8)
+        # train_bias=False: the frozen critic bias has no optimizer state
+        q_no_grad = [] if train_bias else \
+            [i for i, (n, _) in enumerate(qf.named_parameters()) if n == "last_fc.bias"]
         self.qf_optimizers = [AdamStateView(self, list(qf.parameters()), tw(self.adam_m, qf),
-                                            tw(self.adam_v, qf), qf_lr, (0.9, 0.999), 1e-8)]
+                                            tw(self.adam_v, qf), qf_lr, (0.9, 0.999), 1e-8,
+                                            no_grad=q_no_grad)]
         self.alpha_optimizer = AdamStateView(self, [self.log_alpha], [self.alpha_state[1:2]],
                                              [self.alpha_state[2:3]], policy_lr, (0.9, 0.999),
                                              1e-8)
         self.eval_statistics = OrderedDict()
         self._n_train_steps_total = 0
         self._need_to_update_eval_statistics = True
+
+    def _make_cfg(self, batch):
+        c = super()._make_cfg(batch)
+        c.freeze_q_bias = int(not self.train_bias)
+        return c
 
     # ------------------------------------------------------------ diagnostics
     def _fill_eval_statistics(self, plan):

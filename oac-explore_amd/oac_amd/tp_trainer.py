@@ -63,8 +63,11 @@ class _TargetPolicyTrainer(_ArenaTrainer):
                                  no_grad=no_grad)
         self.policy_optimizer = popt(self.policy)
         self.target_policy_optimizer = popt(self.target_policy)
+        q_no_grad = [] if self.train_bias else \
+            [i for i, (n, _) in enumerate(qf.named_parameters()) if n == "last_fc.bias"]
         self.qf_optimizers = [AdamStateView(self, list(qf.parameters()), tw(self.adam_m, qf),
-                                            tw(self.adam_v, qf), qf_lr, (0.9, 0.999), 1e-8)]
+                                            tw(self.adam_v, qf), qf_lr, (0.9, 0.999), 1e-8,
+                                            no_grad=q_no_grad)]
         # SACTrainer's alpha (snapshot keys only)
         self.alpha_optimizer = AdamStateView(self, [self.log_alpha], [self.alpha_state[1:2]],
                                              [self.alpha_state[2:3]], policy_lr, (0.9, 0.999),
@@ -78,6 +81,7 @@ class _TargetPolicyTrainer(_ArenaTrainer):
         c.std_soft_update = int(bool(self.std_soft_update))
         c.std_soft_prob = float(self.std_soft_update_prob)
         c.mean_update = int(bool(self.mean_update))
+        c.freeze_q_bias = int(not self.train_bias)
         return c
 
     @staticmethod

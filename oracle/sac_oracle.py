@@ -390,8 +390,9 @@ class ParticleOACOracle:
 
     def __init__(self, params, obs_dim, act_dim, K, discount=0.99, reward_scale=1.0,
                  policy_lr=3e-4, qf_lr=3e-4, tau=5e-3, target_update_period=1,
-                 target_entropy=None, dtype=torch.float32):
+                 target_entropy=None, train_bias=True, dtype=torch.float32):
         self.dtype = dtype
+        self.train_bias = train_bias
         self.Do, self.Da, self.K = obs_dim, act_dim, K
         self.P = to_torch_params(params["policy"], dtype)
         self.Q = to_torch_params(params["qf1"], dtype)
@@ -429,6 +430,8 @@ class ParticleOACOracle:
         d_sorted = 2.0 * (sorted_qs - y) / B
         dq = torch.zeros_like(qs).scatter_(0, qs_idx, d_sorted).t()   # sort backward
         gq = q_param_grads(c, dq, self.Q)
+        if not self.train_bias:                              # frozen last bias (networks.py:59-60)
+            gq["last_fc.bias"] = torch.zeros_like(gq["last_fc.bias"])
         self.opt_q.step(gq)                                  # 252-256
         pf = policy_forward(obs, self.P, eps2)               # 271-273
         w = pf["logp"] + self.target_entropy                 # 274-281
@@ -483,9 +486,10 @@ class GaussianOACOracle:
     def __init__(self, params, obs_dim, act_dim, delta=0.95, q_min=0.0, q_max=100.0,
                  discount=0.99, reward_scale=1.0, policy_lr=3e-4, qf_lr=3e-4, tau=5e-3,
                  target_update_period=1, std_soft_update_prob=None, mean_update=False,
-                 dtype=torch.float32):
+                 train_bias=True, dtype=torch.float32):
         from scipy.stats import norm
         self.mean_update = mean_update
+        self.train_bias = train_bias
         self.dtype = dtype
         self.Do, self.Da = obs_dim, act_dim
         self.P = to_torch_params(params["policy"], dtype)
@@ -561,6 +565,8 @@ class GaussianOACOracle:
         dq = torch.cat([2.0 * (S["q_preds"] - S["q_target"]) / B,
                         2.0 * (S["std_preds"] - S["std_target"]) / B * S["std_preds"]], dim=1)
         S["gq"] = q_param_grads(S["c"], dq, self.Q)
+        if not self.train_bias:                              # frozen last bias (networks.py:59-60)
+            S["gq"]["last_fc.bias"] = torch.zeros_like(S["gq"]["last_fc.bias"])
         self.crit_flat = self._flat(S["gq"], list(self.Q))
 
     def phase2(self, world=1):
@@ -609,12 +615,12 @@ class ParticleUBOracle(GaussianOACOracle):
     def __init__(self, params, obs_dim, act_dim, K, delta_index, q_min=0.0, q_max=100.0,
                  discount=0.99, reward_scale=1.0, policy_lr=1e-3, qf_lr=1e-3, tau=5e-3,
                  target_update_period=1, std_soft_update_prob=None, mean_update=False,
-                 rescale=False, dtype=torch.float32):
+                 rescale=False, train_bias=True, dtype=torch.float32):
         super().__init__(params, obs_dim, act_dim, q_min=q_min, q_max=q_max, discount=discount,
                          reward_scale=reward_scale, policy_lr=policy_lr, qf_lr=qf_lr, tau=tau,
                          target_update_period=target_update_period,
                          std_soft_update_prob=std_soft_update_prob, mean_update=mean_update,
-                         dtype=dtype)
+                         train_bias=train_bias, dtype=dtype)
         self.K, self.delta_index = K, delta_index
         self.spread = (q_max - q_min) if rescale else None
 
@@ -661,6 +667,8 @@ class ParticleUBOracle(GaussianOACOracle):
     def phase1(self, world=1):
         S = self.S
         S["gq"] = q_param_grads(S["c"], S["dq"], self.Q)
+        if not self.train_bias:
+            S["gq"]["last_fc.bias"] = torch.zeros_like(S["gq"]["last_fc.bias"])
         self.crit_flat = self._flat(S["gq"], list(self.Q))
 
     def phase2(self, world=1):

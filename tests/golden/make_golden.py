@@ -254,7 +254,7 @@ def gen_sac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=7,
 # ------------------------------------------------------------- P-OAC runs
 def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=11,
              delta=0.95, q_min=0.0, q_max=500.0, discount=0.99, lr=3e-4, tau=5e-3,
-             idx_seed=1, eps_seed=2, pi_init_w=1e-3, counts=False):
+             idx_seed=1, eps_seed=2, pi_init_w=1e-3, counts=False, train_bias=True):
     pp, qp = _producers(obs_dim, act_dim, hidden, q_out=K)
     torch.manual_seed(0)
     tr = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Box(-1, 1, (act_dim,)),
@@ -262,7 +262,8 @@ def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=1
                             policy_lr=lr, qf_lr=lr, optimizer_class=Adam14,
                             soft_target_tau=tau, target_update_period=1,
                             use_automatic_entropy_tuning=True, deterministic=False,
-                            q_min=q_min, q_max=q_max, share_layers=True, counts=counts)
+                            q_min=q_min, q_max=q_max, share_layers=True, counts=counts,
+                            train_bias=train_bias)
     bias = np.linspace(q_min, q_max, K)
     crs = np.random.RandomState(77)   # batch counts (ReplayBufferCount's 'counts' key)
     params = sac_params(obs_dim, act_dim, hidden, seed, q_out=K, q_last_bias=bias,
@@ -278,7 +279,7 @@ def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=1
                 steps=steps, n_replay=n_replay, seed=seed, delta=delta, q_min=q_min,
                 q_max=q_max, discount=discount, lr=lr, tau=tau, idx_seed=idx_seed,
                 eps_seed=eps_seed, delta_index=int(tr.delta_index), pi_init_w=pi_init_w,
-                target_entropy=-float(act_dim), counts=counts)
+                target_entropy=-float(act_dim), counts=counts, train_bias=train_bias)
     for s in range(steps):
         EPS_LOG.clear()
         batch, idx = _record_batch(rb, B)
@@ -295,9 +296,12 @@ def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=1
         out[f"s{s}/eps2"] = EPS_LOG[1]   # drawn by policy(obs) (line 271)
         for k, v in tr.get_diagnostics().items():
             out[f"s{s}/stat/{k}"] = np.array(v, np.float64)
-        for gname, opt, order in (("policy", tr.policy_optimizer, PARAM_ORDER_POLICY),
-                                  ("qf", tr.qf_optimizers[0], PARAM_ORDER_Q)):
+        for gname, opt, order, mod in (("policy", tr.policy_optimizer, PARAM_ORDER_POLICY,
+                                        tr.policy),
+                                       ("qf", tr.qf_optimizers[0], PARAM_ORDER_Q, tr.qfs[0])):
             for pname, g in zip(order, opt.recorded[-1]):
+                if g is None:   # frozen (train_bias=False)
+                    g = torch.zeros_like(mod.state_dict()[pname])
                 pack(out, f"s{s}/grad/{gname}/{pname}", g.numpy(), full)
         out[f"s{s}/grad/log_alpha"] = tr.alpha_optimizer.recorded[-1][0].numpy()
         out[f"s{s}/post/log_alpha"] = tr.log_alpha.detach().numpy().copy()
@@ -310,7 +314,7 @@ def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=1
 # ------------------------------------------------------------- g-oac runs
 def gen_goac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=13, delta=0.95,
              r_min=0.0, r_max=5.0, discount=0.99, lr=3e-4, tau=5e-3, idx_seed=1,
-             pi_init_w=1e-3, q_init_w=3e-3, counts=False, soft=None):
+             pi_init_w=1e-3, q_init_w=3e-3, counts=False, soft=None, train_bias=True):
     """GaussianTrainer (g-oac) as reproduce_g-oac*.sh builds it: share_layers,
     deterministic policy (main.py:219-233), q_min/q_max = r_min/r_max / (1 -
     discount); ``soft``: std_soft_update with that probability.  Parameters
@@ -324,7 +328,8 @@ def gen_goac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=13, 
                          qf_lr=lr, optimizer_class=Adam14, soft_target_tau=tau,
                          target_update_period=1, q_min=q_min, q_max=q_max, share_layers=True,
                          counts=counts, std_soft_update=soft is not None,
-                         std_soft_update_prob=0.0 if soft is None else soft)
+                         std_soft_update_prob=0.0 if soft is None else soft,
+                         train_bias=train_bias)
     assert tr.deterministic
     params = goac_params(obs_dim, act_dim, hidden, seed, q_min, q_max, pi_init_w=pi_init_w,
                          q_init_w=q_init_w)
@@ -339,7 +344,7 @@ def gen_goac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=13, 
     meta = dict(kind="goac", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, B=B, steps=steps,
                 n_replay=n_replay, seed=seed, delta=delta, q_min=q_min, q_max=q_max,
                 discount=discount, lr=lr, tau=tau, idx_seed=idx_seed, pi_init_w=pi_init_w,
-                q_init_w=q_init_w, counts=counts, soft=soft,
+                q_init_w=q_init_w, counts=counts, soft=soft, train_bias=train_bias,
                 standard_bound=float(tr.standard_bound), std_init=float(tr.std_init))
     for s in range(steps):
         EPS_LOG.clear()
@@ -375,7 +380,7 @@ def gen_goac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=13, 
 def gen_ptrain(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=17, delta=0.95,
                r_min=0.0, r_max=5.0, discount=0.99, lr=3e-4, tau=5e-3, idx_seed=1,
                pi_init_w=1e-3, q_init_w=3e-3, counts=False, soft=None, mean_update=False,
-               rescale=False, q_range=None):
+               rescale=False, q_range=None, train_bias=True):
     """ParticleTrainer (trainer/particle_trainer.py) as main.py builds it for
     --alg p-oac without --beta_UB (main.py:198-218): share_layers,
     deterministic policy, q_min/q_max = r_min/r_max / (1 - discount) (or
@@ -391,7 +396,7 @@ def gen_ptrain(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed
                          share_layers=True, counts=counts, mean_update=mean_update,
                          std_soft_update=soft is not None,
                          std_soft_update_prob=0.0 if soft is None else soft,
-                         rescale_targets_around_mean=rescale)
+                         rescale_targets_around_mean=rescale, train_bias=train_bias)
     params = ptrain_params(obs_dim, act_dim, hidden, seed, K, q_min, q_max, pi_init_w=pi_init_w,
                            q_init_w=q_init_w)
     load_sd(tr.policy, params["policy"])
@@ -406,7 +411,8 @@ def gen_ptrain(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed
                 steps=steps, n_replay=n_replay, seed=seed, delta=delta, q_min=q_min,
                 q_max=q_max, discount=discount, lr=lr, tau=tau, idx_seed=idx_seed,
                 pi_init_w=pi_init_w, q_init_w=q_init_w, counts=counts, soft=soft,
-                mean_update=mean_update, rescale=rescale, delta_index=int(tr.delta_index))
+                mean_update=mean_update, rescale=rescale, delta_index=int(tr.delta_index),
+                train_bias=train_bias)
     for s in range(steps):
         EPS_LOG.clear()
         batch, idx = _record_batch(rb, B)
@@ -712,6 +718,9 @@ def main():
         save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
                                       pi_init_w=0.3, counts=True))
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "nobias":
+        gen_nobias()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "oac_expl_shared":
         gen_expl_shared()
         return
@@ -756,6 +765,17 @@ def main():
     gen_det_snapshot(os.path.join(HERE, "goac_snapshot.pt"), "goac")
     gen_det_snapshot(os.path.join(HERE, "ptrain_snapshot.pt"), "ptrain")
     gen_expl_shared()
+    gen_nobias()
+
+
+def gen_nobias():
+    """train_bias=False (--no_train_bias): the critics' last-layer bias is frozen."""
+    save("poac_nobias", *gen_poac("poac_nobias", 11, 3, [16, 16], 5, 16, 3, 200, True,
+                                  pi_init_w=0.3, train_bias=False))
+    save("goac_nobias", *gen_goac("goac_nobias", 11, 3, [16, 16], 16, 3, 200, True,
+                                  pi_init_w=0.5, q_init_w=0.5, train_bias=False, counts=True))
+    save("ptrain_nobias", *gen_ptrain("ptrain_nobias", 11, 3, [16, 16], 5, 16, 3, 200, True,
+                                      pi_init_w=0.5, q_init_w=0.5, train_bias=False, counts=True))
 
 
 def gen_expl_shared():

@@ -12,7 +12,7 @@ from gpu_helpers import Space, StateDictModule, batch_from, module_tensors
 
 pytestmark = pytest.mark.gpu
 
-FIXTURES = ["goac_small", "goac_counts", "goac_soft", "goac_humanoid"]
+FIXTURES = ["goac_small", "goac_counts", "goac_soft", "goac_humanoid", "goac_nobias"]
 
 
 def goac_producers(params):
@@ -39,7 +39,8 @@ def goac_trainer_for(meta, params=None, **kw):
                            target_update_period=1, q_min=meta["q_min"], q_max=meta["q_max"],
                            share_layers=True, counts=bool(meta.get("counts")),
                            std_soft_update=soft is not None,
-                           std_soft_update_prob=0.0 if soft is None else soft, **kw)
+                           std_soft_update_prob=0.0 if soft is None else soft,
+                           train_bias=meta.get("train_bias", True), **kw)
 
 
 @pytest.mark.parametrize("name", FIXTURES)

@@ -24,10 +24,10 @@ def particle_trainer_for(meta, **kw):
                            policy_lr=meta["lr"], qf_lr=meta["lr"], soft_target_tau=meta["tau"],
                            target_update_period=1, use_automatic_entropy_tuning=True,
                            deterministic=False, q_min=meta["q_min"], q_max=meta["q_max"],
-                           share_layers=True, **kw)
+                           share_layers=True, train_bias=meta.get("train_bias", True), **kw)
 
 
-@pytest.mark.parametrize("name", ["poac_small", "poac_ant", "poac_counts"])
+@pytest.mark.parametrize("name", ["poac_small", "poac_ant", "poac_counts", "poac_nobias"])
 def test_particle_step_matches_reference_golden(name):
     meta, g = parity.load(name)
     tr = particle_trainer_for(meta, counts=bool(meta.get("counts")))

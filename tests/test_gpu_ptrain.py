@@ -14,7 +14,7 @@ from gpu_helpers import Space, StateDictModule, batch_from, module_tensors
 pytestmark = pytest.mark.gpu
 
 FIXTURES = ["ptrain_small", "ptrain_counts", "ptrain_soft_rescale", "ptrain_mean_update",
-            "ptrain_humanoid"]
+            "ptrain_humanoid", "ptrain_nobias"]
 
 
 def ptrain_producers(params):
@@ -42,7 +42,8 @@ def ptrain_trainer_for(meta, params=None, **kw):
                            mean_update=bool(meta.get("mean_update")),
                            rescale_targets_around_mean=bool(meta.get("rescale")),
                            std_soft_update=soft is not None,
-                           std_soft_update_prob=0.0 if soft is None else soft, **kw)
+                           std_soft_update_prob=0.0 if soft is None else soft,
+                           train_bias=meta.get("train_bias", True), **kw)
 
 
 @pytest.mark.parametrize("name", FIXTURES)

@@ -79,7 +79,7 @@ def test_sac_oracle_matches_reference_golden(name):
 
 
 def test_poac_oracle_matches_reference_golden():
-    for name in ("poac_small", "poac_ant", "poac_counts"):
+    for name in ("poac_small", "poac_ant", "poac_counts", "poac_nobias"):
         meta, g = parity.load(name)
         params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
                             q_out=meta["K"], q_last_bias=np.linspace(meta["q_min"], meta["q_max"],
@@ -87,7 +87,8 @@ def test_poac_oracle_matches_reference_golden():
                             pi_init_w=meta["pi_init_w"])
         orc = so.ParticleOACOracle(params, meta["obs_dim"], meta["act_dim"], meta["K"],
                                    discount=meta["discount"], policy_lr=meta["lr"],
-                                   qf_lr=meta["lr"], tau=meta["tau"])
+                                   qf_lr=meta["lr"], tau=meta["tau"],
+                                   train_bias=meta.get("train_bias", True))
         errs = {}
         for s in range(meta["steps"]):
             b = build_batch(meta, g[f"s{s}/idx"])
@@ -113,7 +114,7 @@ def test_poac_oracle_matches_reference_golden():
         assert not bad, (name, sorted(bad.items(), key=lambda kv: -kv[1])[:10])
 
 
-GOAC_FIXTURES = ["goac_small", "goac_counts", "goac_soft", "goac_humanoid"]
+GOAC_FIXTURES = ["goac_small", "goac_counts", "goac_soft", "goac_humanoid", "goac_nobias"]
 GOAC_STATS = ("QF mean", "QF std", "QF Loss", "STD Loss", "Q Target Mean", "Q STD Target Mean",
               "Policy Loss", "Policy mu Mean", "Policy log std Mean")
 
@@ -126,7 +127,8 @@ def make_goac_oracle(meta, dtype=torch.float32):
                                 q_min=meta["q_min"], q_max=meta["q_max"],
                                 discount=meta["discount"], policy_lr=meta["lr"],
                                 qf_lr=meta["lr"], tau=meta["tau"],
-                                std_soft_update_prob=meta["soft"], dtype=dtype)
+                                std_soft_update_prob=meta["soft"],
+                                train_bias=meta.get("train_bias", True), dtype=dtype)
 
 
 def goac_errors(meta, g, orc):
@@ -170,7 +172,7 @@ def test_goac_oracle_matches_reference_golden(name):
 
 
 PTRAIN_FIXTURES = ["ptrain_small", "ptrain_counts", "ptrain_soft_rescale", "ptrain_mean_update",
-                   "ptrain_humanoid"]
+                   "ptrain_humanoid", "ptrain_nobias"]
 
 
 def make_ptrain_oracle(meta, dtype=torch.float32):
@@ -182,7 +184,7 @@ def make_ptrain_oracle(meta, dtype=torch.float32):
                                discount=meta["discount"], policy_lr=meta["lr"], qf_lr=meta["lr"],
                                tau=meta["tau"], std_soft_update_prob=meta["soft"],
                                mean_update=meta["mean_update"], rescale=meta["rescale"],
-                               dtype=dtype)
+                               train_bias=meta.get("train_bias", True), dtype=dtype)
 
 
 def ptrain_errors(meta, g, orc):
