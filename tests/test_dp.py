@@ -188,3 +188,51 @@ def test_goac_dp_two_ranks_equals_single_process_on_global_batch():
     want = _goac_flat(ref)
     assert parity.rel_err(got, want) < 1e-6
     assert np.max(np.abs(got - want)) < 1e-5
+
+
+# ------------------------------------------------- p-oac (particle_trainer.py)
+def _ptrain_make():
+    from fixtures_lib import ptrain_params
+    from oracle import sac_oracle as so
+    p = ptrain_params(Do, Da, H, 3, 5, 0.0, 50.0, pi_init_w=0.2, q_init_w=0.1)
+    return so.ParticleUBOracle(p, Do, Da, 5, 3, q_min=0.0, q_max=50.0, policy_lr=1e-3,
+                               qf_lr=1e-3)
+
+
+def _ptrain_worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oac_amd.dp import dp_step
+    orc = _ptrain_make()
+    for batch in _goac_inputs(world):
+        sl = slice(rank * BL, (rank + 1) * BL)
+        ex = GaussOracleExecutor(orc, {k: v[sl] for k, v in batch.items()}, world)
+        dp_step(ex, lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM))
+    if rank == 0:
+        out.put(_goac_flat(orc))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ptrain_dp_two_ranks_equals_single_process_on_global_batch():
+    """p-oac ParticleTrainer data-parallel step over gloo, counts=True (the
+    sorted-particle targets and the quantile policy seed are per row; the
+    critic / policy gradients are the only exchanges)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ptrain_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get()
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ref = _ptrain_make()
+    for batch in _goac_inputs(world):
+        ref.step(batch)
+    want = _goac_flat(ref)
+    assert parity.rel_err(got, want) < 1e-6
+    assert np.max(np.abs(got - want)) < 1e-5
