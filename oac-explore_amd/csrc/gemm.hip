@@ -339,16 +339,37 @@ __global__ void __launch_bounds__(256) gemm_grouped_kernel(const GemmBatch batch
 }
 
 // LDS-tiled kernel for the large-batch stages (cfg 1); cfg 0 is the
-// latency-optimised register-direct kernel of gemm_small.hip.
+// latency-optimised register-direct kernel of gemm_small.hip.  Tile variants
+// (OAC_LDS_TILE, read once): 0 = 64x64x32 (32x32 per wave), 1 = 128x128x16
+// (64x64 per wave), 2 = 128x64x32 (64x32 per wave), 3 = 64x128x32 (32x64 per
+// wave).  The k order of every accumulator is the same in all of them, so
+// they are bitwise interchangeable.
 using CfgLarge = GemmCfg<64, 64, 32, 2, 2, 1>;
+using CfgL1 = GemmCfg<128, 128, 16, 2, 2, 1>;
+using CfgL2 = GemmCfg<128, 64, 32, 2, 2, 1>;
+using CfgL3 = GemmCfg<64, 128, 32, 2, 2, 1>;
+using CfgL4 = GemmCfg<64, 64, 16, 2, 2, 1>;
+using CfgL5 = GemmCfg<64, 32, 32, 2, 1, 2>;
+
+static int lds_variant() {
+  static int v = [] {
+    const char* e = getenv("OAC_LDS_TILE");
+    const int x = e ? atoi(e) : 0;
+    return (x >= 0 && x <= 5) ? x : 0;
+  }();
+  return v;
+}
+static int lds_tile_m() { const int v = lds_variant(); return v == 1 || v == 2 ? 128 : 64; }
+static int lds_tile_n() { const int v = lds_variant(); return v == 1 || v == 3 ? 128 : v == 5 ? 32 : 64; }
 
 // cfg 2: the register-direct kernel of gemm_big.hip (128 x 128 workgroup tiles)
-int gemm_big_tile_m();
-int gemm_big_tile_n();
-hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s);
+// cfg 3: the same kernel with the backward tile (dX / dW batches)
+int gemm_big_tile_m(bool bwd);
+int gemm_big_tile_n(bool bwd);
+hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s, bool bwd);
 
-int gemm_tile_m(int cfg) { return cfg == 0 ? 32 : cfg == 2 ? gemm_big_tile_m() : CfgLarge::kBM; }
-int gemm_tile_n(int cfg) { return cfg == 0 ? 32 : cfg == 2 ? gemm_big_tile_n() : CfgLarge::kBN; }
+int gemm_tile_m(int cfg) { return cfg == 0 ? 32 : cfg >= 2 ? gemm_big_tile_m(cfg == 3) : lds_tile_m(); }
+int gemm_tile_n(int cfg) { return cfg == 0 ? 32 : cfg >= 2 ? gemm_big_tile_n(cfg == 3) : lds_tile_n(); }
 
 void gemm_small_finalize(GemmBatch& b);
 hipError_t gemm_small_launch(const GemmBatch& b, hipStream_t s);
@@ -377,8 +398,15 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   for (int i = 0; i < b.ntasks; ++i)               // dual products / head backward: small kernel
     if (b.t[i].K2 > 0 || b.t[i].epi == EPI_HEAD_BWD || b.t[i].epi == EPI_BIAS_RELU_DOT)
       return hipErrorInvalidValue;
-  if (cfg == 2) return gemm_big_launch(b, s);
-  OAC_LAUNCH(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b);
+  if (cfg >= 2) return gemm_big_launch(b, s, cfg == 3);
+  switch (lds_variant()) {
+    case 1: OAC_LAUNCH(gemm_grouped_kernel<CfgL1>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
+    case 2: OAC_LAUNCH(gemm_grouped_kernel<CfgL2>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
+    case 3: OAC_LAUNCH(gemm_grouped_kernel<CfgL3>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
+    case 4: OAC_LAUNCH(gemm_grouped_kernel<CfgL4>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
+    case 5: OAC_LAUNCH(gemm_grouped_kernel<CfgL5>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
+    default: OAC_LAUNCH(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
+  }
   return hipGetLastError();
 }
 

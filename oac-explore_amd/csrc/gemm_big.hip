@@ -1,20 +1,28 @@
-// Register-direct grouped fp32 GEMM for the forward products of the
-// large-batch stages (B >= 1024: BASELINE configs 2-4), gemm_cfg 2 (the
-// backward products stay on the LDS kernel, plan_common.h launch_cfg).
+// Register-direct grouped fp32 GEMM for the large-batch stages (B >= 1024:
+// BASELINE configs 2-4): gemm_cfg 2 (forward batches, 64x32 wave blocks)
+// and 3 (backward batches -- dX = dY W and dW = dY^T [X | 1] -- with 32x32
+// wave blocks and 3 k-groups in flight), chosen per launch in plan_common.h
+// launch_cfg.
 //
 // The LDS-staged 64x64 kernel (gemm.hip) reached ~21 % of the fp32 MFMA peak
 // at B=4096: one barrier per 32-deep K block, dword staging loads and one
 // 32x32 accumulator per wave.  Here every wave owns a (32 WM) x (32 WN) output
 // block -- WM x WN accumulators of v_mfma_f32_32x32x2_f32 -- and feeds the
 // MFMAs straight from L2 into VGPRs (gemm_operand.h: a k-contiguous operand is
-// one 16-byte load per lane per 4 MFMAs), so per 8-deep k-group a lane issues
-// WM + WN loads for 4 WM WN MFMAs, with no LDS and no barrier: the waves of
-// a workgroup run independently and the next group's loads are in flight
-// while the current group's MFMAs issue (register double buffer).  Four
+// one 16-byte load per lane per 4 MFMAs; a batch-major operand of a backward
+// product one coalesced dword per lane and k), so per 8-deep k-group a lane
+// issues WM + WN loads for 4 WM WN MFMAs, with no LDS and no barrier: the
+// waves of a workgroup run independently and the next groups' loads are in
+// flight while the current group's MFMAs issue (register multi-buffer).  Four
 // waves (2 x 2) form a (64 WM) x (64 WN) workgroup tile so neighbouring waves
 // share operand lines in L1/L2.  Split-K (the dW tasks, K = batch) writes
 // slabs exactly like the other kernels; every epilogue reads the accumulator
 // registers directly.
+//
+// Backward products, B=4096 SAC step (rocprofv3 per launch, LDS kernel ->
+// this one, before the split retune): critic layer 1 72.1 -> 59.7 us, critic
+// layer 0 49.9 -> 37.9 us; with 32x32 wave blocks, kchunk >= 128 and 3
+// groups in flight the step went 2,044 -> 2,214 steps/s (tools/env_sweep.sh).
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -141,7 +149,7 @@ __device__ __forceinline__ void rd_epilogue(const GemmTask& t, int mw, int nw,
   }
 }
 
-template <int WM, int WN>
+template <int WM, int WN, int PF>
 __global__ void __launch_bounds__(256)
 gemm_big_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                 const GemmBatch batch) {
@@ -178,9 +186,23 @@ gemm_big_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
     for (int j = 0; j < WN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  // forward products only (both operands k-contiguous; plan_common.h launch_cfg)
-  rd_loop<OP_KC, OP_KC, WM, WN>(t, t.A, t.lda, t.B, t.ldb, t.M, t.b_ones ? t.N - 1 : t.N,
-                                t.b_ones != 0, mw, nw, k_lo, k_hi, acc);
+  // operand kinds per task (wave-uniform): forward products (both operands
+  // k-contiguous), dX = dY W (dY k-contiguous, possibly a rank-1 seed through
+  // a ReLU mask; W n-contiguous) and dW = dY^T [X | 1] (both batch-major, so
+  // m/n-contiguous: one coalesced dword per lane and k)
+  const int nl = t.b_ones ? t.N - 1 : t.N;
+  const bool ones = t.b_ones != 0;
+  const bool r1 = t.a_mode != A_PLAIN;
+  if (t.a_kc && t.b_kc)
+    rd_loop<OP_KC, OP_KC, WM, WN, PF>(t, t.A, t.lda, t.B, t.ldb, t.M, nl, ones, mw, nw, k_lo, k_hi, acc);
+  else if (t.a_kc && !r1)
+    rd_loop<OP_KC, OP_MN, WM, WN, PF>(t, t.A, t.lda, t.B, t.ldb, t.M, nl, ones, mw, nw, k_lo, k_hi, acc);
+  else if (t.a_kc)
+    rd_loop<OP_KC_R1, OP_MN, WM, WN, PF>(t, t.A, t.lda, t.B, t.ldb, t.M, nl, ones, mw, nw, k_lo, k_hi, acc);
+  else if (!r1)
+    rd_loop<OP_MN, OP_MN, WM, WN, PF>(t, t.A, t.lda, t.B, t.ldb, t.M, nl, ones, mw, nw, k_lo, k_hi, acc);
+  else
+    rd_loop<OP_MN_R1, OP_MN, WM, WN, PF>(t, t.A, t.lda, t.B, t.ldb, t.M, nl, ones, mw, nw, k_lo, k_hi, acc);
   rd_epilogue<WM, WN>(t, mw, nw, acc, false);
   if (t.epi == EPI_BIAS_RANK_RELU) {
     // + U V^T: U / V continue A / B along k (the batch actions follow the
@@ -188,7 +210,7 @@ gemm_big_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
     // columns in W0; checked at launch), so the same accumulators run on over
     // k in [K, K + R) -- the critic's 393-wide layer 0 with the obs-only
     // projection P snapshotted on the way
-    rd_loop<OP_KC, OP_KC, WM, WN>(t, t.A, t.lda, t.B, t.ldb, t.M, t.N, false, mw, nw, t.K, t.K + t.R, acc);
+    rd_loop<OP_KC, OP_KC, WM, WN, PF>(t, t.A, t.lda, t.B, t.ldb, t.M, t.N, false, mw, nw, t.K, t.K + t.R, acc);
     rd_epilogue<WM, WN>(t, mw, nw, acc, true);
   }
 }
@@ -197,28 +219,35 @@ gemm_big_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
 // B=4096, 1,828 steps/s against 1,827 for 32 x 64, 1,775 for 64 x 64 and 1,741
 // for 32 x 32; 3 k-groups in flight instead of 2 changed nothing (+-1 %).
 // OAC_BIG_TILE="WM,WN" selects another instantiation (tuning experiments)
-static int big_wm() {
-  static int v = [] { const char* e = getenv("OAC_BIG_TILE"); return e ? atoi(e) : 2; }();
-  return v;
+// Backward batches (dX / dW, cfg 3) default to 32 x 32 wave blocks (64 x 64
+// workgroups): at B=4096 their products are 256 wide, and the 4x larger
+// grid hides the per-wave operand latency better than the larger blocks do.
+// OAC_BIG_TILE / OAC_BIG_BWD_TILE="WM,WN" select other instantiations.
+static int tile_env(const char* name, int which, int dflt) {
+  const char* e = getenv(name);
+  if (!e) return dflt;
+  if (which == 0) return atoi(e);
+  const char* c = strchr(e, ',');
+  return c ? atoi(c + 1) : dflt;
 }
-static int big_wn() {
-  static int v = [] {
-    const char* e = getenv("OAC_BIG_TILE");
-    const char* c = e ? strchr(e, ',') : nullptr;
-    return c ? atoi(c + 1) : 1;
-  }();
-  return v;
+static int big_wm(bool bwd) {
+  static const int f = tile_env("OAC_BIG_TILE", 0, 2), b = tile_env("OAC_BIG_BWD_TILE", 0, 1);
+  return bwd ? b : f;
 }
-int gemm_big_tile_m() { return 64 * big_wm(); }
-int gemm_big_tile_n() { return 64 * big_wn(); }
+static int big_wn(bool bwd) {
+  static const int f = tile_env("OAC_BIG_TILE", 1, 1), b = tile_env("OAC_BIG_BWD_TILE", 1, 1);
+  return bwd ? b : f;
+}
+int gemm_big_tile_m(bool bwd) { return 64 * big_wm(bwd); }
+int gemm_big_tile_n(bool bwd) { return 64 * big_wn(bwd); }
 
-hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s) {
+hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s, bool bwd) {
   if (b.total_tiles <= 0) return hipSuccess;
   for (int i = 0; i < b.ntasks; ++i) {
     const GemmTask& t = b.t[i];
     if (t.K2 > 0 || t.epi == EPI_HEAD_BWD || t.epi == EPI_BIAS_RELU_DOT || b.fuse_adam ||
-        !t.a_kc || !t.b_kc || t.a_mode != A_PLAIN)
-      return hipErrorInvalidValue;   // forward (k-contiguous) products only
+        (t.b_kc && !t.a_kc) || (t.b_kc && t.a_mode != A_PLAIN))
+      return hipErrorInvalidValue;   // kinds handled in gemm_big_kernel
     if (t.epi == EPI_BIAS_RANK_RELU &&
         (!t.C2 || t.ksplit > 1 || t.U != t.A + t.K || t.ldu != t.lda || t.V != t.B + t.K ||
          t.ldv != t.ldb))
@@ -226,12 +255,14 @@ hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s) {
   }
   int tb[8];
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
-#define OAC_BIG(WM_, WN_) \
-  if (big_wm() == WM_ && big_wn() == WN_) { \
-    OAC_LAUNCH((gemm_big_kernel<WM_, WN_>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, \
+  static const int pf_env = tile_env("OAC_BIG_BWD_PF", 0, 3);
+  const int pf = bwd ? pf_env : 2;
+#define OAC_BIG(WM_, WN_, PF_) \
+  if (big_wm(bwd) == WM_ && big_wn(bwd) == WN_ && pf == PF_) { \
+    OAC_LAUNCH((gemm_big_kernel<WM_, WN_, PF_>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, \
                tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
     return hipGetLastError(); }
-  OAC_BIG(2, 2) OAC_BIG(1, 2) OAC_BIG(2, 1) OAC_BIG(1, 1)
+  OAC_BIG(2, 2, 2) OAC_BIG(1, 2, 2) OAC_BIG(2, 1, 2) OAC_BIG(1, 1, 2) OAC_BIG(1, 1, 3) OAC_BIG(1, 1, 4)
 #undef OAC_BIG
   return hipErrorInvalidValue;
 }

@@ -2,6 +2,7 @@
 // bookkeeping, split-K sizing, GEMM task constructors, HIP-event timing.
 #pragma once
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <utility>
 #include <vector>
@@ -44,7 +45,8 @@ static inline Split choose_split(int K, int tiles, int cfg) {
   int S = 1;
   if (K >= 512) {
     int want = (512 + tiles - 1) / tiles;
-    int maxS = K / 256;
+    static const int kmin = [] { const char* e = getenv("OAC_SPLIT_KMIN"); return e ? atoi(e) : 128; }();
+    int maxS = K / (cfg == 0 ? 256 : kmin);
     S = want < maxS ? want : maxS;
     if (S < 1) S = 1;
   }
@@ -151,6 +153,13 @@ static inline void read_tuning(PlanBase& p) {
 // products (both operands k-contiguous, N >= 64: B=4096 layer 0 115 -> 80 us,
 // layer 1 64 -> 40 us) and loses on dX / dW (n- or m-contiguous operands, one
 // dword load per k) and narrow outputs; those launches run on the LDS kernel
+// backward products on the register-direct kernel at large batch
+// (OAC_BIG_BWD=0 keeps them on the LDS kernel, for A/B measurements)
+static inline bool big_bwd() {
+  static const bool v = [] { const char* e = getenv("OAC_BIG_BWD"); return !e || atoi(e) != 0; }();
+  return v;
+}
+
 static inline int launch_cfg(int cfg, const GemmBatch& gb) {
   if (cfg == 0) return 0;
   // narrow products at large batch (width-1 critic heads, dL/da with N = act
@@ -162,11 +171,15 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     narrow = gb.t[i].N <= 32 && gb.t[i].ksplit <= 1 && gb.t[i].K2 == 0;
   if (narrow) return 0;
   if (cfg != 2) return cfg;
+  bool any_bwd = false;
   for (int i = 0; i < gb.ntasks; ++i) {
     const GemmTask& t = gb.t[i];
-    if (!t.a_kc || !t.b_kc || t.a_mode != A_PLAIN || t.N < 64 || t.K2 > 0 ||
-        t.epi == EPI_HEAD_BWD || t.epi == EPI_BIAS_RELU_DOT || gb.fuse_adam)
+    const bool fwd = t.a_kc && t.b_kc && t.a_mode == A_PLAIN;
+    const bool bwd = !t.b_kc && big_bwd();   // dX / dW products (register-direct, gemm_big.hip)
+    if (!(fwd || bwd) || t.N < 64 || t.K2 > 0 || t.epi == EPI_HEAD_BWD ||
+        t.epi == EPI_BIAS_RELU_DOT || gb.fuse_adam)
       return 1;
+    any_bwd |= bwd;
     // the big kernel runs the rank-R columns as a continuation of the same
     // row (the action stored right after the observation); a separate action
     // buffer (the policy's a~) goes to the LDS kernel
@@ -175,7 +188,7 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
          t.ldv != t.ldb))
       return 1;
   }
-  return 2;
+  return any_bwd ? 3 : 2;
 }
 
 static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {

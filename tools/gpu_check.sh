@@ -2,7 +2,7 @@
 # One GPU round trip: parity tests, B=256 / B=4096 bench lines, and a
 # per-launch kernel trace of the B=256 step (rocprofv3).  Outputs under gpurun_out/.
 mkdir -p gpurun_out
-timeout -k 10 700 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
 tail -3 gpurun_out/pytest_gpu.log
