@@ -255,14 +255,15 @@ hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s, bool bwd) {
   }
   int tb[8];
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
-  static const int pf_env = tile_env("OAC_BIG_BWD_PF", 0, 3);
-  const int pf = bwd ? pf_env : 2;
+  static const int pf_bwd = tile_env("OAC_BIG_BWD_PF", 0, 3), pf_fwd = tile_env("OAC_BIG_PF", 0, 2);
+  const int pf = bwd ? pf_bwd : pf_fwd;
 #define OAC_BIG(WM_, WN_, PF_) \
   if (big_wm(bwd) == WM_ && big_wn(bwd) == WN_ && pf == PF_) { \
     OAC_LAUNCH((gemm_big_kernel<WM_, WN_, PF_>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, \
                tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
     return hipGetLastError(); }
-  OAC_BIG(2, 2, 2) OAC_BIG(1, 2, 2) OAC_BIG(2, 1, 2) OAC_BIG(1, 1, 2) OAC_BIG(1, 1, 3) OAC_BIG(1, 1, 4)
+  OAC_BIG(2, 1, 2) OAC_BIG(1, 1, 3) OAC_BIG(2, 1, 3) OAC_BIG(1, 2, 2) OAC_BIG(1, 2, 3)
+  OAC_BIG(1, 1, 2) OAC_BIG(2, 2, 2) OAC_BIG(1, 1, 4)
 #undef OAC_BIG
   return hipErrorInvalidValue;
 }

@@ -1,6 +1,8 @@
 """Ragged shapes on the GPU, every trainer kind against the fp32 CPU oracle:
-batch sizes that are not tile multiples (1, 37, 300), a hidden width that is
-not a multiple of the 32-wide tiles (48), odd observation / action widths.
+batch sizes that are not tile multiples (1, 37, 300, and 1029 / 1100 on the
+large-batch kernels: register-direct forward and backward products, split-K
+chunks that end mid k-group), hidden widths that are not multiples of the
+32- or 64-wide tiles (48, 80), odd observation / action widths.
 One step from identical state; every gradient tensor within 1e-5
 (norm-relative) of the oracle's."""
 import numpy as np
@@ -14,7 +16,8 @@ from gpu_helpers import Space, module_tensors, producers
 
 pytestmark = pytest.mark.gpu
 
-SHAPES = [(11, 3, 32, 1), (11, 3, 32, 37), (7, 5, 48, 300), (376, 17, 256, 37)]
+SHAPES = [(11, 3, 32, 1), (11, 3, 32, 37), (7, 5, 48, 300), (376, 17, 256, 37),
+          (7, 5, 48, 1100), (13, 6, 80, 1029)]
 
 
 def _batch(Do, Da, B, seed):
