@@ -80,6 +80,13 @@ class Space:
         self.low = np.zeros(n, np.float32)
 
 
+def force_dp():
+    """OAC_BENCH_FORCE_DP=1 (under torchrun): the data-parallel step even at
+    one rank -- phase split, unfused Adam, RCCL all-reduces in the graph --
+    to measure what the DP structure costs apart from the link latency."""
+    return os.environ.get("OAC_BENCH_FORCE_DP") == "1"
+
+
 def build(args, rank, world, device):
     import oac_amd
     from oac_amd import DeviceIndexStream, ReplayBufferCount, SACTrainer
@@ -91,7 +98,7 @@ def build(args, rank, world, device):
               policy_lr=3e-4, qf_lr=3e-4, soft_target_tau=5e-3, target_update_period=1,
               use_automatic_entropy_tuning=True, device=device, seed=2 + 1000 * rank,
               gemm_cfg=args.gemm_cfg)
-    if world > 1:
+    if world > 1 or force_dp():
         from oac_amd.dp import DataParallelSACTrainer
         tr = DataParallelSACTrainer(pp, qp, **kw)
     else:
@@ -314,7 +321,8 @@ def main():
     # OAC_BENCH_SAME_DEVICE=1 put every rank on cuda:0 (RCCL refuses that)
     if os.environ.get("OAC_BENCH_SAME_DEVICE") == "1":
         local = 0
-    if world > 1:
+    dp = world > 1 or force_dp()
+    if dp:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         backend = os.environ.get("OAC_BENCH_BACKEND", "nccl")
@@ -331,7 +339,7 @@ def main():
     # (the largest n <= --steps-per-launch dividing the ring chunk, K and W, so
     # any --steps / --warmup work; the defaults keep n = 64)
     n = max(1, args.steps_per_launch)
-    if world > 1:
+    if dp:
         n = min(n, 8)   # data parallel: at most 8 steps (24 RCCL all-reduces) per captured graph
     while n > 1 and (stream.chunk % n or args.steps % n or args.warmup % n):
         n -= 1
@@ -339,7 +347,7 @@ def main():
 
     def barrier():
         torch.cuda.synchronize()
-        if world > 1:
+        if dp:
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
@@ -380,7 +388,7 @@ def main():
                        "obs_dim": args.obs_dim, "act_dim": args.act_dim,
                        "hidden": args.hidden, "batch_per_rank": B, "global_batch": B * world,
                        "replay_per_rank": args.replay,
-                       "parallelism": "dp%d" % world if world > 1 else "single"},
+                       "parallelism": "dp%d" % world if dp else "single"},
             "samples_per_s": round(value * B, 1),
             "steps_per_launch": n,
             "roofline": {"bound": "mfma",
@@ -421,7 +429,7 @@ def main():
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dp:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
 

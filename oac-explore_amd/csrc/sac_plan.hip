@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -440,14 +441,22 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
 // slot 0 (one launch per kXSlots steps), step i uses slot i % kXSlots
 static long c_batch_rows(const SacPlan& p) { return (long)p.c.batch * p.c.row_stride; }
 
+// OAC_STEP_FUSE / OAC_STEP_AHEAD = 0 switch off the fused optimizer epilogue /
+// the next-step critic prefetch (A/B measurements)
+static bool env_on(const char* name) {
+  const char* e = getenv(name);
+  return !e || atoi(e) != 0;
+}
+
 static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) {
+  static const bool fuse_on = env_on("OAC_STEP_FUSE"), ahead_on = env_on("OAC_STEP_AHEAD");
   p.launches = 0;
-  const bool fused = can_fuse_adam(p);
+  const bool fused = can_fuse_adam(p) && fuse_on;
   p.slot = i % kXSlots;
   const int gather_n = p.slot == 0 ? std::min(kXSlots, n - i) : 0;
   // steps after the first of a gather batch had their critic-side forward
   // issued inside the previous step's policy backward (small-batch path)
-  const bool ahead = p.cfg == 0 && (flags & OAC_STEP_GATHER);
+  const bool ahead = p.cfg == 0 && (flags & OAC_STEP_GATHER) && ahead_on;
   if (phase0(p, flags, s, gather_n, ahead && p.slot > 0)) return 1;
   if (phase1(p, s, fused)) return 1;
   if (!fused && phase2_adam(p, s, 0)) return 1;
