@@ -172,11 +172,9 @@ static int dphase1(SacPlan& p, int flags, hipStream_t s, bool fused) {
     add(gb, t_fwd(p.W(G_H2Q), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_Q1), K, EPI_BIAS, q + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {
-    GemmBatch gb{};
-    add(gb, t_fwd(p.W(G_H2T), H, B, H, tq + L.q_last_w, H, K, p.W(OAC_WS_TQ1), K, EPI_BIAS, tq + L.q_last_b));
-    if (run_gemm(p, gb, s)) return 1;
-  }
+  // the target critic's K-output last layer runs inside the targets kernel
+  // (row_heads, rows.hip): one launch fewer on the chain
+  const RowHead th{p.W(G_H2T), tq + L.q_last_w, tq + L.q_last_b, p.W(OAC_WS_TQ1), H};
   const float* counts = (flags & OAC_STEP_COUNTS) ? p.W(OAC_WS_COUNTS) : nullptr;
   if (c.kind == OAC_KIND_GAUSS) {
     GaussTargetArgs a;
@@ -185,7 +183,7 @@ static int dphase1(SacPlan& p, int flags, hipStream_t s, bool fused) {
     a.off_rew = c.off_rew; a.off_term = c.off_term; a.reward_scale = c.reward_scale;
     a.discount = c.discount; a.std_init = c.std_init;
     a.soft_prob = c.std_soft_update ? c.std_soft_prob : -1.f;
-    a.counts = counts;
+    a.counts = counts; a.th = th;
     a.B = B; a.dq = p.W(G_DQ); a.y = p.W(OAC_WS_Y); a.sqe = p.W(OAC_WS_SQE1);
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_gauss_targets(a, s)));
     p.launches++;
@@ -195,7 +193,7 @@ static int dphase1(SacPlan& p, int flags, hipStream_t s, bool fused) {
     a.q = p.W(OAC_WS_Q1); a.tq = p.W(OAC_WS_TQ1); a.batch = X; a.ld_batch = RS;
     a.off_rew = c.off_rew; a.off_term = c.off_term; a.reward_scale = c.reward_scale;
     a.discount = c.discount; a.B = B; a.K = K;
-    a.dq = p.W(G_DQ); a.sqe = p.W(OAC_WS_SQE1); a.y = p.W(OAC_WS_Y); a.counts = counts;
+    a.dq = p.W(G_DQ); a.sqe = p.W(OAC_WS_SQE1); a.y = p.W(OAC_WS_Y); a.counts = counts; a.th = th;
     a.loss_scale = 1.f / (float)K;                       // qf_loss /= num_particles
     a.soft_prob = c.std_soft_update ? c.std_soft_prob : -1.f;
     a.rescale_spread = c.rescale_spread;
@@ -265,23 +263,22 @@ static int dphase2(SacPlan& p, hipStream_t s, bool fused) {
     add(gb, t_fwd(p.W(G_H1N3), H, B, H, q + L.q_fc1_w, H, H, p.W(G_H2N3), H, EPI_BIAS_RELU, q + L.q_fc1_b));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {
-    GemmBatch gb{};
-    add(gb, t_fwd(p.W(G_H2N), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_QN1), K, EPI_BIAS, q + L.q_last_b));
-    add(gb, t_fwd(p.W(G_H2N3), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_QN2), K, EPI_BIAS, q + L.q_last_b));
-    if (run_gemm(p, gb, s)) return 1;
-  }
+  // the post-step critic's last layer on (obs, a~) runs inside the seed
+  // kernel (row_heads); on (obs, a~_T) it is not needed at all: the target
+  // policy's seed is a constant, only the hidden activations (ReLU masks)
+  // of that forward enter its backward
+  const RowHead hn{p.W(G_H2N), q + L.q_last_w, q + L.q_last_b, p.W(OAC_WS_QN1), H};
   if (c.kind == OAC_KIND_GAUSS) {
     GaussSeedArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.qn = p.W(OAC_WS_QN1); a.qt = p.W(OAC_WS_QN2); a.std_bound = c.std_bound; a.B = B;
+    a.qn = p.W(OAC_WS_QN1); a.qt = p.W(OAC_WS_QN2); a.hn = hn; a.std_bound = c.std_bound; a.B = B;
     a.g = p.W(G_GQ); a.gt = p.W(G_GQ3); a.ub = p.W(OAC_WS_QNEW);
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_gauss_seed(a, s)));
     p.launches++;
   } else {
     ParticleUbSeedArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.qn = p.W(OAC_WS_QN1); a.qt = p.W(OAC_WS_QN2); a.B = B; a.K = K;
+    a.qn = p.W(OAC_WS_QN1); a.qt = p.W(OAC_WS_QN2); a.hn = hn; a.B = B; a.K = K;
     a.delta_index = c.delta_index;
     a.g = p.W(G_GQ); a.gt = p.W(G_GQ3); a.ub = p.W(OAC_WS_QNEW);
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_particle_ub_seed(a, s)));

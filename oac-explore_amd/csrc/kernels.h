@@ -162,8 +162,18 @@ hipError_t launch_priority_sample(const int* counts, long size, const double* u,
                                   double* scratch, int* idx_out, hipStream_t s);
 
 // ParticleTrainer (share_layers) per-sample kernels, particle_trainer_oac.py
+// A critic's K-output last layer evaluated inside a row kernel instead of a
+// separate GEMM launch (det_plan.hip): out[r, k] = b[k] + sum_j h[r, j] W[k, j]
+// for the kernel's 16-row block (h null: the outputs were stored by a GEMM)
+struct RowHead {
+  const float* h; const float* w; const float* b;   // h [B, H], W [K, H], b [K]
+  float* out;                                        // [B, K] (workspace view, diagnostics)
+  int H;
+};
+
 struct ParticleTargetArgs {
   const float* q; const float* tq;      // [B, K] critic / target critic outputs
+  RowHead th;                           // th.h set: tq computed here (into th.out)
   const float* batch; long ld_batch; int off_rew, off_term;
   float reward_scale, discount;
   int B, K;
@@ -194,6 +204,7 @@ hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s);
 
 struct GaussTargetArgs {
   const float* q; const float* tq;      // [B, 2] Q(obs, a), Q_target(next_obs, a') raw outputs
+  RowHead th;                           // th.h set: tq computed here (into th.out)
   const float* batch; long ld_batch; int off_rew, off_term;
   float reward_scale, discount, std_init;
   float soft_prob;                      // std_soft_update_prob, < 0: off
@@ -207,7 +218,8 @@ hipError_t launch_gauss_targets(const GaussTargetArgs& a, hipStream_t s);
 
 struct GaussSeedArgs {
   const float* qn;                      // [B, 2] post-step Q(obs, tanh(mean_pi(obs)))
-  const float* qt;                      // [B, 2] post-step Q(obs, tanh(mean_target_pi(obs)))
+  const float* qt;                      // [B, 2] post-step Q(obs, tanh(mean_target_pi(obs))) (unread)
+  RowHead hn;                           // hn.h set: qn computed here
   float std_bound; int B;
   float* g; float* gt;                  // [B, 2] seeds of -mean(upper bound), -mean(q)
   float* ub;                            // [B] upper bound q + std_bound * std
@@ -216,7 +228,8 @@ hipError_t launch_gauss_seed(const GaussSeedArgs& a, hipStream_t s);
 
 struct ParticleUbSeedArgs {            // particle_trainer.py:317-330, :339-348
   const float* qn;                      // [B, K] post-step Q(obs, tanh(mean_pi(obs)))
-  const float* qt;                      // [B, K] post-step Q(obs, tanh(mean_target_pi(obs)))
+  const float* qt;                      // [B, K] post-step Q(obs, tanh(mean_target_pi(obs))) (unread)
+  RowHead hn;                           // hn.h set: qn computed here
   int B, K, delta_index;
   float* g;                             // [B, K] -1/B at the delta_index-th sorted head
   float* gt;                            // [B, K] -1/(B K) on every head (mean over particles)

@@ -188,15 +188,81 @@ __device__ __forceinline__ void load_row16(const float* src, int K, float (&v)[k
   }
 }
 
+// Row kernels of the particle / g-oac targets and seeds: 16 rows per
+// 256-thread block (thread t < 16 owns row 16 b + t).  With a RowHead set, the
+// block first evaluates the critic's K-output last layer for its 16 rows as
+// one 16x16 output tile of v_mfma_f32_16x16x4_f32: the hidden width is split
+// over the 4 waves in 16-wide k-chunks (one 16-byte load per lane and
+// operand, MFMA j of a chunk multiplies element j, as in head.hip), the wave
+// partials are summed through LDS in fixed order, and the result goes to LDS
+// for the row logic and to the workspace view.  This replaces the last-layer
+// GEMM launch that otherwise sits between the hidden layer and this kernel.
+constexpr int kRowBlock = 16;
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float f4a __attribute__((ext_vector_type(4), aligned(4)));
+
+struct RowHeadLds {
+  float red[4][4][64];          // wave partials
+  float out[kRowBlock][kMaxHeads];
+};
+
+__device__ __forceinline__ void row_heads(const RowHead& hd, int K, int B, int r0, RowHeadLds& sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const float* arow = hd.h + (long)min(r0 + l16, B - 1) * hd.H;
+  const float* brow = hd.w + (long)min(l16, K - 1) * hd.H;
+  const bool bv = l16 < K;
+  floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int chunks = (hd.H + 15) >> 4;
+#pragma unroll 1
+  for (int c = wave; c < chunks; c += 4) {
+    const int kb = 16 * c + 4 * g4;
+    float xa[4], xb[4];
+    if (kb + 3 < hd.H) {
+      const f4a a = *reinterpret_cast<const f4a*>(arow + kb);
+      const f4a b = *reinterpret_cast<const f4a*>(brow + kb);
+      xa[0] = a.x; xa[1] = a.y; xa[2] = a.z; xa[3] = a.w;
+      xb[0] = b.x; xb[1] = b.y; xb[2] = b.z; xb[3] = b.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        xa[e] = kb + e < hd.H ? arow[kb + e] : 0.f;
+        xb[e] = kb + e < hd.H ? brow[kb + e] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[e], bv ? xb[e] : 0.f, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) sh.red[wave][r][lane] = acc[r];
+  __syncthreads();
+  {
+    const int r = threadIdx.x >> 6, l = threadIdx.x & 63;   // D reg r of lane l
+    const int row = 4 * (l >> 4) + r, col = l & 15;
+    const float v = ((sh.red[0][r][l] + sh.red[1][r][l]) + sh.red[2][r][l]) + sh.red[3][r][l];
+    if (col < K) {
+      const float o = v + hd.b[col];
+      sh.out[row][col] = o;
+      if (r0 + row < B) hd.out[(long)(r0 + row) * K + col] = o;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArgs p) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= p.B) return;
+  __shared__ RowHeadLds hs;
+  const int r0 = blockIdx.x * kRowBlock, r = r0 + threadIdx.x;
   const int K = p.K;
+  if (p.th.h) {
+    row_heads(p.th, K, p.B, r0, hs);
+    __syncthreads();
+  }
+  if (threadIdx.x >= kRowBlock || r >= p.B) return;
   const float fK = (float)K;
   float q[kMaxHeads], t[kMaxHeads];
   int qi[kMaxHeads], tix[kMaxHeads];
   load_row16(p.q + (long)r * K, K, q, qi);
-  load_row16(p.tq + (long)r * K, K, t, tix);
+  load_row16(p.th.h ? &hs.out[threadIdx.x][0] : p.tq + (long)r * K, K, t, tix);
   sort16(q, qi);
   sort16(t, tix);
   const float rew = p.batch[(long)r * p.ld_batch + p.off_rew];
@@ -299,7 +365,9 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
 }
 
 hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s) {
-  OAC_LAUNCH(particle_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  if (a.K > kMaxHeads || (a.th.h && (!a.th.w || !a.th.b || !a.th.out || a.th.H < 1)))
+    return hipErrorInvalidValue;
+  OAC_LAUNCH(particle_targets_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s) {
@@ -321,10 +389,16 @@ hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s) {
 //   loss = MSE(q0, q_target) + MSE(std, std_target)
 //   dL/dq0 = 2 (q0 - y_q) / B ;  dL/dq1 = 2 (std - y_s) / B * std  (exp backward)
 __global__ void __launch_bounds__(256) gauss_targets_kernel(GaussTargetArgs p) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= p.B) return;
+  __shared__ RowHeadLds hs;
+  const int r0 = blockIdx.x * kRowBlock, r = r0 + threadIdx.x;
+  if (p.th.h) {
+    row_heads(p.th, 2, p.B, r0, hs);
+    __syncthreads();
+  }
+  if (threadIdx.x >= kRowBlock || r >= p.B) return;
+  const float* tq = p.th.h ? &hs.out[threadIdx.x][0] : p.tq + 2L * r;
   const float q0 = p.q[2L * r], sd = expf(p.q[2L * r + 1]);
-  const float t0 = p.tq[2L * r], tsd = expf(p.tq[2L * r + 1]);
+  const float t0 = tq[0], tsd = expf(tq[1]);
   const float rew = p.batch[(long)r * p.ld_batch + p.off_rew];
   const float term = p.batch[(long)r * p.ld_batch + p.off_term];
   const float gd = __fmul_rn(1.f - term, p.discount);
@@ -348,11 +422,17 @@ __global__ void __launch_bounds__(256) gauss_targets_kernel(GaussTargetArgs p) {
 // 338-350): policy: L = -mean(q0 + z*exp(q1)) -> [-1/B, -z/B * std];
 // target policy: L = -mean(q0) -> [-1/B, 0]
 __global__ void __launch_bounds__(256) gauss_seed_kernel(GaussSeedArgs p) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= p.B) return;
+  __shared__ RowHeadLds hs;
+  const int r0 = blockIdx.x * kRowBlock, r = r0 + threadIdx.x;
+  if (p.hn.h) {   // (the target policy's seed is constant: qt is never read)
+    row_heads(p.hn, 2, p.B, r0, hs);
+    __syncthreads();
+  }
+  if (threadIdx.x >= kRowBlock || r >= p.B) return;
+  const float* qn = p.hn.h ? &hs.out[threadIdx.x][0] : p.qn + 2L * r;
   const float g0 = -(1.f / (float)p.B);
-  const float sd = expf(p.qn[2L * r + 1]);
-  p.ub[r] = __fadd_rn(p.qn[2L * r], __fmul_rn(p.std_bound, sd));
+  const float sd = expf(qn[1]);
+  p.ub[r] = __fadd_rn(qn[0], __fmul_rn(p.std_bound, sd));
   p.g[2L * r] = g0;
   p.g[2L * r + 1] = __fmul_rn(__fmul_rn(g0, p.std_bound), sd);
   p.gt[2L * r] = g0;
@@ -363,12 +443,17 @@ __global__ void __launch_bounds__(256) gauss_seed_kernel(GaussSeedArgs p) {
 // policy maximises the delta_index-th sorted particle (:317-330; gradient to
 // the head sort placed there), the target policy the particle mean (:339-348)
 __global__ void __launch_bounds__(256) particle_ub_seed_kernel(ParticleUbSeedArgs p) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= p.B) return;
+  __shared__ RowHeadLds hs;
+  const int r0 = blockIdx.x * kRowBlock, r = r0 + threadIdx.x;
   const int K = p.K;
+  if (p.hn.h) {   // (the target policy's seed is constant: qt is never read)
+    row_heads(p.hn, K, p.B, r0, hs);
+    __syncthreads();
+  }
+  if (threadIdx.x >= kRowBlock || r >= p.B) return;
   float v[kMaxHeads];
   int ix[kMaxHeads];
-  load_row16(p.qn + (long)r * K, K, v, ix);
+  load_row16(p.hn.h ? &hs.out[threadIdx.x][0] : p.qn + (long)r * K, K, v, ix);
   sort16(v, ix);
   const float g0 = -(1.f / (float)p.B);
   int sel = ix[0];
@@ -398,16 +483,21 @@ __global__ void __launch_bounds__(256) det_head_backward_kernel(DetHeadBwdArgs p
   dh[Da + j] = 0.f;
 }
 
+static bool head_ok(const RowHead& h) { return !h.h || (h.w && h.b && h.out && h.H >= 1); }
+
 hipError_t launch_gauss_targets(const GaussTargetArgs& a, hipStream_t s) {
-  OAC_LAUNCH(gauss_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  if (!head_ok(a.th)) return hipErrorInvalidValue;
+  OAC_LAUNCH(gauss_targets_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_gauss_seed(const GaussSeedArgs& a, hipStream_t s) {
-  OAC_LAUNCH(gauss_seed_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  if (!head_ok(a.hn)) return hipErrorInvalidValue;
+  OAC_LAUNCH(gauss_seed_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_particle_ub_seed(const ParticleUbSeedArgs& a, hipStream_t s) {
-  OAC_LAUNCH(particle_ub_seed_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  if (a.K > kMaxHeads || !head_ok(a.hn)) return hipErrorInvalidValue;
+  OAC_LAUNCH(particle_ub_seed_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_det_head_backward(const DetHeadBwdArgs& a, hipStream_t s) {
