@@ -189,6 +189,7 @@ struct ParticleTargetArgs {
 };
 struct ParticleMinArgs {
   const float* qn; int B, K;            // [B, K] Q(obs, a~) with the post-step critic
+  RowHead hn;                           // hn.h set: qn computed here (into hn.out)
   float* gq;                            // [B, K] -1/B at the argmin head
   float* qmin;                          // [B]
   // alpha update (same as CriticTargetArgs)

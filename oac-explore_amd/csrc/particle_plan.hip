@@ -160,14 +160,10 @@ static int pphase1(SacPlan& p, int flags, hipStream_t s) {
     add(gb, t_fwd(p.W(X_H1T), H, B, H, tq + L.q_fc1_w, H, H, p.W(X_H2T), H, EPI_BIAS_RELU, tq + L.q_fc1_b));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {
-    GemmBatch gb{};
-    add(gb, t_fwd(p.W(X_H2T), H, B, H, tq + L.q_last_w, H, K, p.W(OAC_WS_TQ1), K, EPI_BIAS, tq + L.q_last_b));
-    if (run_gemm(p, gb, s)) return 1;
-  }
-  {
+  {  // the target critic's K-output last layer runs inside the targets kernel (row_heads)
     ParticleTargetArgs a;
     std::memset(&a, 0, sizeof(a));
+    a.th = RowHead{p.W(X_H2T), tq + L.q_last_w, tq + L.q_last_b, p.W(OAC_WS_TQ1), H};
     a.q = p.W(OAC_WS_Q1); a.tq = p.W(OAC_WS_TQ1); a.batch = X; a.ld_batch = RS;
     a.off_rew = c.off_rew; a.off_term = c.off_term; a.reward_scale = c.reward_scale;
     a.discount = c.discount; a.B = B; a.K = K;
@@ -231,14 +227,11 @@ static int pphase2(SacPlan& p, hipStream_t s) {
     if (run_gemm(p, gb, s)) return 1;
   }
   {
-    GemmBatch gb{};
-    add(gb, t_fwd(p.W(X_H2N), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_QN1), K, EPI_BIAS, q + L.q_last_b));
-    if (run_gemm(p, gb, s)) return 1;
-  }
-  {
     ParticleMinArgs a;
     std::memset(&a, 0, sizeof(a));
     a.qn = p.W(OAC_WS_QN1); a.B = B; a.K = K; a.gq = p.W(X_GQ); a.qmin = p.W(OAC_WS_QNEW);
+    // the post-step critic's last layer on (obs, a~) runs in this kernel (row_heads)
+    a.hn = RowHead{p.W(X_H2N), q + L.q_last_w, q + L.q_last_b, p.W(OAC_WS_QN1), H};
     a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.state = p.state(); a.logp = p.W(OAC_WS_LOGP1);
     a.target_entropy = c.target_entropy; a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2;
     a.adam_eps = c.adam_eps; a.world_size = c.world_size;

@@ -198,6 +198,7 @@ __device__ __forceinline__ void load_row16(const float* src, int K, float (&v)[k
 // for the row logic and to the workspace view.  This replaces the last-layer
 // GEMM launch that otherwise sits between the hidden layer and this kernel.
 constexpr int kRowBlock = 16;
+static bool head_ok(const RowHead& h) { return !h.h || (h.w && h.b && h.out && h.H >= 1); }
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 typedef float f4a __attribute__((ext_vector_type(4), aligned(4)));
 
@@ -350,13 +351,19 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
       as->alpha = expf(la); as->grad = g; as->alpha_loss = -(la_old * S) / n;
     }
   }
-  const int r = blockIdx.x * 256 + threadIdx.x;
-  if (r >= p.B) return;
+  __shared__ RowHeadLds hs;
+  const int r0 = blockIdx.x * kRowBlock, r = r0 + threadIdx.x;
   const int K = p.K;
+  if (p.hn.h) {
+    row_heads(p.hn, K, p.B, r0, hs);
+    __syncthreads();
+  }
+  if (threadIdx.x >= kRowBlock || r >= p.B) return;
+  const float* qn = p.hn.h ? &hs.out[threadIdx.x][0] : p.qn + (long)r * K;
   int best = 0;
-  float bv = p.qn[(long)r * K];
+  float bv = qn[0];
   for (int i = 1; i < K; ++i) {
-    const float x = p.qn[(long)r * K + i];
+    const float x = qn[i];
     if (x < bv) { bv = x; best = i; }
   }
   const float invB = 1.f / (float)p.B;
@@ -365,13 +372,13 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
 }
 
 hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s) {
-  if (a.K > kMaxHeads || (a.th.h && (!a.th.w || !a.th.b || !a.th.out || a.th.H < 1)))
-    return hipErrorInvalidValue;
+  if (a.K > kMaxHeads || !head_ok(a.th)) return hipErrorInvalidValue;
   OAC_LAUNCH(particle_targets_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s) {
-  OAC_LAUNCH(particle_min_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  if (a.K > kMaxHeads || !head_ok(a.hn)) return hipErrorInvalidValue;
+  OAC_LAUNCH(particle_min_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -482,8 +489,6 @@ __global__ void __launch_bounds__(256) det_head_backward_kernel(DetHeadBwdArgs p
   dh[j] = __fmul_rn(p.da[g][idx], __fsub_rn(1.f, __fmul_rn(a, a)));
   dh[Da + j] = 0.f;
 }
-
-static bool head_ok(const RowHead& h) { return !h.h || (h.w && h.b && h.out && h.H >= 1); }
 
 hipError_t launch_gauss_targets(const GaussTargetArgs& a, hipStream_t s) {
   if (!head_ok(a.th)) return hipErrorInvalidValue;
