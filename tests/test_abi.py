@@ -69,3 +69,19 @@ def test_row_layout_keeps_critic_input_contiguous():
     r = row_layout(376, 17)
     assert r["off_act"] == r["off_obs"] + 376
     assert r["row_stride"] % 4 == 0 and r["row_stride"] >= 2 * 376 + 17 + 2
+
+
+def test_product_path_has_no_fallback(monkeypatch, tmp_path):
+    """Without the HIP library every entry point raises (no CPU fallback), and
+    the product package never imports the oracle (test infrastructure)."""
+    from oac_amd import _lib
+    monkeypatch.setattr(_lib, "_LIB", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "liboac_amd.so"))
+    with pytest.raises(RuntimeError):
+        _lib.lib()
+    pkg = os.path.join(ROOT, "oac-explore_amd", "oac_amd")
+    for f in sorted(os.listdir(pkg)):
+        if f.endswith(".py"):
+            src = open(os.path.join(pkg, f)).read()
+            assert not re.search(r"^\s*(from|import)\s+oracle\b", src, flags=re.M), f
+            assert "sac_oracle" not in src, f
