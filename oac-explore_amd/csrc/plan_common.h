@@ -149,12 +149,13 @@ static inline void read_tuning(PlanBase& p) {
   }
 }
 
-// gemm_cfg 2 (register-direct kernel, gemm_big.hip) wins on the forward
-// products (both operands k-contiguous, N >= 64: B=4096 layer 0 115 -> 80 us,
-// layer 1 64 -> 40 us) and loses on dX / dW (n- or m-contiguous operands, one
-// dword load per k) and narrow outputs; those launches run on the LDS kernel
-// backward products on the register-direct kernel at large batch
-// (OAC_BIG_BWD=0 keeps them on the LDS kernel, for A/B measurements)
+// The register-direct kernel (gemm_big.hip) runs the large-batch products
+// with N >= 64: forward batches as cfg 2 (64x32 wave blocks; B=4096 layer 0
+// 115 -> 80 us, layer 1 64 -> 40 us against the LDS kernel) and backward
+// batches -- dX / dW, batch-major operands, one dword load per lane and k --
+// as cfg 3 (32x32 wave blocks: step 2,044 -> 2,209 steps/s).  Narrow outputs
+// go to the small-batch kernel, the rest to the LDS kernel (cfg 1).
+// OAC_BIG_BWD=0 keeps the backward batches on the LDS kernel (A/B runs).
 static inline bool big_bwd() {
   static const bool v = [] { const char* e = getenv("OAC_BIG_BWD"); return !e || atoi(e) != 0; }();
   return v;
