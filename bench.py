@@ -426,7 +426,7 @@ def main():
                 out[kind] = recipe_timing(kind, args, device, rb)
                 if not args.no_cpu_baseline:
                     out[kind]["cpu_baseline"] = recipe_cpu_baseline(kind, args)
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # the CPU baseline is an N=1 figure
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     if dp:
