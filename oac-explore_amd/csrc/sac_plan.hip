@@ -534,6 +534,20 @@ static void plan_splits(SacPlan& p) {
   p.sp_ph = choose_split(c.batch, tiles(2 * Da, H + 1), p.cfg);
   p.sp_p1 = choose_split(c.batch, tiles(H, H + 1), p.cfg);
   p.sp_p0 = choose_split(c.batch, tiles(H, Do + 1), p.cfg);
+  // OAC_SPLITS="q1,q0,ph,p1,p0": forced split counts (0 = keep), tuning runs
+  if (const char* e = getenv("OAC_SPLITS")) {
+    int v[5] = {0, 0, 0, 0, 0};
+    sscanf(e, "%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4]);
+    Split* sp[5] = {&p.sp_q1, &p.sp_q0, &p.sp_ph, &p.sp_p1, &p.sp_p0};
+    const int bk = p.cfg == 0 ? 64 : 32;
+    for (int i = 0; i < 5; ++i)
+      if (v[i] > 0) {
+        int kc = (c.batch + v[i] - 1) / v[i];
+        kc = ((kc + bk - 1) / bk) * bk;
+        *sp[i] = Split{(c.batch + kc - 1) / kc, kc};
+      }
+    p.sp_ql = p.sp_q1;
+  }
   p.S_q = std::max(std::max(p.sp_q0.S, p.sp_q1.S), p.sp_ql.S);
   p.S_p = std::max(std::max(p.sp_p0.S, p.sp_p1.S), p.sp_ph.S);
 }
