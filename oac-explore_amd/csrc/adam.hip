@@ -23,10 +23,24 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(AdamArgs a) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
     float4 g;
     if (a.S > 1 || a.gslab != a.g) {
-      g = reinterpret_cast<const float4*>(a.gslab)[i];
+      // slabs summed in fixed order 0, 1, ..., S-1; the loads of 8 slabs are
+      // issued together (a one-slab-per-iteration loop waited out S
+      // dependent round trips: B=4096, S=32 -> ~11 us per launch)
+      const float4* gs = reinterpret_cast<const float4*>(a.gslab) + i;
+      const long st4 = a.slab_stride >> 2;
+      g = gs[0];
+      int k = 1;
 #pragma unroll 1
-      for (int k = 1; k < a.S; ++k) {
-        const float4 x = reinterpret_cast<const float4*>(a.gslab + (long)k * a.slab_stride)[i];
+      for (; k + 8 <= a.S; k += 8) {
+        float4 x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[j] = gs[(long)(k + j) * st4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { g.x += x[j].x; g.y += x[j].y; g.z += x[j].z; g.w += x[j].w; }
+      }
+#pragma unroll 1
+      for (; k < a.S; ++k) {
+        const float4 x = gs[(long)k * st4];
         g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
       }
       reinterpret_cast<float4*>(a.g)[i] = g;
