@@ -255,6 +255,11 @@ const float* oac_expl_outputs(oac_expl* h);
  * graph, so a call is one graph replay + one stream synchronisation (NULLs
  * switch it off) */
 int oac_expl_set_host_io(oac_expl* h, const float* host_obs, float* host_out);
+/* --trainer_UB with particle_trainer_oac.ParticleTrainer (optimistic_exploration.py:38-39
+ * -> trainer.predict(upper_bound=True), particle_trainer_oac.py:147-167): with a K-head
+ * handle, index in [0, K) makes Q_UB = sort_k(Q_k)[index] (the trainer's delta_index;
+ * beta_UB unused); -1 restores the mean + beta_UB std bound */
+int oac_expl_set_ub_index(oac_expl* h, int index);
 
 /* ---------------------------------------------------------------- errors */
 const char* oac_last_error(void);

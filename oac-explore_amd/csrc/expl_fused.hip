@@ -177,6 +177,13 @@ __global__ void __launch_bounds__(1024) oac_expl_fused_kernel(ExplFusedArgs a) {
       const float hb = a.beta_UB / 2.f;
       misc[2] = 0.5f + hb * sg;
       misc[3] = 0.5f - hb * sg;
+    } else if (a.ub_index >= 0) {   // trainer_UB: Q_UB = sort_k(q)[ub_index] -> seed 1 on
+                                    // the head ranked there (ties: lower head index first)
+      for (int k = 0; k < KQ; ++k) {
+        int rank = 0;
+        for (int j = 0; j < KQ; ++j) rank += (qk[j] < qk[k]) || (qk[j] == qk[k] && j < k);
+        wk[k] = rank == a.ub_index ? 1.f : 0.f;
+      }
     } else {         // Q_UB = mean_k q + beta std_k q (unbiased): dQ_UB/dq_k =
                      // 1/K + beta (q_k - mean) / ((K-1) std)
       float sm = 0.f;

@@ -27,6 +27,7 @@ static inline int64_t a64(int64_t x) { return (x + 63) & ~int64_t(63); }
 struct ExplPlan {
   int Do, Da, H, N = 1;
   int K = 1;   // critic heads: 1 with twin critics (q1, q2); K with one shared-layer critic (q2 null)
+  int ub_index = -1;   // K heads: sorted-head upper bound (oac_expl_set_ub_index)
   const float* pol; const float* q1; const float* q2;
   float* ws;
   StepState* state;
@@ -77,6 +78,7 @@ static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta,
   a.eps = eps; a.out = w + p.o_out; a.grad = w + p.o_grad;
   a.state = p.state; a.ticket = reinterpret_cast<unsigned*>(w + p.o_cnt);
   a.seed = p.seed; a.beta_UB = beta; a.sqrt_2delta = (float)std::sqrt(2.0 * (double)delta);
+  a.ub_index = p.ub_index;
   a.stage_clock = p.stage_clock;
   OAC_HIP_CHECK(launch_expl_fused(a, s));
   if (p.host_out)
@@ -216,6 +218,20 @@ int oac_expl_debug_stage_clock(oac_expl* h, long long* dev_buf) {
 }
 
 const float* oac_expl_outputs(oac_expl* h) { return h ? h->p.ws + h->p.o_out : nullptr; }
+
+int oac_expl_set_ub_index(oac_expl* h, int index) {
+  if (!h) { set_error("null handle"); return 1; }
+  ExplPlan& p = h->p;
+  if (index < -1 || index >= p.K || (index >= 0 && p.q2)) {
+    set_error("ub index %d: needs a K-head handle and -1 <= index < K (K = %d)", index, p.K);
+    return 1;
+  }
+  if (index == p.ub_index) return 0;
+  p.ub_index = index;
+  if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }   // re-capture
+  if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
+  return 0;
+}
 
 int oac_expl_set_host_io(oac_expl* h, const float* host_obs, float* host_out) {
   if (!h) { set_error("null handle"); return 1; }

@@ -118,6 +118,8 @@ struct ExplFusedArgs {                  // expl_fused.hip: one workgroup per obs
   StepState* state; unsigned* ticket;   // ticket: zeroed device word (re-armed by the kernel)
   unsigned long long seed;
   float beta_UB, sqrt_2delta;
+  int ub_index;                         // K heads: >= 0 -> Q_UB = sorted head ub_index
+                                        // (trainer.predict, particle_trainer_oac.py:147-167)
   long long* stage_clock;               // instrumentation (tools/expl_latency.py) or null
 };
 size_t expl_fused_lds_bytes(int Do, int Da, int H);

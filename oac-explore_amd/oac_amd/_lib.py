@@ -132,6 +132,7 @@ _SIGS = {
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "oac_expl_outputs": (ctypes.c_void_p, [ctypes.c_void_p]),
     "oac_expl_set_host_io": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "oac_expl_set_ub_index": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
 }
 
 # every symbol include/oac_amd.h declares (checked by tests/test_abi.py)

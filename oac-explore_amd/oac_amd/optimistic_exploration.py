@@ -22,7 +22,10 @@ def _owner(policy, qfs, trainer, hyper_params):
     """The oac_amd trainer whose arena holds ``policy`` and ``qfs``.  Twin
     critics take the try branch of optimistic_exploration.py:40-46 whatever
     share_layers says; one shared-layer critic with K heads takes the except
-    branch (:47-56), which only works with share_layers=True."""
+    branch (:47-56), which only works with share_layers=True.  With trainer
+    (--trainer_UB, :38-39) Q_UB is trainer.predict: for SACTrainer the same
+    twin bound (trainer/trainer.py:105-123), for the P-OAC ParticleTrainer the
+    head sorted at its delta_index (particle_trainer_oac.py:147-167)."""
     t = getattr(policy, "oac_trainer", None)
     if t is None:
         raise TypeError("get_optimistic_exploration_action: policy is not an oac_amd policy "
@@ -33,10 +36,11 @@ def _owner(policy, qfs, trainer, hyper_params):
     if trainer is not None:
         if trainer is not t:
             raise NotImplementedError("trainer_UB must be the trainer that owns the policy")
-        if not twin:
-            raise NotImplementedError("trainer_UB with a particle trainer (sorted-particle upper "
-                                      "bound, particle_trainer_oac.py:147-167) is not implemented")
-    if not twin and not hyper_params.get("share_layers", False):
+        if not twin and getattr(t, "delta_index", None) is None:
+            raise NotImplementedError("trainer_UB needs SACTrainer (twin critics) or the P-OAC "
+                                      "ParticleTrainer of particle_trainer_oac.py (sorted-head "
+                                      "upper bound, :147-167)")
+    elif not twin and not hyper_params.get("share_layers", False):
         raise ValueError("one critic with K heads needs hyper_params['share_layers'] = True "
                          "(the reference's except branch fails without it)")
     return t
@@ -47,9 +51,10 @@ def get_optimistic_exploration_action(ob_np, policy=None, qfs=None, trainer=None
                                       return_info=False):
     """optimistic_exploration.py:7-11 / 14-109 (stochastic branch).
 
-    ``trainer`` (--trainer_UB) computes the same Q_UB = mean + beta_UB*|Q1-Q2|/2
-    as the qfs branch (trainer/trainer.py:105-123), so both map to the same
-    kernel.  ``eps`` (float32[Da]) replaces the device Philox draw for parity
+    ``trainer`` (--trainer_UB): for SACTrainer the same Q_UB = mean +
+    beta_UB*|Q1-Q2|/2 as the qfs branch (trainer/trainer.py:105-123); for the
+    P-OAC ParticleTrainer the head sorted at its delta_index
+    (particle_trainer_oac.py:147-167, oac_expl_set_ub_index).  ``eps`` (float32[Da]) replaces the device Philox draw for parity
     runs; ``return_info`` adds mu_E / std / grad to the info dict."""
     if deterministic:
         raise NotImplementedError("the deterministic OAC variant is unreachable from rollout() "
@@ -57,7 +62,8 @@ def get_optimistic_exploration_action(ob_np, policy=None, qfs=None, trainer=None
     assert np.ndim(ob_np) == 1
     t = _owner(policy, qfs, trainer, hyper_params)
     a, info = _actions(t, np.asarray(ob_np)[None, :], hyper_params,
-                       None if eps is None else np.asarray(eps, np.float32)[None, :], return_info)
+                       None if eps is None else np.asarray(eps, np.float32)[None, :], return_info,
+                       trainer is not None)
     return a[0], {k: v[0] for k, v in info.items()}
 
 
@@ -70,15 +76,18 @@ def get_optimistic_exploration_actions(obs_np, policy=None, qfs=None, trainer=No
     assert np.ndim(obs_np) == 2
     t = _owner(policy, qfs, trainer, hyper_params)
     return _actions(t, np.asarray(obs_np), hyper_params,
-                    None if eps is None else np.asarray(eps, np.float32), return_info)
+                    None if eps is None else np.asarray(eps, np.float32), return_info,
+                    trainer is not None)
 
 
-def _actions(t, obs, hyper_params, eps, return_info):
+def _actions(t, obs, hyper_params, eps, return_info, trainer_ub=False):
     """One graph replay: the observations go through pinned host staging
     (uploaded and the results downloaded inside the graph, oac_expl_set_host_io),
     then one synchronisation of the trainer's stream."""
     n = obs.shape[0]
     e = t._expl_handle(n)
+    if t.layout.q2_base < 0:   # K heads: mean + beta std, or trainer.predict's sorted head
+        check(_lib.lib().oac_expl_set_ub_index(e.handle, int(t.delta_index) if trainer_ub else -1))
     e.obs_np[:, :t.obs_dim] = obs                 # float64 observations -> fp32 rows
     s = t.stream
     s.wait_stream(torch.cuda.current_stream(t.device))   # parameter writes on torch's stream

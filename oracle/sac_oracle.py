@@ -738,12 +738,17 @@ def oac_exploration_action(ob_np, P, Q1, Q2, beta_UB, delta, eps_discard, eps,
 
 
 def oac_exploration_action_shared(ob_np, P, Q, beta_UB, delta, eps_discard, eps,
-                                  dtype=torch.float32):
+                                  dtype=torch.float32, ub_index=None):
     """The same action with ONE shared-layer critic of K heads (share_layers=True,
     qfs = [qf]): qfs[1] raises, so the except branch of
     optimistic_exploration.py:47-56 takes mu_Q = mean_k Q_k, sigma_Q = std_k Q_k
     (unbiased), Q_UB = mu_Q + beta_UB sigma_Q;
-    dQ_UB/dQ_k = 1/K + beta_UB (Q_k - mu_Q) / ((K-1) sigma_Q)."""
+    dQ_UB/dQ_k = 1/K + beta_UB (Q_k - mu_Q) / ((K-1) sigma_Q).
+
+    ub_index (--trainer_UB with particle_trainer_oac.ParticleTrainer,
+    optimistic_exploration.py:38-39 -> predict, particle_trainer_oac.py:147-167):
+    Q_UB = sort_k(Q)[ub_index] (the trainer's delta_index), so the seed is 1 on
+    the head sorted there (ties: the lower head index first) and 0 elsewhere."""
     assert np.ndim(ob_np) == 1
     ob = _t(np.asarray(ob_np), dtype)[None]
     pf = policy_forward(ob, P, _t(eps_discard, dtype)[None])
@@ -752,9 +757,14 @@ def oac_exploration_action_shared(ob_np, P, Q, beta_UB, delta, eps_discard, eps,
     c = q_forward(ob, a[None], Q)
     q = c["q"][0]                                              # [K]
     K = q.shape[0]
-    mu = q.mean()
-    sd = q.std()                                               # unbiased, like torch.std
-    w = 1.0 / K + beta_UB * (q - mu) / ((K - 1) * sd)
+    if ub_index is None:
+        mu = q.mean()
+        sd = q.std()                                           # unbiased, like torch.std
+        w = 1.0 / K + beta_UB * (q - mu) / ((K - 1) * sd)
+    else:
+        order = sorted(range(K), key=lambda k: (float(q[k]), k))
+        w = torch.zeros_like(q)
+        w[order[ub_index]] = 1.0
     Do = ob.shape[1]
     ga = q_input_grad(c, w[None], Q)[0, Do:]
     grad = ga * (1 - a * a)

@@ -461,9 +461,12 @@ def gen_ptrain_all():
 
 # ------------------------------------------------------- OAC exploration
 def gen_oac_expl(name, obs_dim, act_dim, hidden, n_obs, beta_UB, delta, seed=5,
-                 pi_init_w=0.1, q_init_w=0.1, eps_seed=3, K=None):
+                 pi_init_w=0.1, q_init_w=0.1, eps_seed=3, K=None, ub_delta=None):
     """K: one shared-layer critic with K heads (share_layers=True, the except
-    branch of optimistic_exploration.py:47-56) instead of twin critics."""
+    branch of optimistic_exploration.py:47-56) instead of twin critics.
+    ub_delta: additionally pass trainer= a particle_trainer_oac.ParticleTrainer
+    built with delta=ub_delta (--trainer_UB: Q_UB = trainer.predict, the
+    sorted head delta_index, particle_trainer_oac.py:147-167)."""
     pp, qp = _producers(obs_dim, act_dim, hidden, q_out=K or 1)
     policy = pp()
     params = sac_params(obs_dim, act_dim, hidden, seed, pi_init_w=pi_init_w, q_init_w=q_init_w,
@@ -472,6 +475,16 @@ def gen_oac_expl(name, obs_dim, act_dim, hidden, n_obs, beta_UB, delta, seed=5,
     load_sd(policy, params["policy"])
     qf1 = qp()
     load_sd(qf1, params["qf1"])
+    trainer, delta_index = None, None
+    if ub_delta is not None:
+        torch.manual_seed(0)
+        trainer = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Box(-1, 1, (act_dim,)),
+                                     delta=ub_delta, optimizer_class=Adam14, q_min=0.0,
+                                     q_max=50.0, share_layers=True, deterministic=False)
+        load_sd(trainer.policy, params["policy"])
+        load_sd(trainer.qfs[0], params["qf1"])
+        policy, qf1 = trainer.policy, trainer.qfs[0]
+        delta_index = int(trainer.delta_index)
     if K is None:
         qf2 = qp()
         load_sd(qf2, params["qf2"])
@@ -498,7 +511,7 @@ def gen_oac_expl(name, obs_dim, act_dim, hidden, n_obs, beta_UB, delta, seed=5,
             EPS_LOG.clear()
             captured.clear()
             a, info = oe.get_optimistic_exploration_action(obs[i], policy=policy, qfs=qfs,
-                                                           trainer=None, hyper_params=hp)
+                                                           trainer=trainer, hyper_params=hp)
             assert len(EPS_LOG) == 2 and len(captured) == 1
             eps_d.append(EPS_LOG[0])
             eps_s.append(EPS_LOG[1])
@@ -511,7 +524,7 @@ def gen_oac_expl(name, obs_dim, act_dim, hidden, n_obs, beta_UB, delta, seed=5,
                eps_discard=np.stack(eps_d), eps=np.stack(eps_s))
     meta = dict(kind="oac_expl", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, n_obs=n_obs,
                 beta_UB=beta_UB, delta=delta, seed=seed, pi_init_w=pi_init_w, q_init_w=q_init_w,
-                K=K)
+                K=K, ub_delta=ub_delta, delta_index=delta_index)
     return meta, out
 
 
@@ -724,6 +737,9 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "oac_expl_shared":
         gen_expl_shared()
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "oac_expl_trainer_ub":
+        gen_expl_trainer_ub()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "det_snapshot":
         gen_det_snapshot(os.path.join(HERE, "goac_snapshot.pt"), "goac")
         gen_det_snapshot(os.path.join(HERE, "ptrain_snapshot.pt"), "ptrain")
@@ -783,6 +799,13 @@ def gen_expl_shared():
                                               4.66, 23.53, K=10, q_init_w=0.3))
     save("oac_expl_shared_small", *gen_oac_expl("oac_expl_shared_small", 11, 3, [32, 32], 16,
                                                 2.0, 5.0, K=4, q_init_w=0.5))
+
+
+def gen_expl_trainer_ub():
+    save("oac_expl_ub_ant", *gen_oac_expl("oac_expl_ub_ant", 111, 8, [256, 256], 16,
+                                          4.66, 23.53, K=10, q_init_w=0.3, ub_delta=0.6))
+    save("oac_expl_ub_small", *gen_oac_expl("oac_expl_ub_small", 11, 3, [32, 32], 16,
+                                            2.0, 5.0, K=4, q_init_w=0.5, ub_delta=0.75))
 
 
 def gen_goac_all():

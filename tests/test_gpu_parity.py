@@ -220,3 +220,44 @@ def test_oac_exploration_shared_matches_reference_golden(name):
     with pytest.raises(ValueError):
         get_optimistic_exploration_action(g["obs"][0], policy=tr.policy, qfs=tr.qfs,
                                           hyper_params=dict(hp, share_layers=False))
+
+
+@pytest.mark.parametrize("name", ["oac_expl_ub_ant", "oac_expl_ub_small"])
+def test_oac_exploration_trainer_ub_matches_reference_golden(name):
+    """--trainer_UB with the P-OAC ParticleTrainer (particle_trainer_oac.py:147-167):
+    Q_UB = the head sorted at delta_index.  Single calls against the reference
+    golden, the batched call bitwise equal to them, and the qfs-only call of the
+    same handle switching back to mean + beta std."""
+    from oac_amd import (ParticleTrainerOAC, get_optimistic_exploration_action,
+                         get_optimistic_exploration_actions)
+    from gpu_helpers import Space, producers
+    meta, g = parity.load(name)
+    K = meta["K"]
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                        pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"], q_out=K,
+                        q_last_bias=np.linspace(0.0, 50.0, K))
+    pp, qp = producers(params, q_keys=("qf1", "qf2", "target_qf1", "target_qf2", "qf1",
+                                       "target_qf1"))
+    tr = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Space(meta["act_dim"]),
+                            deterministic=False, q_min=0.0, q_max=50.0, share_layers=True,
+                            delta=meta["ub_delta"])
+    assert tr.delta_index == meta["delta_index"]
+    hp = dict(beta_UB=meta["beta_UB"], delta=meta["delta"], share_layers=True)
+    A, _ = get_optimistic_exploration_actions(g["obs"], policy=tr.policy, qfs=tr.qfs, trainer=tr,
+                                              hyper_params=hp, eps=g["eps"])
+    for i in range(meta["n_obs"]):
+        a, info = get_optimistic_exploration_action(g["obs"][i], policy=tr.policy, qfs=tr.qfs,
+                                                    trainer=tr, hyper_params=hp, eps=g["eps"][i],
+                                                    return_info=True)
+        assert parity.rel_err(info["std"], g["std"][i]) <= 1e-5
+        assert parity.rel_err(info["mu_E"], g["mu_E"][i]) <= parity.TOL
+        assert parity.rel_err(a, g["action"][i]) <= parity.TOL
+        np.testing.assert_array_equal(a, A[i])
+    # the same handle without trainer: the mean + beta std bound again (oracle)
+    P = so.to_torch_params(params["policy"])
+    Q = so.to_torch_params(params["qf1"])
+    a, _ = get_optimistic_exploration_action(g["obs"][0], policy=tr.policy, qfs=tr.qfs,
+                                             hyper_params=hp, eps=g["eps"][0])
+    r = so.oac_exploration_action_shared(g["obs"][0], P, Q, meta["beta_UB"], meta["delta"],
+                                         g["eps_discard"][0], g["eps"][0])
+    assert parity.rel_err(a, r["action"].numpy()) <= parity.TOL

@@ -258,3 +258,23 @@ def test_oac_exploration_shared_oracle_matches_reference_golden(name):
         assert parity.rel_err(r["std"].numpy(), g["std"][i]) <= 1e-6
         assert parity.rel_err(r["mu_E"].numpy(), g["mu_E"][i]) <= parity.TOL
         assert parity.rel_err(r["action"].numpy(), g["action"][i]) <= parity.TOL
+
+
+@pytest.mark.parametrize("name", ["oac_expl_ub_ant", "oac_expl_ub_small"])
+def test_oac_exploration_trainer_ub_oracle_matches_reference_golden(name):
+    """--trainer_UB with particle_trainer_oac.ParticleTrainer: Q_UB =
+    trainer.predict = the sorted head delta_index (particle_trainer_oac.py:147-167)."""
+    meta, g = parity.load(name)
+    K = meta["K"]
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                        pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"], q_out=K,
+                        q_last_bias=np.linspace(0.0, 50.0, K))
+    P = so.to_torch_params(params["policy"])
+    Q = so.to_torch_params(params["qf1"])
+    for i in range(meta["n_obs"]):
+        r = so.oac_exploration_action_shared(g["obs"][i], P, Q, meta["beta_UB"], meta["delta"],
+                                             g["eps_discard"][i], g["eps"][i],
+                                             ub_index=meta["delta_index"])
+        assert parity.rel_err(r["std"].numpy(), g["std"][i]) <= 1e-6
+        assert parity.rel_err(r["mu_E"].numpy(), g["mu_E"][i]) <= parity.TOL
+        assert parity.rel_err(r["action"].numpy(), g["action"][i]) <= parity.TOL
