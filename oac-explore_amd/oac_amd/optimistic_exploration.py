@@ -36,10 +36,13 @@ def _owner(policy, qfs, trainer, hyper_params):
     if trainer is not None:
         if trainer is not t:
             raise NotImplementedError("trainer_UB must be the trainer that owns the policy")
-        if not twin and getattr(t, "delta_index", None) is None:
-            raise NotImplementedError("trainer_UB needs SACTrainer (twin critics) or the P-OAC "
-                                      "ParticleTrainer of particle_trainer_oac.py (sorted-head "
-                                      "upper bound, :147-167)")
+        from .particle_trainer_oac import ParticleTrainer as _ParticleTrainerOAC
+        if not twin and not isinstance(t, _ParticleTrainerOAC):
+            # the reference fails here too: particle_trainer.py:157 / gaussian_trainer.py
+            # predict() take no upper_bound / beta_UB keywords (optimistic_exploration.py:39)
+            raise TypeError("trainer_UB needs SACTrainer (twin critics) or the P-OAC "
+                            "ParticleTrainer of particle_trainer_oac.py (sorted-head upper "
+                            "bound, :147-167); this trainer's predict() has no upper_bound")
     elif not twin and not hyper_params.get("share_layers", False):
         raise ValueError("one critic with K heads needs hyper_params['share_layers'] = True "
                          "(the reference's except branch fails without it)")
