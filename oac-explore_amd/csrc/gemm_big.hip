@@ -205,12 +205,19 @@ gemm_big_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
     rd_loop<OP_MN_R1, OP_MN, WM, WN, PF>(t, t.A, t.lda, t.B, t.ldb, t.M, nl, ones, mw, nw, k_lo, k_hi, acc);
   rd_epilogue<WM, WN>(t, mw, nw, acc, false);
   if (t.epi == EPI_BIAS_RANK_RELU) {
-    // + U V^T: U / V continue A / B along k (the batch actions follow the
+    // + U V^T: when U / V continue A / B along k (the batch actions follow the
     // observations in a replay row, the action columns follow the observation
-    // columns in W0; checked at launch), so the same accumulators run on over
-    // k in [K, K + R) -- the critic's 393-wide layer 0 with the obs-only
-    // projection P snapshotted on the way
-    rd_loop<OP_KC, OP_KC, WM, WN, PF>(t, t.A, t.lda, t.B, t.ldb, t.M, t.N, false, mw, nw, t.K, t.K + t.R, acc);
+    // columns in W0), the same accumulators run on over k in [K, K + R) --
+    // the critic's 393-wide layer 0 with the obs-only projection P
+    // snapshotted on the way
+    // (a separate rank-R operand -- the policy's action buffer a~ against the
+    // action columns of W0 -- runs the same accumulators over k in [0, R) of U / V)
+    if (t.U == t.A + t.K && t.ldu == t.lda && t.V == t.B + t.K && t.ldv == t.ldb)
+      rd_loop<OP_KC, OP_KC, WM, WN, PF>(t, t.A, t.lda, t.B, t.ldb, t.M, t.N, false, mw, nw, t.K,
+                                        t.K + t.R, acc);
+    else
+      rd_loop<OP_KC, OP_KC, WM, WN, PF>(t, t.U, t.ldu, t.V, t.ldv, t.M, t.N, false, mw, nw, 0, t.R,
+                                        acc);
     rd_epilogue<WM, WN>(t, mw, nw, acc, true);
   }
 }
@@ -248,10 +255,7 @@ hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s, bool bwd) {
     if (t.K2 > 0 || t.epi == EPI_HEAD_BWD || t.epi == EPI_BIAS_RELU_DOT || b.fuse_adam ||
         (t.b_kc && !t.a_kc) || (t.b_kc && t.a_mode != A_PLAIN))
       return hipErrorInvalidValue;   // kinds handled in gemm_big_kernel
-    if (t.epi == EPI_BIAS_RANK_RELU &&
-        (!t.C2 || t.ksplit > 1 || t.U != t.A + t.K || t.ldu != t.lda || t.V != t.B + t.K ||
-         t.ldv != t.ldb))
-      return hipErrorInvalidValue;
+    if (t.epi == EPI_BIAS_RANK_RELU && (!t.C2 || t.ksplit > 1)) return hipErrorInvalidValue;
   }
   int tb[8];
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;

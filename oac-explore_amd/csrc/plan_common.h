@@ -181,13 +181,10 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
         t.epi == EPI_BIAS_RELU_DOT || gb.fuse_adam)
       return 1;
     any_bwd |= bwd;
-    // the big kernel runs the rank-R columns as a continuation of the same
-    // row (the action stored right after the observation); a separate action
-    // buffer (the policy's a~) goes to the LDS kernel
-    if (t.epi == EPI_BIAS_RANK_RELU &&
-        (!t.C2 || t.ksplit > 1 || t.U != t.A + t.K || t.ldu != t.lda || t.V != t.B + t.K ||
-         t.ldv != t.ldb))
-      return 1;
+    // the big kernel runs the rank-R columns on the same accumulators: as a
+    // continuation of the row (the action stored right after the observation)
+    // or from a separate action buffer (the policy's a~)
+    if (t.epi == EPI_BIAS_RANK_RELU && (!t.C2 || t.ksplit > 1)) return 1;
   }
   return any_bwd ? 3 : 2;
 }
