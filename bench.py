@@ -28,10 +28,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "oac-explore_amd"))
 
 FLOP_PER_SAMPLE = 4_377_600        # algorithmic GEMM FLOPs per sample (SAC, Humanoid)
+FLOP_PER_SAMPLE_POAC_ANT = 1_792_512   # P-OAC K=10, Ant dims
 GATHER_BYTES_PER_SAMPLE = 3_081 + 4
 ADAM_BYTES_PER_STEP = 18_142_244
 PEAK_FP32_TFLOPS = 157.3           # MI355X fp32 MFMA dense peak (MI355X_MICROARCH.md)
-LAUNCH_FLOOR_US = 5.2      # grouped-GEMM launch floor in a graph chain (tools/micro, r01)
 PEAK_HBM_GBS = 8000.0
 
 
@@ -49,10 +49,14 @@ def parse():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the exploration and g-oac legs (profiling runs: keeps the "
                          "per-kernel statistics to the headline step)")
-    ap.add_argument("--cpu-steps", type=int, default=1200)
-    ap.add_argument("--cpu-threads", type=int, default=1)
     ap.add_argument("--timing-steps", type=int, default=50)
     ap.add_argument("--gemm-cfg", type=int, default=-1)
+    ap.add_argument("--mode", choices=("dropin", "ring"), default="dropin",
+                    help="dropin: the reference loop (random_batch + train per step, "
+                         "rl_algorithm.py:160-167); ring: train_from_ring with the device "
+                         "index stream, --steps-per-launch steps per graph")
+    ap.add_argument("--selftest-launcher", action="store_true",
+                    help="CPU-only check of the --gpus N rank launcher (gloo all-reduce)")
     ap.add_argument("--steps-per-launch", type=int, default=64,
                     help="gradient steps per graph launch (1 = one graph per step); the "
                          "default is the device index ring's refill period, i.e. one "
@@ -89,7 +93,7 @@ def force_dp():
 
 def build(args, rank, world, device):
     import oac_amd
-    from oac_amd import DeviceIndexStream, ReplayBufferCount, SACTrainer
+    from oac_amd import DeviceIndexStream, ReplayBuffer, SACTrainer
     torch.manual_seed(0)   # identical init on every rank
     hid = [args.hidden, args.hidden]
     pp = oac_amd.get_policy_producer(args.obs_dim, args.act_dim, hid, device=device)
@@ -103,9 +107,8 @@ def build(args, rank, world, device):
         tr = DataParallelSACTrainer(pp, qp, **kw)
     else:
         tr = SACTrainer(pp, qp, **kw)
-    # ReplayBufferCount (per-row counts for the counts=True recipe legs; the
-    # SAC step ignores them)
-    rb = ReplayBufferCount(args.replay, args.obs_dim, args.act_dim, device=device)
+    # the reference SAC / OAC recipes use the plain ReplayBuffer (main.py:179-183)
+    rb = ReplayBuffer(args.replay, args.obs_dim, args.act_dim, device=device)
     rb.load_transitions(synthetic_rows(args.replay, rb.rows, args.obs_dim, args.act_dim,
                                        device, seed=rank))
     stream = DeviceIndexStream(rb, args.batch, chunk=64, seed=1 + rank)
@@ -121,19 +124,117 @@ def step_fn(tr, rb, stream, B, n=1):
     return step
 
 
-def kernel_timing(tr, rb, stream, B, n):
-    """Per-kernel timing of n steps (direct launches on the trainer's stream):
-    every launch carries a HIP start/stop event pair recorded on its own
-    dispatch (hipExtLaunchKernel), so a duration is the kernel's begin->end
-    interval -- the one rocprofv3's kernel trace reports -- with no event
-    packets or launch gaps inside it."""
+def timed(run, steps, warmup, world, device):
+    """run(warmup), then time run(steps) between barriers + device syncs;
+    the max over ranks."""
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+            torch.cuda.synchronize()
+    run(warmup)
+    barrier()
+    t0 = time.perf_counter()
+    run(steps)
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def dropin_run(tr, rb, B):
+    def run(k):
+        for _ in range(k):
+            train_data = rb.random_batch(B)
+            train_data["buffer"] = rb
+            tr.train(train_data)
+    return run
+
+
+def roofline_of(kt, flop_per_sample, B, n):
+    gk = kt["gemm_grouped"]
+    fpl = flop_per_sample * B * n / max(gk["launches"], 1)
+    ach = fpl / (gk["avg_us"] * 1e-6) / 1e12
+    return {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4),
+            "traffic": load_traffic(B), "flops_per_launch": round(fpl),
+            "avg_launch_us": round(gk["avg_us"], 3), "launches_per_step": gk["launches"] / n}
+
+
+def batch_leg(name, tr, rb, B, steps, warmup, flop_per_sample, world, device, timing_steps=8,
+              rank=0, seed=101):
+    """The drop-in loop at another batch size on the same trainer (every rank
+    steps: at world > 1 this is the data-parallel step), with its own
+    kernel timing and roofline."""
+    np.random.seed(seed + rank)
+    el = timed(dropin_run(tr, rb, B), steps, warmup, world, device)
+    kt = kernel_timing(tr, rb, B, timing_steps)
+    v = world * steps / el
+    return {"workload": name, "steps_per_s": round(v, 1), "ms_per_step": round(1e3 * el / steps, 4),
+            "samples_per_s": round(v * B, 1), "batch_per_rank": B, "steps": steps,
+            "step_roofline_frac": round(flop_per_sample * B * v / world / 1e12 / PEAK_FP32_TFLOPS, 4),
+            "roofline": roofline_of(kt, flop_per_sample, B, timing_steps)}
+
+
+def ring_timing(tr, stream, rb, B, steps=640, n=64):
+    """train_from_ring: device MT19937 index ring, n steps per graph launch."""
+    step = step_fn(tr, rb, stream, B, n)
+
+    def run(k):
+        for _ in range(k // n):
+            step()
+    el = timed(run, steps, n, 1, None)
+    return {"steps_per_s": round(steps / el, 1), "ms_per_step": round(1e3 * el / steps, 4),
+            "steps_per_launch": n}
+
+
+def poac_ant_leg(args, device, B=4096, steps=128, warmup=16, timing_steps=8):
+    """BASELINE configs[4]: particle_trainer_oac.ParticleTrainer, K=10 shared
+    critic heads, Ant-v2 dims (obs 111, act 8), 2x256, batch 4096, replay 1e6,
+    on the drop-in loop."""
+    import oac_amd
+    from oac_amd import ParticleTrainerOAC, ReplayBuffer
+    Do, Da, K = 111, 8, 10
+    torch.manual_seed(0)
+    pp = oac_amd.get_policy_producer(Do, Da, [256, 256], device=device)
+    qp = oac_amd.get_q_producer(Do, Da, [256, 256], output_size=K, device=device)
+    tr = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Space(Da), discount=0.99,
+                            policy_lr=3e-4, qf_lr=3e-4, soft_target_tau=5e-3,
+                            use_automatic_entropy_tuning=True, deterministic=False, q_min=0.0,
+                            q_max=500.0, share_layers=True, device=device)
+    rb = ReplayBuffer(args.replay, Do, Da, device=device)
+    rb.load_transitions(synthetic_rows(args.replay, rb.rows, Do, Da, device, seed=3))
+    out = batch_leg("particle_trainer_oac K=10, Ant-v2 dims (111, 8), 2x256, batch 4096, "
+                    "replay 1e6 (BASELINE configs[4])", tr, rb, B, steps, warmup,
+                    FLOP_PER_SAMPLE_POAC_ANT, 1, device, timing_steps)
+    assert torch.isfinite(tr.params).all().item(), "non-finite P-OAC parameters"
+    del tr, rb
+    return out
+
+
+def kernel_timing(tr, rb, B, n, seed=12345):
+    """Per-kernel timing of n drop-in steps (direct launches: every launch
+    carries a HIP start/stop event pair recorded on its own dispatch,
+    hipExtLaunchKernel, so a duration is the kernel's begin->end interval --
+    the one rocprofv3's kernel trace reports -- with no event packets or
+    launch gaps inside it).  The kernels are the ones the step's graph runs."""
     from oac_amd import _lib
-    step = step_fn(tr, rb, stream, B)
-    if hasattr(tr, "capture"):
+    capture = getattr(tr, "capture", None)
+    if capture is not None:
         tr.capture = False   # data-parallel: eager phases while the per-kernel events record
+    st = np.random.get_state()
+    np.random.seed(seed)
+
+    def step():
+        b = rb.random_batch(B)
+        tr.train(b)
     step()  # build the plan
     plan = tr._last_plan
     L = _lib.lib()
+    torch.cuda.synchronize()
     _lib.check(L.oac_sac_set_timing(plan.handle, 1))
     ms = (ctypes.c_double * 4)()
     cnt = (ctypes.c_int64 * 4)()
@@ -143,19 +244,31 @@ def kernel_timing(tr, rb, stream, B, n):
     torch.cuda.synchronize()
     _lib.check(L.oac_sac_read_timing(plan.handle, ms, cnt, 4))
     _lib.check(L.oac_sac_set_timing(plan.handle, 0))
+    np.random.set_state(st)
+    if capture is not None:
+        tr.capture = capture
     names = ["gemm_grouped", "row", "adam", "gather"]
     return {names[k]: dict(ms=ms[k], launches=int(cnt[k]),
                            avg_us=1e3 * ms[k] / max(cnt[k], 1)) for k in range(4)}
 
 
-def cpu_baseline(args):
+def cpu_threads_all():
+    """All cores this process may run on (len(os.sched_getaffinity(0)), capped
+    by OMP_NUM_THREADS where the host sets it: the GPU box's CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return (min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n), n
+
+
+def cpu_baseline(args, runs=5, steps=150):
     """The oracle's PyTorch-CPU restatement of the reference step (incl. the
-    host numpy gather + fp32 conversion), timed on this host's cores."""
+    host numpy gather + fp32 conversion), timed on this host's cores: median
+    of `runs` runs of `steps` steps at 1 thread (the reference launcher's
+    torch.set_num_threads(1), launcher_util.py:90) and at all cores."""
     sys.path.insert(0, ROOT)
     from oracle import sac_oracle as so
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from fixtures_lib import sac_params
-    torch.set_num_threads(args.cpu_threads)
     Do, Da, H, B = args.obs_dim, args.act_dim, args.hidden, args.batch
     n = 100_000
     rs = np.random.RandomState(0)
@@ -173,17 +286,28 @@ def cpu_baseline(args):
         e1 = torch.randn(B, Da, generator=g)
         e2 = torch.randn(B, Da, generator=g)
         orc.step(so.NumpyReplay.to_torch(b), e1, e2)
-    for _ in range(5):
-        step()
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
-        step()
-    dt = time.perf_counter() - t0
-    return dict(value=args.cpu_steps / dt, unit="grad-steps/s", cores=args.cpu_threads,
-                kind="port",
-                sample=f"{args.cpu_steps} oracle SAC steps (Humanoid dims, 2x256, B={B}, "
-                       f"numpy f64 replay of {n} rows, torch CPU fp32, "
-                       f"{args.cpu_threads} thread(s))")
+
+    def median_rate(threads):
+        torch.set_num_threads(threads)
+        for _ in range(3):
+            step()
+        rates = []
+        for _ in range(runs):
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            rates.append(steps / (time.perf_counter() - t0))
+        return float(np.median(rates)), [round(r, 2) for r in rates]
+    one, one_runs = median_rate(1)
+    T, aff = cpu_threads_all()
+    allc, all_runs = median_rate(T)
+    torch.set_num_threads(1)
+    sample = (f"median of {runs} runs x {steps} oracle SAC steps (Humanoid dims, 2x256, B={B}, "
+              f"numpy f64 replay of {n} rows, torch CPU fp32)")
+    return dict(value=round(one, 2), unit="grad-steps/s", cores=1, kind="port",
+                sample=sample + ", 1 thread", runs=one_runs,
+                all_cores=dict(value=round(allc, 2), cores=T, affinity_cpus=aff, runs=all_runs,
+                               sample=sample + f", {T} threads"))
 
 
 def recipe_cpu_baseline(kind, args, steps=200):
@@ -194,7 +318,7 @@ def recipe_cpu_baseline(kind, args, steps=200):
     from oracle import sac_oracle as so
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from fixtures_lib import goac_params, ptrain_params
-    torch.set_num_threads(args.cpu_threads)
+    torch.set_num_threads(1)
     Do, Da, H, B = args.obs_dim, args.act_dim, args.hidden, args.batch
     n = 20_000
     rs = np.random.RandomState(0)
@@ -224,10 +348,9 @@ def recipe_cpu_baseline(kind, args, steps=200):
     for _ in range(steps):
         step()
     dt = time.perf_counter() - t0
-    return dict(value=round(steps / dt, 2), unit="grad-steps/s", cores=args.cpu_threads,
-                kind="port",
+    return dict(value=round(steps / dt, 2), unit="grad-steps/s", cores=1, kind="port",
                 sample=f"{steps} oracle {kind} steps (Humanoid dims, 2x256, B={B}, counts, "
-                       f"torch CPU fp32, {args.cpu_threads} thread(s))")
+                       f"torch CPU fp32, 1 thread)")
 
 
 def exploration_timing(tr, obs_dim, reps=200):
@@ -254,6 +377,16 @@ def exploration_timing(tr, obs_dim, reps=200):
     return {"us_per_call_1obs": round(1e6 * (t1 - t0) / reps, 1),
             "actions_per_s_64obs": round(64 * reps / (t2 - t1), 1),
             "beta_UB": 4.66, "delta": 23.53}
+
+
+def count_replay(args, device):
+    """ReplayBufferCount with the same synthetic transitions (the counts=True
+    recipes of the g-oac / p-oac legs)."""
+    from oac_amd import ReplayBufferCount
+    rb = ReplayBufferCount(args.replay, args.obs_dim, args.act_dim, device=device)
+    rb.load_transitions(synthetic_rows(args.replay, rb.rows, args.obs_dim, args.act_dim,
+                                       device, seed=0))
+    return rb
 
 
 def recipe_timing(kind, args, device, rb, steps=640, warmup=64, n=64):
@@ -312,11 +445,83 @@ def load_traffic(B):
         return None
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv=None):
+    """``bench.py --gpus N`` without a launcher: start N rank processes of this
+    script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment,
+    rendezvous on 127.0.0.1) and return the worst exit code.  The parent never
+    touches the GPU (no torch.cuda call), so the ranks start on a clean
+    device; a rank that fails takes the others down."""
+    import subprocess
+    argv = sys.argv[1:] if argv is None else argv
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + argv,
+                                      env=env))
+    rc = 0
+    pending = set(range(n))
+    while pending:
+        for r in list(pending):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            pending.discard(r)
+            if code != 0:
+                rc = rc or code
+                for q in pending:   # one rank down: the collectives of the others would hang
+                    procs[q].terminate()
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc if rc >= 0 else 1
+
+
+def launcher_selftest(args):
+    """--selftest-launcher: the N-rank launch path without a GPU (gloo): every
+    rank all-reduces its rank id, rank 0 prints the bench-shaped line."""
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    world, rank = dist.get_world_size(), dist.get_rank()
+    t = torch.tensor([float(rank)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": "launcher selftest", "n_gpus": world,
+                          "rank_sum": float(t.item())}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # started as `python bench.py --gpus N` (no torchrun): become the launcher
+        if not args.selftest_launcher and os.environ.get("OAC_BENCH_SAME_DEVICE") != "1" \
+                and torch.cuda.device_count() < args.gpus:
+            print(f"bench.py --gpus {args.gpus}: only {torch.cuda.device_count()} GPU(s) visible "
+                  "(OAC_BENCH_SAME_DEVICE=1 OAC_BENCH_BACKEND=gloo rehearses N ranks on one GPU)",
+                  file=sys.stderr)
+            sys.exit(2)
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if args.selftest_launcher:
+        launcher_selftest(args)
+        return
     # rehearsal of the N-rank path on a 1-GPU box: OAC_BENCH_BACKEND=gloo and
     # OAC_BENCH_SAME_DEVICE=1 put every rank on cuda:0 (RCCL refuses that)
     if os.environ.get("OAC_BENCH_SAME_DEVICE") == "1":
@@ -334,16 +539,32 @@ def main():
     torch.cuda.set_device(device)
     B = args.batch
     tr, rb, stream = build(args, rank, world, device)
-    # n steps per graph replay (data-parallel: the phases and RCCL all-reduces
-    # of n steps captured together, oac_amd/dp.py)
-    # (the largest n <= --steps-per-launch dividing the ring chunk, K and W, so
-    # any --steps / --warmup work; the defaults keep n = 64)
-    n = max(1, args.steps_per_launch)
-    if dp:
-        n = min(n, 8)   # data parallel: at most 8 steps (24 RCCL all-reduces) per captured graph
-    while n > 1 and (stream.chunk % n or args.steps % n or args.warmup % n):
-        n -= 1
-    step = step_fn(tr, rb, stream, B, n)
+    n = 1
+    if args.mode == "dropin":
+        # the reference's own loop, rl_algorithm.py:160-167: per step
+        # random_batch(B) (np.random.randint on numpy's global stream, rank r
+        # seeded 1 + r) and trainer.train(batch) -- no pre-drawn
+        # indices, every draw inside the timed region
+        np.random.seed(1 + rank)
+
+        def run(k):
+            for _ in range(k):
+                train_data = rb.random_batch(B)
+                train_data["buffer"] = rb
+                tr.train(train_data)
+    else:
+        # train_from_ring: device MT19937 index ring, n steps per graph launch
+        # (the largest n <= --steps-per-launch dividing the ring chunk, K and W)
+        n = max(1, args.steps_per_launch)
+        if dp:
+            n = min(n, 8)   # data parallel: at most 8 steps (24 RCCL all-reduces) per graph
+        while n > 1 and (stream.chunk % n or args.steps % n or args.warmup % n):
+            n -= 1
+        step = step_fn(tr, rb, stream, B, n)
+
+        def run(k):
+            for _ in range(k // n):
+                step()
 
     def barrier():
         torch.cuda.synchronize()
@@ -351,12 +572,10 @@ def main():
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
-    for _ in range(args.warmup // n):
-        step()
+    run(args.warmup)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps // n):
-        step()
+    run(args.steps)
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -368,13 +587,20 @@ def main():
     # sanity: the trained state is finite
     assert torch.isfinite(tr.params).all().item(), "non-finite parameters"
 
-    kt = kernel_timing(tr, rb, stream, B, args.timing_steps)   # every rank steps (collectives)
+    kt = kernel_timing(tr, rb, B, args.timing_steps)   # every rank steps (collectives)
+    # configs[2] (N = 1) / configs[3] (N > 1): the same trainer at batch 4096 per rank
+    big = None
+    if not args.no_extras and B != 4096:
+        big = batch_leg("SAC/OAC trainer step, Humanoid-v2 dims, 2x256, batch 4096 per rank, "
+                        "replay 1e6 (BASELINE configs[%d])" % (3 if world > 1 else 2),
+                        tr, rb, 4096, 96, 8, FLOP_PER_SAMPLE, world, device, rank=rank)
     out = None
     if rank == 0:
-        gk = kt["gemm_grouped"]
-        flops_per_launch = FLOP_PER_SAMPLE * B * args.timing_steps / max(gk["launches"], 1)
-        achieved = flops_per_launch / (gk["avg_us"] * 1e-6) / 1e12
-        traffic = load_traffic(B)
+        roof = roofline_of(kt, FLOP_PER_SAMPLE, B, args.timing_steps)
+        # B >= 1024: per-launch choice among gemm_big_kernel (forward),
+        # gemm_grouped_kernel (backward) and gemm_small_kernel (narrow)
+        roof["kernel"] = ("gemm_small_kernel" if B < 1024 else
+                          "gemm launches (gemm_big/gemm_grouped/gemm_small)")
         out = {
             "metric": "OAC gradient steps/sec, Humanoid-v2 dims, batch 256, 1->8 MI355X",
             "value": round(value, 2),
@@ -388,42 +614,33 @@ def main():
                        "obs_dim": args.obs_dim, "act_dim": args.act_dim,
                        "hidden": args.hidden, "batch_per_rank": B, "global_batch": B * world,
                        "replay_per_rank": args.replay,
-                       "parallelism": "dp%d" % world if dp else "single"},
+                       "parallelism": "dp%d" % world if dp else "single",
+                       "loop": ("rl_algorithm.py:160-167: random_batch(B) + train(batch) per step"
+                                if args.mode == "dropin" else
+                                "train_from_ring, %d steps per graph launch" % n)},
             "samples_per_s": round(value * B, 1),
-            "steps_per_launch": n,
-            "roofline": {"bound": "mfma",
-                         # B >= 1024: per-launch choice among gemm_big_kernel (forward),
-                         # gemm_grouped_kernel (backward) and gemm_small_kernel (narrow)
-                         "kernel": "gemm_small_kernel" if B < 1024 else
-                                   "gemm launches (gemm_big/gemm_grouped/gemm_small)",
-                         "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP32_TFLOPS, 4),
-                         "traffic": traffic,
-                         "flops_per_launch": round(flops_per_launch),
-                         "avg_launch_us": round(gk["avg_us"], 3)},
+            "mode": args.mode,
+            "roofline": roof,
             "step_roofline_frac": round(FLOP_PER_SAMPLE * B * value / world / 1e12
                                         / PEAK_FP32_TFLOPS, 5),
-            # the bound that actually applies at B=256: a dependent chain of
-            # launches, each costing at least the measured floor of a grouped
-            # GEMM launch in a hipGraph chain (tools/micro/floor_micro.hip:
-            # 5.2 us for 256 tiles of 32x32, K=256)
-            "latency_floor": {"launches_per_step": int(_launches(tr)),
-                              "floor_us_per_launch": LAUNCH_FLOOR_US,
-                              "floor_us_per_step": round(LAUNCH_FLOOR_US * _launches(tr), 2),
-                              "frac": round(LAUNCH_FLOOR_US * _launches(tr)
-                                            / (1e3 * ms_per_step), 4)},
             "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv
                             for kk, vv in v.items()} for k, v in kt.items()},
         }
+        if big is not None:
+            out["b4096"] = big
         ga, ad = kt["gather"], kt["adam"]
         if ga["launches"]:
             out["gather_GBps"] = round(GATHER_BYTES_PER_SAMPLE * B / (ga["avg_us"] * 1e-6) / 1e9, 1)
         if ad["launches"]:
             out["adam_GBps"] = round(ADAM_BYTES_PER_STEP * args.timing_steps / (ad["ms"] * 1e-3) / 1e9, 1)
         if world == 1 and not args.no_extras:
+            if args.mode == "dropin":
+                out["ring"] = ring_timing(tr, stream, rb, B)
             out["exploration"] = exploration_timing(tr, args.obs_dim)
+            out["poac_ant_b4096"] = poac_ant_leg(args, device)
+            rbc = count_replay(args, device)
             for kind in ("goac", "poac"):
-                out[kind] = recipe_timing(kind, args, device, rb)
+                out[kind] = recipe_timing(kind, args, device, rbc)
                 if not args.no_cpu_baseline:
                     out[kind]["cpu_baseline"] = recipe_cpu_baseline(kind, args)
         if not args.no_cpu_baseline and world == 1:   # the CPU baseline is an N=1 figure

@@ -154,6 +154,22 @@ int oac_sac_step(oac_sac* h, int flags, void* stream);
  * n steps.  Used by rl_algorithm-style loops that run num_trains_per_train_loop
  * steps back to back (rl_algorithm.py: trainer.train per step). */
 int oac_sac_step_n(oac_sac* h, int flags, int n_steps, void* stream);
+/* Drop-in stepping with host-drawn indices -- rl_algorithm.py:160-167 calls
+ * replay_buffer.random_batch(B) (np.random.randint on numpy's global stream,
+ * replay_buffer.py:107) and then trainer.train(batch) once per step.
+ * set_host_ring registers a pinned host staging ring [ring_slots][batch] int32
+ * (ring_slots = the handle's idx_ring slots, a multiple of 16).  step_host_idx
+ * copies the step's B int64 indices (host memory, each in [0, replay_rows))
+ * into staging slot bc % ring_slots, enqueues the H2D copy into the idx_ring
+ * slot the step's gather reads, and enqueues the captured one-step graph --
+ * all on `stream`, with no host synchronisation (a staging slot is rewritten
+ * only after the copy that last read it has completed).  bc = the device
+ * step_state batch counter at this step (the caller mirrors it). */
+int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring);
+int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags, void* stream);
+/* the staging + H2D copy of step_host_idx alone (the data-parallel step then
+ * runs its phases and all-reduces on the same stream) */
+int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream);
 /* data-parallel split (config.world_size > 1): phase 0 = forward through the
  * policy sample and the local sum(logp + target_entropy) into alpha_state[6];
  * 1 = alpha update from the caller's all-reduced sum through the critic

@@ -27,7 +27,13 @@ struct PlanBase {
   hipStream_t graph_stream = nullptr;
   int graph_flags = -1;
   int graph_n = 0;          // steps captured in the graph
+  hipStream_t cap_stream = nullptr;   // capture stream (graphs launch on the caller's stream)
   int launches = 0;
+  // drop-in host-index staging (oac_sac_set_host_ring): pinned [slots][B] int32,
+  // one completion event per 16-slot chunk
+  int32_t* host_ring = nullptr;
+  std::vector<hipEvent_t> ring_ev;
+  std::vector<char> ring_ev_set;
   // per-launch small-GEMM geometry overrides (tuning experiments: env
   // OAC_TUNE="launch:nw:gpw,..." read at plan creation; 0 = automatic)
   int tune_nw[64] = {0}, tune_gpw[64] = {0};

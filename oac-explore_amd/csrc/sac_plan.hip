@@ -585,8 +585,10 @@ int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_s
 int oac_sac_destroy(oac_sac* h) {
   if (!h) return 0;
   for (hipEvent_t e : h->plan.ev_pool) (void)hipEventDestroy(e);
+  for (hipEvent_t e : h->plan.ring_ev) (void)hipEventDestroy(e);
   if (h->plan.exec) (void)hipGraphExecDestroy(h->plan.exec);
   if (h->plan.graph) (void)hipGraphDestroy(h->plan.graph);
+  if (h->plan.cap_stream) (void)hipStreamDestroy(h->plan.cap_stream);
   delete h;
   return 0;
 }
@@ -608,15 +610,27 @@ int oac_sac_step_n(oac_sac* h, int flags, int n_steps, void* stream) {
   };
   if (!(flags & OAC_STEP_USE_GRAPH) || p.timing) return steps(flags);
   const int gflags = flags & ~OAC_STEP_USE_GRAPH;
-  if (!p.exec || p.graph_stream != s || p.graph_flags != gflags || p.graph_n != n_steps) {
+  if (!p.exec || p.graph_flags != gflags || p.graph_n != n_steps) {
     if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
     if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
     // the step sequence is static (counters live on the device), so n
-    // consecutive steps capture into one graph
-    OAC_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    const int rc = steps(gflags);
+    // consecutive steps capture into one graph.  Captured on the plan's own
+    // stream (the caller's may be the null stream, which cannot capture) and
+    // launched on the caller's.
+    if (!p.cap_stream) OAC_HIP_CHECK(hipStreamCreateWithFlags(&p.cap_stream, hipStreamNonBlocking));
+    hipStream_t cs = p.cap_stream;
+    OAC_HIP_CHECK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    const int rc = [&] {
+      for (int i = 0; i < n_steps; ++i) {
+        const int r = p.c.kind == OAC_KIND_PARTICLE ? particle_run_step(p, gflags, cs)
+                      : has_target_policy(p.c.kind) ? det_run_step(p, gflags, cs)
+                                                    : run_step(p, gflags, cs, i, n_steps);
+        if (r) return r;
+      }
+      return 0;
+    }();
     hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(s, &g);
+    const hipError_t e = hipStreamEndCapture(cs, &g);
     if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
     if (e != hipSuccess) { set_error("hipStreamEndCapture: %s", hipGetErrorString(e)); return 1; }
     p.graph = g;
@@ -630,6 +644,61 @@ int oac_sac_step_n(oac_sac* h, int flags, int n_steps, void* stream) {
 }
 
 int oac_sac_step(oac_sac* h, int flags, void* stream) { return oac_sac_step_n(h, flags, 1, stream); }
+
+static constexpr int kRingChunk = 16;
+
+int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
+  if (!h) { set_error("null handle"); return 1; }
+  SacPlan& p = h->plan;
+  if (!p.b.idx_ring || p.b.ring_slots < kRingChunk || p.b.ring_slots % kRingChunk) {
+    set_error("host ring: the handle needs an idx_ring of a multiple of %d slots", kRingChunk);
+    return 1;
+  }
+  const int nch = p.b.ring_slots / kRingChunk;
+  while ((int)p.ring_ev.size() < nch) {
+    hipEvent_t e;
+    OAC_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    p.ring_ev.push_back(e);
+  }
+  p.ring_ev_set.assign(nch, 0);
+  p.host_ring = pinned_ring;
+  return 0;
+}
+
+int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream) {
+  if (!h) { set_error("null handle"); return 1; }
+  SacPlan& p = h->plan;
+  if (!p.host_ring) { set_error("oac_sac_set_host_ring first"); return 1; }
+  if (bc < 0) { set_error("bad batch counter %lld", (long long)bc); return 1; }
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int B = p.c.batch, S = p.b.ring_slots;
+  const int slot = (int)(bc % S), ch = slot / kRingChunk;
+  // first slot of a chunk: the copies that read this chunk S steps ago are done
+  if (slot % kRingChunk == 0 && p.ring_ev_set[ch]) OAC_HIP_CHECK(hipEventSynchronize(p.ring_ev[ch]));
+  int32_t* dst = p.host_ring + (long)slot * B;
+  const int64_t rows = p.b.replay_rows;
+  for (int i = 0; i < B; ++i) {
+    const int64_t v = idx[i];
+    if (v < 0 || v >= rows) {   // the gather would read outside the replay
+      set_error("index %lld of step %lld outside the replay [0, %lld)", (long long)v,
+                (long long)bc, (long long)rows);
+      return 1;
+    }
+    dst[i] = (int32_t)v;
+  }
+  OAC_HIP_CHECK(hipMemcpyAsync(const_cast<int32_t*>(p.b.idx_ring) + (long)slot * B, dst,
+                               sizeof(int32_t) * B, hipMemcpyHostToDevice, s));
+  if (slot % kRingChunk == kRingChunk - 1 || slot == S - 1) {
+    OAC_HIP_CHECK(hipEventRecord(p.ring_ev[ch], s));
+    p.ring_ev_set[ch] = 1;
+  }
+  return 0;
+}
+
+int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags, void* stream) {
+  if (oac_sac_stage_host_idx(h, idx, bc, stream)) return 1;
+  return oac_sac_step_n(h, flags | OAC_STEP_GATHER | OAC_STEP_USE_GRAPH, 1, stream);
+}
 
 int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
   if (!h) { set_error("null handle"); return 1; }

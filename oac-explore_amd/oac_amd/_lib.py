@@ -81,6 +81,11 @@ _SIGS = {
                                       ctypes.c_void_p]),
     "oac_sac_step_phase": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_void_p]),
+    "oac_sac_set_host_ring": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "oac_sac_step_host_idx": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                             ctypes.c_int, ctypes.c_void_p]),
+    "oac_sac_stage_host_idx": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                              ctypes.c_void_p]),
     "oac_sac_workspace_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
                                               ctypes.POINTER(ctypes.c_int64),
                                               ctypes.POINTER(ctypes.c_int64),

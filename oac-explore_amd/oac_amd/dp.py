@@ -22,6 +22,9 @@ checks this with the CPU oracle over gloo).
 below (liboac_amd phases + torch.distributed over RCCL) and, in the CPU
 tests, with an oracle-backed executor over gloo.
 """
+import ctypes
+
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -108,9 +111,31 @@ class _DataParallel:
         for _ in range(n_steps):
             dp_step(ex, self._all_reduce)
 
+    def _train_host_indices(self, dbatch):
+        """The drop-in call (random_batch + train per step) at world > 1: this
+        rank's host-drawn indices are staged into the pinned ring and copied to
+        the device index ring on the trainer stream, then the captured
+        one-step data-parallel graph (phases + the three all-reduces) runs."""
+        plan = self._dropin_plan(dbatch)
+        if self._bc_mirror is None:
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+            self._bc_mirror = int(self.step_state[1].item())
+        idx = dbatch.host_indices
+        if idx.dtype != np.int64 or not idx.flags.c_contiguous:
+            idx = np.ascontiguousarray(idx, dtype=np.int64)
+        bc = self._bc_mirror
+
+        def stage(sp):
+            check(_lib.lib().oac_sac_stage_host_idx(plan.handle, ctypes.c_void_p(idx.ctypes.data),
+                                                    bc, sp))
+        self._run(plan, _lib.OAC_STEP_GATHER, n_steps=1, pre=stage)
+        self._bc_mirror = bc + 1
+
     def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None, n_steps=1,
-             counts=None):
+             counts=None, pre=None):
         def go(sp):
+            if pre is not None:
+                pre(sp)
             f = flags
             if batch is not None:
                 self._pack_batch(plan, batch)
@@ -142,6 +167,8 @@ class _DataParallel:
                 g.replay()
         self._on_stream(go)
         self._last_plan = plan
+        if self._bc_mirror is not None:
+            self._bc_mirror += n_steps
         if self._need_to_update_eval_statistics:
             self._need_to_update_eval_statistics = False
             self._fill_eval_statistics(plan)

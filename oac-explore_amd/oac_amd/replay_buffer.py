@@ -48,11 +48,22 @@ class DeviceBatch(dict):
 
     device_gather = True
 
-    def __init__(self, buffer, indices):
+    def __init__(self, buffer, indices=None, host_indices=None):
         super().__init__()
-        self._buffer, self.indices = buffer, indices
+        self._buffer, self._indices = buffer, indices
+        # host_indices: the np.random.randint draw itself (int64); the trainer
+        # stages it through pinned memory inside its step (no pageable copy)
+        self.host_indices = host_indices
         self.storage = buffer._storage
-        self.batch_size = int(indices.numel())
+        self.batch_size = int(indices.numel() if indices is not None else len(host_indices))
+
+    @property
+    def indices(self):
+        """The drawn indices as a device int32 tensor (uploaded on first use)."""
+        if self._indices is None:
+            self._indices = torch.from_numpy(self.host_indices.astype(np.int32)).to(
+                self._buffer.device)
+        return self._indices
 
     def __missing__(self, key):
         if key not in BATCH_KEYS:
@@ -195,11 +206,8 @@ class ReplayBuffer(object):
     def random_batch(self, batch_size):
         """replay_buffer.py:106-115."""
         if self.index_source == "device":
-            idx = self.sample_indices_device(batch_size)
-        else:
-            idx_np = np.random.randint(0, self._size, batch_size)
-            idx = torch.from_numpy(idx_np.astype(np.int32)).to(self.device, non_blocking=True)
-        return DeviceBatch(self, idx)
+            return DeviceBatch(self, self.sample_indices_device(batch_size))
+        return DeviceBatch(self, host_indices=np.random.randint(0, self._size, batch_size))
 
     def gather(self, indices):
         out = torch.empty(indices.numel(), self.rows["row_stride"], dtype=torch.float32,

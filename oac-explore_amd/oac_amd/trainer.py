@@ -156,6 +156,7 @@ class _ArenaTrainer(object):
         self.step_state = torch.zeros(16, dtype=torch.int64, device=device)
         self.log_alpha = self.alpha_state[0:1]
         self._plans = {}
+        self._bc_mirror = None   # host copy of step_state.batch_counter (drop-in path)
         self._idx = None
         self._expl = None
         self._last_plan = None
@@ -230,7 +231,7 @@ class _ArenaTrainer(object):
     def __del__(self):
         try:
             L = _lib.lib()
-            for p in self._plans.values():
+            for p in self._plans.values():   # (the drop-in plans are among them)
                 L.oac_sac_destroy(p.handle)
             for e in (self._expl or {}).values():
                 L.oac_expl_destroy(e.handle)
@@ -278,6 +279,8 @@ class _ArenaTrainer(object):
                 check(_lib.lib().oac_sac_step_n(plan.handle, f, n_steps, sp))
         self._on_stream(go)
         self._last_plan = plan
+        if self._bc_mirror is not None:
+            self._bc_mirror += n_steps
         if self._need_to_update_eval_statistics:
             self._need_to_update_eval_statistics = False
             self._fill_eval_statistics(plan)
@@ -311,7 +314,53 @@ class _ArenaTrainer(object):
             raise KeyError("counts=True needs batch['counts'] (ReplayBufferCount)")
         return batch["counts"]
 
+    # host-index drop-in ring: slots of the pinned staging / device index ring
+    # (a multiple of the library's 16-slot completion chunk)
+    _DROPIN_SLOTS = 128
+
+    def _dropin_plan(self, dbatch):
+        """Plan + rings of the drop-in path for this (batch size, replay store)."""
+        key = (dbatch.batch_size, dbatch.storage.data_ptr())
+        if not hasattr(self, "_dropin"):
+            self._dropin = {}
+        d = self._dropin.get(key)
+        if d is None:
+            S, B = self._DROPIN_SLOTS, dbatch.batch_size
+            ring = torch.zeros(S * B, dtype=torch.int32, device=self.device)
+            pinned = torch.zeros(S * B, dtype=torch.int32, pin_memory=True)
+            d = self._plan(B, replay=dbatch.storage, idx=ring, ring_slots=S)
+            check(_lib.lib().oac_sac_set_host_ring(d.handle, ctypes.c_void_p(pinned.data_ptr())))
+            d.rings = (ring, pinned)   # keep both alive with the plan
+            self._dropin[key] = d
+        return d
+
+    def _train_host_indices(self, dbatch):
+        """rl_algorithm.py:160-167 as the reference calls it: random_batch drew
+        the indices on numpy's global stream; this call stages them through a
+        pinned ring and enqueues copy + one-step graph on torch's current
+        stream (ordered after replay inserts and before any later use of the
+        parameters, with no host synchronisation)."""
+        plan = self._dropin_plan(dbatch)
+        if self._bc_mirror is None:   # device batch counter (one read after other paths ran)
+            torch.cuda.current_stream(self.device).wait_stream(self.stream)
+            self._bc_mirror = int(self.step_state[1].item())
+        idx = dbatch.host_indices
+        if idx.dtype != np.int64 or not idx.flags.c_contiguous:
+            idx = np.ascontiguousarray(idx, dtype=np.int64)
+        check(_lib.lib().oac_sac_step_host_idx(
+            plan.handle, ctypes.c_void_p(idx.ctypes.data), self._bc_mirror,
+            _lib.OAC_STEP_DEVICE_EPS, stream_ptr(torch.cuda.current_stream(self.device))))
+        self._bc_mirror += 1
+        self._last_plan = plan
+        if self._need_to_update_eval_statistics:
+            self._need_to_update_eval_statistics = False
+            self._fill_eval_statistics(plan)
+        self._n_train_steps_total += 1
+
     def train_device_batch(self, dbatch, eps1=None, eps2=None):
+        if (dbatch.host_indices is not None and eps1 is None and self.use_graph
+                and self._batch_counts(dbatch) is None and not getattr(self, "_no_dropin", False)):
+            return self._train_host_indices(dbatch)
         B = dbatch.batch_size
         if self._idx is None or self._idx.numel() != B:
             self._idx = torch.zeros(B, dtype=torch.int32, device=self.device)

@@ -81,6 +81,34 @@ def rel_err(got, ref):
     return d / n
 
 
+def relu_boundary_units(x, W, b, tol=1e-5):
+    """Hidden units j of relu(x W^T + b) with a pre-activation within
+    tol * rms(pre) of 0 for some row (float64).  There the fp32 sign -- the
+    ReLU mask -- depends on the summation order, so two correct fp32
+    implementations may disagree on that one (row, unit) entry: the weight
+    gradient row j then differs by one sample's contribution."""
+    pre = np.asarray(x, np.float64) @ np.asarray(W, np.float64).T + np.asarray(b, np.float64)
+    rms = np.sqrt(np.mean(pre * pre))
+    return sorted(set(np.nonzero(np.abs(pre) < tol * rms)[1].tolist())), pre
+
+
+def rel_err_rows(got, ref, rows_allowed, gate=1e-5, max_rows=2):
+    """Norm-relative error of a [units, ...] gradient, where rows listed in
+    ``rows_allowed`` (ReLU boundary units, relu_boundary_units) may be left
+    out -- and only if the tensor fails the gate with them in.  Returns
+    (error, rows left out)."""
+    got = np.asarray(got, np.float64)
+    ref = np.asarray(ref, np.float64)
+    e = rel_err(got, ref)
+    if e <= gate or not rows_allowed:
+        return e, []
+    d = np.abs(got - ref).reshape(got.shape[0], -1).max(axis=1)
+    bad = [int(j) for j in np.argsort(d)[::-1][:max_rows] if j in rows_allowed]
+    keep = np.ones(got.shape[0], bool)
+    keep[bad] = False
+    return rel_err(got[keep], ref[keep]), bad
+
+
 def compare(gold, key, got):
     """Return the error of ``got`` against the golden entry ``key``:
     full tensors -> norm-relative error; sampled -> max(norm error, relative

@@ -193,3 +193,172 @@ def test_dp_rccl_graph_capture_single_rank_equals_single_gpu():
     assert n_graphs == 1
     want = _ring_run(_trainer(False), 4, 4)
     assert parity.rel_err(got, want) < 1e-6, parity.rel_err(got, want)
+
+
+# ---------------------------------------------------------------- configs[3]
+# BASELINE configs[3] at its per-rank scale: Humanoid dims, 2x256 MLPs, per-rank
+# batch 4096, two ranks (gloo on one GPU).  The data-parallel HIP step must
+# equal the single-GPU step on the concatenated 8,192-row batch, and both the
+# CPU oracle on that batch (SURVEY 8e "Parity for DP").
+HD, HA, HH, HB = 376, 17, 256, 4096
+
+
+def _h_inputs(world, steps=2):
+    data = synthetic_transitions(3 * HB * world, HD, HA, seed=0)
+    rs = np.random.RandomState(9)
+    out = []
+    for _ in range(steps):
+        idx = rs.randint(0, len(data["rewards"]), HB * world)
+        e1 = rs.standard_normal((HB * world, HA)).astype(np.float32)
+        e2 = rs.standard_normal((HB * world, HA)).astype(np.float32)
+        out.append(({k: v[idx] for k, v in data.items()}, e1, e2))
+    return out
+
+
+def _h_trainer(dp):
+    from gpu_helpers import producers, Space
+    from oac_amd import SACTrainer
+    from oac_amd.dp import DataParallelSACTrainer
+    pp, qp = producers(sac_params(HD, HA, [HH, HH], 4, pi_init_w=1e-3, q_init_w=3e-3))
+    cls = DataParallelSACTrainer if dp else SACTrainer
+    return cls(pp, qp, action_space=Space(HA), discount=0.99, reward_scale=1.0, policy_lr=3e-4,
+               qf_lr=3e-4, soft_target_tau=5e-3, use_automatic_entropy_tuning=True)
+
+
+def _flat_state(tr):
+    return torch.cat([tr.params, tr.targets, tr.alpha_state[:4]]).cpu().numpy()
+
+
+def _h_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    tr = _h_trainer(True)
+    grads0 = None
+    for step, (batch, e1, e2) in enumerate(_h_inputs(world)):
+        sl = slice(rank * HB, (rank + 1) * HB)
+        tr.train_from_torch({k: v[sl] for k, v in batch.items()}, eps1=e1[sl], eps2=e2[sl])
+        if step == 0:   # the all-reduced SUM of the ranks' gradients
+            grads0 = (tr.grads / world).cpu().numpy()
+    torch.cuda.synchronize()
+    if rank == 0:
+        q.put((grads0, _flat_state(tr)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_humanoid_b4096_two_ranks_equals_single_gpu_and_oracle():
+    from gpu_helpers import module_tensors
+    from oracle import sac_oracle as so
+    world = 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    procs = [ctx.Process(target=_h_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    dp_grads0, dp_state = q.get()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    inputs = _h_inputs(world)
+    tr = _h_trainer(False)
+    single_grads0 = None
+    for step, (batch, e1, e2) in enumerate(inputs):
+        tr.train_from_torch(batch, eps1=e1, eps2=e2)
+        if step == 0:
+            single_grads0 = tr.grads.clone()
+    torch.cuda.synchronize()
+    # DP == single GPU on the global batch
+    assert parity.rel_err(dp_grads0, single_grads0.cpu().numpy()) < 1e-5
+    assert parity.rel_err(dp_state, _flat_state(tr)) < 1e-5
+    # both == the CPU oracle on the global batch, per tensor (step 0 gradients)
+    orc = so.SACOracle(sac_params(HD, HA, [HH, HH], 4, pi_init_w=1e-3, q_init_w=3e-3), HD, HA,
+                       policy_lr=3e-4, qf_lr=3e-4, tau=5e-3)
+    batch, e1, e2 = inputs[0]
+    out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
+    dp_view = torch.from_numpy(dp_grads0).to(tr.grads.device)
+    # ReLU-boundary entries of the critics' hidden layers (parity.relu_boundary_units):
+    # the only rows a correct fp32 step may disagree on at this batch size
+    prm = sac_params(HD, HA, [HH, HH], 4, pi_init_w=1e-3, q_init_w=3e-3)
+    x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
+    allowed = {}
+    for grp in ("qf1", "qf2"):
+        q = prm[grp]
+        u0, pre0 = parity.relu_boundary_units(x0, q["fc0.weight"], q["fc0.bias"])
+        u1, _ = parity.relu_boundary_units(np.maximum(pre0, 0), q["fc1.weight"], q["fc1.bias"])
+        allowed[grp] = {"fc0.weight": u0, "fc0.bias": u0, "fc1.weight": u1, "fc1.bias": u1}
+    left_out = {}
+    for grp, mod in (("policy", tr.policy), ("qf1", tr.qf1), ("qf2", tr.qf2)):
+        got_single = module_tensors(tr, mod, single_grads0)
+        got_dp = module_tensors(tr, mod, dp_view)
+        for name, ref in out["grads"][grp].items():
+            ref = ref.numpy()
+            rows = allowed.get(grp, {}).get(name, [])
+            for tag, got in (("single", got_single), ("dp", got_dp)):
+                e, bad = parity.rel_err_rows(got[name].cpu().numpy(), ref, rows)
+                assert e < 1e-5, (tag, grp, name, e, rows)
+                if bad:
+                    left_out[(tag, grp, name)] = bad
+    print("ReLU-boundary rows left out:", left_out)
+
+
+def _dropin_worker(rank, world, port, q, dropin):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oac_amd import ReplayBuffer
+    from gpu_helpers import Space
+    tr = _trainer(True)
+    tr._no_dropin = not dropin   # False: the device-index path (indices uploaded, no ring)
+    rb = ReplayBuffer(500, Space(Do), Space(Da), device="cuda:0")
+    d = synthetic_transitions(500, Do, Da, seed=rank)
+    rb.add_paths([dict(observations=d["observations"], actions=d["actions"],
+                       rewards=d["rewards"], next_observations=d["next_observations"],
+                       terminals=d["terminals"])])
+    np.random.seed(1 + rank)
+    for _ in range(140):        # past the 128-slot staging ring
+        b = rb.random_batch(BL)
+        b["buffer"] = rb
+        tr.train(b)
+    torch.cuda.synchronize()
+    if rank == 0:
+        q.put(torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_dropin_loop_equals_device_index_path():
+    """rl_algorithm.py:160-167 on every rank (own replay shard, own numpy
+    seed): the staged host-index path equals the device-index path."""
+    world = 2
+    got = {}
+    for dropin in (True, False):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        ctx = mp.get_context("spawn")
+        q = ctx.SimpleQueue()
+        procs = [ctx.Process(target=_dropin_worker, args=(r, world, port, q, dropin))
+                 for r in range(world)]
+        for p in procs:
+            p.start()
+        got[dropin] = q.get()
+        for p in procs:
+            p.join(timeout=300)
+            assert p.exitcode == 0
+    assert np.array_equal(got[True], got[False])
