@@ -188,6 +188,9 @@ int oac_sac_launch_count(oac_sac* h);
  * kernels, 2 fused Adam, 3 gather. */
 int oac_sac_set_timing(oac_sac* h, int enable);
 int oac_sac_read_timing(oac_sac* h, double* ms_by_kind, int64_t* count_by_kind, int nkinds);
+/* the same timing per launch, in issue order (before read_timing resets it):
+ * returns the number of launches written (<= max_n), -1 on error */
+int oac_sac_read_launch_times(oac_sac* h, double* ms, int* kinds, int max_n);
 
 /* ---------------------------------------------------------------- replay */
 /* numpy legacy seeding (init_genrand) of a 625-word MT19937 state, on the host */

@@ -751,6 +751,22 @@ int oac_sac_set_timing(oac_sac* h, int enable) {
   return 0;
 }
 
+int oac_sac_read_launch_times(oac_sac* h, double* ms, int* kinds, int max_n) {
+  if (!h) { set_error("null handle"); return -1; }
+  SacPlan& p = h->plan;
+  int n = 0;
+  for (auto& pr : p.ev_pending) {
+    if (n >= max_n) break;
+    float t = 0.f;
+    OAC_HIP_CHECK(hipEventSynchronize(p.ev_pool[pr.second + 1]));
+    OAC_HIP_CHECK(hipEventElapsedTime(&t, p.ev_pool[pr.second], p.ev_pool[pr.second + 1]));
+    ms[n] = t;
+    kinds[n] = pr.first;
+    ++n;
+  }
+  return n;
+}
+
 int oac_sac_read_timing(oac_sac* h, double* ms_by_kind, int64_t* count_by_kind, int nkinds) {
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
