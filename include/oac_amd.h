@@ -280,6 +280,30 @@ int oac_expl_set_host_io(oac_expl* h, const float* host_obs, float* host_out);
  * beta_UB unused); -1 restores the mean + beta_UB std bound */
 int oac_expl_set_ub_index(oac_expl* h, int index);
 
+/* ----------------------------------------------------- network evaluation */
+/* Row-wise forward of the trainer's networks outside the gradient step, one
+ * workgroup per (row, network).  offsets = {fc0.weight, fc0.bias, fc1.weight,
+ * fc1.bias, last_fc.weight, last_fc.bias} inside each parameter block
+ * (oac_sac_layout q_* or pol_* fields; the policy's last_fc is the stacked
+ * [2*act_dim, hidden] head).
+ * oac_critic_eval: FlattenMlp(obs, act) (networks.py:154-161) of n_nets (1 or 2)
+ * critic blocks -> q [n, n_nets*q_out]; jac (optional) [n, n_nets*q_out,
+ * obs_dim+act_dim] = d q / d [obs | act], for SACTrainer.predict /
+ * ParticleTrainer.predict whose Q_UB the exploration differentiates
+ * (trainer/trainer.py:105-123, particle_trainer_oac.py:147-167,
+ * optimistic_exploration.py:39,64). */
+int oac_critic_eval(const float* const* nets, int n_nets, const int64_t* offsets, int obs_dim,
+                    int act_dim, int hidden, int q_out, const float* obs, int64_t ld_obs,
+                    const float* act, int64_t ld_act, int n, float* q, float* jac, void* stream);
+/* TanhGaussianPolicy.forward (trainer/policies.py:260-316) of n rows: eps
+ * [n, act_dim] standard normals (stochastic) or NULL (deterministic: tanh(mean));
+ * outputs [n, act_dim] action, mean, log_std (clamped), std, pre_tanh (z), and
+ * log_prob [n] (summed over the action dims; may be NULL) */
+int oac_policy_eval(const float* net, const int64_t* offsets, int obs_dim, int act_dim, int hidden,
+                    const float* obs, int64_t ld_obs, int n, const float* eps, float* action,
+                    float* mean, float* log_std, float* log_prob, float* std_out, float* pre_tanh,
+                    void* stream);
+
 /* ---------------------------------------------------------------- errors */
 const char* oac_last_error(void);
 int oac_abi_version(void);

@@ -40,11 +40,22 @@ struct ExplPlan {
   // captured into the graph
   const float* host_obs = nullptr; float* host_out = nullptr;
   long long* stage_clock = nullptr;   // instrumentation: per-stage wall clock of row 0
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
-  hipStream_t gstream = nullptr;
-  const float* g_eps = nullptr;
-  float g_beta = NAN, g_delta = NAN;
+  // captured call graphs by (eps slot, beta_UB, delta, ub_index): alternating
+  // bounds on one handle (e.g. --trainer_UB and plain calls) replay their own
+  // graph instead of re-capturing
+  struct Graph {
+    hipGraph_t g; hipGraphExec_t e;
+    const float* eps; float beta, delta; int ub;
+  };
+  Graph graphs[4];
+  int n_graphs = 0, next_evict = 0;
+  void drop_graphs() {
+    for (int i = 0; i < n_graphs; ++i) {
+      (void)hipGraphExecDestroy(graphs[i].e);
+      (void)hipGraphDestroy(graphs[i].g);
+    }
+    n_graphs = 0; next_evict = 0;
+  }
 };
 
 static void expl_layout(ExplPlan& p) {
@@ -169,8 +180,7 @@ int oac_expl_create(int obs_dim, int act_dim, int hidden, const float* policy, c
 
 int oac_expl_destroy(oac_expl* h) {
   if (!h) return 0;
-  if (h->p.exec) (void)hipGraphExecDestroy(h->p.exec);
-  if (h->p.graph) (void)hipGraphDestroy(h->p.graph);
+  h->p.drop_graphs();
   delete h;
   return 0;
 }
@@ -182,22 +192,36 @@ int oac_expl_action(oac_expl* h, const float* eps, float beta_UB, float delta, f
   if (!h) { set_error("null handle"); return 1; }
   ExplPlan& p = h->p;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const bool same = p.exec && p.gstream == s && p.g_eps == eps && p.g_beta == beta_UB &&
-                    p.g_delta == delta;
-  if (!same) {
-    if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
-    if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
+  int gi = -1;
+  for (int i = 0; i < p.n_graphs && gi < 0; ++i) {
+    const ExplPlan::Graph& g = p.graphs[i];
+    if (g.eps == eps && g.beta == beta_UB && g.delta == delta && g.ub == p.ub_index) gi = i;
+  }
+  if (gi < 0) {
     OAC_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     const int rc = expl_sequence(p, eps, beta_UB, delta, s);
     hipGraph_t g = nullptr;
     const hipError_t e = hipStreamEndCapture(s, &g);
     if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
     if (e != hipSuccess) { set_error("hipStreamEndCapture: %s", hipGetErrorString(e)); return 1; }
-    p.graph = g;
-    OAC_HIP_CHECK(hipGraphInstantiate(&p.exec, p.graph, nullptr, nullptr, 0));
-    p.gstream = s; p.g_eps = eps; p.g_beta = beta_UB; p.g_delta = delta;
+    hipGraphExec_t ex = nullptr;
+    const hipError_t ie = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    if (ie != hipSuccess) {
+      (void)hipGraphDestroy(g);
+      set_error("hipGraphInstantiate: %s", hipGetErrorString(ie));
+      return 1;
+    }
+    if (p.n_graphs < 4) {
+      gi = p.n_graphs++;
+    } else {   // evict round-robin
+      gi = p.next_evict;
+      p.next_evict = (p.next_evict + 1) % 4;
+      (void)hipGraphExecDestroy(p.graphs[gi].e);
+      (void)hipGraphDestroy(p.graphs[gi].g);
+    }
+    p.graphs[gi] = ExplPlan::Graph{g, ex, eps, beta_UB, delta, p.ub_index};
   }
-  OAC_HIP_CHECK(hipGraphLaunch(p.exec, s));
+  OAC_HIP_CHECK(hipGraphLaunch(p.graphs[gi].e, s));
   const size_t nb = sizeof(float) * p.Da * p.N;
   const float* o = p.ws + p.o_out;
   if (action) OAC_HIP_CHECK(hipMemcpyAsync(action, o, nb, hipMemcpyDeviceToDevice, s));
@@ -212,8 +236,7 @@ int oac_expl_action(oac_expl* h, const float* eps, float beta_UB, float delta, f
 int oac_expl_debug_stage_clock(oac_expl* h, long long* dev_buf) {
   if (!h) return 1;
   h->p.stage_clock = dev_buf;
-  if (h->p.exec) { (void)hipGraphExecDestroy(h->p.exec); h->p.exec = nullptr; }
-  if (h->p.graph) { (void)hipGraphDestroy(h->p.graph); h->p.graph = nullptr; }
+  h->p.drop_graphs();
   return 0;
 }
 
@@ -226,10 +249,7 @@ int oac_expl_set_ub_index(oac_expl* h, int index) {
     set_error("ub index %d: needs a K-head handle and -1 <= index < K (K = %d)", index, p.K);
     return 1;
   }
-  if (index == p.ub_index) return 0;
-  p.ub_index = index;
-  if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }   // re-capture
-  if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
+  p.ub_index = index;   // selects (or captures) the call graph of this bound
   return 0;
 }
 
@@ -237,8 +257,7 @@ int oac_expl_set_host_io(oac_expl* h, const float* host_obs, float* host_out) {
   if (!h) { set_error("null handle"); return 1; }
   ExplPlan& p = h->p;
   p.host_obs = host_obs; p.host_out = host_out;
-  if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }   // re-capture
-  if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
+  p.drop_graphs();   // re-capture with the new staging
   return 0;
 }
 

@@ -125,6 +125,20 @@ struct ExplFusedArgs {                  // expl_fused.hip: one workgroup per obs
 size_t expl_fused_lds_bytes(int Do, int Da, int H);
 hipError_t launch_expl_fused(const ExplFusedArgs& a, hipStream_t s);
 
+// row-wise network evaluation off the gradient step (mlp_eval.hip)
+struct MlpEvalArgs {
+  const float* x0; long ld_x0; int d0;   // input = [x0 | x1] per row
+  const float* x1; long ld_x1; int d1;
+  const float* net[2]; int n_nets;       // parameter blocks
+  long w0, b0, w1, b1, wl, bl;           // layer offsets inside a block
+  int H, Q, N;                           // hidden width, outputs, rows
+  float* out; long ld_out;               // critic: [N, n_nets*Q]
+  float* jac;                            // critic: [N, n_nets*Q, d0+d1] d out / d input, or null
+  // policy outputs ([N, Q/2] each; log_prob [N] or null); eps null = deterministic
+  const float* p_eps;
+  float* p_action; float* p_mean; float* p_log_std; float* p_log_prob; float* p_std; float* p_pre_tanh;
+};
+
 // ------------------------------------------------------------ replay/adam
 struct GatherArgs {
   const float* replay; long row_stride;   // [N, row_stride]

@@ -96,6 +96,15 @@ _SIGS = {
                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
     "oac_sac_read_launch_times": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                                  ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    "oac_critic_eval": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "oac_policy_eval": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]),
     "oac_mt_seed_host": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_void_p]),
     "oac_replay_sample_indices": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                                  ctypes.c_void_p, ctypes.c_void_p]),

@@ -8,15 +8,22 @@ and registration order (``fc0, fc1, ..., last_fc[, last_fc_log_std]`` --
 ``state_dict()`` / ``load_state_dict()`` / snapshots are interchangeable with
 the reference's modules.
 
-Their ``forward`` is the plain torch expression of the same math; it exists
-for the callers outside the gradient-step hot path (evaluation rollouts via
-``MakeDeterministic``, ``policy.get_action``).  The hot path itself -- the
-gradient step and the optimistic exploration action -- runs in liboac_amd.
+Their ``forward`` (evaluation rollouts via ``MakeDeterministic``,
+``policy.get_action``, ``trainer.predict``, user code) runs on liboac_amd's
+row-wise network kernels (csrc/mlp_eval.hip); the critic forward is
+differentiable w.r.t. its inputs (the kernel also returns d q / d [obs, act],
+which the reference's exploration takes the gradient of:
+optimistic_exploration.py:39, 64).  The gradient step and the optimistic
+exploration action themselves run in liboac_amd's step / exploration plans.
 """
+import ctypes
+
 import numpy as np
 import torch
 from torch import nn
 import torch.nn.functional as F
+
+from . import _lib
 
 LOG_SIG_MAX = 2
 LOG_SIG_MIN = -20
@@ -38,6 +45,65 @@ def _view(arena, off, *shape):
     return arena[off:off + n].view(*shape)
 
 
+def _as_input(x, device):
+    t = x if torch.is_tensor(x) else torch.as_tensor(np.asarray(x))
+    return t.to(device=device, dtype=torch.float32)
+
+
+def _offsets(*offs):
+    return (ctypes.c_int64 * 6)(*[int(o) for o in offs])
+
+
+def critic_forward(mods, obs, act, need_jac):
+    """q [N, len(mods) * Q] (and d q / d [obs | act] [N, len(mods) * Q, Do + Da])
+    of one or two arena critics with the same layout (oac_critic_eval)."""
+    m0 = mods[0]
+    N, Do = obs.shape
+    Da = act.shape[1] if act is not None else 0
+    n, Q = len(mods), m0.output_size
+    q = torch.empty(N, n * Q, dtype=torch.float32, device=obs.device)
+    jac = torch.empty(N, n * Q, Do + Da, dtype=torch.float32, device=obs.device) if need_jac else None
+    nets = (ctypes.c_void_p * 2)(*[m.arena.data_ptr() + 4 * m.base for m in mods] + [None] * (2 - n))
+    _lib.check(_lib.lib().oac_critic_eval(
+        nets, n, m0._offs, Do, Da, m0.hidden, Q, _lib.ptr(obs), Do,
+        _lib.ptr(act) if act is not None else None, Da, N, _lib.ptr(q), _lib.ptr(jac),
+        _lib.stream_ptr(torch.cuda.current_stream(obs.device))))
+    return q, jac
+
+
+class _CriticFn(torch.autograd.Function):
+    """q = critics(obs, act) with the input gradient from the kernel's Jacobian."""
+
+    @staticmethod
+    def forward(ctx, obs, act, mods):
+        need = ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+        q, jac = critic_forward(mods, obs, act, need)
+        ctx.save_for_backward(jac if need else None)
+        ctx.Do = obs.shape[1]
+        return q
+
+    @staticmethod
+    def backward(ctx, gq):
+        jac, = ctx.saved_tensors
+        gx = torch.bmm(gq.unsqueeze(1), jac).squeeze(1)
+        return gx[:, :ctx.Do], gx[:, ctx.Do:], None
+
+
+def critics_apply(mods, obs, act):
+    """[N, len(mods) * Q] outputs of arena critics (before any `positive` exp)."""
+    dev = mods[0].arena.device
+    obs, act = _as_input(obs, dev), _as_input(act, dev)
+    one = obs.dim() == 1
+    if one:
+        obs, act = obs[None], act[None]
+    obs, act = obs.contiguous(), act.contiguous()
+    if torch.is_grad_enabled() and (obs.requires_grad or act.requires_grad):
+        q = _CriticFn.apply(obs, act, mods)
+    else:
+        q = critic_forward(mods, obs, act, False)[0]
+    return q[0] if one else q
+
+
 class ArenaFlattenMlp(nn.Module):
     """FlattenMlp (networks.py:154-161): relu hidden layers, identity output,
     inputs concatenated along dim 1."""
@@ -56,12 +122,15 @@ class ArenaFlattenMlp(nn.Module):
                                     _view(arena, base + L.q_last_b, out_dim))
         self.fcs = [self.fc0, self.fc1]
         self.arena, self.base = arena, base
+        self.hidden, self.obs_dim, self.act_dim = hidden, obs_dim, act_dim
+        self._offs = _offsets(L.q_fc0_w, L.q_fc0_b, L.q_fc1_w, L.q_fc1_b, L.q_last_w, L.q_last_b)
 
     def forward(self, *inputs, **kwargs):
-        h = torch.cat(inputs, dim=1)
-        for fc in self.fcs:
-            h = F.relu(fc(h))
-        out = self.last_fc(h)
+        if len(inputs) == 2:
+            out = critics_apply([self], inputs[0], inputs[1])
+        else:   # FlattenMlp concatenates whatever it is given along dim 1
+            x = torch.cat([_as_input(i, self.arena.device) for i in inputs], dim=1)
+            out = critics_apply([self], x[:, :self.obs_dim], x[:, self.obs_dim:])
         if isinstance(self.positive, (list, tuple)):
             out = torch.stack([torch.exp(out[:, i]) if v else out[:, i]
                                for i, v in enumerate(self.positive)], dim=1)
@@ -91,31 +160,41 @@ class ArenaTanhGaussianPolicy(nn.Module):
         self.input_size, self.output_size = obs_dim, act_dim
         self.std = None
         self.arena, self.base = arena, base
+        self.hidden = hidden
+        self._offs = _offsets(L.pol_fc0_w, L.pol_fc0_b, L.pol_fc1_w, L.pol_fc1_b, L.pol_head_w,
+                              L.pol_head_b)
         self.oac_trainer = None  # set by the owning trainer (exploration handle)
 
     def forward(self, obs, reparameterize=True, deterministic=False, return_log_prob=False):
-        h = obs
-        for fc in self.fcs:
-            h = F.relu(fc(h))
-        mean = self.last_fc(h)
-        log_std = torch.clamp(self.last_fc_log_std(h), LOG_SIG_MIN, LOG_SIG_MAX)
-        std = torch.exp(log_std)
-        log_prob = None
-        if deterministic:
-            action = torch.tanh(mean)
-            pre_tanh = mean
+        """policies.py:260-316 on oac_policy_eval: the same 6-tuple (a
+        non-sampled call returns log_prob = zeros_like(action) and pre_tanh =
+        mean, as the reference does).  The noise is a torch.normal draw, as in
+        TanhNormal.rsample (policies.py:182-186)."""
+        dev = self.arena.device
+        obs = _as_input(obs, dev)
+        if torch.is_grad_enabled() and obs.requires_grad:
+            raise NotImplementedError("oac_amd policy forward: no gradient w.r.t. the observation "
+                                      "(the gradient step runs in the trainer's plan)")
+        one = obs.dim() == 1
+        x = (obs[None] if one else obs).contiguous()
+        N, Da = x.shape[0], self.action_dim
+        e = lambda *sh: torch.empty(*sh, dtype=torch.float32, device=dev)
+        action, mean, log_std, std, pre = e(N, Da), e(N, Da), e(N, Da), e(N, Da), e(N, Da)
+        sample = not deterministic
+        eps = torch.randn(N, Da, device=dev) if sample else None
+        lp = e(N) if (sample and return_log_prob) else None
+        _lib.check(_lib.lib().oac_policy_eval(
+            ctypes.c_void_p(self.arena.data_ptr() + 4 * self.base), self._offs, self.obs_dim, Da,
+            self.hidden, _lib.ptr(x), self.obs_dim, N, _lib.ptr(eps), _lib.ptr(action),
+            _lib.ptr(mean), _lib.ptr(log_std), _lib.ptr(lp), _lib.ptr(std), _lib.ptr(pre),
+            _lib.stream_ptr(torch.cuda.current_stream(dev))))
+        if lp is not None:
+            log_prob = lp.view(N, 1)
         else:
-            z = mean + std * torch.randn_like(mean)
-            action = torch.tanh(z)
-            pre_tanh = z
-            if return_log_prob:
-                lp = (-((z - mean) ** 2) / (2 * std ** 2) - torch.log(std)
-                      - np.log(np.sqrt(2 * np.pi)) - torch.log(1 - action * action + 1e-6))
-                log_prob = lp.sum(dim=-1, keepdim=True)
-        if log_prob is None:
             log_prob = torch.zeros_like(action)
-            pre_tanh = mean
-        return action, mean, log_std, log_prob, std, pre_tanh
+            pre = mean
+        out = (action, mean, log_std, log_prob, std, pre)
+        return tuple(t[0] for t in out) if one else out
 
     def get_action(self, obs_np, deterministic=False):
         actions = self.get_actions(obs_np[None], deterministic=deterministic)

@@ -43,6 +43,10 @@ def _owner(policy, qfs, trainer, hyper_params):
             raise TypeError("trainer_UB needs SACTrainer (twin critics) or the P-OAC "
                             "ParticleTrainer of particle_trainer_oac.py (sorted-head upper "
                             "bound, :147-167); this trainer's predict() has no upper_bound")
+        if not twin and getattr(t, "delta_index", None) is None:
+            raise ValueError("trainer_UB with the P-OAC ParticleTrainer needs its delta_index: "
+                             "delta must be a quantile level in (0, 1) "
+                             f"(particle_trainer_oac.py:60-67), got delta={t.delta}")
     elif not twin and not hyper_params.get("share_layers", False):
         raise ValueError("one critic with K heads needs hyper_params['share_layers'] = True "
                          "(the reference's except branch fails without it)")

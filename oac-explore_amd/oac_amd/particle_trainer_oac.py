@@ -162,17 +162,24 @@ class ParticleTrainer(_ArenaTrainer):
         self._need_to_update_eval_statistics = True
 
     def predict(self, obs, action, all_particles=False, upper_bound=True, beta_UB=None):
-        """particle_trainer_oac.py:147-167 (share_layers: heads are particles)."""
-        obs = torch.as_tensor(np.asarray(obs) if not torch.is_tensor(obs) else obs,
-                              dtype=torch.float32, device=self.device)
-        action = torch.as_tensor(np.asarray(action) if not torch.is_tensor(action) else action,
-                                 dtype=torch.float32, device=self.device)
-        with torch.no_grad():
-            qs = self.qfs[0](obs, action).t().unsqueeze(-1)     # [K, B, 1]
-        sorted_qs = torch.sort(qs, dim=0)[0]
-        out = sorted_qs[self.delta_index] if upper_bound else torch.mean(qs, dim=0)
+        """particle_trainer_oac.py:147-167 (share_layers: the K heads of the one
+        critic are the particles), on oac_critic_eval; differentiable w.r.t.
+        obs and action like the reference's."""
+        from .networks import critics_apply
+        q = critics_apply([self.qfs[0]], obs, action)
+        if q.dim() == 1:
+            q = q.unsqueeze(0)
+        qs = q.t().unsqueeze(-1)                  # [K, B, 1] (stack + permute(2, 1, 0))
+        if upper_bound:
+            if self.delta_index is None:
+                raise ValueError("predict(upper_bound=True) needs delta_index: delta must be a "
+                                 "quantile level in (0, 1) (particle_trainer_oac.py:60-67), "
+                                 f"got delta={self.delta}")
+            out = torch.sort(qs, dim=0)[0][self.delta_index]
+        else:
+            out = torch.mean(qs, dim=0)
         if all_particles:
-            return sorted_qs, out
+            return torch.sort(qs, dim=0)[0], out
         return out
 
     @property

@@ -530,15 +530,15 @@ class SACTrainer(_ArenaTrainer):
 
     # ------------------------------------------------------------ misc API
     def predict(self, obs, action, upper_bound=True, beta_UB=4.46, both_values=False):
-        """trainer.py:105-123 (Q_UB = mean + beta_UB * |Q1-Q2|/2)."""
-        obs = torch.as_tensor(np.asarray(obs) if not torch.is_tensor(obs) else obs,
-                              dtype=torch.float32, device=self.device)
-        action = torch.as_tensor(np.asarray(action) if not torch.is_tensor(action) else action,
-                                 dtype=torch.float32, device=self.device)
+        """trainer.py:105-123: Q_UB = (Q1+Q2)/2 + beta_UB |Q1-Q2|/2, both critics
+        in one oac_critic_eval launch; differentiable w.r.t. obs and action
+        (the reference's exploration takes autograd.grad of it)."""
+        from .networks import _as_input, critics_apply
+        obs, action = _as_input(obs, self.device), _as_input(action, self.device)
         if obs.dim() == 1:
-            obs, action = obs[None], action[None]
-        with torch.no_grad():
-            q1, q2 = self.qf1(obs, action), self.qf2(obs, action)
+            obs, action = obs.unsqueeze(0), action.unsqueeze(0)
+        q = critics_apply([self.qf1, self.qf2], obs, action)
+        q1, q2 = q[:, 0:1], q[:, 1:2]
         mu, sigma = (q1 + q2) / 2.0, torch.abs(q1 - q2) / 2.0
         if both_values:
             return mu, sigma
