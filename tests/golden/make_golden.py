@@ -195,7 +195,10 @@ def _record_batch(rb, B):
 def gen_sac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=7,
             pi_init_w=1e-3, q_init_w=3e-3, auto_alpha=True, log_alpha0=0.0,
             discount=0.99, reward_scale=1.0, tau=5e-3, lr=3e-4, idx_seed=1,
-            eps_seed=2):
+            eps_seed=2, full_s0=False):
+    """full_s0: step 0's gradients and post-step parameters stored whole (not
+    sampled) even at hidden 256, so the headline configs are checked
+    element for element at 1e-5."""
     pp, qp = _producers(obs_dim, act_dim, hidden)
     torch.manual_seed(0)
     tr = SACTrainer(pp, qp, action_space=Box(-1, 1, (act_dim,)), discount=discount,
@@ -235,13 +238,13 @@ def gen_sac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=7,
         for gname, opt, order in groups:
             grads = opt.recorded[-1]
             for pname, g in zip(order, grads):
-                pack(out, f"s{s}/grad/{gname}/{pname}", g.numpy(), full)
+                pack(out, f"s{s}/grad/{gname}/{pname}", g.numpy(), full or (full_s0 and s == 0))
         if auto_alpha:
             out[f"s{s}/grad/log_alpha"] = tr.alpha_optimizer.recorded[-1][0].numpy()
             out[f"s{s}/post/log_alpha"] = tr.log_alpha.detach().numpy().copy()
         for gname in ("policy", "qf1", "qf2", "target_qf1", "target_qf2"):
             for pname, t in getattr(tr, gname).state_dict().items():
-                pack(out, f"s{s}/post/{gname}/{pname}", t.numpy(), full)
+                pack(out, f"s{s}/post/{gname}/{pname}", t.numpy(), full or (full_s0 and s == 0))
         for gname, opt in (("policy", tr.policy_optimizer), ("qf1", tr.qf1_optimizer)):
             order = PARAM_ORDER_POLICY if gname == "policy" else PARAM_ORDER_Q
             for pname, p in zip(order, opt.param_groups[0]["params"]):
@@ -731,6 +734,9 @@ def main():
         save("poac_counts", *gen_poac("poac_counts", 111, 8, [32, 32], 10, 32, 2, 500, True,
                                       pi_init_w=0.3, counts=True))
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "humanoid":
+        gen_humanoid()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "nobias":
         gen_nobias()
         return
@@ -762,9 +768,7 @@ def main():
     save("sac_noalpha", *gen_sac("sac_noalpha", 5, 2, [16, 16], 8, 2, 100, True,
                                  auto_alpha=False, pi_init_w=0.2))
     save("sac_riverswim", *gen_sac("sac_riverswim", 1, 1, [256, 256], 256, 2, 10000, False))
-    save("sac_humanoid", *gen_sac("sac_humanoid", 376, 17, [256, 256], 256, 3, 20000, False))
-    save("sac_humanoid_b4096", *gen_sac("sac_humanoid_b4096", 376, 17, [256, 256], 4096, 1,
-                                        20000, False))
+    gen_humanoid()
     save("poac_small", *gen_poac("poac_small", 111, 8, [32, 32], 10, 32, 2, 500, True,
                                  pi_init_w=0.3))
     save("poac_ant", *gen_poac("poac_ant", 111, 8, [256, 256], 10, 512, 2, 20000, False))
@@ -782,6 +786,14 @@ def main():
     gen_det_snapshot(os.path.join(HERE, "ptrain_snapshot.pt"), "ptrain")
     gen_expl_shared()
     gen_nobias()
+
+
+def gen_humanoid():
+    """The headline configs (BASELINE configs[1] / [2] dims): step 0 whole."""
+    save("sac_humanoid", *gen_sac("sac_humanoid", 376, 17, [256, 256], 256, 3, 20000, False,
+                                  full_s0=True))
+    save("sac_humanoid_b4096", *gen_sac("sac_humanoid_b4096", 376, 17, [256, 256], 4096, 1,
+                                        20000, False, full_s0=True))
 
 
 def gen_nobias():
