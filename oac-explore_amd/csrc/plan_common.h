@@ -47,7 +47,7 @@ struct PlanBase {
 };
 
 static inline Split choose_split(int K, int tiles, int cfg) {
-  const int bk = (cfg == 0) ? 64 : 32;
+  const int bk = (cfg == 0 || cfg == 4) ? 64 : 32;   // cfg 4: whole LDS stages (32 or 64 deep)
   int S = 1;
   if (K >= 512) {
     int want = (512 + tiles - 1) / tiles;
@@ -167,8 +167,26 @@ static inline bool big_bwd() {
   return v;
 }
 
+// Large-batch default: the register-direct kernel (gemm_big.hip, cfg 2 / 3).
+// OAC_LDS2=1 selects the LDS-staged kernel (gemm_lds.hip, cfg 4) instead: at
+// B=4096 the SAC step ran 1,943 / 1,925 / 1,721 / 2,044 steps/s with its
+// 64x64 / 128x64 / 64x64-KD64 / 64x128 tiles (OAC_LDS_GEOM 0-3) against 2,303
+// on the register-direct pair (tools/gpu_geom.sh; every variant parity-green).
+static inline int large_batch_cfg() {
+  static const int v = [] { const char* e = getenv("OAC_LDS2"); return (e && atoi(e) != 0) ? 4 : 2; }();
+  return v;
+}
+bool gemm_lds_supports(const GemmBatch& b);
+
 static inline int launch_cfg(int cfg, const GemmBatch& gb) {
   if (cfg == 0) return 0;
+  if (cfg == 4) {
+    bool narrow = !gb.fuse_adam;
+    for (int i = 0; i < gb.ntasks && narrow; ++i)
+      narrow = gb.t[i].N <= 32 && gb.t[i].ksplit <= 1 && gb.t[i].K2 == 0;
+    if (narrow) return 0;
+    return gemm_lds_supports(gb) ? 4 : 1;
+  }
   // narrow products at large batch (width-1 critic heads, dL/da with N = act
   // dim): a 64-wide LDS tile computes 1-17 useful columns over 8 barriered K
   // blocks; the small-batch kernel's 32x32 tiles with K split over waves

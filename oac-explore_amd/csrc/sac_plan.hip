@@ -523,7 +523,7 @@ static int validate(const oac_sac_config* c) {
 
 static void plan_splits(SacPlan& p) {
   const oac_sac_config& c = p.c;
-  p.cfg = c.gemm_cfg >= 0 ? c.gemm_cfg : (c.batch >= 1024 ? 2 : 0);
+  p.cfg = c.gemm_cfg >= 0 ? c.gemm_cfg : (c.batch >= 1024 ? large_batch_cfg() : 0);
   const int tm = gemm_tile_m(p.cfg), tn = gemm_tile_n(p.cfg);
   auto tiles = [&](int M, int N) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
   const int H = c.hidden, Dq = c.obs_dim + c.act_dim, Do = c.obs_dim, Da = c.act_dim;
@@ -539,7 +539,7 @@ static void plan_splits(SacPlan& p) {
     int v[5] = {0, 0, 0, 0, 0};
     sscanf(e, "%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4]);
     Split* sp[5] = {&p.sp_q1, &p.sp_q0, &p.sp_ph, &p.sp_p1, &p.sp_p0};
-    const int bk = p.cfg == 0 ? 64 : 32;
+    const int bk = (p.cfg == 0 || p.cfg == 4) ? 64 : 32;
     for (int i = 0; i < 5; ++i)
       if (v[i] > 0) {
         int kc = (c.batch + v[i] - 1) / v[i];

@@ -38,7 +38,8 @@ for kind in ("fetch", "write", "sq"):
     for k, d in load(kind).items():
         for c, v in d.items():
             out.setdefault(k, {})[c] = sum(v) / len(v)
-            if any(n in k for n in ("gemm_small_kernel", "gemm_grouped_kernel", "gemm_big_kernel")):
+            if any(n in k for n in ("gemm_small_kernel", "gemm_grouped_kernel", "gemm_big_kernel",
+                                    "gemm_lds_kernel")):
                 gemm[c].extend(v)
 for k, d in sorted(out.items()):
     if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
