@@ -274,6 +274,14 @@ const float* oac_expl_outputs(oac_expl* h);
  * graph, so a call is one graph replay + one stream synchronisation (NULLs
  * switch it off) */
 int oac_expl_set_host_io(oac_expl* h, const float* host_obs, float* host_out);
+/* Latency path (the per-env-step call of optimistic_exploration.py:14-109 from
+ * path_collector.py:176-257): the handle's own host-coherent buffers -- obs
+ * [n_obs, obs_dim + act_dim] (write the first obs_dim floats of each row) and
+ * results [3][n_obs][act_dim] (action | mu_E | std) -- are read and written by
+ * the kernel itself; oac_expl_action_now launches on `stream` (behind the
+ * work already queued there) and returns once the results are in *out. */
+int oac_expl_host_staging(oac_expl* h, float** obs, float** out);
+int oac_expl_action_now(oac_expl* h, const float* eps, float beta_UB, float delta, void* stream);
 /* --trainer_UB with particle_trainer_oac.ParticleTrainer (optimistic_exploration.py:38-39
  * -> trainer.predict(upper_bound=True), particle_trainer_oac.py:147-167): with a K-head
  * handle, index in [0, K) makes Q_UB = sort_k(Q_k)[index] (the trainer's delta_index;

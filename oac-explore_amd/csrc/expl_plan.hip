@@ -1,6 +1,6 @@
 // OAC optimistic exploration action on MI355X, for N observations at once
-// (N = 1: the reference's per-step call; N > 1: one launch sequence for the
-// observations of N parallel environments, each row exactly as alone):
+// (N = 1: the reference's per-step call; N > 1: one launch for the
+// observations of N parallel environments, each row bitwise as alone):
 // get_optimistic_exploration_action_stochastic
 // (/root/reference/optimistic_exploration.py:14-109, trainer=None, two critics):
 //   mu_T, std = policy(ob);  a = tanh(mu_T)
@@ -8,13 +8,21 @@
 //   mu_C = sqrt(2 delta) Sigma g / (sqrt(g^T Sigma g) + 1e-5), Sigma = std^2
 //   action = tanh(mu_E + std * eps),  mu_E = mu_T + mu_C
 // The critics and policy are read in place from the trainer's parameter arena,
-// so the action always uses the current weights.  The whole computation is one
-// launch (expl_fused.hip, a workgroup per observation), captured into a
-// hipGraph together with -- when the caller registers pinned host buffers --
-// the observation upload and the result download, so a call is one graph
-// replay and one stream synchronisation.
+// so the action always uses the current weights.  The computation is one
+// launch (expl_split.hip: a group of workgroups per observation).  Two ways to
+// call it:
+//   oac_expl_action      a captured hipGraph (with the observation upload and
+//                        result download when pinned buffers are registered),
+//                        replayed on the caller's stream;
+//   oac_expl_action_now  the latency path: the kernel reads the observations
+//                        from, and writes the results to, the plan's own
+//                        host-coherent buffers, and the call returns when the
+//                        kernel's completion word lands in host memory (no
+//                        graph replay, no copies, no stream synchronisation).
 #include <cmath>
 #include <cstring>
+#include <algorithm>
+#include <cstdlib>
 
 #include "../../include/oac_amd.h"
 #include "kernels.h"
@@ -35,11 +43,16 @@ struct ExplPlan {
   oac_sac_layout L;
   // workspace offsets (floats): observation rows [N, Do + Da], outputs
   // [3][N][Da] (action | mu_E | std), dQ_UB/dmu_T [N, Da], ticket word
-  int64_t o_x, o_out, o_grad, o_cnt, total;
+  int64_t o_x, o_out, o_grad, o_cnt, o_split, total;
   // optional pinned host staging (oac_expl_set_host_io): uploads / downloads
   // captured into the graph
   const float* host_obs = nullptr; float* host_out = nullptr;
   long long* stage_clock = nullptr;   // instrumentation: per-stage wall clock of row 0
+  // oac_expl_action_now: host-coherent observation rows [N, Do + Da], results
+  // [3][N][Da] and completion word (hipHostMalloc, allocated on first use)
+  float* hc_obs = nullptr; float* hc_out = nullptr; unsigned* hc_done = nullptr;
+  unsigned seq = 0;
+  hipStream_t cap_stream = nullptr;   // graph capture (the graphs launch on the caller's stream)
   // captured call graphs by (eps slot, beta_UB, delta, ub_index): alternating
   // bounds on one handle (e.g. --trainer_UB and plain calls) replay their own
   // graph instead of re-capturing
@@ -66,35 +79,102 @@ static void expl_layout(ExplPlan& p) {
   p.o_out = take(3 * N * p.Da);
   p.o_grad = take(N * p.Da);
   p.o_cnt = take(2);
+  // expl_split.hip: published vectors + hand-off counters of the groups of one launch
+  p.o_split = take((int64_t)std::min(N, (int64_t)kExplRows) * expl_split_scratch_floats(p.H));
   p.total = o + 64;
 }
 
-static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta, hipStream_t s) {
-  const int Do = p.Do, Da = p.Da, N = p.N;
+// OAC_EXPL_SPLIT=0: the one-workgroup-per-observation kernel (expl_fused.hip)
+static bool expl_split_on() {
+  static const bool v = [] { const char* e = getenv("OAC_EXPL_SPLIT"); return !e || atoi(e) != 0; }();
+  return v;
+}
+
+static ExplFusedArgs expl_args(ExplPlan& p, const float* eps, float beta, float delta) {
   const oac_sac_layout& L = p.L;
   float* w = p.ws;
-  if (p.host_obs)   // rows [N, Do + Da]: the caller's pinned copy of the observations
-    OAC_HIP_CHECK(hipMemcpyAsync(w + p.o_x, p.host_obs, sizeof(float) * N * (Do + Da),
-                                 hipMemcpyHostToDevice, s));
   ExplFusedArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.obs = w + p.o_x; a.ld_obs = Do + Da;
+  a.obs = w + p.o_x; a.ld_obs = p.Do + p.Da;
   a.pol = p.pol; a.q[0] = p.q1; a.q[1] = p.q2;
   a.p_fc0_w = L.pol_fc0_w; a.p_fc0_b = L.pol_fc0_b; a.p_fc1_w = L.pol_fc1_w;
   a.p_fc1_b = L.pol_fc1_b; a.p_head_w = L.pol_head_w; a.p_head_b = L.pol_head_b;
   a.q_fc0_w = L.q_fc0_w; a.q_fc0_b = L.q_fc0_b; a.q_fc1_w = L.q_fc1_w; a.q_fc1_b = L.q_fc1_b;
   a.q_last_w = L.q_last_w; a.q_last_b = L.q_last_b;
-  a.Do = Do; a.Da = Da; a.H = p.H; a.n = N;
+  a.Do = p.Do; a.Da = p.Da; a.H = p.H; a.n = p.N;
   a.nq = p.q2 ? 2 : 1; a.K = p.K;
   a.eps = eps; a.out = w + p.o_out; a.grad = w + p.o_grad;
   a.state = p.state; a.ticket = reinterpret_cast<unsigned*>(w + p.o_cnt);
   a.seed = p.seed; a.beta_UB = beta; a.sqrt_2delta = (float)std::sqrt(2.0 * (double)delta);
   a.ub_index = p.ub_index;
   a.stage_clock = p.stage_clock;
-  OAC_HIP_CHECK(launch_expl_fused(a, s));
+  return a;
+}
+
+static int expl_launch(ExplPlan& p, const ExplFusedArgs& a, hipStream_t s) {
+  if (expl_split_on() && !p.stage_clock) {
+    for (int row0 = 0; row0 < p.N; row0 += kExplRows)
+      OAC_HIP_CHECK(launch_expl_split(a, row0, std::min(kExplRows, p.N - row0), p.ws + p.o_split, s));
+  } else {
+    OAC_HIP_CHECK(launch_expl_fused(a, s));
+  }
+  return 0;
+}
+
+static int expl_sequence(ExplPlan& p, const float* eps, float beta, float delta, hipStream_t s) {
+  const int Do = p.Do, Da = p.Da, N = p.N;
+  float* w = p.ws;
+  if (p.host_obs)   // rows [N, Do + Da]: the caller's pinned copy of the observations
+    OAC_HIP_CHECK(hipMemcpyAsync(w + p.o_x, p.host_obs, sizeof(float) * N * (Do + Da),
+                                 hipMemcpyHostToDevice, s));
+  const ExplFusedArgs a = expl_args(p, eps, beta, delta);
+  if (expl_launch(p, a, s)) return 1;
   if (p.host_out)
     OAC_HIP_CHECK(hipMemcpyAsync(p.host_out, w + p.o_out, sizeof(float) * 3 * N * Da,
                                  hipMemcpyDeviceToHost, s));
+  return 0;
+}
+
+static int expl_host_alloc(ExplPlan& p) {
+  if (p.hc_obs) return 0;
+  const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+  OAC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p.hc_obs),
+                              sizeof(float) * (size_t)p.N * (p.Do + p.Da), fl));
+  OAC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p.hc_out),
+                              sizeof(float) * 3 * (size_t)p.N * p.Da, fl));
+  OAC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p.hc_done), 64, fl));
+  std::memset(p.hc_obs, 0, sizeof(float) * (size_t)p.N * (p.Do + p.Da));
+  std::memset(p.hc_out, 0, sizeof(float) * 3 * (size_t)p.N * p.Da);
+  *p.hc_done = p.seq;
+  return 0;
+}
+
+static inline void cpu_relax() {
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+  __builtin_ia32_pause();
+#endif
+}
+
+// spin on the completion word; every ~4k polls ask the stream whether it
+// failed (or finished without writing the word)
+static int expl_wait(ExplPlan& p, unsigned seq, hipStream_t s) {
+  volatile unsigned* f = p.hc_done;
+  unsigned polls = 0;
+  while (*f != seq) {
+    cpu_relax();
+    if ((++polls & 4095) == 0) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess && *f != seq) {
+        set_error("exploration: the launch finished without its completion word");
+        return 1;
+      }
+      if (e != hipSuccess && e != hipErrorNotReady) {
+        set_error("exploration: %s", hipGetErrorString(e));
+        return 1;
+      }
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
   return 0;
 }
 
@@ -181,6 +261,10 @@ int oac_expl_create(int obs_dim, int act_dim, int hidden, const float* policy, c
 int oac_expl_destroy(oac_expl* h) {
   if (!h) return 0;
   h->p.drop_graphs();
+  if (h->p.cap_stream) (void)hipStreamDestroy(h->p.cap_stream);
+  if (h->p.hc_obs) (void)hipHostFree(h->p.hc_obs);
+  if (h->p.hc_out) (void)hipHostFree(h->p.hc_out);
+  if (h->p.hc_done) (void)hipHostFree(h->p.hc_done);
   delete h;
   return 0;
 }
@@ -198,10 +282,11 @@ int oac_expl_action(oac_expl* h, const float* eps, float beta_UB, float delta, f
     if (g.eps == eps && g.beta == beta_UB && g.delta == delta && g.ub == p.ub_index) gi = i;
   }
   if (gi < 0) {
-    OAC_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    const int rc = expl_sequence(p, eps, beta_UB, delta, s);
+    if (!p.cap_stream) OAC_HIP_CHECK(hipStreamCreateWithFlags(&p.cap_stream, hipStreamNonBlocking));
+    OAC_HIP_CHECK(hipStreamBeginCapture(p.cap_stream, hipStreamCaptureModeThreadLocal));
+    const int rc = expl_sequence(p, eps, beta_UB, delta, p.cap_stream);
     hipGraph_t g = nullptr;
-    const hipError_t e = hipStreamEndCapture(s, &g);
+    const hipError_t e = hipStreamEndCapture(p.cap_stream, &g);
     if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
     if (e != hipSuccess) { set_error("hipStreamEndCapture: %s", hipGetErrorString(e)); return 1; }
     hipGraphExec_t ex = nullptr;
@@ -229,6 +314,32 @@ int oac_expl_action(oac_expl* h, const float* eps, float beta_UB, float delta, f
   if (std_out) OAC_HIP_CHECK(hipMemcpyAsync(std_out, o + 2 * p.Da * p.N, nb, hipMemcpyDeviceToDevice, s));
   if (grad_out) OAC_HIP_CHECK(hipMemcpyAsync(grad_out, p.ws + p.o_grad, nb, hipMemcpyDeviceToDevice, s));
   return 0;
+}
+
+int oac_expl_host_staging(oac_expl* h, float** obs, float** out) {
+  if (!h || !obs || !out) { set_error("oac_expl_host_staging: null pointer"); return 1; }
+  if (expl_host_alloc(h->p)) return 1;
+  *obs = h->p.hc_obs;
+  *out = h->p.hc_out;
+  return 0;
+}
+
+int oac_expl_action_now(oac_expl* h, const float* eps, float beta_UB, float delta, void* stream) {
+  if (!h) { set_error("null handle"); return 1; }
+  ExplPlan& p = h->p;
+  if (expl_host_alloc(p)) return 1;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  ExplFusedArgs a = expl_args(p, eps, beta_UB, delta);
+  a.obs = p.hc_obs;
+  a.out = p.hc_out;
+  const bool split = expl_split_on() && !p.stage_clock;
+  if (split) { a.done = p.hc_done; a.done_seq = ++p.seq; }
+  if (expl_launch(p, a, s)) return 1;
+  if (!split) {   // the one-workgroup kernel (A/B runs, stage clocks) has no completion word
+    OAC_HIP_CHECK(hipStreamSynchronize(s));
+    return 0;
+  }
+  return expl_wait(p, a.done_seq, s);
 }
 
 // instrumentation hook (tools/expl_latency.py; not in include/oac_amd.h):

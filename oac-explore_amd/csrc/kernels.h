@@ -121,9 +121,20 @@ struct ExplFusedArgs {                  // expl_fused.hip: one workgroup per obs
   int ub_index;                         // K heads: >= 0 -> Q_UB = sorted head ub_index
                                         // (trainer.predict, particle_trainer_oac.py:147-167)
   long long* stage_clock;               // instrumentation (tools/expl_latency.py) or null
+  unsigned* done; unsigned done_seq;    // expl_split.hip: completion word (host-polled) or null
 };
 size_t expl_fused_lds_bytes(int Do, int Da, int H);
 hipError_t launch_expl_fused(const ExplFusedArgs& a, hipStream_t s);
+// expl_split.hip: one observation per group of expl_split_group(rows) <=
+// kExplGroup workgroups; a launch carries at most kExplRows observations
+constexpr int kExplGroup = 32;
+constexpr int kExplRows = 256;
+int expl_split_group(int n_rows);
+int expl_split_threads();
+size_t expl_split_lds_bytes(int Do, int Da, int H);
+long expl_split_scratch_floats(int H);
+hipError_t launch_expl_split(const ExplFusedArgs& a, int row0, int n_rows, float* scratch,
+                             hipStream_t s);
 
 // row-wise network evaluation off the gradient step (mlp_eval.hip)
 struct MlpEvalArgs {

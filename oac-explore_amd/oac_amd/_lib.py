@@ -149,6 +149,10 @@ _SIGS = {
     "oac_expl_outputs": (ctypes.c_void_p, [ctypes.c_void_p]),
     "oac_expl_set_host_io": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "oac_expl_set_ub_index": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "oac_expl_host_staging": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p),
+                                             ctypes.POINTER(ctypes.c_void_p)]),
+    "oac_expl_action_now": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
+                                           ctypes.c_float, ctypes.c_void_p]),
 }
 
 # every symbol include/oac_amd.h declares (checked by tests/test_abi.py)

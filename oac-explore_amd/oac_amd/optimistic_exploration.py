@@ -1,6 +1,6 @@
 """Drop-in ``get_optimistic_exploration_action``
 (/root/reference/optimistic_exploration.py:7-11) -- the OAC action shift,
-computed by liboac_amd in one launch (csrc/expl_plan.hip, expl_fused.hip), for
+computed by liboac_amd in one launch (csrc/expl_plan.hip, expl_split.hip), for
 twin critics (SACTrainer) or one shared-layer critic with K heads
 (ParticleTrainerOAC, share_layers: Q_UB = mean_k + beta_UB std_k).
 
@@ -11,6 +11,8 @@ sequence, each row exactly as a single call.  ``policy`` must be the policy of a
 (its parameters live in the trainer's HBM arena, which the kernels read in
 place); there is no torch/CPU fallback.
 """
+import os
+
 import numpy as np
 import torch
 
@@ -87,26 +89,35 @@ def get_optimistic_exploration_actions(obs_np, policy=None, qfs=None, trainer=No
                     trainer is not None)
 
 
+_USE_GRAPH = os.environ.get("OAC_EXPL_GRAPH", "0") == "1"
+
+
 def _actions(t, obs, hyper_params, eps, return_info, trainer_ub=False):
-    """One graph replay: the observations go through pinned host staging
-    (uploaded and the results downloaded inside the graph, oac_expl_set_host_io),
-    then one synchronisation of the trainer's stream."""
+    """One launch on torch's current stream: the kernel reads the observations
+    from and writes the results to the handle's host-coherent staging, and the
+    call returns when its completion word lands (oac_expl_action_now).
+    OAC_EXPL_GRAPH=1: the captured-graph path instead (oac_expl_action: upload,
+    kernel and download replayed, then a stream synchronisation)."""
     n = obs.shape[0]
     e = t._expl_handle(n)
     if t.layout.q2_base < 0:   # K heads: mean + beta std, or trainer.predict's sorted head
         check(_lib.lib().oac_expl_set_ub_index(e.handle, int(t.delta_index) if trainer_ub else -1))
     e.obs_np[:, :t.obs_dim] = obs                 # float64 observations -> fp32 rows
-    s = t.stream
-    s.wait_stream(torch.cuda.current_stream(t.device))   # parameter writes on torch's stream
+    # torch's current stream: every trainer call leaves it behind its updates
+    # (_on_stream; the drop-in step runs on it), so the weights read are the
+    # latest, with no cross-stream join on this path
+    s = torch.cuda.current_stream(t.device)
     ed = None
     if eps is not None:
-        with torch.cuda.stream(s):
-            e.eps.copy_(torch.from_numpy(np.ascontiguousarray(eps, np.float32)).reshape(e.eps.shape))
+        e.eps.copy_(torch.from_numpy(np.ascontiguousarray(eps, np.float32)).reshape(e.eps.shape))
         ed = e.eps
-    check(_lib.lib().oac_expl_action(e.handle, ptr(ed), float(hyper_params["beta_UB"]),
-                                     float(hyper_params["delta"]), None, None, None, None,
-                                     stream_ptr(s)))
-    s.synchronize()
+    beta, delta = float(hyper_params["beta_UB"]), float(hyper_params["delta"])
+    if _USE_GRAPH:
+        check(_lib.lib().oac_expl_action(e.handle, ptr(ed), beta, delta, None, None, None, None,
+                                         stream_ptr(s)))
+        s.synchronize()
+    else:
+        check(_lib.lib().oac_expl_action_now(e.handle, ptr(ed), beta, delta, stream_ptr(s)))
     res = e.out_np
     info = {}
     if return_info:

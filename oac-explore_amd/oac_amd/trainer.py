@@ -119,10 +119,9 @@ class AdamStateView:
 
 
 class _ExplHandle:
-    def __init__(self, handle, ws, eps, obs_pin, out_pin):
+    def __init__(self, handle, ws, eps, obs_np, out_np):
         self.handle, self.ws, self.eps = handle, ws, eps
-        self.obs_pin, self.out_pin = obs_pin, out_pin      # keep the pinned pages alive
-        self.obs_np, self.out_np = obs_pin.numpy(), out_pin.numpy()
+        self.obs_np, self.out_np = obs_np, out_np   # views of the handle's host-coherent buffers
 
     def __getitem__(self, i):   # (handle, ...) unpacking of older callers
         return (self.handle, self.ws)[i]
@@ -395,9 +394,9 @@ class _ArenaTrainer(object):
     def _expl_handle(self, n=1):
         """Exploration plan for n observations per call (cached per n): the
         liboac_amd handle, its workspace, a device eps slot [n, act_dim]
-        (parity runs), and pinned host staging -- observation rows
-        [n, obs_dim + act_dim] and results [3, n, act_dim] (action | mu_E |
-        std) -- that the call's graph uploads / downloads itself."""
+        (parity runs), and numpy views of the handle's host-coherent staging --
+        observation rows [n, obs_dim + act_dim] and results [3, n, act_dim]
+        (action | mu_E | std) -- that the kernel reads and writes itself."""
         if self._expl is None:
             self._expl = {}
         if n not in self._expl:
@@ -419,12 +418,16 @@ class _ArenaTrainer(object):
                                                self._q_out, ptr(p), q1, ptr(ws),
                                                ptr(self.step_state),
                                                ctypes.c_uint64(self.seed + 1), ctypes.byref(h)))
-            obs_pin = torch.zeros(n, self.obs_dim + self.act_dim, dtype=torch.float32,
-                                  pin_memory=True)
-            out_pin = torch.zeros(3, n, self.act_dim, dtype=torch.float32, pin_memory=True)
-            check(L.oac_expl_set_host_io(h, ctypes.c_void_p(obs_pin.data_ptr()),
-                                         ctypes.c_void_p(out_pin.data_ptr())))
-            self._expl[n] = _ExplHandle(h, ws, eps, obs_pin, out_pin)
+            po, pr = ctypes.c_void_p(), ctypes.c_void_p()
+            check(L.oac_expl_host_staging(h, ctypes.byref(po), ctypes.byref(pr)))
+            w = self.obs_dim + self.act_dim
+            obs_np = np.ctypeslib.as_array((ctypes.c_float * (n * w)).from_address(po.value))
+            out_np = np.ctypeslib.as_array(
+                (ctypes.c_float * (3 * n * self.act_dim)).from_address(pr.value))
+            # the graph path (oac_expl_action) stages through the same buffers
+            check(L.oac_expl_set_host_io(h, po, pr))
+            self._expl[n] = _ExplHandle(h, ws, eps, obs_np.reshape(n, w),
+                                        out_np.reshape(3, n, self.act_dim))
         return self._expl[n]
 
 

@@ -189,6 +189,54 @@ def test_batched_oac_exploration_equals_single_calls(name):
     assert int(tr.step_state[2].item()) == c0 + 1
 
 
+@pytest.mark.parametrize("n", [64, 300])
+def test_exploration_group_sizes_and_paths_bitwise(n):
+    """The split kernel's group size follows the observations per launch (16
+    workgroups per row at 1..16 rows, 4 at 64, 1 at >= 256 -- then two launches
+    for 300 rows) and its hand-off form with it; every row is bitwise the
+    single-observation call, the golden rows stay within tolerance, and the
+    captured-graph path (oac_expl_action) equals the direct one."""
+    from oac_amd import get_optimistic_exploration_action, get_optimistic_exploration_actions
+    from oac_amd import optimistic_exploration as oe
+    meta, g = parity.load("oac_expl_humanoid")
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                        pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"])
+    m = dict(obs_dim=meta["obs_dim"], act_dim=meta["act_dim"], hidden=meta["hidden"],
+             discount=0.99, reward_scale=1.0, lr=3e-4, tau=5e-3, auto_alpha=True, log_alpha0=0.0,
+             seed=meta["seed"], pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"])
+    tr = sac_trainer_for(m, params=params)
+    hp = dict(beta_UB=meta["beta_UB"], delta=meta["delta"], share_layers=False)
+    k = meta["n_obs"]
+    rs = np.random.RandomState(n)
+    obs = np.concatenate([g["obs"], rs.standard_normal((n - k, meta["obs_dim"]))])
+    eps = np.concatenate([g["eps"], rs.standard_normal((n - k, meta["act_dim"]))]).astype(np.float32)
+    A, info = get_optimistic_exploration_actions(obs, policy=tr.policy, qfs=tr.qfs,
+                                                 hyper_params=hp, eps=eps, return_info=True)
+    assert np.isfinite(A).all()
+    for i in range(k):
+        assert parity.rel_err(A[i], g["action"][i]) <= parity.TOL
+        assert parity.rel_err(info["mu_E"][i], g["mu_E"][i]) <= parity.TOL
+    for i in sorted({0, 1, k, n // 2, 255 % n, min(256, n - 1), n - 1}):
+        a, _ = get_optimistic_exploration_action(obs[i], policy=tr.policy, qfs=tr.qfs,
+                                                 hyper_params=hp, eps=eps[i])
+        np.testing.assert_array_equal(a, A[i])
+    oe._USE_GRAPH = True
+    try:
+        Ag, _ = get_optimistic_exploration_actions(obs, policy=tr.policy, qfs=tr.qfs,
+                                                   hyper_params=hp, eps=eps)
+        a0, _ = get_optimistic_exploration_action(obs[3], policy=tr.policy, qfs=tr.qfs,
+                                                  hyper_params=hp, eps=eps[3])
+    finally:
+        oe._USE_GRAPH = False
+    np.testing.assert_array_equal(Ag, A)
+    np.testing.assert_array_equal(a0, A[3])
+    c0 = int(tr.step_state[2].item())
+    A2, _ = get_optimistic_exploration_actions(obs, policy=tr.policy, qfs=tr.qfs, hyper_params=hp)
+    assert np.isfinite(A2).all() and np.abs(A2).max() <= 1   # random rows may saturate tanh
+    assert not np.array_equal(A2, A)
+    assert int(tr.step_state[2].item()) == c0 + 1
+
+
 @pytest.mark.parametrize("name", ["oac_expl_shared_ant", "oac_expl_shared_small"])
 def test_oac_exploration_shared_matches_reference_golden(name):
     """One shared-layer critic with K heads (ParticleTrainerOAC, share_layers):

@@ -42,18 +42,36 @@ def main():
     ob = np.random.RandomState(0).standard_normal(Do)
     full = bench(lambda: oac_amd.get_optimistic_exploration_action(ob, policy=tr.policy,
                                                                    qfs=tr.qfs, hyper_params=hp))
+    from oac_amd import optimistic_exploration as oe
+    oe._USE_GRAPH = True
+    full_graph = bench(lambda: oac_amd.get_optimistic_exploration_action(
+        ob, policy=tr.policy, qfs=tr.qfs, hyper_params=hp))
+    oe._USE_GRAPH = False
     e = tr._expl_handle(1)
     L = _lib.lib()
     s = tr.stream
+    t_now = bench(lambda: check(L.oac_expl_action_now(e.handle, None, 4.66, 23.53, stream_ptr(s))))
+    obs64 = np.random.RandomState(1).standard_normal((64, Do))
+    t64 = bench(lambda: oac_amd.get_optimistic_exploration_actions(obs64, policy=tr.policy,
+                                                                   qfs=tr.qfs, hyper_params=hp))
 
     def launch():
         check(L.oac_expl_action(e.handle, None, 4.66, 23.53, None, None, None, None,
                                 stream_ptr(s)))
         s.synchronize()
     t_launch = bench(launch)
+    z = torch.zeros(1, device=dev)
+
+    def tiny():
+        with torch.cuda.stream(s):
+            z.add_(1.0)
+        s.synchronize()
+    t_tiny = bench(tiny)
+    po, pr = ctypes.c_void_p(), ctypes.c_void_p()
     check(L.oac_expl_set_host_io(e.handle, None, None))   # device-only graph
     t_kernel = bench(launch)
-    check(L.oac_expl_set_host_io(e.handle, e.obs_pin.data_ptr(), e.out_pin.data_ptr()))
+    check(L.oac_expl_host_staging(e.handle, ctypes.byref(po), ctypes.byref(pr)))
+    check(L.oac_expl_set_host_io(e.handle, po, pr))
     clk = torch.zeros(16, dtype=torch.int64, device=dev)
     fn = L.oac_expl_debug_stage_clock
     fn.argtypes, fn.restype = [ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int
@@ -68,8 +86,10 @@ def main():
     print("head matvec+sync", (c[9] - c[2]) / 100.0, "tanh+sync", (c[3] - c[9]) / 100.0,
           "Q1 L0", (c[10] - c[3]) / 100.0, "Q2 L0+sync", (c[4] - c[10]) / 100.0)
     fn(e.handle, None)
-    print({"full_call_us": round(full, 1), "graph_with_host_io_sync_us": round(t_launch, 1),
-           "graph_device_only_sync_us": round(t_kernel, 1)})
+    print({"full_call_us": round(full, 1), "full_call_graph_us": round(full_graph, 1),
+           "action_now_us": round(t_now, 1), "call_64obs_us": round(t64, 1), "graph_with_host_io_sync_us": round(t_launch, 1),
+           "graph_device_only_sync_us": round(t_kernel, 1),
+           "tiny_kernel_sync_us": round(t_tiny, 1)})
 
 
 if __name__ == "__main__":
