@@ -177,6 +177,15 @@ static inline int large_batch_cfg() {
   return v;
 }
 bool gemm_lds_supports(const GemmBatch& b);
+bool gemm_bwd_supports(const GemmBatch& b);
+
+// Backward batches at large batch go to gemm_bwd.hip (cfg 5: float2 fetch of
+// the batch-major operands, K split over the workgroup's waves); OAC_BWD2=0
+// keeps them on the register-direct kernel (cfg 3) for A/B runs.
+static inline bool bwd2_on() {
+  static const bool v = [] { const char* e = getenv("OAC_BWD2"); return !e || atoi(e) != 0; }();
+  return v;
+}
 
 static inline int launch_cfg(int cfg, const GemmBatch& gb) {
   if (cfg == 0) return 0;
@@ -196,6 +205,11 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     narrow = gb.t[i].N <= 32 && gb.t[i].ksplit <= 1 && gb.t[i].K2 == 0;
   if (narrow) return 0;
   if (cfg != 2) return cfg;
+  if (bwd2_on() && big_bwd()) {
+    bool all_bwd = true;
+    for (int i = 0; i < gb.ntasks; ++i) all_bwd = all_bwd && !gb.t[i].b_kc;
+    if (all_bwd && gemm_bwd_supports(gb)) return 5;
+  }
   bool any_bwd = false;
   for (int i = 0; i < gb.ntasks; ++i) {
     const GemmTask& t = gb.t[i];
@@ -219,6 +233,14 @@ static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {
   if (p.launches < 64 && p.tune_nw[p.launches] > 0) {
     gb.force_nw = p.tune_nw[p.launches];
     gb.force_gpw = p.tune_gpw[p.launches];
+  }
+  static const bool dbg = getenv("OAC_DEBUG_CFG") != nullptr;
+  if (dbg) {
+    fprintf(stderr, "launch %d cfg %d tiles %d:", p.launches, cfg, gb.total_tiles);
+    for (int i = 0; i < gb.ntasks; ++i)
+      fprintf(stderr, " [M%d N%d K%d akc%d bkc%d r1%d epi%d S%d]", gb.t[i].M, gb.t[i].N, gb.t[i].K,
+              gb.t[i].a_kc, gb.t[i].b_kc, gb.t[i].a_mode, gb.t[i].epi, gb.t[i].ksplit);
+    fprintf(stderr, "\n");
   }
   TIMED(p, K_GEMM, s, OAC_HIP_CHECK(gemm_batch_launch(gb, cfg, s)));
   p.launches++;
