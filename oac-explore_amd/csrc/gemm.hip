@@ -400,6 +400,7 @@ void gemm_batch_finalize(GemmBatch& b, int cfg) {
     t.tiles_n = tn;
     if (t.ksplit < 1) t.ksplit = 1;
     tiles += tm * tn * t.ksplit;
+    if (cfg == 5) tiles = (tiles + 7) & ~7;   // gemm_bwd.hip: XCD-aligned block ranges
   }
   b.total_tiles = tiles;
 }

@@ -33,7 +33,6 @@ typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));
 
 enum BwdA { BA_KC = 0, BA_KC_R1 = 1, BA_MN = 2, BA_MN_R1 = 3 };
 
-constexpr int kBwdPF = 3;   // k-groups in flight per wave
 
 // raw operand fragments of one 8-deep k-group (lane: k = 8g + 4*half + c)
 struct BwdFrag {
@@ -43,12 +42,23 @@ struct BwdFrag {
 
 __device__ __forceinline__ int acc_row_b(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-template <int AK>
+template <int AK, int kBwdPF>   // kBwdPF: k-groups in flight per wave
 __device__ __forceinline__ void bwd_tile(GemmTask t, int local, float* red) {
+  // XCD-aware order: a task's block range is padded to a multiple of 8 and
+  // starts on a multiple of 8, so blocks local, local + 8, ... share an XCD
+  // (round-robin placement; speed only, never correctness).  Each XCD takes a
+  // contiguous run of the (split-major) work list: the K chunks of a split-K
+  // dW land on one XCD with all their tiles, and its L2 serves the chunk's
+  // operand rows to every tile instead of each XCD fetching them.
+  const int T = ((t.M + 63) >> 6) * t.tiles_n;
+  const int S = t.ksplit > 1 ? t.ksplit : 1;
+  const int per = (T * S + 7) >> 3;
+  const int lin = (local & 7) * per + (local >> 3);
+  if (lin >= T * S) return;
+  local = lin % T;
   int k_lo = 0, k_hi = t.K;
   if (t.ksplit > 1) {
-    const int split = local % t.ksplit;
-    local /= t.ksplit;
+    const int split = lin / T;
     k_lo = split * t.kchunk;
     k_hi = min(t.K, k_lo + t.kchunk);
     t.C += (long)split * t.slab_stride;
@@ -235,6 +245,7 @@ __device__ __forceinline__ void bwd_tile(GemmTask t, int local, float* red) {
   }
 }
 
+template <int PF>
 __global__ void __launch_bounds__(256)
 gemm_bwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                 const GemmBatch batch) {
@@ -253,10 +264,10 @@ gemm_bwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
   // operand kind of the task's A (workgroup-uniform)
   const int ak = (t.a_kc ? BA_KC : BA_MN) + (t.a_mode == A_RANK1_MASK ? 1 : 0);
   switch (ak) {
-    case BA_KC: bwd_tile<BA_KC>(t, local, red); break;
-    case BA_KC_R1: bwd_tile<BA_KC_R1>(t, local, red); break;
-    case BA_MN: bwd_tile<BA_MN>(t, local, red); break;
-    default: bwd_tile<BA_MN_R1>(t, local, red); break;
+    case BA_KC: bwd_tile<BA_KC, PF>(t, local, red); break;
+    case BA_KC_R1: bwd_tile<BA_KC_R1, PF>(t, local, red); break;
+    case BA_MN: bwd_tile<BA_MN, PF>(t, local, red); break;
+    default: bwd_tile<BA_MN_R1, PF>(t, local, red); break;
   }
 }
 
@@ -280,8 +291,17 @@ hipError_t gemm_bwd_launch(const GemmBatch& b, hipStream_t s) {
   if (!gemm_bwd_supports(b)) return hipErrorInvalidValue;
   int tb[8];
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
-  OAC_LAUNCH(gemm_bwd_kernel, dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, tb[1], tb[2],
-             tb[3], tb[4], tb[5], tb[6], tb[7], b);
+  // OAC_BWD2_PF: k-groups in flight per wave (2 / 3 / 4)
+  static const int pf = [] { const char* e = getenv("OAC_BWD2_PF"); return e ? atoi(e) : 3; }();
+  if (pf == 2)
+    OAC_LAUNCH(gemm_bwd_kernel<2>, dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, tb[1],
+               tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b);
+  else if (pf == 4)
+    OAC_LAUNCH(gemm_bwd_kernel<4>, dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, tb[1],
+               tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b);
+  else
+    OAC_LAUNCH(gemm_bwd_kernel<3>, dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, tb[1],
+               tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b);
   return hipGetLastError();
 }
 
