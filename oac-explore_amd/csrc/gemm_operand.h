@@ -31,15 +31,18 @@ struct Lane {
   bool ones;          // virtual ones column (dW bias)
 };
 
+// rows (k-contiguous kinds only): row mn of the operand is buffer row rows[mn]
 template <int KIND>
 __device__ __forceinline__ Lane lane_init(int mn, int n_mn, bool ones, const float* p, long ld,
-                                          const float* s, const float* v) {
+                                          const float* s, const float* v,
+                                          const int* rows = nullptr) {
   Lane o;
   o.valid = mn < n_mn;
   o.ones = ones && mn == n_mn;
   const int m = o.valid ? mn : 0;
   o.ld = ld;
-  o.p = (KIND == OP_KC || KIND == OP_KC_R1) ? p + (long)m * ld : p + m;
+  const long mr = rows ? (long)rows[m] : (long)m;
+  o.p = (KIND == OP_KC || KIND == OP_KC_R1) ? p + mr * ld : p + m;
   o.s = KIND == OP_KC_R1 ? v : s;
   o.f = KIND == OP_KC_R1 ? s[m] : (KIND == OP_MN_R1 ? v[m] : 1.f);
   return o;

@@ -36,14 +36,14 @@ __device__ long long g_gs_clock[4096 * 8];
 // acc += A[m0.., k_lo..k_hi) . B[k_lo..k_hi), n0..]  for this wave's k-groups
 template <int NW, int AK, int BK, int GPW = (NW >= 16 ? 4 : 5)>
 __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
-                                       floatx16& acc) {
+                                       floatx16& acc, const int* rows = nullptr) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   const int l32 = lane & 31;
   const int half = lane >> 5;
   const bool ar1 = (AK == OP_KC_R1 || AK == OP_MN_R1);
   const Lane la = lane_init<AK>(m0 + l32, t.M, false, ar1 ? t.a_mask : t.A,
-                                ar1 ? t.ld_mask : t.lda, t.a_s, t.a_v);
+                                ar1 ? t.ld_mask : t.lda, t.a_s, t.a_v, rows);
   const Lane lb = lane_init<BK>(n0 + l32, t.b_ones ? t.N - 1 : t.N, t.b_ones != 0, t.B, t.ldb,
                                 nullptr, nullptr);
   constexpr int kGPW = GPW;                   // k-groups in flight per wave (<= 128 VGPRs at 8 waves)
@@ -76,9 +76,9 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
 
 template <int NW, int GPW>
 __device__ __forceinline__ void k_dispatch(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
-                                           floatx16& acc) {
+                                           floatx16& acc, const int* rows) {
   const bool r1 = t.a_mode == A_RANK1_MASK;
-  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW>(t, m0, n0, k_lo, k_hi, acc);      // forward
+  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW>(t, m0, n0, k_lo, k_hi, acc, rows);   // forward
   else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dX
   else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dX, rank-1 seed
   else if (!r1)                k_loop<NW, OP_MN, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dW
@@ -197,6 +197,31 @@ gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int t
   GS_STAGE(0);
   if (publish && bid == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
+  const int* rows = nullptr;   // direct drop-in gather: this step's index slot (host memory)
+  long long bc = 0;
+  if (batch.rg.ring) {
+    bc = batch.rg.state->batch_counter;
+    rows = batch.rg.ring + (long)(bc % batch.rg.slots) * batch.rg.B;
+  }
+  if (bid >= total_tiles + batch.adam_blocks) {   // side blocks: the batch copy and the eps draws
+    const RowGather& g = batch.rg;
+    const long n4 = g.row_stride >> 2, nrow = (long)g.B * n4;
+    const long stride = (long)g.blocks * 64 * NW;
+    const float4* src = reinterpret_cast<const float4*>(g.replay);
+    float4* dst = reinterpret_cast<float4*>(g.out);
+    for (long i = (long)(bid - total_tiles - batch.adam_blocks) * 64 * NW + threadIdx.x;
+         i < nrow + (g.eps1 ? g.n_eps : 0); i += stride) {
+      if (i < nrow) {
+        const long r = i / n4, c = i - r * n4;
+        dst[r * n4 + c] = src[(long)rows[r] * n4 + c];
+      } else {
+        const unsigned e = (unsigned)(i - nrow);
+        g.eps1[e] = philox_normal(g.seed, (unsigned long long)bc, 1u, e);
+        g.eps2[e] = philox_normal(g.seed, (unsigned long long)bc, 2u, e);
+      }
+    }
+    return;
+  }
   if (bid >= total_tiles) {   // fused optimizer: flat Adam over the other ranges
     const AdamArgs& a = batch.adam;
     const AdamConsts c = adam_consts(a.state, a.advance, a.lr, a.beta1, a.beta2, a.eps,
@@ -245,7 +270,7 @@ gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int t
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  k_dispatch<NW, GPW>(t, m0, n0, k_lo, k_hi, acc);
+  k_dispatch<NW, GPW>(t, m0, n0, k_lo, k_hi, acc, t.a_rows ? rows : nullptr);
   if (t.K2 > 0) {   // second product into the same accumulator (unsplit dX tasks only)
     GemmTask t2 = t;
     t2.A = t.A2; t2.B = t.B2; t2.K = t.K2;
@@ -275,7 +300,8 @@ gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int t
     const int Rp = t.R | 1;
     for (int e = threadIdx.x; e < 32 * t.R; e += 64 * NW) {
       const int r = e / t.R, j = e % t.R;
-      lds_u[r * Rp + j] = t.U[(long)min(m0 + r, t.M - 1) * t.ldu + j];
+      const int mr = min(m0 + r, t.M - 1);
+      lds_u[r * Rp + j] = t.U[(long)(t.a_rows ? rows[mr] : mr) * t.ldu + j];
       lds_v[r * Rp + j] = t.V[(long)min(n0 + r, t.N - 1) * t.ldv + j];
     }
     __syncthreads();
@@ -353,7 +379,7 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
     b.adam_blocks = (int)std::min<long>((n4 + 64 * nw - 1) / (64 * nw), 1024);
     if (b.adam_blocks < 1) b.adam_blocks = 1;
   }
-  const int grid = b.total_tiles + b.adam_blocks;
+  const int grid = b.total_tiles + b.adam_blocks + (b.rg.ring ? b.rg.blocks : 0);
   const GemmHead h = gemm_head(b);
 #define OAC_GS(NW_, G_) \
   if (nw == NW_ && gpw == G_) { \

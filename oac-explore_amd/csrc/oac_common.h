@@ -69,6 +69,7 @@ struct GemmTask {
   const float* B2;
   int K2;
   const float* ex[6];   // extra epilogue operands (EPI_HEAD_BWD)
+  int a_rows;           // small kernel: A (and U) row m is row batch.rg rows[m] of the buffer
 };
 
 struct StepState;
@@ -91,6 +92,19 @@ struct AdamArgs {
 
 constexpr int kMaxTasks = 8;
 
+// The layer-0 launch of a direct drop-in step (small kernel, sac_plan phase0):
+// the batch's rows are read straight from the replay through the host-written
+// index slot rows = ring + (batch_counter % slots) * B, and `blocks` extra
+// workgroups copy those rows to `out` (the step's batch for the later launches)
+// and draw the step's Philox eps -- the gather launch's work, off the chain.
+struct RowGather {
+  const int* ring; int slots, B;
+  const StepState* state;
+  int blocks;
+  const float* replay; long row_stride; float* out;
+  float* eps1; float* eps2; int n_eps; unsigned long long seed;
+};
+
 struct GemmBatch {
   GemmTask t[kMaxTasks];
   int ntasks;
@@ -108,6 +122,7 @@ struct GemmBatch {
   int force_nw, force_gpw;   // small kernel: waves per workgroup / k-groups in flight (0 = auto)
   long seg_off[2], seg_n[2]; // flat ranges (floats, multiples of 4) from the group base
   AdamArgs adam;
+  RowGather rg;              // rg.ring != null: direct row gather (small kernel only)
 };
 
 // ---------------------------------------------------------------------------

@@ -34,6 +34,13 @@ struct PlanBase {
   int32_t* host_ring = nullptr;
   std::vector<hipEvent_t> ring_ev;
   std::vector<char> ring_ev_set;
+  // direct mode (oac_sac_set_host_ring(NULL)): the ring is the plan's own
+  // host-coherent allocation and the small-batch layer-0 launch reads the
+  // indices from it (no H2D copy, no gather launch); the chunk's completion
+  // event is recorded at the next staging call, behind the step that read it
+  bool rows_direct = false;
+  bool owns_host_ring = false;
+  int pending_ev = -1;
   // per-launch small-GEMM geometry overrides (tuning experiments: env
   // OAC_TUNE="launch:nw:gpw,..." read at plan creation; 0 = automatic)
   int tune_nw[64] = {0}, tune_gpw[64] = {0};

@@ -186,9 +186,11 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
   const int Dq = Do + Da;
   float* X = p.X();
-  const float* obs = X + c.off_obs;
-  const float* nobs = X + c.off_next_obs;
-  if (gather_n > 0 && (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS)))
+  // direct drop-in step: the layer-0 launch reads the batch rows through the
+  // host-written index slot and its side blocks do the gather's copy + eps
+  const bool direct = p.rows_direct && p.cfg == 0 && gather_n == 1 && !critic_done &&
+                      (flags & OAC_STEP_GATHER) && p.b.ring_slots > 0;
+  if (!direct && gather_n > 0 && (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS)))
     if (gather_steps(p, flags, gather_n, s)) return 1;
   const float* pol = p.b.params;
   const float* q1 = p.b.params + L.q1_base;
@@ -198,11 +200,25 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
   {  // layer 0: policy(obs), policy(next_obs), critic obs-projections
     GemmBatch gb{};
     gb.publish = p.state(); gb.pub_beta1 = c.beta1; gb.pub_beta2 = c.beta2;   // step's Adam constants
-    add(gb, t_fwd(obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
-    add(gb, t_fwd(nobs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
+    const float* R0 = direct ? p.b.replay : X;   // rows base: the replay (indexed) or the batch
+    add(gb, t_fwd(R0 + c.off_obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
+    add(gb, t_fwd(R0 + c.off_next_obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
     if (!critic_done) {
-      add_critic_l0(p, gb, X);
-      add_target_l0(p, gb, X);
+      add_critic_l0(p, gb, R0);
+      add_target_l0(p, gb, R0);
+    }
+    if (direct) {
+      for (int i = 0; i < gb.ntasks; ++i) gb.t[i].a_rows = 1;
+      RowGather& g = gb.rg;
+      g.ring = p.host_ring; g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
+      g.replay = p.b.replay; g.row_stride = RS; g.out = X;
+      if (flags & OAC_STEP_DEVICE_EPS) {
+        g.eps1 = p.E1(); g.eps2 = p.E2(); g.n_eps = B * Da;
+      }
+      g.seed = c.seed;
+      // enough workgroups that each thread moves ~4 float4 of rows / eps
+      const long items = (long)B * (RS / 4) + (g.eps1 ? g.n_eps : 0);
+      g.blocks = (int)std::min<long>(64, std::max<long>(1, (items + 4095) / 4096));
     }
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -589,6 +605,7 @@ int oac_sac_destroy(oac_sac* h) {
   if (h->plan.exec) (void)hipGraphExecDestroy(h->plan.exec);
   if (h->plan.graph) (void)hipGraphDestroy(h->plan.graph);
   if (h->plan.cap_stream) (void)hipStreamDestroy(h->plan.cap_stream);
+  if (h->plan.owns_host_ring && h->plan.host_ring) (void)hipHostFree(h->plan.host_ring);
   delete h;
   return 0;
 }
@@ -647,6 +664,13 @@ int oac_sac_step(oac_sac* h, int flags, void* stream) { return oac_sac_step_n(h,
 
 static constexpr int kRingChunk = 16;
 
+// direct mode needs the small-batch kernel (cfg 0); OAC_DROPIN_DIRECT=0 keeps
+// the H2D copy + gather launch (A/B runs)
+static bool dropin_direct_on() {
+  static const bool v = [] { const char* e = getenv("OAC_DROPIN_DIRECT"); return !e || atoi(e) != 0; }();
+  return v;
+}
+
 int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
@@ -661,9 +685,30 @@ int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
     p.ring_ev.push_back(e);
   }
   p.ring_ev_set.assign(nch, 0);
+  p.pending_ev = -1;
+  if (p.owns_host_ring && p.host_ring) (void)hipHostFree(p.host_ring);
+  p.host_ring = nullptr;
+  p.owns_host_ring = false;
+  p.rows_direct = false;
+  if (!pinned_ring) {   // the plan's own host-coherent ring
+    int32_t* r = nullptr;
+    OAC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&r), sizeof(int32_t) * (size_t)p.b.ring_slots * p.c.batch,
+                                hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(r, 0, sizeof(int32_t) * (size_t)p.b.ring_slots * p.c.batch);
+    p.host_ring = r;
+    p.owns_host_ring = true;
+    p.rows_direct = p.cfg == 0 && dropin_direct_on() && !has_target_policy(p.c.kind) &&
+                    p.c.kind != OAC_KIND_PARTICLE;   // sac_plan's run_step / phase0 only
+    // not direct (large batch): the copy path still stages through this ring
+    if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
+    if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
+    return 0;
+  }
   p.host_ring = pinned_ring;
   return 0;
 }
+
+int32_t* oac_sac_host_ring(oac_sac* h) { return h ? h->plan.host_ring : nullptr; }
 
 int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream) {
   if (!h) { set_error("null handle"); return 1; }
@@ -673,6 +718,11 @@ int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* str
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int B = p.c.batch, S = p.b.ring_slots;
   const int slot = (int)(bc % S), ch = slot / kRingChunk;
+  if (p.rows_direct && p.pending_ev >= 0) {   // behind the step that read the chunk's last slot
+    OAC_HIP_CHECK(hipEventRecord(p.ring_ev[p.pending_ev], s));
+    p.ring_ev_set[p.pending_ev] = 1;
+    p.pending_ev = -1;
+  }
   // first slot of a chunk: the copies that read this chunk S steps ago are done
   if (slot % kRingChunk == 0 && p.ring_ev_set[ch]) OAC_HIP_CHECK(hipEventSynchronize(p.ring_ev[ch]));
   int32_t* dst = p.host_ring + (long)slot * B;
@@ -685,6 +735,10 @@ int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* str
       return 1;
     }
     dst[i] = (int32_t)v;
+  }
+  if (p.rows_direct) {   // the layer-0 launch reads the slot from host memory
+    if (slot % kRingChunk == kRingChunk - 1 || slot == S - 1) p.pending_ev = ch;
+    return 0;
   }
   OAC_HIP_CHECK(hipMemcpyAsync(const_cast<int32_t*>(p.b.idx_ring) + (long)slot * B, dst,
                                sizeof(int32_t) * B, hipMemcpyHostToDevice, s));

@@ -82,6 +82,7 @@ _SIGS = {
     "oac_sac_step_phase": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_void_p]),
     "oac_sac_set_host_ring": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "oac_sac_host_ring": (ctypes.c_void_p, [ctypes.c_void_p]),
     "oac_sac_step_host_idx": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_int, ctypes.c_void_p]),
     "oac_sac_stage_host_idx": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,

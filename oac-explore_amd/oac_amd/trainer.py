@@ -326,10 +326,11 @@ class _ArenaTrainer(object):
         if d is None:
             S, B = self._DROPIN_SLOTS, dbatch.batch_size
             ring = torch.zeros(S * B, dtype=torch.int32, device=self.device)
-            pinned = torch.zeros(S * B, dtype=torch.int32, pin_memory=True)
             d = self._plan(B, replay=dbatch.storage, idx=ring, ring_slots=S)
-            check(_lib.lib().oac_sac_set_host_ring(d.handle, ctypes.c_void_p(pinned.data_ptr())))
-            d.rings = (ring, pinned)   # keep both alive with the plan
+            # the plan's own host-coherent staging ring: at small batch the
+            # step's first launch reads the indices from it directly
+            check(_lib.lib().oac_sac_set_host_ring(d.handle, None))
+            d.rings = (ring,)   # keep the device ring alive with the plan
             self._dropin[key] = d
         return d
 
