@@ -184,16 +184,20 @@ static GemmHead gemm_head(const GemmBatch& b) {
   return h;
 }
 
+// one workgroup's share of a launch: block `bid` of the batch (the kernel
+// below passes blockIdx.x; tools/micro/persist_micro.hip runs several batches
+// in one persistent launch with a grid barrier between them)
+template <int NW>
+struct SmallLds {
+  static constexpr int RED = NW * 16 * 64;   // partial tiles: NW x 16 regs x 64 lanes
+  static constexpr int N = RED > 2 * 32 * 65 ? RED : 2 * 32 * 65;   // reused for the epilogue operands
+};
+
 template <int NW, int GPW>
-__global__ void __launch_bounds__(64 * NW)
-gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6,
-                  int tb7, const GemmBatch batch) {
-  // partial tiles: NW x 16 regs x 64 lanes ; reused for the epilogue operands
-  constexpr int RED = NW * 16 * 64;
-  constexpr int LDS = RED > 2 * 32 * 65 ? RED : 2 * 32 * 65;
+__device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int publish, int tb1,
+                                                 int tb2, int tb3, int tb4, int tb5, int tb6,
+                                                 int tb7, const GemmBatch& batch, float* red) {
   constexpr int PER = 1024 / (64 * NW);   // epilogue elements per thread
-  __shared__ __attribute__((aligned(16))) float red[LDS];
-  const int bid = blockIdx.x;
   GS_STAGE(0);
   if (publish && bid == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
@@ -330,6 +334,15 @@ gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int t
   if (batch.fuse_adam && bid == 0 && threadIdx.x == 0)
     step_bookkeeping(batch.adam.state, batch.adam.alpha, batch.adam.advance);
   GS_STAGE(4);
+}
+
+template <int NW, int GPW>
+__global__ void __launch_bounds__(64 * NW)
+gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6,
+                  int tb7, const GemmBatch batch) {
+  __shared__ __attribute__((aligned(16))) float red[SmallLds<NW>::N];
+  gemm_small_block<NW, GPW>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6, tb7,
+                            batch, red);
 }
 
 // tile geometry shared with the plan builder
