@@ -185,6 +185,18 @@ static inline int large_batch_cfg() {
 }
 bool gemm_lds_supports(const GemmBatch& b);
 bool gemm_bwd_supports(const GemmBatch& b);
+bool gemm_fwd_supports(const GemmBatch& b);
+
+// Forward batches at large batch go to gemm_fwd.hip (cfg 6: LDS-staged
+// 128-row tiles, one global load per workgroup instead of per wave) only when
+// OAC_FWD2=1: parity-green, but at B=4096 layer 0 took 99 / 85 us with
+// 128x128 / 128x64 tiles against 71 us on the register-direct kernel, layer 1
+// 41 against 34 us (252 / 228 VGPRs: one or two waves per SIMD, and a 32-deep
+// stage is too short to cover the next stage's global loads)
+static inline bool fwd2_on() {
+  static const bool v = [] { const char* e = getenv("OAC_FWD2"); return e && atoi(e) != 0; }();
+  return v;
+}
 
 // Backward batches at large batch go to gemm_bwd.hip (cfg 5: float2 fetch of
 // the batch-major operands, K split over the workgroup's waves); OAC_BWD2=0
@@ -212,6 +224,12 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     narrow = gb.t[i].N <= 32 && gb.t[i].ksplit <= 1 && gb.t[i].K2 == 0;
   if (narrow) return 0;
   if (cfg != 2) return cfg;
+  if (fwd2_on()) {
+    bool all_fwd = true;
+    for (int i = 0; i < gb.ntasks; ++i)
+      all_fwd = all_fwd && gb.t[i].a_kc && gb.t[i].b_kc && gb.t[i].N >= 64;
+    if (all_fwd && gemm_fwd_supports(gb)) return 6;
+  }
   if (bwd2_on() && big_bwd()) {
     bool all_bwd = true;
     for (int i = 0; i < gb.ntasks; ++i) all_bwd = all_bwd && !gb.t[i].b_kc;
