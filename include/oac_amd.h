@@ -183,7 +183,10 @@ int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* str
  * the caller's critic-grad all-reduce, averaged) through the policy gradient
  * (grads arena); 3 = policy Adam + step advance (after the policy-grad
  * all-reduce).  oac_sac_step (world_size 1) runs the same sequence with the
- * split-K reduction fused into the Adam passes. */
+ * split-K reduction fused into the Adam passes.  SAC kind only: phase 4 = the
+ * part of phase 1 that needs no alpha (the critics on the fresh actions) and
+ * phase 5 = the rest of phase 1, so 0, [alpha all-reduce || 4], 5, 2, 3 is
+ * the same step with the first exchange overlapped. */
 int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream);
 int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows, int64_t* cols);
 /* number of kernel launches of one step (for the launch/graph accounting) */

@@ -269,7 +269,10 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
 
 // phase 1: fresh-action critics, TD target, critic gradients (split-K slabs);
 // fused: the critic Adam + Polyak runs inside the layer-0 gradient launch
-static int phase1(SacPlan& p, hipStream_t s, bool fused) {
+// part 0: the whole phase; 1: the fresh-action critic forward only (layer 1 +
+// last layer: no alpha needed, so the data-parallel alpha all-reduce overlaps
+// it); 2: the rest (targets through the critic gradients)
+static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -279,7 +282,7 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused) {
   const float* q2 = p.b.params + L.q2_base;
   const float* t1 = p.b.targets;
   const float* t2 = p.b.targets + L.q_size;
-  {  // layer 1
+  if (part != 2) {  // layer 1
     GemmBatch gb{};
     const float* nets[4] = {q1, q2, t1, t2};
     const int ins[4] = {W_H1N1, W_H1N2, W_H1T1, W_H1T2};
@@ -288,7 +291,7 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused) {
     for (int i = 0; i < 4; ++i) add(gb, q_l1(p, p.W(ins[i]), nets[i], p.W(outs[i]), qv[i]));
     if (run_gemm(p, gb, s)) return 1;
   }
-  if (!qdot(p)) {  // last layer
+  if (part != 2 && !qdot(p)) {  // last layer
     GemmBatch gb{};
     const float* nets[4] = {q1, q2, t1, t2};
     const int ins[4] = {W_H2N1, W_H2N2, W_H2T1, W_H2T2};
@@ -298,6 +301,7 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused) {
                     nets[i] + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
+  if (part == 1) return 0;
   {  // TD target, MSE gradients, policy seeds
     CriticTargetArgs a;
     std::memset(&a, 0, sizeof(a));
@@ -763,12 +767,15 @@ int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
   switch (phase) {
     case 0: return phase0(p, flags, s);
     case 1:
-      if (phase1(p, s, false)) return 1;
+    case 5:   // phase 1 without its first part (after phase 4)
+      if (phase1(p, s, false, phase == 5 ? 2 : 0)) return 1;
       if (p.S_q > 1) {
         AdamArgs a = critic_adam(p, 1, nullptr);
         OAC_HIP_CHECK(launch_adam(a, s));
       }
       return 0;
+    case 4:   // phase 1's fresh-action critic forward (needs no alpha)
+      return phase1(p, s, false, 1);
     case 2:
       if (phase2_adam(p, s, 1)) return 1;
       if (phase2(p, s, false)) return 1;

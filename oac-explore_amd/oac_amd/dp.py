@@ -23,6 +23,7 @@ below (liboac_amd phases + torch.distributed over RCCL) and, in the CPU
 tests, with an oracle-backed executor over gloo.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -36,14 +37,23 @@ from .particle_trainer_oac import ParticleTrainer as ParticleTrainerOAC
 from .trainer import SACTrainer
 
 
-def dp_step(ex, all_reduce):
+def dp_step(ex, all_reduce, all_reduce_async=None):
     """Drive one data-parallel step.  ``ex`` exposes phase(i) and the views
     alpha_sum() / critic_grads() / policy_grads(); ``all_reduce(t)`` sums a
-    tensor over ranks in place (the executor's Adam divides by world size)."""
+    tensor over ranks in place (the executor's Adam divides by world size).
+    With ``all_reduce_async(t) -> join`` and an executor that splits phase 1
+    (``ex.split_phase1``: "1a" = the critics on the fresh actions, which need
+    no alpha, "1b" = the rest), the alpha exchange runs beside "1a"."""
     ex.phase(0)
-    if ex.auto_alpha:
-        all_reduce(ex.alpha_sum())
-    ex.phase(1)
+    if ex.auto_alpha and all_reduce_async is not None and getattr(ex, "split_phase1", False):
+        join = all_reduce_async(ex.alpha_sum())
+        ex.phase("1a")
+        join()
+        ex.phase("1b")
+    else:
+        if ex.auto_alpha:
+            all_reduce(ex.alpha_sum())
+        ex.phase(1)
     all_reduce(ex.critic_grads())
     ex.phase(2)
     all_reduce(ex.policy_grads())
@@ -54,14 +64,17 @@ class _GpuExecutor:
     def __init__(self, trainer, plan, flags, stream):
         self.t, self.plan, self.flags, self.stream = trainer, plan, flags, stream
         self.auto_alpha = trainer.use_automatic_entropy_tuning
+        self.split_phase1 = trainer._kind == _lib.OAC_KIND_SAC   # phases 4 / 5 (sac_plan.hip)
         lay = trainer.layout
         self._crit = trainer.grads[lay.q1_base:lay.q1_base + lay.n_critics * lay.q_size]
         self._pol = trainer.grads[:lay.q1_base]   # policy Adam group
 
+    _SPLIT = {"1a": 4, "1b": 5}
+
     def phase(self, i):
         # every phase sees the step flags: phase 0 gathers / draws, phase 1
         # reads OAC_STEP_COUNTS (particle / gaussian targets)
-        check(_lib.lib().oac_sac_step_phase(self.plan.handle, i, self.flags,
+        check(_lib.lib().oac_sac_step_phase(self.plan.handle, self._SPLIT.get(i, i), self.flags,
                                             _lib.stream_ptr(self.stream)))
 
     def alpha_sum(self):
@@ -91,6 +104,10 @@ class _DataParallel:
         self.pg = process_group
         self.world = dist.get_world_size(process_group)
         self.capture = (dist.get_backend(process_group) == "nccl") if capture is None else capture
+        # the alpha exchange beside the fresh-action critic forward (RCCL only:
+        # with gloo the collective is a host call and there is nothing to overlap)
+        self._overlap = (dist.get_backend(process_group) == "nccl"
+                         and os.environ.get("OAC_DP_OVERLAP", "1") != "0")
         self._graphs, self._eager_seen = {}, set()
         super().__init__(*args, **kwargs)
         # make sure every rank starts from rank 0's state
@@ -106,10 +123,25 @@ class _DataParallel:
     def _all_reduce(self, t):
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
 
+    def _all_reduce_async(self, t):
+        """The all-reduce on a side stream forked from the current one; the
+        returned join makes the current stream wait for it (captured into the
+        step graph as a fork / join, so the exchange overlaps the work issued
+        between the fork and the join)."""
+        cur = torch.cuda.current_stream(self.device)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        side = self._side
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+        return lambda: cur.wait_stream(side)
+
     def _steps(self, plan, f, n_steps, stream):
         ex = _GpuExecutor(self, plan, f, stream)
+        overlap = self._all_reduce_async if self._overlap else None
         for _ in range(n_steps):
-            dp_step(ex, self._all_reduce)
+            dp_step(ex, self._all_reduce, overlap)
 
     def _train_host_indices(self, dbatch):
         """The drop-in call (random_batch + train per step) at world > 1: this

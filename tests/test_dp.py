@@ -18,11 +18,19 @@ Do, Da, H, BL, STEPS = 11, 3, [32, 32], 16, 3
 
 
 class OracleExecutor:
-    def __init__(self, orc, batch, e1, e2, world):
+    def __init__(self, orc, batch, e1, e2, world, split=False):
         self.o, self.b, self.e1, self.e2, self.w = orc, batch, e1, e2, world
         self.auto_alpha = orc.auto_alpha
+        # the GPU executor's phase-1 split (sac_plan phases 4 / 5): the oracle's
+        # phase 1 is one piece, so "1a" (the critics on the fresh actions) is
+        # folded into "1b"
+        self.split_phase1 = split
 
     def phase(self, i):
+        if i == "1a":
+            return
+        if i == "1b":
+            i = 1
         if i == 0:
             self.o.phase0(self.b, self.e1, self.e2)
         elif i == 1:
@@ -60,7 +68,7 @@ def _make(auto_alpha):
     return so.SACOracle(p, Do, Da, auto_alpha=auto_alpha, policy_lr=1e-3, qf_lr=1e-3)
 
 
-def _worker(rank, world, port, auto_alpha, out):
+def _worker(rank, world, port, auto_alpha, out, overlap=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -69,8 +77,13 @@ def _worker(rank, world, port, auto_alpha, out):
     for batch, e1, e2 in _inputs(world):
         sl = slice(rank * BL, (rank + 1) * BL)
         shard = {k: v[sl] for k, v in batch.items()}
-        ex = OracleExecutor(orc, shard, e1[sl], e2[sl], world)
-        dp_step(ex, lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM))
+        ex = OracleExecutor(orc, shard, e1[sl], e2[sl], world, split=overlap)
+
+        def ar_async(t):   # the exchange in flight while "1a" runs; join = wait
+            work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
+            return work.wait
+        dp_step(ex, lambda t: dist.all_reduce(t, op=dist.ReduceOp.SUM),
+                ar_async if overlap else None)
     if rank == 0:
         flat = torch.cat([t.reshape(-1) for d in (orc.P, orc.Q1, orc.Q2, orc.T1, orc.T2)
                           for t in d.values()] + [orc.log_alpha])
@@ -87,13 +100,16 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("auto_alpha", [True, False])
-def test_dp_two_ranks_equals_single_process_on_global_batch(auto_alpha):
+@pytest.mark.parametrize("auto_alpha,overlap", [(True, False), (False, False), (True, True)])
+def test_dp_two_ranks_equals_single_process_on_global_batch(auto_alpha, overlap):
+    """overlap: the alpha exchange issued asynchronously beside phase "1a"
+    and joined before "1b" (dp_step's overlapped schedule)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, auto_alpha, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, auto_alpha, q, overlap))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = q.get()
