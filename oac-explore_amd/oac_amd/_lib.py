@@ -8,7 +8,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboac_amd.so")
+# OAC_LIB: another in-tree build of the same library (same-box A/B runs of a
+# kernel change, e.g. tools/ab_lib.sh); the default is the package's own
+LIB_PATH = os.environ.get("OAC_LIB") or os.path.join(HERE, "liboac_amd.so")
 
 OAC_KIND_SAC = 0
 OAC_KIND_PARTICLE = 1
