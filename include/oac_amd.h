@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define OAC_ABI_VERSION 1
+#define OAC_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- config */
 enum oac_kind {
@@ -117,6 +117,11 @@ typedef struct oac_sac_buffers {
    * each step reads its batch counts and bumps the drawn rows on the device
    * (replay_buffer.py:186-197), so the counts recipes run from the ring. */
   int32_t* counts; int32_t* count_tags; int32_t* count_epoch;
+  /* GAUSS / PARTICLE_UB with use_target_policy and no mean_update
+   * (particle_trainer.py:150-154, 196-199; gaussian_trainer.py:154-158,
+   * 196-199): a policy-shaped block (layout pol_* offsets) whose actions on
+   * next_obs replace the policy's in the TD target; NULL = the policy */
+  const float* next_policy;
 } oac_sac_buffers;
 
 typedef struct oac_sac oac_sac;

@@ -110,7 +110,9 @@ static int dphase0(SacPlan& p, int flags, hipStream_t s) {
   }
     const float* pol = p.b.params;
   const float* tpol = p.b.params + L.tpol_base;
-  const float* npol = c.mean_update ? tpol : pol;   // the policy acting on next_obs
+  // the policy acting on next_obs: target_policy (mean_update), the
+  // use_target_policy network, or the policy itself
+  const float* npol = c.mean_update ? tpol : (p.b.next_policy ? p.b.next_policy : pol);
   const float* q = p.b.params + L.q1_base;
   const float* tq = p.b.targets;
   {

@@ -65,7 +65,7 @@ class SacBuffers(ctypes.Structure):
         ("replay_rows", ctypes.c_int64), ("idx_ring", ctypes.c_void_p),
         ("ring_slots", ctypes.c_int),
         ("counts", ctypes.c_void_p), ("count_tags", ctypes.c_void_p),
-        ("count_epoch", ctypes.c_void_p),
+        ("count_epoch", ctypes.c_void_p), ("next_policy", ctypes.c_void_p),
     ]
 
 
@@ -178,7 +178,7 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.oac_abi_version() != 1:
+    if L.oac_abi_version() != 2:
         raise RuntimeError("liboac_amd ABI version mismatch")
     _LIB = L
     return L

@@ -37,14 +37,13 @@ class GaussianTrainer(_TargetPolicyTrainer):
                  rescale_targets_around_mean=False,
                  device=None, seed=0, use_graph=True, gemm_cfg=-1):
         unsupported = dict(share_layers=not share_layers, deterministic=not deterministic,
-                           ensemble=ensemble, global_opt=global_opt,
-                           use_target_policy=use_target_policy)
+                           ensemble=ensemble, global_opt=global_opt)
         bad = [k for k, v in unsupported.items() if v]
         if bad:
             raise NotImplementedError(
                 "oac_amd.GaussianTrainer implements the g-oac recipe configuration "
                 "(share_layers=True, deterministic policy, counts / std_soft_update / "
-                f"mean_update, no ensemble / global-opt); unsupported: {bad}")
+                f"mean_update / use_target_policy, no ensemble / global-opt); unsupported: {bad}")
         assert not counts or not std_soft_update   # gaussian_trainer.py:88
         self._common_init(device, soft_target_tau, target_update_period, deterministic,
                           discount, reward_scale, policy_lr, qf_lr, use_graph, seed, gemm_cfg)
@@ -77,6 +76,7 @@ class GaussianTrainer(_TargetPolicyTrainer):
         ref_qt = q_producer(bias=qb, positive=[False, True], train_bias=train_bias)
         ref_tp = policy_producer()
         self._build(ref_pol, ref_q, ref_qt, ref_tp, policy_lr, qf_lr)
+        self._make_target_policy_network(policy_producer)
         self.q, self.q_target = self.qfs[0], self.tfs[0]
         self.q_optimizer = self.qf_optimizers[0]
 

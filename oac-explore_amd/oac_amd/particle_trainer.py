@@ -36,15 +36,14 @@ class ParticleTrainer(_TargetPolicyTrainer):
                  rescale_targets_around_mean=False,
                  device=None, seed=0, use_graph=True, gemm_cfg=-1):
         unsupported = dict(share_layers=not share_layers, deterministic=not deterministic,
-                           ensemble=ensemble, global_opt=global_opt,
-                           use_target_policy=use_target_policy)
+                           ensemble=ensemble, global_opt=global_opt)
         bad = [k for k, v in unsupported.items() if v]
         if bad:
             raise NotImplementedError(
                 "oac_amd.ParticleTrainer implements the p-oac recipe configuration "
                 "(share_layers=True, deterministic policy, counts / std_soft_update / "
-                "mean_update / rescale_targets_around_mean / train_bias, no ensemble / "
-                f"global-opt / DDPG target network); unsupported: {bad}")
+                "mean_update / rescale_targets_around_mean / train_bias / "
+                f"use_target_policy, no ensemble / global-opt); unsupported: {bad}")
         assert not counts or not std_soft_update   # particle_trainer.py:92
         self._common_init(device, soft_target_tau, target_update_period, deterministic,
                           discount, reward_scale, policy_lr, qf_lr, use_graph, seed, gemm_cfg)
@@ -84,6 +83,7 @@ class ParticleTrainer(_TargetPolicyTrainer):
         q_producer(bias=init_values, train_bias=train_bias)
         ref_tp = policy_producer()
         self._build(ref_pol, ref_q, ref_q, ref_tp, policy_lr, qf_lr)
+        self._make_target_policy_network(policy_producer)
 
     def _make_cfg(self, batch):
         c = super()._make_cfg(batch)

@@ -76,6 +76,27 @@ class _TargetPolicyTrainer(_ArenaTrainer):
         self._n_train_steps_total = 0
         self._need_to_update_eval_statistics = True
 
+    def _make_target_policy_network(self, policy_producer):
+        """use_target_policy without mean_update (particle_trainer.py:150-154,
+        gaussian_trainer.py:154-158): a policy_producer() network overwritten
+        with a copy of the policy (soft update, tau 1) that supplies the next
+        actions of the TD target (:196-199).  The reference's per-step soft
+        update copies this network onto itself (:386-388 / :385-387), so it
+        keeps the weights it has -- here a frozen block outside the Adam arena
+        (oac_sac_buffers.next_policy), loadable like the reference's."""
+        self.target_policy_network = None
+        self._tpn = None
+        if not (self.use_target_policy and not self.mean_update):
+            return
+        policy_producer()   # the reference's producer call (its init is overwritten)
+        lay = self.layout
+        self._tpn = self.params[:lay.pol_size].clone()
+        self.target_policy_network = ArenaTanhGaussianPolicy(
+            self._tpn, 0, lay, self.obs_dim, self.act_dim, self.hidden)
+
+    def _next_policy_ptr(self):
+        return None if getattr(self, "_tpn", None) is None else self._tpn.data_ptr()
+
     def _make_cfg(self, batch):
         c = super()._make_cfg(batch)
         c.std_soft_update = int(bool(self.std_soft_update))
@@ -104,11 +125,14 @@ class _TargetPolicyTrainer(_ArenaTrainer):
 
     @property
     def networks(self):
-        return [self.policy] + self.qfs + self.tfs + [self.target_policy]
+        nets = [self.policy] + self.qfs + self.tfs + [self.target_policy]
+        if getattr(self, "target_policy_network", None) is not None:
+            nets.append(self.target_policy_network)
+        return nets
 
     def get_snapshot(self):
         """gaussian_trainer.py:452-482 / particle_trainer.py:449-478 (keys)."""
-        return dict(policy_state_dict=self.policy.state_dict(),
+        d = dict(policy_state_dict=self.policy.state_dict(),
                     policy_optim_state_dict=self.policy_optimizer.state_dict(),
                     log_alpha=self.log_alpha,
                     alpha_optim_state_dict=self.alpha_optimizer.state_dict(),
@@ -120,6 +144,9 @@ class _TargetPolicyTrainer(_ArenaTrainer):
                     target_qfs_state_dicts=[t.state_dict() for t in self.tfs],
                     target_policy_state_dict=self.target_policy.state_dict(),
                     target_policy_opt_state_dict=self.target_policy_optimizer.state_dict())
+        if getattr(self, "target_policy_network", None) is not None:
+            d["target_policy_network"] = self.target_policy_network.state_dict()
+        return d
 
     def restore_from_snapshot(self, ss):
         """gaussian_trainer.py:484-517 / particle_trainer.py:480-505."""
@@ -136,4 +163,6 @@ class _TargetPolicyTrainer(_ArenaTrainer):
         self._need_to_update_eval_statistics = ss["_need_to_update_eval_statistics"]
         self.target_policy.load_state_dict(ss["target_policy_state_dict"])
         self.target_policy_optimizer.load_state_dict(ss["target_policy_opt_state_dict"])
+        if getattr(self, "target_policy_network", None) is not None:
+            self.target_policy_network.load_state_dict(ss["target_policy_network"])
         self.step_state[0] = self._n_train_steps_total

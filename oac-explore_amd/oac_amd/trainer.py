@@ -164,6 +164,11 @@ class _ArenaTrainer(object):
         self.stream = torch.cuda.Stream(device)
         return lay
 
+    def _next_policy_ptr(self):
+        """oac_sac_buffers.next_policy: a separate network acting on next_obs
+        (the g-oac / p-oac trainers' use_target_policy), or None."""
+        return None
+
     def _on_stream(self, fn):
         cur = torch.cuda.current_stream(self.device)
         self.stream.wait_stream(cur)
@@ -215,6 +220,7 @@ class _ArenaTrainer(object):
         bufs.ring_slots = ring_slots
         if count_state is not None:   # ReplayBufferCount device state (ring path, counts=True)
             bufs.counts, bufs.count_tags, bufs.count_epoch = (t.data_ptr() for t in count_state)
+        bufs.next_policy = self._next_policy_ptr()
         h = ctypes.c_void_p()
         check(L.oac_sac_create(ctypes.byref(cfg), ctypes.byref(bufs), ctypes.byref(h)))
         views = {}

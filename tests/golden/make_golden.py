@@ -317,7 +317,8 @@ def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=1
 # ------------------------------------------------------------- g-oac runs
 def gen_goac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=13, delta=0.95,
              r_min=0.0, r_max=5.0, discount=0.99, lr=3e-4, tau=5e-3, idx_seed=1,
-             pi_init_w=1e-3, q_init_w=3e-3, counts=False, soft=None, train_bias=True):
+             pi_init_w=1e-3, q_init_w=3e-3, counts=False, soft=None, train_bias=True,
+             use_target_policy=False):
     """GaussianTrainer (g-oac) as reproduce_g-oac*.sh builds it: share_layers,
     deterministic policy (main.py:219-233), q_min/q_max = r_min/r_max / (1 -
     discount); ``soft``: std_soft_update with that probability.  Parameters
@@ -332,7 +333,7 @@ def gen_goac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=13, 
                          target_update_period=1, q_min=q_min, q_max=q_max, share_layers=True,
                          counts=counts, std_soft_update=soft is not None,
                          std_soft_update_prob=0.0 if soft is None else soft,
-                         train_bias=train_bias)
+                         train_bias=train_bias, use_target_policy=use_target_policy)
     assert tr.deterministic
     params = goac_params(obs_dim, act_dim, hidden, seed, q_min, q_max, pi_init_w=pi_init_w,
                          q_init_w=q_init_w)
@@ -340,14 +341,21 @@ def gen_goac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=13, 
     load_sd(tr.target_policy, params["target_policy"])
     load_sd(tr.q, params["qf1"])
     load_sd(tr.q_target, params["target_qf1"])
+    out = {}
+    if use_target_policy:   # the DDPG target network: its own weights, recorded
+        tpn = goac_params(obs_dim, act_dim, hidden, seed + 100, q_min, q_max,
+                          pi_init_w=pi_init_w, q_init_w=q_init_w)["policy"]
+        load_sd(tr.target_policy_network, tpn)
+        for pname, t in tr.target_policy_network.state_dict().items():
+            out[f"tpn/{pname}"] = t.numpy().copy()
     rb, _ = _fill_buffer(obs_dim, act_dim, n_replay)
     crs = np.random.RandomState(77)
     np.random.seed(idx_seed)
-    out = {}
     meta = dict(kind="goac", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, B=B, steps=steps,
                 n_replay=n_replay, seed=seed, delta=delta, q_min=q_min, q_max=q_max,
                 discount=discount, lr=lr, tau=tau, idx_seed=idx_seed, pi_init_w=pi_init_w,
                 q_init_w=q_init_w, counts=counts, soft=soft, train_bias=train_bias,
+                use_target_policy=use_target_policy,
                 standard_bound=float(tr.standard_bound), std_init=float(tr.std_init))
     for s in range(steps):
         EPS_LOG.clear()
@@ -383,7 +391,7 @@ def gen_goac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=13, 
 def gen_ptrain(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=17, delta=0.95,
                r_min=0.0, r_max=5.0, discount=0.99, lr=3e-4, tau=5e-3, idx_seed=1,
                pi_init_w=1e-3, q_init_w=3e-3, counts=False, soft=None, mean_update=False,
-               rescale=False, q_range=None, train_bias=True):
+               rescale=False, q_range=None, train_bias=True, use_target_policy=False):
     """ParticleTrainer (trainer/particle_trainer.py) as main.py builds it for
     --alg p-oac without --beta_UB (main.py:198-218): share_layers,
     deterministic policy, q_min/q_max = r_min/r_max / (1 - discount) (or
@@ -399,23 +407,30 @@ def gen_ptrain(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed
                          share_layers=True, counts=counts, mean_update=mean_update,
                          std_soft_update=soft is not None,
                          std_soft_update_prob=0.0 if soft is None else soft,
-                         rescale_targets_around_mean=rescale, train_bias=train_bias)
+                         rescale_targets_around_mean=rescale, train_bias=train_bias,
+                         use_target_policy=use_target_policy)
     params = ptrain_params(obs_dim, act_dim, hidden, seed, K, q_min, q_max, pi_init_w=pi_init_w,
                            q_init_w=q_init_w)
     load_sd(tr.policy, params["policy"])
     load_sd(tr.target_policy, params["target_policy"])
     load_sd(tr.qfs[0], params["qf1"])
     load_sd(tr.tfs[0], params["target_qf1"])
+    out = {}
+    if use_target_policy:   # the DDPG target network: its own weights, recorded
+        tpn = ptrain_params(obs_dim, act_dim, hidden, seed + 100, K, q_min, q_max,
+                            pi_init_w=pi_init_w, q_init_w=q_init_w)["policy"]
+        load_sd(tr.target_policy_network, tpn)
+        for pname, t in tr.target_policy_network.state_dict().items():
+            out[f"tpn/{pname}"] = t.numpy().copy()
     rb, _ = _fill_buffer(obs_dim, act_dim, n_replay)
     crs = np.random.RandomState(77)
     np.random.seed(idx_seed)
-    out = {}
     meta = dict(kind="ptrain", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, K=K, B=B,
                 steps=steps, n_replay=n_replay, seed=seed, delta=delta, q_min=q_min,
                 q_max=q_max, discount=discount, lr=lr, tau=tau, idx_seed=idx_seed,
                 pi_init_w=pi_init_w, q_init_w=q_init_w, counts=counts, soft=soft,
                 mean_update=mean_update, rescale=rescale, delta_index=int(tr.delta_index),
-                train_bias=train_bias)
+                train_bias=train_bias, use_target_policy=use_target_policy)
     for s in range(steps):
         EPS_LOG.clear()
         batch, idx = _record_batch(rb, B)
@@ -725,6 +740,17 @@ def save(name, meta, out):
     print(f"{name}: {os.path.getsize(path) / 1e3:.0f} KB, {len(out)} arrays")
 
 
+def gen_tpn():
+    """use_target_policy (the DDPG target network, particle_trainer.py:150-154,
+    196-199, 386-388; gaussian_trainer.py the same): next actions from a
+    separate policy network that the reference's soft update never moves."""
+    save("ptrain_tpn", *gen_ptrain("ptrain_tpn", 11, 3, [16, 16], 5, 16, 3, 200, True,
+                                   pi_init_w=0.5, q_init_w=0.5, lr=1e-3,
+                                   use_target_policy=True))
+    save("goac_tpn", *gen_goac("goac_tpn", 11, 3, [16, 16], 16, 3, 200, True, pi_init_w=0.5,
+                               q_init_w=0.5, lr=1e-3, use_target_policy=True))
+
+
 def main():
     torch.set_num_threads(8)
     if len(sys.argv) > 1 and sys.argv[1] == "sac_snapshot":
@@ -752,6 +778,9 @@ def main():
         return
     if len(sys.argv) > 1 and sys.argv[1] == "ptrain":
         gen_ptrain_all()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "target_policy_network":
+        gen_tpn()
         return
     if len(sys.argv) > 1 and sys.argv[1] == "goac":
         gen_goac_all()

@@ -12,14 +12,17 @@ from gpu_helpers import Space, StateDictModule, batch_from, module_tensors
 
 pytestmark = pytest.mark.gpu
 
-FIXTURES = ["goac_small", "goac_counts", "goac_soft", "goac_humanoid", "goac_nobias"]
+FIXTURES = ["goac_small", "goac_counts", "goac_soft", "goac_humanoid", "goac_nobias",
+            "goac_tpn"]
 
 
 def goac_producers(params):
     """Producers in the reference constructor's call order: SACTrainer's
     policy and four critics, the shared-layer critic and its target, then
     target_policy (gaussian_trainer.py:51-63, 91-99, 146)."""
-    pols = iter([params["policy"], params["target_policy"]])
+    # a third policy_producer() call builds use_target_policy's network (its
+    # weights are then overwritten: a copy of the policy, then the fixture's)
+    pols = iter([params["policy"], params["target_policy"], params["policy"]])
     qs = iter([params["qf1"]] * 4 + [params["qf1"], params["target_qf1"]])
     return (lambda **k: StateDictModule(next(pols)),
             lambda **k: StateDictModule(next(qs)))
@@ -40,13 +43,17 @@ def goac_trainer_for(meta, params=None, **kw):
                            share_layers=True, counts=bool(meta.get("counts")),
                            std_soft_update=soft is not None,
                            std_soft_update_prob=0.0 if soft is None else soft,
-                           train_bias=meta.get("train_bias", True), **kw)
+                           train_bias=meta.get("train_bias", True),
+                           use_target_policy=bool(meta.get("use_target_policy")), **kw)
 
 
 @pytest.mark.parametrize("name", FIXTURES)
 def test_goac_step_matches_reference_golden(name):
     meta, g = parity.load(name)
     tr = goac_trainer_for(meta)
+    if meta.get("use_target_policy"):   # the fixture's DDPG target network weights
+        tr.target_policy_network.load_state_dict(
+            {k[4:]: torch.as_tensor(v) for k, v in g.items() if k.startswith("tpn/")})
     assert abs(tr.standard_bound - meta["standard_bound"]) < 1e-12
     errs = {}
     for s in range(meta["steps"]):

@@ -14,13 +14,15 @@ from gpu_helpers import Space, StateDictModule, batch_from, module_tensors
 pytestmark = pytest.mark.gpu
 
 FIXTURES = ["ptrain_small", "ptrain_counts", "ptrain_soft_rescale", "ptrain_mean_update",
-            "ptrain_humanoid", "ptrain_nobias"]
+            "ptrain_humanoid", "ptrain_nobias", "ptrain_tpn"]
 
 
 def ptrain_producers(params):
     """Producers in the reference constructor's call order
     (particle_trainer.py:47-59, 96-106, 141)."""
-    pols = iter([params["policy"], params["target_policy"]])
+    # a third policy_producer() call builds use_target_policy's network (its
+    # weights are then overwritten: a copy of the policy, then the fixture's)
+    pols = iter([params["policy"], params["target_policy"], params["policy"]])
     qs = iter([params["qf1"]] * 4 + [params["qf1"], params["target_qf1"]])
     return (lambda **k: StateDictModule(next(pols)),
             lambda **k: StateDictModule(next(qs)))
@@ -43,13 +45,17 @@ def ptrain_trainer_for(meta, params=None, **kw):
                            rescale_targets_around_mean=bool(meta.get("rescale")),
                            std_soft_update=soft is not None,
                            std_soft_update_prob=0.0 if soft is None else soft,
-                           train_bias=meta.get("train_bias", True), **kw)
+                           train_bias=meta.get("train_bias", True),
+                           use_target_policy=bool(meta.get("use_target_policy")), **kw)
 
 
 @pytest.mark.parametrize("name", FIXTURES)
 def test_ptrain_step_matches_reference_golden(name):
     meta, g = parity.load(name)
     tr = ptrain_trainer_for(meta)
+    if meta.get("use_target_policy"):   # the fixture's DDPG target network weights
+        tr.target_policy_network.load_state_dict(
+            {k[4:]: torch.as_tensor(v) for k, v in g.items() if k.startswith("tpn/")})
     assert tr.delta_index == meta["delta_index"]
     errs = {}
     for s in range(meta["steps"]):
