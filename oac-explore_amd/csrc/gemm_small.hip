@@ -34,16 +34,20 @@ __device__ long long g_gs_clock[4096 * 8];
 #endif
 
 // acc += A[m0.., k_lo..k_hi) . B[k_lo..k_hi), n0..]  for this wave's k-groups
+// arow >= 0: this lane's A row is buffer row arow (the direct gather's index,
+// loaded by the caller ahead of everything else)
 template <int NW, int AK, int BK, int GPW = (NW >= 16 ? 4 : 5)>
 __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
-                                       floatx16& acc, const int* rows = nullptr) {
+                                       floatx16& acc, int arow = -1) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   const int l32 = lane & 31;
   const int half = lane >> 5;
   const bool ar1 = (AK == OP_KC_R1 || AK == OP_MN_R1);
-  const Lane la = lane_init<AK>(m0 + l32, t.M, false, ar1 ? t.a_mask : t.A,
-                                ar1 ? t.ld_mask : t.lda, t.a_s, t.a_v, rows);
+  Lane la = lane_init<AK>(m0 + l32, t.M, false, ar1 ? t.a_mask : t.A,
+                          ar1 ? t.ld_mask : t.lda, t.a_s, t.a_v);
+  if (arow >= 0 && (AK == OP_KC || AK == OP_KC_R1))
+    la.p = (ar1 ? t.a_mask : t.A) + (long)arow * (ar1 ? t.ld_mask : t.lda);
   const Lane lb = lane_init<BK>(n0 + l32, t.b_ones ? t.N - 1 : t.N, t.b_ones != 0, t.B, t.ldb,
                                 nullptr, nullptr);
   constexpr int kGPW = GPW;                   // k-groups in flight per wave (<= 128 VGPRs at 8 waves)
@@ -57,8 +61,8 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
     for (int j = 0; j < kGPW; ++j)
       if (g0 + j * NW < g_hi) {
         const int kb = 8 * (g0 + j * NW) + 4 * half;
+        load4<BK>(lb, kb, kmax, bx[j], by[j]);   // B first: it never waits on a row index
         load4<AK>(la, kb, kmax, ax[j], ay[j]);
-        load4<BK>(lb, kb, kmax, bx[j], by[j]);
       }
 #pragma unroll
     for (int j = 0; j < kGPW; ++j)
@@ -76,9 +80,9 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
 
 template <int NW, int GPW>
 __device__ __forceinline__ void k_dispatch(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
-                                           floatx16& acc, const int* rows) {
+                                           floatx16& acc, int arow) {
   const bool r1 = t.a_mode == A_RANK1_MASK;
-  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW>(t, m0, n0, k_lo, k_hi, acc, rows);   // forward
+  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW>(t, m0, n0, k_lo, k_hi, acc, arow);   // forward
   else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dX
   else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dX, rank-1 seed
   else if (!r1)                k_loop<NW, OP_MN, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dW
@@ -263,6 +267,9 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   GS_STAGE(1);
+  // the direct gather's row index (host memory, the longest wait of the
+  // launch) is requested before anything else
+  const int arow = (t.a_rows && rows) ? rows[min(m0 + (lane & 31), t.M - 1)] : -1;
 
   EpiIn xin[PER];
 #pragma unroll
@@ -274,7 +281,7 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  k_dispatch<NW, GPW>(t, m0, n0, k_lo, k_hi, acc, t.a_rows ? rows : nullptr);
+  k_dispatch<NW, GPW>(t, m0, n0, k_lo, k_hi, acc, arow);
   if (t.K2 > 0) {   // second product into the same accumulator (unsplit dX tasks only)
     GemmTask t2 = t;
     t2.A = t.A2; t2.B = t.B2; t2.K = t.K2;

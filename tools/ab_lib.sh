@@ -9,4 +9,4 @@ for r in 1 2; do
     echo "$v run $r: $(head -1 gpurun_out/ab_${v}_$r.txt)"
   done
 done
-paste gpurun_out/ab_base_2.txt gpurun_out/ab_new_2.txt | tail -n +2 | awk '{printf "%s %s %s | %s\n", $2, $3, $4, $8}'
+paste gpurun_out/ab_base_2.txt gpurun_out/ab_new_2.txt | tail -n +2 | awk '{printf "%s %s %s | %s\n", $2, $3, $4, $9}'
