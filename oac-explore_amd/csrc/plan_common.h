@@ -1,6 +1,7 @@
 // Shared machinery of the launch plans (SAC / particle trainers): workspace
 // bookkeeping, split-K sizing, GEMM task constructors, HIP-event timing.
 #pragma once
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -184,6 +185,16 @@ static inline int large_batch_cfg() {
   return v;
 }
 bool gemm_lds_supports(const GemmBatch& b);
+
+// forward batches with fewer 128x64 tiles than this run on 64x64 tiles
+// (OAC_SMALL_FWD=<tiles>; 0: always 128x64).  configs[4] P-OAC (single N = 256
+// products at B=4096: 128 tiles) 2,872 -> 3,105 / 3,132 / 3,174 steps/s at 256 /
+// 512 / 1024; the SAC step 2,473 -> 2,475 / 2,476 / 2,301 (its 512- and
+// 768-tile layer launches must stay on 128x64)
+static inline int small_fwd_tiles() {
+  static const int v = [] { const char* e = getenv("OAC_SMALL_FWD"); return e ? atoi(e) : 512; }();
+  return v;
+}
 bool gemm_bwd_supports(const GemmBatch& b);
 bool gemm_fwd_supports(const GemmBatch& b);
 
@@ -248,6 +259,14 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     // continuation of the row (the action stored right after the observation)
     // or from a separate action buffer (the policy's a~)
     if (t.epi == EPI_BIAS_RANK_RELU && (!t.C2 || t.ksplit > 1)) return 1;
+  }
+  if (!any_bwd) {
+    // a forward batch with fewer 128x64 tiles than CUs (one GEMM of N = 256 at
+    // B=4096: 128 tiles) runs on 64x64 tiles instead: twice the workgroups
+    int tiles = 0;
+    for (int i = 0; i < gb.ntasks; ++i)
+      tiles += ((gb.t[i].M + 127) / 128) * ((gb.t[i].N + 63) / 64) * std::max(1, gb.t[i].ksplit);
+    if (tiles < small_fwd_tiles()) return 3;
   }
   return any_bwd ? 3 : 2;
 }

@@ -20,13 +20,29 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--rate-steps", type=int, default=2000)
+    ap.add_argument("--poac", action="store_true",
+                    help="BASELINE configs[4]: ParticleTrainerOAC K=10, Ant dims")
     a = ap.parse_args()
     sys.argv = [sys.argv[0], "--no-cpu-baseline", "--batch", str(a.batch)]
     import bench
     from oac_amd import _lib
     args = bench.parse()
     dev = torch.device("cuda", 0)
-    tr, rb, _ = bench.build(args, 0, 1, dev)
+    if a.poac:   # the trainer and replay of bench.poac_ant_leg
+        import oac_amd
+        Do, Da, K = 111, 8, 10
+        torch.manual_seed(0)
+        pp = oac_amd.get_policy_producer(Do, Da, [256, 256], device=dev)
+        qp = oac_amd.get_q_producer(Do, Da, [256, 256], output_size=K, device=dev)
+        tr = oac_amd.ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=bench.Space(Da),
+                                        discount=0.99, policy_lr=3e-4, qf_lr=3e-4,
+                                        soft_target_tau=5e-3, use_automatic_entropy_tuning=True,
+                                        deterministic=False, q_min=0.0, q_max=500.0,
+                                        share_layers=True, device=dev)
+        rb = oac_amd.ReplayBuffer(args.replay, Do, Da, device=dev)
+        rb.load_transitions(bench.synthetic_rows(args.replay, rb.rows, Do, Da, dev, seed=3))
+    else:
+        tr, rb, _ = bench.build(args, 0, 1, dev)
     B = a.batch
     np.random.seed(1)
     run = bench.dropin_run(tr, rb, B)
