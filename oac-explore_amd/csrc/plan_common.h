@@ -242,9 +242,15 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     if (all_fwd && gemm_fwd_supports(gb)) return 6;
   }
   if (bwd2_on() && big_bwd()) {
-    bool all_bwd = true;
-    for (int i = 0; i < gb.ntasks; ++i) all_bwd = all_bwd && !gb.t[i].b_kc;
-    if (all_bwd && gemm_bwd_supports(gb)) return 5;
+    // a dX with a short K (the head's 2 Da, the K-output critic's K) leaves
+    // gemm_bwd's K-split waves idle and its epilogue to two waves: those
+    // launches stay on the register-direct kernel (cfg 3)
+    bool all_bwd = true, short_dx = false;
+    for (int i = 0; i < gb.ntasks; ++i) {
+      all_bwd = all_bwd && !gb.t[i].b_kc;
+      short_dx = short_dx || (gb.t[i].a_kc && gb.t[i].K < 64);
+    }
+    if (all_bwd && !short_dx && gemm_bwd_supports(gb)) return 5;
   }
   bool any_bwd = false;
   for (int i = 0; i < gb.ntasks; ++i) {
