@@ -413,9 +413,11 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   if (b.total_tiles <= 0) return hipSuccess;
   if (cfg == 0) return gemm_small_launch(b, s);
   if (b.fuse_adam) return hipErrorInvalidValue;   // fused optimizer: small-batch kernel only
-  for (int i = 0; i < b.ntasks; ++i)               // dual products / head backward: small kernel
-    if (b.t[i].K2 > 0 || b.t[i].epi == EPI_HEAD_BWD || b.t[i].epi == EPI_BIAS_RELU_DOT)
-      return hipErrorInvalidValue;
+  for (int i = 0; i < b.ntasks; ++i) {             // dual products / head backward: small kernel
+    if (b.t[i].K2 > 0 || b.t[i].epi == EPI_HEAD_BWD) return hipErrorInvalidValue;
+    // the width-1 head dot: small kernel or the register-direct one (cfg 2 / 3)
+    if (b.t[i].epi == EPI_BIAS_RELU_DOT && cfg != 2 && cfg != 3) return hipErrorInvalidValue;
+  }
   if (cfg == 4) return gemm_lds_launch(b, s);
   if (cfg == 5) return gemm_bwd_launch(b, s);
   if (cfg == 6) return gemm_fwd_launch(b, s);

@@ -115,6 +115,31 @@ template <int WM, int WN>
 __device__ __forceinline__ void rd_epilogue(const GemmTask& t, int mw, int nw,
                                             const floatx16 (&acc)[WM][WN], bool second) {
   const int lane = threadIdx.x & 63;
+  if (t.epi == EPI_BIAS_RELU_DOT) {
+    // C = relu(acc + b) and, per row, the partial dot of this 32-column block
+    // with aux[n] (the width-1 output layer on the hidden activations):
+    // the 32 lanes of a half-wave hold one row's 32 columns, summed by a
+    // fixed butterfly, block-major partials C2[(n / 32) * ldc2 + m]
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int n = nw + 32 * j + (lane & 31);
+      const bool nin = n < t.N;
+      const float bias = nin ? t.bias[n] : 0.f, w = nin ? t.aux[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = mw + 32 * i + acc_row(r, lane);
+          const float h = fmaxf(acc[i][j][r] + bias, 0.f);
+          if (nin && m < t.M) t.C[(long)m * t.ldc + n] = h;
+          float x = (nin && m < t.M) ? h * w : 0.f;
+#pragma unroll
+          for (int off = 16; off > 0; off >>= 1) x += __shfl_xor(x, off, 32);
+          if ((lane & 31) == 0 && m < t.M) t.C2[(long)((nw + 32 * j) >> 5) * t.ldc2 + m] = x;
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < WN; ++j) {
     const int n = nw + 32 * j + (lane & 31);
@@ -252,7 +277,7 @@ hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s, bool bwd) {
   if (b.total_tiles <= 0) return hipSuccess;
   for (int i = 0; i < b.ntasks; ++i) {
     const GemmTask& t = b.t[i];
-    if (t.K2 > 0 || t.epi == EPI_HEAD_BWD || t.epi == EPI_BIAS_RELU_DOT || b.fuse_adam ||
+    if (t.K2 > 0 || t.epi == EPI_HEAD_BWD || b.fuse_adam ||
         (t.b_kc && !t.a_kc) || (t.b_kc && t.a_mode != A_PLAIN))
       return hipErrorInvalidValue;   // kinds handled in gemm_big_kernel
     if (t.epi == EPI_BIAS_RANK_RELU && (!t.C2 || t.ksplit > 1)) return hipErrorInvalidValue;

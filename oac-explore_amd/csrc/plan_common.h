@@ -257,8 +257,7 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     const GemmTask& t = gb.t[i];
     const bool fwd = t.a_kc && t.b_kc && t.a_mode == A_PLAIN;
     const bool bwd = !t.b_kc && big_bwd();   // dX / dW products (register-direct, gemm_big.hip)
-    if (!(fwd || bwd) || t.N < 64 || t.K2 > 0 || t.epi == EPI_HEAD_BWD ||
-        t.epi == EPI_BIAS_RELU_DOT || gb.fuse_adam)
+    if (!(fwd || bwd) || t.N < 64 || t.K2 > 0 || t.epi == EPI_HEAD_BWD || gb.fuse_adam)
       return 1;
     any_bwd |= bwd;
     // the big kernel runs the rank-R columns on the same accumulators: as a

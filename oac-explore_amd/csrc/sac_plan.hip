@@ -107,9 +107,16 @@ static void layout_workspace(SacPlan& p) {
 // phase 0: gather, forward of everything that does not need alpha, policy
 //          sample (+ alpha update when world_size == 1)
 // The width-1 critic heads ride on the layer-1 epilogue (EPI_BIAS_RELU_DOT;
-// critic_targets adds the per-tile partials) on the small-batch kernel.
+// critic_targets adds the per-32-column partials): on the small-batch kernel
+// and, since round 2, on the large-batch register-direct kernel (two N = 1
+// launches fewer at B=4096; OAC_QDOT_BIG=0 keeps them)
+static bool qdot_big() {
+  static const bool v = [] { const char* e = getenv("OAC_QDOT_BIG"); return !e || atoi(e) != 0; }();
+  return v;
+}
 static bool qdot(const SacPlan& p) {
-  return p.cfg == 0 && p.c.q_out == 1 && (p.c.hidden + 31) / 32 <= 16;
+  return (p.cfg == 0 || (p.cfg == 2 && qdot_big())) && p.c.q_out == 1 &&
+         (p.c.hidden + 31) / 32 <= 16;
 }
 static GemmTask q_l1(SacPlan& p, const float* in, const float* net, float* out, int qv) {
   const oac_sac_config& c = p.c;
