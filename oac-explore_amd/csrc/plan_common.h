@@ -219,6 +219,8 @@ static inline bool bwd2_on() {
 
 static inline int launch_cfg(int cfg, const GemmBatch& gb) {
   if (cfg == 0) return 0;
+  for (int i = 0; i < gb.ntasks; ++i)   // the fused head backward exists on the small kernel only
+    if (gb.t[i].epi == EPI_HEAD_BWD) return 0;
   if (cfg == 4) {
     bool narrow = !gb.fuse_adam;
     for (int i = 0; i < gb.ntasks && narrow; ++i)

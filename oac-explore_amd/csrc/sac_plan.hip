@@ -114,6 +114,14 @@ static bool qdot_big() {
   static const bool v = [] { const char* e = getenv("OAC_QDOT_BIG"); return !e || atoi(e) != 0; }();
   return v;
 }
+// the large-batch step runs dL/da + the tanh-Gaussian head backward as one
+// small-kernel launch too (the dL/da product is 17 wide; its epilogue is the
+// head backward) instead of a GEMM launch and a row launch; OAC_HEADBWD_BIG=0
+// keeps the two
+static bool head_bwd_fused_big() {
+  static const bool v = [] { const char* e = getenv("OAC_HEADBWD_BIG"); return !e || atoi(e) != 0; }();
+  return v;
+}
 static bool qdot(const SacPlan& p) {
   return (p.cfg == 0 || (p.cfg == 2 && qdot_big())) && p.c.q_out == 1 &&
          (p.c.hidden + 31) / 32 <= 16;
@@ -403,7 +411,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     if (prefetch) add_critic_l0(p, gb, prefetch);
     if (run_gemm(p, gb, s)) return 1;
   }
-  if (p.cfg == 0) {  // dL/da through both critics' action columns + head backward, one launch
+  if (p.cfg == 0 || head_bwd_fused_big()) {  // dL/da through both critics' action columns + head backward, one launch (small kernel)
     GemmBatch gb{};
     GemmTask t = t_dx(p.W(W_DH1N1), H, B, H, q1 + L.q_fc0_w + Do, Dq, Da, p.W(W_DHEAD), 2 * Da,
                       nullptr, 0);
