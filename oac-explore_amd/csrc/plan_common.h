@@ -254,18 +254,22 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     }
     if (all_bwd && !short_dx && gemm_bwd_supports(gb)) return 5;
   }
-  bool any_bwd = false;
+  // a width-1 head riding on a layer-1 epilogue (EPI_BIAS_RELU_DOT) exists on
+  // the small and register-direct kernels only: a batch the register-direct
+  // kernel does not take (hidden < 64, ragged dims) runs on the small kernel
+  bool any_bwd = false, dot = false;
+  for (int i = 0; i < gb.ntasks; ++i) dot = dot || gb.t[i].epi == EPI_BIAS_RELU_DOT;
   for (int i = 0; i < gb.ntasks; ++i) {
     const GemmTask& t = gb.t[i];
     const bool fwd = t.a_kc && t.b_kc && t.a_mode == A_PLAIN;
     const bool bwd = !t.b_kc && big_bwd();   // dX / dW products (register-direct, gemm_big.hip)
     if (!(fwd || bwd) || t.N < 64 || t.K2 > 0 || t.epi == EPI_HEAD_BWD || gb.fuse_adam)
-      return 1;
+      return dot ? 0 : 1;
     any_bwd |= bwd;
     // the big kernel runs the rank-R columns on the same accumulators: as a
     // continuation of the row (the action stored right after the observation)
     // or from a separate action buffer (the policy's a~)
-    if (t.epi == EPI_BIAS_RANK_RELU && (!t.C2 || t.ksplit > 1)) return 1;
+    if (t.epi == EPI_BIAS_RANK_RELU && (!t.C2 || t.ksplit > 1)) return dot ? 0 : 1;
   }
   if (!any_bwd) {
     // a forward batch with fewer 128x64 tiles than CUs (one GEMM of N = 256 at
