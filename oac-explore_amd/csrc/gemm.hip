@@ -374,17 +374,18 @@ int gemm_lds_tile_m();
 int gemm_lds_tile_n();
 
 hipError_t gemm_bwd_launch(const GemmBatch& b, hipStream_t s);
-hipError_t gemm_fwd_launch(const GemmBatch& b, hipStream_t s);
-int gemm_fwd_tile_n();
+hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s);
+int gemm_fwd_tile_m(int cfg);
+int gemm_fwd_tile_n(int cfg);
 
 int gemm_tile_m(int cfg) {
   if (cfg == 5) return 64;
-  if (cfg == 6) return 128;
+  if (cfg >= 6) return gemm_fwd_tile_m(cfg);
   return cfg == 0 ? 32 : cfg == 4 ? gemm_lds_tile_m() : cfg >= 2 ? gemm_big_tile_m(cfg == 3) : lds_tile_m();
 }
 int gemm_tile_n(int cfg) {
   if (cfg == 5) return 64;
-  if (cfg == 6) return gemm_fwd_tile_n();
+  if (cfg >= 6) return gemm_fwd_tile_n(cfg);
   return cfg == 0 ? 32 : cfg == 4 ? gemm_lds_tile_n() : cfg >= 2 ? gemm_big_tile_n(cfg == 3) : lds_tile_n();
 }
 
@@ -415,12 +416,12 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   if (b.fuse_adam) return hipErrorInvalidValue;   // fused optimizer: small-batch kernel only
   for (int i = 0; i < b.ntasks; ++i) {             // dual products / head backward: small kernel
     if (b.t[i].K2 > 0 || b.t[i].epi == EPI_HEAD_BWD) return hipErrorInvalidValue;
-    // the width-1 head dot: small kernel or the register-direct one (cfg 2 / 3)
-    if (b.t[i].epi == EPI_BIAS_RELU_DOT && cfg != 2 && cfg != 3) return hipErrorInvalidValue;
+    // the width-1 head dot: small kernel, the register-direct one (cfg 2 / 3) or gemm_fwd (6-8)
+    if (b.t[i].epi == EPI_BIAS_RELU_DOT && cfg != 2 && cfg != 3 && cfg < 6) return hipErrorInvalidValue;
   }
   if (cfg == 4) return gemm_lds_launch(b, s);
   if (cfg == 5) return gemm_bwd_launch(b, s);
-  if (cfg == 6) return gemm_fwd_launch(b, s);
+  if (cfg >= 6) return gemm_fwd_launch(b, cfg, s);
   if (cfg >= 2) return gemm_big_launch(b, s, cfg == 3);
   switch (lds_variant()) {
     case 1: OAC_LAUNCH(gemm_grouped_kernel<CfgL1>, dim3(b.total_tiles), dim3(256), 0, s, b); break;

@@ -30,11 +30,10 @@
 #include "oac_common.h"
 #include "kernels.h"
 #include "gemm_operand.h"
+#include "gemm_epilogue.h"
 #include "adam_common.h"
 
 namespace oac {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 template <int AK, int BK, int WM, int WN>
 struct Frag {
@@ -108,72 +107,6 @@ __device__ __forceinline__ void rd_loop(const GemmTask& t, const float* A, long 
   }
 }
 
-// element (m, n) of an accumulator register: lane l, register r of a 32x32 block
-__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
-
-template <int WM, int WN>
-__device__ __forceinline__ void rd_epilogue(const GemmTask& t, int mw, int nw,
-                                            const floatx16 (&acc)[WM][WN], bool second) {
-  const int lane = threadIdx.x & 63;
-  if (t.epi == EPI_BIAS_RELU_DOT) {
-    // C = relu(acc + b) and, per row, the partial dot of this 32-column block
-    // with aux[n] (the width-1 output layer on the hidden activations):
-    // the 32 lanes of a half-wave hold one row's 32 columns, summed by a
-    // fixed butterfly, block-major partials C2[(n / 32) * ldc2 + m]
-#pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      const int n = nw + 32 * j + (lane & 31);
-      const bool nin = n < t.N;
-      const float bias = nin ? t.bias[n] : 0.f, w = nin ? t.aux[n] : 0.f;
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = mw + 32 * i + acc_row(r, lane);
-          const float h = fmaxf(acc[i][j][r] + bias, 0.f);
-          if (nin && m < t.M) t.C[(long)m * t.ldc + n] = h;
-          float x = (nin && m < t.M) ? h * w : 0.f;
-#pragma unroll
-          for (int off = 16; off > 0; off >>= 1) x += __shfl_xor(x, off, 32);
-          if ((lane & 31) == 0 && m < t.M) t.C2[(long)((nw + 32 * j) >> 5) * t.ldc2 + m] = x;
-        }
-    }
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < WN; ++j) {
-    const int n = nw + 32 * j + (lane & 31);
-    if (n >= t.N) continue;
-    float bias = 0.f;
-    if (t.epi == EPI_BIAS || t.epi == EPI_BIAS_RELU || t.epi == EPI_BIAS_RANK_RELU) bias = t.bias[n];
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mw + 32 * i + acc_row(r, lane);
-        if (m >= t.M) continue;
-        const float v = acc[i][j][r];
-        const long o = (long)m * t.ldc + n;
-        switch (t.epi) {
-          case EPI_STORE: t.C[o] = v; break;
-          case EPI_GRAD:
-            if (t.b_ones && n == t.N - 1) t.bias_grad[m] = v;
-            else t.C[o] = v;
-            break;
-          case EPI_BIAS: t.C[o] = v + bias; break;
-          case EPI_BIAS_RELU: t.C[o] = fmaxf(v + bias, 0.f); break;
-          case EPI_BIAS_RANK_RELU:   // pass 1: C = X W^T + b ; pass 2 (acc += U V^T): C2 = relu(. + b)
-            if (!second) t.C[o] = v + bias;
-            else t.C2[(long)m * t.ldc2 + n] = fmaxf(v + bias, 0.f);
-            break;
-          case EPI_ADD_RELU: t.C[o] = fmaxf(v + t.aux[(long)m * t.ld_aux + n], 0.f); break;
-          case EPI_MASK: t.C[o] = t.aux[(long)m * t.ld_aux + n] > 0.f ? v : 0.f; break;
-          default: break;
-        }
-      }
-  }
-}
-
 template <int WM, int WN, int PF>
 __global__ void __launch_bounds__(256)
 gemm_big_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
@@ -243,7 +176,7 @@ gemm_big_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
     else
       rd_loop<OP_KC, OP_KC, WM, WN, PF>(t, t.U, t.ldu, t.V, t.ldv, t.M, t.N, false, mw, nw, 0, t.R,
                                         acc);
-    rd_epilogue<WM, WN>(t, mw, nw, acc, true);
+    epi_dispatch<WM, WN, EPI_BIAS_RANK_RELU>(t, mw, nw, acc, true);
   }
 }
 

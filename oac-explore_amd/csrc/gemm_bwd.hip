@@ -215,7 +215,22 @@ __device__ __forceinline__ void bwd_tile(GemmTask t, int local, float* red) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) fin[j][r] = acc[bi][j][r] + red[(bi * 32 + j * 16 + r) * 64 + lane];
 
-  // ---- epilogue: rows m of block bi, the lane's column pair
+  // ---- epilogue: rows m of block bi, the lane's column pair.  The ReLU
+  // masks of a dX are all loaded before the first store (C and aux may alias
+  // as far as the compiler knows, so interleaved they would cost one
+  // dependent memory round trip per register)
+  float mk0[16], mk1[16];
+  if (t.epi == EPI_MASK) {
+    const int N = t.N;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rho = acc_row_b(r, lane);
+      const int m = a_mn ? mt + 2 * rho + bi : mt + 32 * bi + rho;
+      const float* mk = t.aux + (long)min(m, M - 1) * t.ld_aux + bn0;
+      mk0[r] = bn0 < N ? mk[0] : 0.f;
+      mk1[r] = bn0 + 1 < N ? mk[1] : 0.f;
+    }
+  }
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int rho = acc_row_b(r, lane);
@@ -235,9 +250,8 @@ __device__ __forceinline__ void bwd_tile(GemmTask t, int local, float* red) {
       const int N = t.N;
       float w0 = v0, w1 = v1;
       if (t.epi == EPI_MASK) {
-        const float* mk = t.aux + (long)m * t.ld_aux + bn0;
-        w0 = bn0 < N && mk[0] > 0.f ? v0 : 0.f;
-        w1 = bn0 + 1 < N && mk[1] > 0.f ? v1 : 0.f;
+        w0 = mk0[r] > 0.f ? v0 : 0.f;
+        w1 = mk1[r] > 0.f ? v1 : 0.f;
       }
       if (bn0 + 1 < N) *reinterpret_cast<f2u*>(t.C + o) = f2u{w0, w1};
       else if (bn0 < N) t.C[o] = w0;

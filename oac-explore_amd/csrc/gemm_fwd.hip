@@ -1,187 +1,214 @@
 // Large-batch forward products (gemm_cfg 6): Y = X W^T (+ b, ReLU; the
-// critic's rank-Da action columns as a continuation of the same accumulators)
-// at B >= 1024, both operands k-contiguous.
+// critic's rank-Da action columns as a continuation of the same
+// accumulators; the width-1 head partials) at B >= 1024, both operands
+// k-contiguous.
 //
 // The register-direct forward kernel (gemm_big.hip, cfg 2) spends one 16-byte
 // global load per lane for every 4 MFMAs of each 32x32 block it owns; on the
 // B=4096 step its launches keep the TA (vector address) unit ~70 % busy at
-// 43 % of the MFMA peak (tools/pmc_bwd.sh), so the load path, not the MFMA
-// pipe, bounds them.  Here a 256-thread workgroup stages TM x 32 of X and
-// TN x 32 of W per K stage into LDS with 16-byte loads (once per workgroup,
-// not once per wave), keeping the k-contiguous layout ([row][k], rows padded to
-// 36 floats: ds_write_b128 / ds_read_b128 without bank conflicts), and each
-// wave reads its fragments with one ds_read_b128 per 32x32 block and 4 k, the
-// same lane layout the register-direct kernels use (k = 8g + 4 half + c).
-// Double-buffered: the next stage's global loads are in flight while the
-// current stage's 64 MFMAs per wave issue; one barrier per stage.
+// 43 % of the MFMA peak (tools/pmc_bwd.sh): the load path, not the MFMA pipe,
+// bounds them.  Here a 256-thread workgroup (2 x 2 waves, each a (BM/2) x
+// (BN/2) block of v_mfma_f32_32x32x2_f32 accumulators) stages BM x 32 of X
+// and BN x 32 of W per K stage into LDS with LDS-DMA loads
+// (global_load_lds_dwordx4: no VGPR round trip, one 1-KB wave instruction per
+// 8 rows), in a ring of three stages: two stages are in flight while the
+// third is read, the waits are counted (vmcnt = one stage's loads), and one
+// raw barrier per stage orders both the DMA's landing and the ring's reuse.
+// The LDS image is lane-linear, so the bank swizzle (16-byte chunk c of row r
+// at slot c ^ (r & 7)) is applied to the per-lane SOURCE address and undone
+// on the ds_read_b128 fragment reads.
+//
+// The MFMA sequence per accumulator is the register-direct kernel's (8-deep
+// k-groups from k = 8 floor(k_lo / 8), c = 0..3 per group, lanes 32-63 on
+// the group's upper half), so both kernels produce bitwise equal outputs.
 #include <cstdlib>
 
 #include "oac_common.h"
 #include "kernels.h"
+#include "gemm_epilogue.h"
 #include "adam_common.h"
 
 namespace oac {
 
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+#ifdef OAC_FWD_CLOCK   // micro-benchmark build (tools/micro/fwd_micro): per-stage clocks of wave 0
+#define gemm_fwd_kernel gemm_fwd_kernel_clk   // distinct from the library's kernel of the same name
+__device__ long long g_fwd_clock[4096 * 32];
+#define FWD_CLK(slot) do { if (threadIdx.x == 0 && blockIdx.x < 4096 && (slot) < 32) \
+    g_fwd_clock[blockIdx.x * 32 + (slot)] = (long long)__builtin_readcyclecounter(); } while (0)
+#else
+#define FWD_CLK(slot) do {} while (0)
+#endif
 
-constexpr int kFwdKD = 32;          // k per stage
-constexpr int kFwdRow = kFwdKD + 4; // LDS row stride (floats)
+constexpr int kFK = 32;     // k per stage: one 128-byte row piece per operand row
+constexpr int kFBuf = 3;    // stages in the LDS ring
 
-template <int TM, int TN>
-struct FwdGeom {
-  static constexpr int WM = TM / 64, WN = TN / 64;         // 32x32 blocks per wave (2 x 2 waves)
-  static constexpr int PA = TM * kFwdKD / (4 * 256);       // float4 per thread per stage, A
-  static constexpr int PB = TN * kFwdKD / (4 * 256);
-  static constexpr int floats = 2 * (TM + TN) * kFwdRow;
+template <int BM, int BN>
+struct FwdG {
+  static constexpr int WM = BM / 64, WN = BN / 64;   // 32x32 blocks per wave (2 x 2 waves)
+  static constexpr int PA = BM / 32, PB = BN / 32;   // LDS-DMA instructions per wave and stage
+  static constexpr int LPW = PA + PB;
+  static constexpr int STAGE = (BM + BN) * kFK;      // floats
 };
 
-__device__ __forceinline__ int fwd_acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-// acc += A[m0 + .., k_lo..k_hi) . B[n0 + .., k_lo..k_hi)^T over this wave's blocks
-template <int TM, int TN>
-__device__ __forceinline__ void fwd_loop(const float* A, long lda, int M, const float* B, long ldb,
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS-DMA of 16 bytes per lane into dst + 16 lane (dst wave-uniform).  Inline
+// asm, so the compiler neither tracks it nor inserts its conservative
+// vmcnt(0) before every later ds_read of the same LDS array (the builtin
+// does: it cannot tell the ring's stages apart); the waits are counted here.
+__device__ __forceinline__ void glds16(const float* src, float* dst) {
+  const unsigned d = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(__attribute__((address_space(3))) void*)dst);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(d) : "memory");
+}
+
+// one stage's fragments and MFMAs; mask (wave-uniform): zero k outside [k_lo, k_hi)
+template <int WM, int WN>
+__device__ __forceinline__ void fwd_stage(const float* as, const float* bs, const int (&aoff)[WM],
+                                          const int (&boff)[WN], int xh, int hl, int kst, int half,
+                                          int k_lo, int k_hi, bool mask, floatx16 (&acc)[WM][WN]) {
+#pragma unroll
+  for (int g = 0; g < kFK / 8; ++g) {
+    const int slot = 4 * (((2 * g) ^ xh) + hl);   // chunk 2g + half, swizzled by the row
+    float4 af[WM], bf[WN];
+#pragma unroll
+    for (int i = 0; i < WM; ++i) af[i] = *reinterpret_cast<const float4*>(as + aoff[i] + slot);
+#pragma unroll
+    for (int j = 0; j < WN; ++j) bf[j] = *reinterpret_cast<const float4*>(bs + boff[j] + slot);
+    if (mask) {
+      const int k = kst + 8 * g + 4 * half;
+      const bool o0 = k >= k_lo && k < k_hi, o1 = k + 1 >= k_lo && k + 1 < k_hi;
+      const bool o2 = k + 2 >= k_lo && k + 2 < k_hi, o3 = k + 3 >= k_lo && k + 3 < k_hi;
+#pragma unroll
+      for (int i = 0; i < WM; ++i) {
+        af[i].x = o0 ? af[i].x : 0.f; af[i].y = o1 ? af[i].y : 0.f;
+        af[i].z = o2 ? af[i].z : 0.f; af[i].w = o3 ? af[i].w : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        bf[j].x = o0 ? bf[j].x : 0.f; bf[j].y = o1 ? bf[j].y : 0.f;
+        bf[j].z = o2 ? bf[j].z : 0.f; bf[j].w = o3 ? bf[j].w : 0.f;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+          const float a = c == 0 ? af[i].x : c == 1 ? af[i].y : c == 2 ? af[i].z : af[i].w;
+          const float b = c == 0 ? bf[j].x : c == 1 ? bf[j].y : c == 2 ? bf[j].z : bf[j].w;
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
+        }
+  }
+}
+
+// acc += A[m0 .. m0+BM, k_lo..k_hi) . B[n0 .. n0+BN, k_lo..k_hi)^T over this wave's blocks.
+// Rows past M / N are clamped to the last row (their outputs are not stored);
+// the k range runs in 32-deep stages from 8 floor(k_lo / 8).  A chunk wholly
+// past k_hi is fetched from the stage's first chunk instead (always in the
+// row); the chunk that straddles k_hi reads up to 3 floats past it (every
+// operand buffer is followed by >= 8 readable floats, gemm_operand.h).
+template <int BM, int BN>
+__device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const float* B, long ldb,
                                          int N, int k_lo, int k_hi, int m0, int n0, float* lds,
-                                         floatx16 (&acc)[TM / 64][TN / 64]) {
-  using G = FwdGeom<TM, TN>;
+                                         floatx16 (&acc)[BM / 64][BN / 64]) {
+  using G = FwdG<BM, BN>;
   constexpr int WM = G::WM, WN = G::WN, PA = G::PA, PB = G::PB;
-  const int nst = (k_hi - k_lo + kFwdKD - 1) / kFwdKD;
+  const int kb0 = k_lo & ~7;
+  const int nst = (k_hi - kb0 + kFK - 1) / kFK;
   if (nst <= 0) return;
-  float* As[2] = {lds, lds + TM * kFwdRow};
-  float* Bs[2] = {lds + 2 * TM * kFwdRow, lds + 2 * TM * kFwdRow + TN * kFwdRow};
-  const int t = threadIdx.x, lane = t & 63, l32 = lane & 31, half = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  // staging map: float4 e = t + 256 q -> row e / 8, k 4 (e % 8)
-  const float* arow[PA];
-  const float* brow[PB];
-  bool aok[PA], bok[PB];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // LDS-DMA sources: piece p (8 rows) of an operand is wave p / P's
+  // instruction p % P; lane j fills row 8p + j / 8, slot j % 8 = chunk
+  // (j % 8) ^ (row & 7)
+  const float* sa[PA];
+  const float* sb[PB];
+  int ca[PA], cb[PB];
 #pragma unroll
   for (int q = 0; q < PA; ++q) {
-    const int r = (t + 256 * q) >> 3;
-    aok[q] = m0 + r < M;
-    arow[q] = A + (long)(aok[q] ? m0 + r : 0) * lda;
+    const int r = 8 * (wave * PA + q) + (lane >> 3);
+    ca[q] = 4 * ((lane & 7) ^ (r & 7));
+    sa[q] = A + (long)min(m0 + r, M - 1) * lda;
   }
 #pragma unroll
   for (int q = 0; q < PB; ++q) {
-    const int r = (t + 256 * q) >> 3;
-    bok[q] = n0 + r < N;
-    brow[q] = B + (long)(bok[q] ? n0 + r : 0) * ldb;
+    const int r = 8 * (wave * PB + q) + (lane >> 3);
+    cb[q] = 4 * ((lane & 7) ^ (r & 7));
+    sb[q] = B + (long)min(n0 + r, N - 1) * ldb;
   }
-  const int kq = 4 * (t & 7);
-  f4u ra[PA], rb[PB];
-  auto gload = [&](int k0) {
-    const int k = k0 + kq;
+  auto issue = [&](int st) {
+    const int kst = kb0 + st * kFK;
+    float* base = lds + (st % kFBuf) * G::STAGE;
 #pragma unroll
     for (int q = 0; q < PA; ++q) {
-      f4u v = *reinterpret_cast<const f4u*>(arow[q] + k);
-      if (!aok[q] || k + 4 > k_hi) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = (aok[q] && k + c < k_hi) ? v[c] : 0.f;
-      }
-      ra[q] = v;
+      const int k = kst + ca[q];
+      glds16(sa[q] + (k < k_hi ? k : kst), base + (wave * PA + q) * 256);
     }
 #pragma unroll
     for (int q = 0; q < PB; ++q) {
-      f4u v = *reinterpret_cast<const f4u*>(brow[q] + k);
-      if (!bok[q] || k + 4 > k_hi) {
-#pragma unroll
-        for (int c = 0; c < 4; ++c) v[c] = (bok[q] && k + c < k_hi) ? v[c] : 0.f;
-      }
-      rb[q] = v;
+      const int k = kst + cb[q];
+      glds16(sb[q] + (k < k_hi ? k : kst), base + BM * kFK + (wave * PB + q) * 256);
     }
   };
-  auto sstore = [&](int buf) {
+  // fragment reads: row r = (wave block) + 32 i + l32, chunk (2g + half) ^ (r & 7)
+  const int l32 = lane & 31, half = lane >> 5;
+  const int xh = l32 & 6, hl = half ^ (l32 & 1);
+  int aoff[WM], boff[WN];
 #pragma unroll
-    for (int q = 0; q < PA; ++q) {
-      const int r = (t + 256 * q) >> 3;
-      *reinterpret_cast<float4*>(As[buf] + r * kFwdRow + kq) = make_float4(ra[q][0], ra[q][1], ra[q][2], ra[q][3]);
-    }
+  for (int i = 0; i < WM; ++i) aoff[i] = ((wave >> 1) * (BM / 2) + 32 * i + l32) * kFK;
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      const int r = (t + 256 * q) >> 3;
-      *reinterpret_cast<float4*>(Bs[buf] + r * kFwdRow + kq) = make_float4(rb[q][0], rb[q][1], rb[q][2], rb[q][3]);
-    }
-  };
-  // The loads read up to 3 floats past k_hi inside a row (masked): every
-  // operand buffer is followed by >= 8 readable floats (gemm_operand.h).
-  gload(k_lo);
-  sstore(0);
-  __syncthreads();
-  const int ar0 = (TM / 2) * wm + l32, br0 = (TN / 2) * wn + l32;
+  for (int j = 0; j < WN; ++j) boff[j] = ((wave & 1) * (BN / 2) + 32 * j + l32) * kFK;
+
+  raw_barrier();   // the ring's previous pass (a continuation) is fully read
+  FWD_CLK(1);
+  issue(0);
+  if (nst > 1) issue(1);
 #pragma unroll 1
   for (int st = 0; st < nst; ++st) {
-    const int cur = st & 1;
-    const bool more = st + 1 < nst;
-    if (more) gload(k_lo + (st + 1) * kFwdKD);
-    const float* ab = As[cur];
-    const float* bb = Bs[cur];
-#pragma unroll
-    for (int g = 0; g < kFwdKD / 8; ++g) {
-      const int kk = 8 * g + 4 * half;
-      float4 af[WM], bf[WN];
-#pragma unroll
-      for (int i = 0; i < WM; ++i) af[i] = *reinterpret_cast<const float4*>(ab + (ar0 + 32 * i) * kFwdRow + kk);
-#pragma unroll
-      for (int j = 0; j < WN; ++j) bf[j] = *reinterpret_cast<const float4*>(bb + (br0 + 32 * j) * kFwdRow + kk);
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int i = 0; i < WM; ++i)
-#pragma unroll
-          for (int j = 0; j < WN; ++j) {
-            const float a = c == 0 ? af[i].x : c == 1 ? af[i].y : c == 2 ? af[i].z : af[i].w;
-            const float b = c == 0 ? bf[j].x : c == 1 ? bf[j].y : c == 2 ? bf[j].z : bf[j].w;
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i][j], 0, 0, 0);
-          }
-    }
-    if (more) sstore(cur ^ 1);
-    __syncthreads();
+    if (st + 1 < nst) wait_vm<G::LPW>();
+    else wait_vm<0>();
+    raw_barrier();   // stage st landed for every wave; stage st - 1 is read by all
+    FWD_CLK(2 + st);
+    if (st + 2 < nst) issue(st + 2);
+    const int kst = kb0 + st * kFK;
+    const float* as = lds + (st % kFBuf) * G::STAGE;
+    const float* bs = as + BM * kFK;
+    fwd_stage<WM, WN>(as, bs, aoff, boff, xh, hl, kst, half, k_lo, k_hi,
+                      kst < k_lo || kst + kFK > k_hi, acc);
   }
 }
 
-template <int TM, int TN>
-__device__ __forceinline__ void fwd_epilogue(const GemmTask& t, int m0, int n0,
-                                             const floatx16 (&acc)[TM / 64][TN / 64], bool second) {
-  constexpr int WM = TM / 64, WN = TN / 64;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int mw = m0 + (TM / 2) * (wave >> 1), nw = n0 + (TN / 2) * (wave & 1);
-#pragma unroll
-  for (int j = 0; j < WN; ++j) {
-    const int n = nw + 32 * j + (lane & 31);
-    if (n >= t.N) continue;
-    const float bias = t.bias ? t.bias[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < WM; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = mw + 32 * i + fwd_acc_row(r, lane);
-        if (m >= t.M) continue;
-        const float v = acc[i][j][r] + bias;
-        switch (t.epi) {
-          case EPI_STORE: t.C[(long)m * t.ldc + n] = acc[i][j][r]; break;
-          case EPI_BIAS: t.C[(long)m * t.ldc + n] = v; break;
-          case EPI_BIAS_RELU: t.C[(long)m * t.ldc + n] = fmaxf(v, 0.f); break;
-          case EPI_BIAS_RANK_RELU:
-            if (!second) t.C[(long)m * t.ldc + n] = v;
-            else t.C2[(long)m * t.ldc2 + n] = fmaxf(v, 0.f);
-            break;
-          default: break;
-        }
-      }
-  }
+// blocks dispatch round-robin over the 8 XCDs; a tile's neighbours along n
+// (same X rows) are given consecutive ids on one XCD so its L2 serves the
+// second read of the rows (bijective for any grid size)
+__device__ __forceinline__ int xcd_tile(int bid, int n) {
+  const int q = n >> 3, r = n & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 
-template <int TM, int TN>
+template <int BM, int BN>
 __global__ void __launch_bounds__(256)
 gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                 const GemmBatch batch) {
-  constexpr int WM = TM / 64, WN = TN / 64;
-  __shared__ __attribute__((aligned(16))) float lds[FwdGeom<TM, TN>::floats];
-  const int bid = blockIdx.x;
-  if (batch.publish && bid == 0 && threadIdx.x == 0)
+  using G = FwdG<BM, BN>;
+  constexpr int WM = G::WM, WN = G::WN;
+  __shared__ __attribute__((aligned(16))) float lds[kFBuf * G::STAGE];
+  if (batch.publish && blockIdx.x == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
-  if (bid >= total_tiles) return;
+  const int bid = xcd_tile(blockIdx.x, gridDim.x);
+  if (bid >= total_tiles) return;   // grid == total_tiles: never taken
   int ti = 0;
   ti = bid >= tb1 ? 1 : ti; ti = bid >= tb2 ? 2 : ti; ti = bid >= tb3 ? 3 : ti;
   ti = bid >= tb4 ? 4 : ti; ti = bid >= tb5 ? 5 : ti; ti = bid >= tb6 ? 6 : ti;
@@ -189,8 +216,10 @@ gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
   ti = __builtin_amdgcn_readfirstlane(ti);
   const GemmTask& t = batch.t[ti];
   const int local = bid - t.tile_begin;
-  const int m0 = (local / t.tiles_n) * TM;
-  const int n0 = (local % t.tiles_n) * TN;
+  const int m0 = (local / t.tiles_n) * BM;
+  const int n0 = (local % t.tiles_n) * BN;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int mw = m0 + (wave >> 1) * (BM / 2), nw = n0 + (wave & 1) * (BN / 2);
   floatx16 acc[WM][WN];
 #pragma unroll
   for (int i = 0; i < WM; ++i)
@@ -198,50 +227,71 @@ gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
     for (int j = 0; j < WN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  fwd_loop<TM, TN>(t.A, t.lda, t.M, t.B, t.ldb, t.N, 0, t.K, m0, n0, lds, acc);
-  fwd_epilogue<TM, TN>(t, m0, n0, acc, false);
-  if (t.epi == EPI_BIAS_RANK_RELU) {   // + U V^T on the same accumulators
+  FWD_CLK(0);
+  fwd_pipe<BM, BN>(t.A, t.lda, t.M, t.B, t.ldb, t.N, 0, t.K, m0, n0, lds, acc);
+  FWD_CLK(29);
+  rd_epilogue<WM, WN, kEpiFwd>(t, mw, nw, acc, false);
+  FWD_CLK(30);
+  if (t.epi == EPI_BIAS_RANK_RELU) {   // + U V^T on the same accumulators (gemm_big.hip)
     if (t.U == t.A + t.K && t.ldu == t.lda && t.V == t.B + t.K && t.ldv == t.ldb)
-      fwd_loop<TM, TN>(t.A, t.lda, t.M, t.B, t.ldb, t.N, t.K, t.K + t.R, m0, n0, lds, acc);
+      fwd_pipe<BM, BN>(t.A, t.lda, t.M, t.B, t.ldb, t.N, t.K, t.K + t.R, m0, n0, lds, acc);
     else
-      fwd_loop<TM, TN>(t.U, t.ldu, t.M, t.V, t.ldv, t.N, 0, t.R, m0, n0, lds, acc);
-    fwd_epilogue<TM, TN>(t, m0, n0, acc, true);
+      fwd_pipe<BM, BN>(t.U, t.ldu, t.M, t.V, t.ldv, t.N, 0, t.R, m0, n0, lds, acc);
+    epi_dispatch<WM, WN, EPI_BIAS_RANK_RELU>(t, mw, nw, acc, true);
   }
+  FWD_CLK(31);
 }
 
 // forward batches this kernel takes: both operands k-contiguous, plain A, no
-// split, no second product, bias / ReLU / rank epilogues
+// split, no second product, the forward epilogues of the register-direct kernel
 bool gemm_fwd_supports(const GemmBatch& b) {
   if (b.fuse_adam || b.ntasks < 1) return false;
   for (int i = 0; i < b.ntasks; ++i) {
     const GemmTask& t = b.t[i];
-    if (!t.a_kc || !t.b_kc || t.a_mode != A_PLAIN || t.ksplit > 1 || t.K2 > 0) return false;
+    if (!t.a_kc || !t.b_kc || t.a_mode != A_PLAIN || t.ksplit > 1 || t.K2 > 0 || t.a_rows) return false;
     if (t.epi != EPI_STORE && t.epi != EPI_BIAS && t.epi != EPI_BIAS_RELU &&
-        t.epi != EPI_BIAS_RANK_RELU)
+        t.epi != EPI_BIAS_RANK_RELU && t.epi != EPI_BIAS_RELU_DOT)
       return false;
     if (t.epi == EPI_BIAS_RANK_RELU && !t.C2) return false;
+    if (t.epi == EPI_BIAS_RELU_DOT && (!t.C2 || !t.aux)) return false;
   }
   return true;
 }
 
-// OAC_FWD2_TILE: 128 (128 x 128 tiles, default) or 64 (128 x 64)
-int gemm_fwd_tile_n() {
-  static const int v = [] { const char* e = getenv("OAC_FWD2_TILE"); return (e && atoi(e) == 64) ? 64 : 128; }();
-  return v;
+// Tiles by gemm_cfg: 6 = 128 x 128, 7 = 128 x 64, 8 = 64 x 64 (plan_common.h
+// launch_cfg picks one per launch).  OAC_FWD2_TILE = "BM,BN" forces one tile
+// for every forward launch (tile sweeps: tools/gpu_fwd3.sh).
+static int fwd_env(int which) {
+  static const char* e = getenv("OAC_FWD2_TILE");
+  if (!e) return 0;
+  if (which == 0) return atoi(e);
+  const char* c = e;
+  while (*c && *c != ',') ++c;
+  return *c ? atoi(c + 1) : 0;
+}
+int gemm_fwd_tile_m(int cfg) {
+  static const int v = fwd_env(0);
+  return v ? v : cfg == 8 ? 64 : 128;
+}
+int gemm_fwd_tile_n(int cfg) {
+  static const int v = fwd_env(1);
+  return v ? v : cfg == 6 ? 128 : 64;
 }
 
-hipError_t gemm_fwd_launch(const GemmBatch& b, hipStream_t s) {
+hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   if (b.total_tiles <= 0) return hipSuccess;
   if (!gemm_fwd_supports(b)) return hipErrorInvalidValue;
   int tb[8];
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
-  if (gemm_fwd_tile_n() == 64)
-    OAC_LAUNCH((gemm_fwd_kernel<128, 64>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles,
-               tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b);
-  else
-    OAC_LAUNCH((gemm_fwd_kernel<128, 128>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles,
-               tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b);
-  return hipGetLastError();
+  const int bm = gemm_fwd_tile_m(cfg), bn = gemm_fwd_tile_n(cfg);
+#define OAC_FWD(BM_, BN_) \
+  if (bm == BM_ && bn == BN_) { \
+    OAC_LAUNCH((gemm_fwd_kernel<BM_, BN_>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, \
+               tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
+    return hipGetLastError(); }
+  OAC_FWD(128, 128) OAC_FWD(128, 64) OAC_FWD(64, 128) OAC_FWD(64, 64)
+#undef OAC_FWD
+  return hipErrorInvalidValue;
 }
 
 }  // namespace oac

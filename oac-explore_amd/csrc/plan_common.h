@@ -198,15 +198,23 @@ static inline int small_fwd_tiles() {
 bool gemm_bwd_supports(const GemmBatch& b);
 bool gemm_fwd_supports(const GemmBatch& b);
 
-// Forward batches at large batch go to gemm_fwd.hip (cfg 6: LDS-staged
-// 128-row tiles, one global load per workgroup instead of per wave) only when
-// OAC_FWD2=1: parity-green, but at B=4096 layer 0 took 99 / 85 us with
-// 128x128 / 128x64 tiles against 71 us on the register-direct kernel, layer 1
-// 41 against 34 us (252 / 228 VGPRs: one or two waves per SIMD, and a 32-deep
-// stage is too short to cover the next stage's global loads)
+// Forward batches at large batch go to gemm_fwd.hip (LDS-DMA pipelined
+// 128x128 / 128x64 / 64x64 tiles, cfg 6 / 7 / 8); OAC_FWD2=0 keeps them on the
+// register-direct kernel (cfg 2) for A/B runs.  Measured per launch at B=4096
+// (tools/micro/fwd_micro, bitwise equal to cfg 2): SAC layer 0 (6 tasks)
+// 77.5 -> 66.4 us on 128x64 (74.6 on 128x128: 384 tiles = 1.5 rounds), critic
+// layer 1 + head partials (4 tasks) 35.6 -> 27.7 us on 128x128, policy layer 1
+// (2 tasks) 21.9 -> 15.4 us on 128x64.
 static inline bool fwd2_on() {
-  static const bool v = [] { const char* e = getenv("OAC_FWD2"); return e && atoi(e) != 0; }();
+  static const bool v = [] { const char* e = getenv("OAC_FWD2"); return !e || atoi(e) != 0; }();
   return v;
+}
+// 128x128 tiles when they fill the chip in one round (one workgroup per CU:
+// 96 KB of LDS), 128x64 otherwise
+static inline int fwd2_cfg(const GemmBatch& gb) {
+  int t128 = 0;
+  for (int i = 0; i < gb.ntasks; ++i) t128 += ((gb.t[i].M + 127) / 128) * ((gb.t[i].N + 127) / 128);
+  return (t128 >= 192 && t128 <= 256) ? 6 : 7;
 }
 
 // Backward batches at large batch go to gemm_bwd.hip (cfg 5: float2 fetch of
@@ -241,7 +249,7 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     bool all_fwd = true;
     for (int i = 0; i < gb.ntasks; ++i)
       all_fwd = all_fwd && gb.t[i].a_kc && gb.t[i].b_kc && gb.t[i].N >= 64;
-    if (all_fwd && gemm_fwd_supports(gb)) return 6;
+    if (all_fwd && gemm_fwd_supports(gb)) return fwd2_cfg(gb);
   }
   if (bwd2_on() && big_bwd()) {
     // a dX with a short K (the head's 2 Da, the K-output critic's K) leaves
