@@ -378,12 +378,18 @@ hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s);
 int gemm_fwd_tile_m(int cfg);
 int gemm_fwd_tile_n(int cfg);
 
+hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s);
+int gemm_bwdp_tile_m(int cfg);
+int gemm_bwdp_tile_n(int cfg);
+
 int gemm_tile_m(int cfg) {
+  if (cfg >= 9) return gemm_bwdp_tile_m(cfg);
   if (cfg == 5) return 64;
   if (cfg >= 6) return gemm_fwd_tile_m(cfg);
   return cfg == 0 ? 32 : cfg == 4 ? gemm_lds_tile_m() : cfg >= 2 ? gemm_big_tile_m(cfg == 3) : lds_tile_m();
 }
 int gemm_tile_n(int cfg) {
+  if (cfg >= 9) return gemm_bwdp_tile_n(cfg);
   if (cfg == 5) return 64;
   if (cfg >= 6) return gemm_fwd_tile_n(cfg);
   return cfg == 0 ? 32 : cfg == 4 ? gemm_lds_tile_n() : cfg >= 2 ? gemm_big_tile_n(cfg == 3) : lds_tile_n();
@@ -400,7 +406,9 @@ void gemm_batch_finalize(GemmBatch& b, int cfg) {
   for (int i = 0; i < b.ntasks; ++i) {
     GemmTask& t = b.t[i];
     const int tm = (t.M + bm - 1) / bm;
-    const int tn = (t.N + bn - 1) / bn;
+    // gemm_bwdp.hip (cfg 9-11): a dW's ones column is not a column tile
+    const int nx = (cfg >= 9 && t.epi == EPI_GRAD && t.b_ones) ? t.N - 1 : t.N;
+    const int tn = (nx + bn - 1) / bn;
     t.tile_begin = tiles;
     t.tiles_n = tn;
     if (t.ksplit < 1) t.ksplit = 1;
@@ -417,10 +425,11 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   for (int i = 0; i < b.ntasks; ++i) {             // dual products / head backward: small kernel
     if (b.t[i].K2 > 0 || b.t[i].epi == EPI_HEAD_BWD) return hipErrorInvalidValue;
     // the width-1 head dot: small kernel, the register-direct one (cfg 2 / 3) or gemm_fwd (6-8)
-    if (b.t[i].epi == EPI_BIAS_RELU_DOT && cfg != 2 && cfg != 3 && cfg < 6) return hipErrorInvalidValue;
+    if (b.t[i].epi == EPI_BIAS_RELU_DOT && cfg != 2 && cfg != 3 && (cfg < 6 || cfg > 8)) return hipErrorInvalidValue;
   }
   if (cfg == 4) return gemm_lds_launch(b, s);
   if (cfg == 5) return gemm_bwd_launch(b, s);
+  if (cfg >= 9) return gemm_bwdp_launch(b, cfg, s);
   if (cfg >= 6) return gemm_fwd_launch(b, cfg, s);
   if (cfg >= 2) return gemm_big_launch(b, s, cfg == 3);
   switch (lds_variant()) {

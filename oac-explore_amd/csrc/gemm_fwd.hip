@@ -26,21 +26,14 @@
 #include "oac_common.h"
 #include "kernels.h"
 #include "gemm_epilogue.h"
+#include "gemm_pipe.h"
 #include "adam_common.h"
 
 namespace oac {
 
-#ifdef OAC_FWD_CLOCK   // micro-benchmark build (tools/micro/fwd_micro): per-stage clocks of wave 0
+#ifdef OAC_PIPE_CLOCK
 #define gemm_fwd_kernel gemm_fwd_kernel_clk   // distinct from the library's kernel of the same name
-__device__ long long g_fwd_clock[4096 * 32];
-#define FWD_CLK(slot) do { if (threadIdx.x == 0 && blockIdx.x < 4096 && (slot) < 32) \
-    g_fwd_clock[blockIdx.x * 32 + (slot)] = (long long)__builtin_readcyclecounter(); } while (0)
-#else
-#define FWD_CLK(slot) do {} while (0)
 #endif
-
-constexpr int kFK = 32;     // k per stage: one 128-byte row piece per operand row
-constexpr int kFBuf = 3;    // stages in the LDS ring
 
 template <int BM, int BN>
 struct FwdG {
@@ -49,28 +42,6 @@ struct FwdG {
   static constexpr int LPW = PA + PB;
   static constexpr int STAGE = (BM + BN) * kFK;      // floats
 };
-
-template <int N>
-__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-// LDS-DMA of 16 bytes per lane into dst + 16 lane (dst wave-uniform).  Inline
-// asm, so the compiler neither tracks it nor inserts its conservative
-// vmcnt(0) before every later ds_read of the same LDS array (the builtin
-// does: it cannot tell the ring's stages apart); the waits are counted here.
-__device__ __forceinline__ void glds16(const float* src, float* dst) {
-  const unsigned d = __builtin_amdgcn_readfirstlane(
-      (unsigned)(size_t)(__attribute__((address_space(3))) void*)dst);
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(d) : "memory");
-}
 
 // one stage's fragments and MFMAs; mask (wave-uniform): zero k outside [k_lo, k_hi)
 template <int WM, int WN>
@@ -172,7 +143,7 @@ __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const 
   for (int j = 0; j < WN; ++j) boff[j] = ((wave & 1) * (BN / 2) + 32 * j + l32) * kFK;
 
   raw_barrier();   // the ring's previous pass (a continuation) is fully read
-  FWD_CLK(1);
+  PIPE_CLK(1);
   issue(0);
   if (nst > 1) issue(1);
 #pragma unroll 1
@@ -180,7 +151,7 @@ __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const 
     if (st + 1 < nst) wait_vm<G::LPW>();
     else wait_vm<0>();
     raw_barrier();   // stage st landed for every wave; stage st - 1 is read by all
-    FWD_CLK(2 + st);
+    PIPE_CLK(2 + st);
     if (st + 2 < nst) issue(st + 2);
     const int kst = kb0 + st * kFK;
     const float* as = lds + (st % kFBuf) * G::STAGE;
@@ -188,14 +159,6 @@ __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const 
     fwd_stage<WM, WN>(as, bs, aoff, boff, xh, hl, kst, half, k_lo, k_hi,
                       kst < k_lo || kst + kFK > k_hi, acc);
   }
-}
-
-// blocks dispatch round-robin over the 8 XCDs; a tile's neighbours along n
-// (same X rows) are given consecutive ids on one XCD so its L2 serves the
-// second read of the rows (bijective for any grid size)
-__device__ __forceinline__ int xcd_tile(int bid, int n) {
-  const int q = n >> 3, r = n & 7, x = bid & 7;
-  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 
 template <int BM, int BN>
@@ -227,11 +190,11 @@ gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
     for (int j = 0; j < WN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  FWD_CLK(0);
+  PIPE_CLK(0);
   fwd_pipe<BM, BN>(t.A, t.lda, t.M, t.B, t.ldb, t.N, 0, t.K, m0, n0, lds, acc);
-  FWD_CLK(29);
+  PIPE_CLK(29);
   rd_epilogue<WM, WN, kEpiFwd>(t, mw, nw, acc, false);
-  FWD_CLK(30);
+  PIPE_CLK(30);
   if (t.epi == EPI_BIAS_RANK_RELU) {   // + U V^T on the same accumulators (gemm_big.hip)
     if (t.U == t.A + t.K && t.ldu == t.lda && t.V == t.B + t.K && t.ldv == t.ldb)
       fwd_pipe<BM, BN>(t.A, t.lda, t.M, t.B, t.ldb, t.N, t.K, t.K + t.R, m0, n0, lds, acc);
@@ -239,7 +202,7 @@ gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
       fwd_pipe<BM, BN>(t.U, t.ldu, t.M, t.V, t.ldv, t.N, 0, t.R, m0, n0, lds, acc);
     epi_dispatch<WM, WN, EPI_BIAS_RANK_RELU>(t, mw, nw, acc, true);
   }
-  FWD_CLK(31);
+  PIPE_CLK(31);
 }
 
 // forward batches this kernel takes: both operands k-contiguous, plain A, no

@@ -1,0 +1,51 @@
+// Building blocks of the LDS-DMA pipelined large-batch GEMMs (gemm_fwd.hip,
+// gemm_bwdp.hip): 32-deep K stages staged global -> LDS with
+// global_load_lds_dwordx4 (no VGPR round trip) in a ring of three, counted
+// vmcnt waits and one raw barrier per stage.
+#pragma once
+#include "oac_common.h"
+
+namespace oac {
+
+#ifdef OAC_PIPE_CLOCK   // micro-benchmark builds (tools/micro): per-stage clocks of wave 0
+__device__ long long g_pipe_clock[4096 * 32];
+#define PIPE_CLK(slot) do { if (threadIdx.x == 0 && blockIdx.x < 4096 && (slot) < 32) \
+    g_pipe_clock[blockIdx.x * 32 + (slot)] = (long long)__builtin_readcyclecounter(); } while (0)
+#else
+#define PIPE_CLK(slot) do {} while (0)
+#endif
+
+constexpr int kFK = 32;     // k per stage: one 128-byte row piece per operand row
+constexpr int kFBuf = 3;    // stages in the LDS ring
+
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// LDS-DMA of 16 bytes per lane into dst + 16 lane (dst wave-uniform).  Inline
+// asm, so the compiler neither tracks it nor inserts its conservative
+// vmcnt(0) before every later ds_read of the same LDS array (the builtin
+// does: it cannot tell the ring's stages apart); the waits are counted here.
+__device__ __forceinline__ void glds16(const float* src, float* dst) {
+  const unsigned d = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(__attribute__((address_space(3))) void*)dst);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+               "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(d) : "memory");
+}
+
+// blocks dispatch round-robin over the 8 XCDs; a tile's neighbours along n
+// (same X rows) are given consecutive ids on one XCD so its L2 serves the
+// second read of the rows (bijective for any grid size)
+__device__ __forceinline__ int xcd_tile(int bid, int n) {
+  const int q = n >> 3, r = n & 7, x = bid & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
+}
+
+}  // namespace oac

@@ -225,6 +225,23 @@ static inline bool bwd2_on() {
   return v;
 }
 
+// Backward batches at large batch go to gemm_bwdp.hip (LDS-DMA pipelined,
+// cfg 9 = 128x64 tiles, 10 = 64x64 when 128x64 leaves CUs idle);
+// OAC_BWDP=0 keeps them on gemm_bwd.hip / the register-direct kernel.
+bool gemm_bwdp_supports(const GemmBatch& b);
+static inline bool bwdp_on() {
+  static const bool v = [] { const char* e = getenv("OAC_BWDP"); return !e || atoi(e) != 0; }();
+  return v;
+}
+static inline int bwdp_cfg(const GemmBatch& gb) {
+  // 64x64 tiles (three workgroups per CU: 52 KB of LDS) beat 128x64 on every
+  // backward launch of the B=4096 SAC step (tools/micro/bwd_micro: critic
+  // layer 1 48.8 -> 38.6 us, layer 0 dW 37.9 -> 33.0, -min Q dX 20.7 -> 19.0)
+  static const int forced = [] { const char* e = getenv("OAC_BWDP_CFG"); return e ? atoi(e) : 0; }();
+  (void)gb;
+  return (forced >= 9 && forced <= 11) ? forced : 10;
+}
+
 static inline int launch_cfg(int cfg, const GemmBatch& gb) {
   if (cfg == 0) return 0;
   for (int i = 0; i < gb.ntasks; ++i)   // the fused head backward exists on the small kernel only
@@ -250,6 +267,11 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     for (int i = 0; i < gb.ntasks; ++i)
       all_fwd = all_fwd && gb.t[i].a_kc && gb.t[i].b_kc && gb.t[i].N >= 64;
     if (all_fwd && gemm_fwd_supports(gb)) return fwd2_cfg(gb);
+  }
+  if (bwdp_on()) {
+    bool all_bwd = true;
+    for (int i = 0; i < gb.ntasks; ++i) all_bwd = all_bwd && !gb.t[i].b_kc;
+    if (all_bwd && gemm_bwdp_supports(gb)) return bwdp_cfg(gb);
   }
   if (bwd2_on() && big_bwd()) {
     // a dX with a short K (the head's 2 Da, the K-output critic's K) leaves

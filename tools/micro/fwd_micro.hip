@@ -18,41 +18,21 @@ namespace oac {
 void gemm_batch_finalize(GemmBatch& b, int cfg);
 hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s);
 }
-#ifdef OAC_FWD_CLOCK
+#ifdef OAC_PIPE_CLOCK
 // this TU's own gemm_fwd.hip, built with the per-stage clocks of wave 0
 #include "../../oac-explore_amd/csrc/gemm_fwd.hip"
+#include "pipe_clock.h"
 #endif
 using namespace oac;
 
-#ifdef OAC_FWD_CLOCK
+#ifdef OAC_PIPE_CLOCK
 // one clocked launch of the cfg-6 kernel: per-phase cycles averaged over workgroups
 static void clocks(const GemmBatch& b0, hipStream_t s) {
   GemmBatch b = b0;
   gemm_batch_finalize(b, 6);
   CK(gemm_fwd_launch(b, 6, s));
   CK(hipStreamSynchronize(s));
-  const int n = b.total_tiles < 4096 ? b.total_tiles : 4096;
-  std::vector<long long> c((size_t)n * 32);
-  CK(hipMemcpyFromSymbol(c.data(), HIP_SYMBOL(g_fwd_clock), c.size() * 8));
-  long long t0 = c[0], tend = 0;
-  for (int i = 0; i < n; ++i) { t0 = std::min(t0, c[i * 32]); tend = std::max(tend, c[i * 32 + 31]); }
-  double st[32] = {0};
-  int nst = 0;
-  while (nst < 27 && c[2 + nst] > c[1]) ++nst;
-  for (int i = 0; i < n; ++i) {
-    const long long* r = &c[(size_t)i * 32];
-    st[0] += r[1] - r[0];                 // task lookup -> pipe start
-    st[1] += r[2] - r[1];                 // prologue issue -> stage 0 ready
-    for (int k = 1; k < nst; ++k) st[1 + k] += r[2 + k] - r[1 + k];
-    st[28] += r[29] - r[1 + nst];         // last stage compute
-    st[29] += r[30] - r[29];              // epilogue
-    st[30] += r[31] - r[30];              // continuation + 2nd epilogue
-    st[31] += r[0] - t0;                  // start skew
-  }
-  printf("  clocks (cycles, avg over %d wgs, %d stages): start skew %.0f  lookup %.0f  prologue %.0f  stages",
-         n, nst, st[31] / n, st[0] / n, st[1] / n);
-  for (int k = 1; k < nst; ++k) printf(" %.0f", st[1 + k] / n);
-  printf("  last %.0f  epilogue %.0f  cont %.0f | span %lld\n", st[28] / n, st[29] / n, st[30] / n, tend - t0);
+  print_pipe_clocks(b.total_tiles);
 }
 #endif
 
@@ -171,7 +151,7 @@ int main(int argc, char** argv) {
     if (diff) printf("  first @%zu: %.9g vs %.9g", first, r2[first], r6[first]);
     printf("\n");
     bad += diff != 0;
-#ifdef OAC_FWD_CLOCK
+#ifdef OAC_PIPE_CLOCK
     clocks(*bs[k], s);
     snap(outs);
 #endif
