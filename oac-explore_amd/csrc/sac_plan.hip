@@ -569,6 +569,15 @@ static void plan_splits(SacPlan& p) {
   p.sp_ph = choose_split(c.batch, tiles(2 * Da, H + 1), p.cfg);
   p.sp_p1 = choose_split(c.batch, tiles(H, H + 1), p.cfg);
   p.sp_p0 = choose_split(c.batch, tiles(H, Do + 1), p.cfg);
+  if (p.cfg == 2 && bwdp_on()) {   // the large-batch dW products run on gemm_bwdp.hip
+    auto t64 = [](int M, int Nx) { return ((M + 63) / 64) * ((Nx + 63) / 64); };
+    p.sp_q1 = choose_split_pipe(c.batch, nq * (t64(H, H) + t64(c.q_out, H)));
+    p.sp_ql = p.sp_q1;
+    p.sp_q0 = choose_split_pipe(c.batch, nq * t64(H, Dq));
+    p.sp_ph = choose_split_pipe(c.batch, t64(2 * Da, H));
+    p.sp_p1 = choose_split_pipe(c.batch, t64(H, H));
+    p.sp_p0 = choose_split_pipe(c.batch, t64(H, Do));
+  }
   // OAC_SPLITS="q1,q0,ph,p1,p0": forced split counts (0 = keep), tuning runs
   if (const char* e = getenv("OAC_SPLITS")) {
     int v[5] = {0, 0, 0, 0, 0};
