@@ -90,7 +90,7 @@ __device__ __forceinline__ void fwd_stage(const float* as, const float* bs, cons
 // past k_hi is fetched from the stage's first chunk instead (always in the
 // row); the chunk that straddles k_hi reads up to 3 floats past it (every
 // operand buffer is followed by >= 8 readable floats, gemm_operand.h).
-template <int BM, int BN>
+template <int BM, int BN, int NB>
 __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const float* B, long ldb,
                                          int N, int k_lo, int k_hi, int m0, int n0, float* lds,
                                          floatx16 (&acc)[BM / 64][BN / 64]) {
@@ -121,7 +121,7 @@ __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const 
   }
   auto issue = [&](int st) {
     const int kst = kb0 + st * kFK;
-    float* base = lds + (st % kFBuf) * G::STAGE;
+    float* base = lds + (st % NB) * G::STAGE;
 #pragma unroll
     for (int q = 0; q < PA; ++q) {
       const int k = kst + ca[q];
@@ -144,30 +144,32 @@ __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const 
 
   raw_barrier();   // the ring's previous pass (a continuation) is fully read
   PIPE_CLK(1);
+  // NB = 3: two stages in flight while one is read; NB = 2 (a smaller LDS
+  // footprint, one more workgroup per CU): one
   issue(0);
-  if (nst > 1) issue(1);
+  if (NB == 3 && nst > 1) issue(1);
 #pragma unroll 1
   for (int st = 0; st < nst; ++st) {
-    if (st + 1 < nst) wait_vm<G::LPW>();
+    if (NB == 3 && st + 1 < nst) wait_vm<G::LPW>();
     else wait_vm<0>();
     raw_barrier();   // stage st landed for every wave; stage st - 1 is read by all
     PIPE_CLK(2 + st);
-    if (st + 2 < nst) issue(st + 2);
+    if (st + NB - 1 < nst) issue(st + NB - 1);
     const int kst = kb0 + st * kFK;
-    const float* as = lds + (st % kFBuf) * G::STAGE;
+    const float* as = lds + (st % NB) * G::STAGE;
     const float* bs = as + BM * kFK;
     fwd_stage<WM, WN>(as, bs, aoff, boff, xh, hl, kst, half, k_lo, k_hi,
                       kst < k_lo || kst + kFK > k_hi, acc);
   }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NB>
 __global__ void __launch_bounds__(256)
 gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                 const GemmBatch batch) {
   using G = FwdG<BM, BN>;
   constexpr int WM = G::WM, WN = G::WN;
-  __shared__ __attribute__((aligned(16))) float lds[kFBuf * G::STAGE];
+  __shared__ __attribute__((aligned(16))) float lds[NB * G::STAGE];
   if (batch.publish && blockIdx.x == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
   const int bid = xcd_tile(blockIdx.x, gridDim.x);
@@ -191,15 +193,15 @@ gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   PIPE_CLK(0);
-  fwd_pipe<BM, BN>(t.A, t.lda, t.M, t.B, t.ldb, t.N, 0, t.K, m0, n0, lds, acc);
+  fwd_pipe<BM, BN, NB>(t.A, t.lda, t.M, t.B, t.ldb, t.N, 0, t.K, m0, n0, lds, acc);
   PIPE_CLK(29);
   rd_epilogue<WM, WN, kEpiFwd>(t, mw, nw, acc, false);
   PIPE_CLK(30);
   if (t.epi == EPI_BIAS_RANK_RELU) {   // + U V^T on the same accumulators (gemm_big.hip)
     if (t.U == t.A + t.K && t.ldu == t.lda && t.V == t.B + t.K && t.ldv == t.ldb)
-      fwd_pipe<BM, BN>(t.A, t.lda, t.M, t.B, t.ldb, t.N, t.K, t.K + t.R, m0, n0, lds, acc);
+      fwd_pipe<BM, BN, NB>(t.A, t.lda, t.M, t.B, t.ldb, t.N, t.K, t.K + t.R, m0, n0, lds, acc);
     else
-      fwd_pipe<BM, BN>(t.U, t.ldu, t.M, t.V, t.ldv, t.N, 0, t.R, m0, n0, lds, acc);
+      fwd_pipe<BM, BN, NB>(t.U, t.ldu, t.M, t.V, t.ldv, t.N, 0, t.R, m0, n0, lds, acc);
     epi_dispatch<WM, WN, EPI_BIAS_RANK_RELU>(t, mw, nw, acc, true);
   }
   PIPE_CLK(31);
@@ -247,12 +249,18 @@ hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   int tb[8];
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
   const int bm = gemm_fwd_tile_m(cfg), bn = gemm_fwd_tile_n(cfg);
-#define OAC_FWD(BM_, BN_) \
-  if (bm == BM_ && bn == BN_) { \
-    OAC_LAUNCH((gemm_fwd_kernel<BM_, BN_>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, \
+  // LDS ring depth: 2 for 128x64 tiles (48 KB: three workgroups per CU;
+  // B=4096 SAC layer 0, 768 tiles, 65.6 -> 61.1 us), 3 otherwise (128x128 is
+  // register-bound to one workgroup per CU either way); OAC_FWD2_NB forces one
+  static const int nb_env = [] { const char* e = getenv("OAC_FWD2_NB"); return e ? atoi(e) : 0; }();
+  const int nb = (nb_env == 2 || nb_env == 3) ? nb_env : (bm == 128 && bn == 64) ? 2 : 3;
+#define OAC_FWD(BM_, BN_, NB_) \
+  if (bm == BM_ && bn == BN_ && nb == NB_) { \
+    OAC_LAUNCH((gemm_fwd_kernel<BM_, BN_, NB_>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, \
                tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
     return hipGetLastError(); }
-  OAC_FWD(128, 128) OAC_FWD(128, 64) OAC_FWD(64, 128) OAC_FWD(64, 64)
+  OAC_FWD(128, 128, 3) OAC_FWD(128, 64, 3) OAC_FWD(64, 128, 3) OAC_FWD(64, 64, 3)
+  OAC_FWD(128, 128, 2) OAC_FWD(128, 64, 2) OAC_FWD(64, 64, 2)
 #undef OAC_FWD
   return hipErrorInvalidValue;
 }
