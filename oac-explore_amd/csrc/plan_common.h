@@ -76,7 +76,11 @@ static inline Split choose_split(int K, int tiles, int cfg) {
 // rest 16 splits -- 3,225 steps/s against 3,108 with the register-direct
 // kernel's splits (19 / 16 / 32).
 static inline Split choose_split_pipe(int K, int tiles) {
-  int S = std::max(1, std::min(K / 256, 768 / std::max(1, tiles)));
+  tiles = std::max(1, tiles);
+  int S = std::max(1, std::min(K / 256, 768 / tiles));
+  // a small dW (configs[4]'s 256 x 119 critic layer 0: 8 tiles) would leave
+  // CUs idle: chunks down to 128 rows until one workgroup per CU
+  if (S * tiles < 256) S = std::max(S, std::min(K / 128, (256 + tiles - 1) / tiles));
   int kchunk = (K + S - 1) / S;
   kchunk = ((kchunk + 31) / 32) * 32;
   S = (K + kchunk - 1) / kchunk;
@@ -222,12 +226,14 @@ static inline bool fwd2_on() {
   static const bool v = [] { const char* e = getenv("OAC_FWD2"); return !e || atoi(e) != 0; }();
   return v;
 }
-// 128x128 tiles when they fill the chip in one round (one workgroup per CU:
-// 96 KB of LDS), 128x64 otherwise
+// 128x64 tiles (three workgroups per CU on the 2-stage ring) when they give
+// every CU at least one, 64x64 otherwise (a single 4096 x 256 product: 128
+// tiles of 128x64 would leave half the chip idle).  128x128 measured equal to
+// 128x64 at 256 tiles and worse elsewhere (tools/micro/fwd_micro).
 static inline int fwd2_cfg(const GemmBatch& gb) {
-  int t128 = 0;
-  for (int i = 0; i < gb.ntasks; ++i) t128 += ((gb.t[i].M + 127) / 128) * ((gb.t[i].N + 127) / 128);
-  return (t128 >= 192 && t128 <= 256) ? 6 : 7;
+  int t = 0;
+  for (int i = 0; i < gb.ntasks; ++i) t += ((gb.t[i].M + 127) / 128) * ((gb.t[i].N + 63) / 64);
+  return t >= 256 ? 7 : 8;
 }
 
 // Backward batches at large batch go to gemm_bwd.hip (cfg 5: float2 fetch of
@@ -282,9 +288,15 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     if (all_fwd && gemm_fwd_supports(gb)) return fwd2_cfg(gb);
   }
   if (bwdp_on()) {
-    bool all_bwd = true;
-    for (int i = 0; i < gb.ntasks; ++i) all_bwd = all_bwd && !gb.t[i].b_kc;
-    if (all_bwd && gemm_bwdp_supports(gb)) return bwdp_cfg(gb);
+    // a dX with a short K (the head's 2 Da: one or two stages, the pipeline
+    // never fills) stays on the register-direct kernel: the head dW + dh2
+    // launch at B=4096 takes 8.6 us there against 13.3 here
+    bool all_bwd = true, short_dx = false;
+    for (int i = 0; i < gb.ntasks; ++i) {
+      all_bwd = all_bwd && !gb.t[i].b_kc;
+      short_dx = short_dx || (gb.t[i].a_kc && gb.t[i].K < 64);
+    }
+    if (all_bwd && !short_dx && gemm_bwdp_supports(gb)) return bwdp_cfg(gb);
   }
   if (bwd2_on() && big_bwd()) {
     // a dX with a short K (the head's 2 Da, the K-output critic's K) leaves

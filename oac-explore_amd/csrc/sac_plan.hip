@@ -574,7 +574,7 @@ static void plan_splits(SacPlan& p) {
     p.sp_q1 = choose_split_pipe(c.batch, nq * (t64(H, H) + t64(c.q_out, H)));
     p.sp_ql = p.sp_q1;
     p.sp_q0 = choose_split_pipe(c.batch, nq * t64(H, Dq));
-    p.sp_ph = choose_split_pipe(c.batch, t64(2 * Da, H));
+    // (the head dW rides with the short-K dh2 product: register-direct kernel, sp_ph as is)
     p.sp_p1 = choose_split_pipe(c.batch, t64(H, H));
     p.sp_p0 = choose_split_pipe(c.batch, t64(H, Do));
   }
