@@ -281,6 +281,20 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     narrow = gb.t[i].N <= 32 && gb.t[i].ksplit <= 1 && gb.t[i].K2 == 0;
   if (narrow) return 0;
   if (cfg != 2) return cfg;
+  {  // OAC_NARROWM_SMALL=1: a batch of narrow-row dW products (M <= 32: the
+     // head's 2 Da, a K-output critic's last layer) with short-K dX products
+     // only on the small kernel's 32-row tiles.  Measured (same box, B=4096):
+     // SAC 3,277 -> 3,274, configs[4] 4,077 -> 4,023 steps/s -- off by default
+    static const int nm = [] { const char* e = getenv("OAC_NARROWM_SMALL"); return e ? atoi(e) : 0; }();
+    bool nar = nm != 0 && !gb.fuse_adam;
+    for (int i = 0; i < gb.ntasks && nar; ++i) {
+      const GemmTask& t = gb.t[i];
+      const bool dw = t.epi == EPI_GRAD && !t.a_kc && t.M <= 32;
+      const bool dx = t.a_kc && !t.b_kc && t.K < 64 && t.ksplit <= 1;
+      nar = (dw || dx) && t.K2 == 0 && (t.ksplit <= 1 || t.kchunk % 64 == 0);
+    }
+    if (nar) return 0;
+  }
   if (fwd2_on()) {
     bool all_fwd = true;
     for (int i = 0; i < gb.ntasks; ++i)
