@@ -302,15 +302,17 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     if (all_fwd && gemm_fwd_supports(gb)) return fwd2_cfg(gb);
   }
   if (bwdp_on()) {
-    // a dX with a short K (the head's 2 Da: one or two stages, the pipeline
-    // never fills) stays on the register-direct kernel: the head dW + dh2
-    // launch at B=4096 takes 8.6 us there against 13.3 here
+    // a dX with a short K (the head's 2 Da, a K-output critic's K) rides
+    // along with its batch's dW (same-box A/B, B=4096: SAC 3,276 -> 3,310,
+    // configs[4] 4,106 -> 4,200 steps/s against keeping those batches on the
+    // register-direct kernel; OAC_BWDP_SHORT=0 restores that)
     bool all_bwd = true, short_dx = false;
     for (int i = 0; i < gb.ntasks; ++i) {
       all_bwd = all_bwd && !gb.t[i].b_kc;
       short_dx = short_dx || (gb.t[i].a_kc && gb.t[i].K < 64);
     }
-    if (all_bwd && !short_dx && gemm_bwdp_supports(gb)) return bwdp_cfg(gb);
+    static const bool short_ok = [] { const char* e = getenv("OAC_BWDP_SHORT"); return !e || atoi(e) != 0; }();
+    if (all_bwd && (!short_dx || short_ok) && gemm_bwdp_supports(gb)) return bwdp_cfg(gb);
   }
   if (bwd2_on() && big_bwd()) {
     // a dX with a short K (the head's 2 Da, the K-output critic's K) leaves
