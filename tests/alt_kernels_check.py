@@ -1,0 +1,27 @@
+"""Run by tests/test_gpu_altkernels.py in a child process whose environment
+selects a non-default large-batch kernel (the kernel choice is read once per
+process): the ragged large-batch parity cases of test_gpu_ragged.py (B = 1029
+/ 1100, hidden 48 / 80) for all four trainers against the fp32 CPU oracle."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, os.path.join(ROOT, "oac-explore_amd"), HERE):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import test_gpu_ragged as tr  # noqa: E402
+
+
+def main():
+    shapes = [s for s in tr.SHAPES if s[3] >= 1024]
+    for fn in (tr.test_sac_ragged, tr.test_particle_oac_ragged, tr.test_goac_ragged,
+               tr.test_ptrain_ragged):
+        for s in shapes:
+            fn(*s)
+            print(f"ok {fn.__name__}{s}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

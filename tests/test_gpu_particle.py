@@ -75,12 +75,13 @@ def test_particle_stats_keys_match_reference_order():
 @pytest.mark.parametrize("B", [1024, 4096])
 def test_particle_large_batch_matches_oracle(B):
     """BASELINE configs[4] (particle_trainer_oac K=10, Ant-v2 dims, batch
-    4096) on the large-batch kernels (register-direct forward and backward,
-    gemm_big.hip; the post-step critic layer 0 on a~ as a rank-R operand;
-    narrow products on the small-tile kernel; OAC_BIG_BWD=0 in the
-    environment moves the backward products to the LDS kernel, gemm.hip, for
-    A/B runs of this test): one step against the fp32 CPU oracle on the same
-    inputs and eps (1e-5 on every gradient tensor)."""
+    4096) on the large-batch kernels (the LDS-DMA pipelined forward and
+    backward GEMMs, gemm_fwd.hip / gemm_bwdp.hip, incl. the post-step critic
+    layer 0 on a~ as a rank-R continuation; narrow products on the small-tile
+    kernel; OAC_FWD2=0 / OAC_BWDP=0 in the environment move the products to
+    the register-direct kernels, gemm_big.hip / gemm_bwd.hip, for A/B runs of
+    this test): one step against the fp32 CPU oracle on the same inputs and
+    eps (1e-5 on every gradient tensor)."""
     from oracle import sac_oracle as so
     from gpu_helpers import batch_from
     meta = dict(obs_dim=111, act_dim=8, hidden=[256, 256], K=10, seed=11, q_min=0.0,

@@ -1,8 +1,9 @@
 """Ragged shapes on the GPU, every trainer kind against the fp32 CPU oracle:
 batch sizes that are not tile multiples (1, 37, 300, and 1029 / 1100 on the
-large-batch kernels: register-direct forward and backward products, split-K
-chunks that end mid k-group), hidden widths that are not multiples of the
-32- or 64-wide tiles (48, 80), odd observation / action widths.
+large-batch kernels: the LDS-DMA pipelined forward and backward products with
+partial tiles and partial K stages, split-K chunks that end mid stage),
+hidden widths that are not multiples of the 32- or 64-wide tiles (48, 80),
+odd observation / action widths.
 One step from identical state; every gradient tensor within 1e-5
 (norm-relative) of the oracle's."""
 import numpy as np
