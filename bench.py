@@ -154,18 +154,18 @@ def dropin_run(tr, rb, B):
     return run
 
 
-def roofline_of(kt, flop_per_sample, B, n):
+def roofline_of(kt, flop_per_sample, B, n, traffic_key=None):
     gk = kt["gemm_grouped"]
     fpl = flop_per_sample * B * n / max(gk["launches"], 1)
     ach = fpl / (gk["avg_us"] * 1e-6) / 1e12
     return {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4),
-            "traffic": load_traffic(B), "flops_per_launch": round(fpl),
+            "traffic": load_traffic(traffic_key or B), "flops_per_launch": round(fpl),
             "avg_launch_us": round(gk["avg_us"], 3), "launches_per_step": gk["launches"] / n}
 
 
 def batch_leg(name, tr, rb, B, steps, warmup, flop_per_sample, world, device, timing_steps=8,
-              rank=0, seed=101):
+              rank=0, seed=101, traffic_key=None):
     """The drop-in loop at another batch size on the same trainer (every rank
     steps: at world > 1 this is the data-parallel step), with its own
     kernel timing and roofline."""
@@ -176,7 +176,7 @@ def batch_leg(name, tr, rb, B, steps, warmup, flop_per_sample, world, device, ti
     return {"workload": name, "steps_per_s": round(v, 1), "ms_per_step": round(1e3 * el / steps, 4),
             "samples_per_s": round(v * B, 1), "batch_per_rank": B, "steps": steps,
             "step_roofline_frac": round(flop_per_sample * B * v / world / 1e12 / PEAK_FP32_TFLOPS, 4),
-            "roofline": roofline_of(kt, flop_per_sample, B, timing_steps)}
+            "roofline": roofline_of(kt, flop_per_sample, B, timing_steps, traffic_key)}
 
 
 def ring_timing(tr, stream, rb, B, steps=640, n=64):
@@ -209,7 +209,7 @@ def poac_ant_leg(args, device, B=4096, steps=128, warmup=16, timing_steps=8):
     rb.load_transitions(synthetic_rows(args.replay, rb.rows, Do, Da, device, seed=3))
     out = batch_leg("particle_trainer_oac K=10, Ant-v2 dims (111, 8), 2x256, batch 4096, "
                     "replay 1e6 (BASELINE configs[4])", tr, rb, B, steps, warmup,
-                    FLOP_PER_SAMPLE_POAC_ANT, 1, device, timing_steps)
+                    FLOP_PER_SAMPLE_POAC_ANT, 1, device, timing_steps, traffic_key="poac4096")
     assert torch.isfinite(tr.params).all().item(), "non-finite P-OAC parameters"
     del tr, rb
     return out

@@ -15,4 +15,5 @@ python3 tools/trace.py gpurun_out/prof_b256 ${NLAUNCH:-11} > $D/b256_step_trace.
 rm -f profiles/pmc_gemm_traffic.json
 python3 tools/pmc_summary.py b256 $D/pmc_b256.json --traffic 256 profiles/pmc_gemm_traffic.json > $D/pmc_b256.txt
 python3 tools/pmc_summary.py b4096 $D/pmc_b4096.json --traffic 4096 profiles/pmc_gemm_traffic.json > $D/pmc_b4096.txt
+python3 tools/pmc_summary.py poac4096 $D/pmc_poac4096.json --traffic poac4096 profiles/pmc_gemm_traffic.json > $D/pmc_poac4096.txt
 echo "profiles -> $D"

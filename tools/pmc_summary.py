@@ -6,7 +6,7 @@ so HBM bytes = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.
 
 usage: python tools/pmc_summary.py <tag> [json-out] [--traffic BATCH FILE]
   --traffic: also merge {BATCH: HBM bytes per GEMM launch} (the mean over every
-  dispatch of the step's GEMM kernels, gemm_small / gemm_grouped / gemm_big)
+  dispatch of the step's GEMM kernels: every oac::gemm_* family)
   into FILE -- the `roofline.traffic` bench.py reports."""
 import collections
 import csv
@@ -38,8 +38,7 @@ for kind in ("fetch", "write", "sq"):
     for k, d in load(kind).items():
         for c, v in d.items():
             out.setdefault(k, {})[c] = sum(v) / len(v)
-            if any(n in k for n in ("gemm_small_kernel", "gemm_grouped_kernel", "gemm_big_kernel",
-                                    "gemm_lds_kernel")):
+            if "oac::gemm_" in k:   # every GEMM kernel family of the step
                 gemm[c].extend(v)
 for k, d in sorted(out.items()):
     if "FETCH_SIZE" in d and "WRITE_SIZE" in d:

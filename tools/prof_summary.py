@@ -18,7 +18,7 @@ for row in csv.DictReader(open(f)):
     n, t = int(row["Calls"]), float(row["TotalDurationNs"])
     short = name.split("(")[0].replace("void ", "")
     print(f"{short:48s} calls {n:6d}  avg {t / n / 1e3:8.3f} us")
-    if any(k in name for k in ("gemm_small_kernel", "gemm_grouped_kernel", "gemm_big_kernel")):
+    if "oac::gemm_" in name:   # every GEMM kernel family
         calls += n
         total += t
 if calls:
