@@ -22,8 +22,19 @@ namespace oac {
 // then a 256-wide tree.  red: 256 floats of LDS.  Every thread gets the sum.
 __device__ __forceinline__ float logp_sum256(const float* logp, int B, float te, float* red) {
   if (threadIdx.x < 256) {
+    // the same sequential order per thread, its loads issued 16 at a time
+    // (a plain loop waited one memory round trip per 256 rows: at B=4096
+    // that was most of the critic-targets launch)
     float acc = 0.f;
-    for (int i = threadIdx.x; i < B; i += 256) acc += logp[i] + te;
+    int i = threadIdx.x;
+    for (; i + 15 * 256 < B; i += 16 * 256) {
+      float v[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v[k] = logp[i + 256 * k];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) acc += v[k] + te;
+    }
+    for (; i < B; i += 256) acc += logp[i] + te;
     red[threadIdx.x] = acc;
   }
   __syncthreads();
