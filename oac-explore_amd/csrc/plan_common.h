@@ -231,9 +231,17 @@ static inline bool fwd2_on() {
 // tiles of 128x64 would leave half the chip idle).  128x128 measured equal to
 // 128x64 at 256 tiles and worse elsewhere (tools/micro/fwd_micro).
 static inline int fwd2_cfg(const GemmBatch& gb) {
-  int t = 0;
-  for (int i = 0; i < gb.ntasks; ++i) t += ((gb.t[i].M + 127) / 128) * ((gb.t[i].N + 63) / 64);
-  return t >= 256 ? 7 : 8;
+  // rounds of tiles per CU x tile area, 64x64 tiles charged ~18 % more per
+  // unit of work (fewer MFMAs per LDS read): 384 tiles of 128x64 (configs[4]
+  // policy layer 1) leave half the CUs with one tile and half with two, where
+  // 768 tiles of 64x64 are three everywhere
+  int t7 = 0, t8 = 0;
+  for (int i = 0; i < gb.ntasks; ++i) {
+    t7 += ((gb.t[i].M + 127) / 128) * ((gb.t[i].N + 63) / 64);
+    t8 += ((gb.t[i].M + 63) / 64) * ((gb.t[i].N + 63) / 64);
+  }
+  const double c7 = 2.0 * ((t7 + 255) / 256), c8 = 1.18 * ((t8 + 255) / 256);
+  return c8 < c7 ? 8 : 7;
 }
 
 // Backward batches at large batch go to gemm_bwd.hip (cfg 5: float2 fetch of
