@@ -20,38 +20,8 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(AdamArgs a) {
                                    a.tau, a.period);
   const long n4 = a.n >> 2;
   const long stride = (long)gridDim.x * 256;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) {
-    float4 g;
-    if (a.S > 1 || a.gslab != a.g) {
-      // slabs summed in fixed order 0, 1, ..., S-1; the loads of 8 slabs are
-      // issued together (a one-slab-per-iteration loop waited out S
-      // dependent round trips: B=4096, S=32 -> ~11 us per launch)
-      const float4* gs = reinterpret_cast<const float4*>(a.gslab) + i;
-      const long st4 = a.slab_stride >> 2;
-      g = gs[0];
-      int k = 1;
-#pragma unroll 1
-      for (; k + 8 <= a.S; k += 8) {
-        float4 x[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x[j] = gs[(long)(k + j) * st4];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) { g.x += x[j].x; g.y += x[j].y; g.z += x[j].z; g.w += x[j].w; }
-      }
-#pragma unroll 1
-      for (; k < a.S; ++k) {
-        const float4 x = gs[(long)k * st4];
-        g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
-      }
-      reinterpret_cast<float4*>(a.g)[i] = g;
-    } else {
-      g = reinterpret_cast<const float4*>(a.g)[i];
-    }
-    if (a.reduce_only) continue;
-    if (a.gscale != 1.f) { g.x *= a.gscale; g.y *= a.gscale; g.z *= a.gscale; g.w *= a.gscale; }
-    adam_float4(c, a, i, g);
-  }
-  if (a.reduce_only) return;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) adam_flat_elem(c, a, i);
+  if (a.reduce_only || a.no_book) return;
   step_bookkeeping(a.state, a.alpha, a.advance);
 }
 

@@ -66,8 +66,7 @@ __device__ __forceinline__ float polyak1(const AdamConsts& c, float t, float p) 
 // non-null: SAC commits in the critic Adam, the particle trainer -- whose
 // alpha update comes after the critic step -- in the policy Adam).  No other
 // block of the launch reads these fields.
-__device__ __forceinline__ void step_bookkeeping(StepState* st, AlphaState* as, int advance) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+__device__ __forceinline__ void step_bookkeeping_lead(StepState* st, AlphaState* as, int advance) {
   if (advance) {
     st->n_steps = st->t_snapshot + 1;
     st->batch_counter += 1;
@@ -75,6 +74,10 @@ __device__ __forceinline__ void step_bookkeeping(StepState* st, AlphaState* as, 
     st->t_snapshot = st->n_steps;
   }
   if (as) { as->log_alpha = as->next_log_alpha; as->m = as->next_m; as->v = as->next_v; }
+}
+__device__ __forceinline__ void step_bookkeeping(StepState* st, AlphaState* as, int advance) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  step_bookkeeping_lead(st, as, advance);
 }
 
 // one float4 of a flat range: g (already reduced) -> p, m, v (+ target)
@@ -95,6 +98,58 @@ __device__ __forceinline__ void adam_float4(const AdamConsts& c, const AdamArgs&
     t.z = polyak1(c, t.z, p.z); t.w = polyak1(c, t.w, p.w);
     reinterpret_cast<float4*>(a.target)[i] = t;
   }
+}
+
+// float4 i of a flat range: the split-K slabs summed in fixed order 0 .. S-1
+// (written back to g), optionally scaled, then Adam (+ Polyak) -- the body of
+// adam_flat_kernel (adam.hip) and of the large-batch GEMMs' side workgroups
+__device__ __forceinline__ void adam_flat_elem(const AdamConsts& c, const AdamArgs& a, long i) {
+  float4 g;
+  if (a.S > 1 || a.gslab != a.g) {
+    // the loads of 8 slabs are issued together (a one-slab-per-iteration loop
+    // waited out S dependent round trips: B=4096, S=32 -> ~11 us per launch)
+    const float4* gs = reinterpret_cast<const float4*>(a.gslab) + i;
+    const long st4 = a.slab_stride >> 2;
+    g = gs[0];
+    int k = 1;
+#pragma unroll 1
+    for (; k + 8 <= a.S; k += 8) {
+      float4 x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = gs[(long)(k + j) * st4];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { g.x += x[j].x; g.y += x[j].y; g.z += x[j].z; g.w += x[j].w; }
+    }
+#pragma unroll 1
+    for (; k < a.S; ++k) {
+      const float4 x = gs[(long)k * st4];
+      g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
+    }
+    reinterpret_cast<float4*>(a.g)[i] = g;
+  } else {
+    g = reinterpret_cast<const float4*>(a.g)[i];
+  }
+  if (a.reduce_only) return;
+  if (a.gscale != 1.f) { g.x *= a.gscale; g.y *= a.gscale; g.z *= a.gscale; g.w *= a.gscale; }
+  adam_float4(c, a, i, g);
+}
+
+// side workgroup `blk` of `nblk` (256 threads each): the flat ranges of
+// b.adam listed in b.seg_off / b.seg_n (GemmBatch::side_adam)
+__device__ __forceinline__ void adam_side_block(const GemmBatch& b, int blk, int nblk) {
+  const AdamArgs& a = b.adam;
+  const AdamConsts c = adam_consts(a.state, a.advance, a.lr, a.beta1, a.beta2, a.eps, a.target,
+                                   a.tau, a.period);
+  const long stride = (long)nblk * 256;
+  for (int sgi = 0; sgi < b.nseg; ++sgi) {
+    AdamArgs r = a;
+    const long off = b.seg_off[sgi];
+    r.p += off; r.g += off; r.m += off; r.v += off; r.gslab += off;
+    if (r.target) r.target += off;
+    const long n4 = b.seg_n[sgi] >> 2;
+    for (long i = (long)blk * 256 + threadIdx.x; i < n4; i += stride) adam_flat_elem(c, r, i);
+  }
+  if (b.side_book && blk == 0 && threadIdx.x == 0) step_bookkeeping_lead(a.state, a.alpha, a.advance);
 }
 
 // one element at index i of the group (GEMM epilogue)

@@ -290,8 +290,13 @@ gemm_bwdp_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, i
   __shared__ __attribute__((aligned(16))) float lds[kFBuf * BwdG<BM, BN>::STAGE + kVec];
   if (batch.publish && blockIdx.x == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
-  const int bid = xcd_tile(blockIdx.x, gridDim.x);
-  if (bid >= total_tiles) return;
+  const int side0 = batch.side_first ? 0 : total_tiles;   // side workgroups: the flat Adam
+  const int tile0 = batch.side_first ? batch.side_adam : 0;  // (GemmBatch::side_adam)
+  if ((int)blockIdx.x >= side0 && (int)blockIdx.x < side0 + batch.side_adam) {
+    adam_side_block(batch, blockIdx.x - side0, batch.side_adam);
+    return;
+  }
+  const int bid = xcd_tile(blockIdx.x - tile0, total_tiles);
   int ti = 0;
   ti = bid >= tb1 ? 1 : ti; ti = bid >= tb2 ? 2 : ti; ti = bid >= tb3 ? 3 : ti;
   ti = bid >= tb4 ? 4 : ti; ti = bid >= tb5 ? 5 : ti; ti = bid >= tb6 ? 6 : ti;
@@ -337,7 +342,7 @@ hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
 #define OAC_BWDP(C_, BM_, BN_) \
   if (cfg == C_) { \
-    OAC_LAUNCH((gemm_bwdp_kernel<BM_, BN_>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, \
+    OAC_LAUNCH((gemm_bwdp_kernel<BM_, BN_>), dim3(b.total_tiles + b.side_adam), dim3(256), 0, s, b.total_tiles, \
                tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
     return hipGetLastError(); }
   OAC_BWDP(9, 128, 64) OAC_BWDP(10, 64, 64) OAC_BWDP(11, 128, 128)

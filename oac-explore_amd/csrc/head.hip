@@ -19,6 +19,7 @@
 #include "oac_common.h"
 #include "kernels.h"
 #include "policy_math.h"
+#include <algorithm>
 
 namespace oac {
 
@@ -44,8 +45,11 @@ constexpr int kHeadWaves = 8;
 constexpr int kRows = 16;
 
 // NT = column tiles of the stacked head (2*act_dim <= 16*NT), a compile-time
-// count so the MFMA sequence is branch-free
-template <int NT>
+// count so the MFMA sequence is branch-free; KP = (net, 16-column tile) pairs
+// per wave of step 3 (2: <= 16 pairs per workgroup; 4: a whole 256-column
+// hidden layer of both nets in one workgroup, the large-batch form, no
+// recomputed heads); KS = k-steps of 4 action dims held per pair (Da <= 4*KS)
+template <int NT, int KP, int KS>
 __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const HeadArgs a) {
   // one LDS array: reduction scratch, then the head tile and the actions
   constexpr int kRed = kHeadWaves * 4 * 4 * 64;   // waves x col tiles x regs x lanes
@@ -67,7 +71,7 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
   const int n_lo = chunk * cols;
   const int tiles = (cols + 15) / 16;
   const int pairs = sg.n_nets * tiles;
-  const int ksteps = (Da + 3) >> 2;              // <= 8 (Da <= 32)
+  const int ksteps = (Da + 3) >> 2;              // <= KS
   const int srow = threadIdx.x >> 5, sj = threadIdx.x & 31;   // step 2: row, action dim
   const float eps_pf = a.det ? 0.f : sg.eps[(long)min(m0 + srow, B - 1) * Da + min(sj, Da - 1)];
   float bh_pf[2];
@@ -76,8 +80,8 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
     const int e = threadIdx.x + i * 64 * kHeadWaves;          // head element (see step 1)
     bh_pf[i] = bh[min(((e >> 8) << 4) + (e & 15), D2 - 1)];
   }
-  constexpr int kPairs = 2;                      // pairs per wave prefetched
-  float bw_pf[kPairs][8], pre_pf[kPairs][4];
+  constexpr int kPairs = KP;                     // pairs per wave prefetched
+  float bw_pf[kPairs][KS], pre_pf[kPairs][4];
 #pragma unroll
   for (int q = 0; q < kPairs; ++q) {
     const int pi = wave + q * kHeadWaves;
@@ -87,7 +91,7 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
       const bool nv = n < H && n < n_lo + cols;
       const float* wrow = sg.wa[net] + (long)(nv ? n : 0) * a.ld_wa;
 #pragma unroll
-      for (int st = 0; st < 8; ++st) bw_pf[q][st] = wrow[min(4 * st + g4, Da - 1)];
+      for (int st = 0; st < KS; ++st) bw_pf[q][st] = wrow[min(4 * st + g4, Da - 1)];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         pre_pf[q][r] = sg.pre[net][(long)min(m0 + 4 * g4 + r, B - 1) * H + (nv ? n : 0)];
@@ -206,7 +210,7 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
     const bool nv = n < H && n < n_lo + cols;
     floatx4 c = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int st = 0; st < 8; ++st)
+    for (int st = 0; st < KS; ++st)
       if (st < ksteps) {
         const int k = 4 * st + g4;
         const float av = k < Da ? as[l16 * 33 + k] : 0.f;
@@ -222,23 +226,36 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
   STAGE(4);
 }
 
+template <int KP, int KS>
+static void launch_head_nt(const HeadArgs& a, dim3 grid, dim3 block, hipStream_t s) {
+  switch ((2 * a.Da + 15) / 16) {
+    case 1: OAC_LAUNCH((policy_head_kernel<1, KP, KS>), grid, block, 0, s, a); break;
+    case 2: OAC_LAUNCH((policy_head_kernel<2, KP, KS>), grid, block, 0, s, a); break;
+    case 3: OAC_LAUNCH((policy_head_kernel<3, KP, KS>), grid, block, 0, s, a); break;
+    default: OAC_LAUNCH((policy_head_kernel<4, KP, KS>), grid, block, 0, s, a); break;
+  }
+}
+
 hipError_t launch_policy_head(const HeadArgs& a, int nseg, hipStream_t s) {
   if (a.Da < 1 || 2 * a.Da > 64 || a.col_chunks < 1 || nseg < 1 || nseg > 3 ||
       (nseg > 2 && !a.det))
     return hipErrorInvalidValue;
   for (int i = 0; i < nseg; ++i)
     if (a.seg[i].n_nets < 0 || a.seg[i].n_nets > 2) return hipErrorInvalidValue;
-  // every (net, 16-column tile) of a workgroup's chunk is prefetched: <= 2 per wave
+  // every (net, 16-column tile) of a workgroup's chunk is prefetched: <= 4 per wave
   const int cols = (a.H + a.col_chunks - 1) / a.col_chunks;
-  for (int i = 0; i < nseg; ++i)
-    if (a.seg[i].n_nets * ((cols + 15) / 16) > 2 * kHeadWaves) return hipErrorInvalidValue;
+  int pairs = 0;
+  for (int i = 0; i < nseg; ++i) pairs = std::max(pairs, a.seg[i].n_nets * ((cols + 15) / 16));
+  if (pairs > 4 * kHeadWaves) return hipErrorInvalidValue;
   const int rblocks = (a.B + kRows - 1) / kRows;
   const dim3 grid(rblocks * a.col_chunks, nseg), block(64 * kHeadWaves);
-  switch ((2 * a.Da + 15) / 16) {
-    case 1: OAC_LAUNCH(policy_head_kernel<1>, grid, block, 0, s, a); break;
-    case 2: OAC_LAUNCH(policy_head_kernel<2>, grid, block, 0, s, a); break;
-    case 3: OAC_LAUNCH(policy_head_kernel<3>, grid, block, 0, s, a); break;
-    default: OAC_LAUNCH(policy_head_kernel<4>, grid, block, 0, s, a); break;
+  const bool kp4 = pairs > 2 * kHeadWaves;
+  if (a.Da <= 8) {
+    if (kp4) launch_head_nt<4, 2>(a, grid, block, s); else launch_head_nt<2, 2>(a, grid, block, s);
+  } else if (a.Da <= 20) {
+    if (kp4) launch_head_nt<4, 5>(a, grid, block, s); else launch_head_nt<2, 5>(a, grid, block, s);
+  } else {
+    if (kp4) launch_head_nt<4, 8>(a, grid, block, s); else launch_head_nt<2, 8>(a, grid, block, s);
   }
   return hipGetLastError();
 }

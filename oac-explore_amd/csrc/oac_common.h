@@ -88,6 +88,7 @@ struct AdamArgs {
   AlphaState* alpha; // commit next_* (critic Adam only); may be null
   float gscale;      // gradient scale (1/world_size after an all-reduce SUM)
   int reduce_only;   // data-parallel: only reduce the slabs into g (all-reduce next)
+  int no_book;       // skip the state / alpha bookkeeping (a partial range of the group)
 };
 
 constexpr int kMaxTasks = 8;
@@ -122,6 +123,16 @@ struct GemmBatch {
   int force_nw, force_gpw;   // small kernel: waves per workgroup / k-groups in flight (0 = auto)
   long seg_off[2], seg_n[2]; // flat ranges (floats, multiples of 4) from the group base
   AdamArgs adam;
+  // Side optimizer (large-batch kernels, gemm_bwdp.hip): side_adam > 0 extra
+  // workgroups (blockIdx >= total_tiles) run the flat Adam -- split-K slabs
+  // summed in fixed order, as adam_flat_kernel -- over the ranges
+  // seg_off/seg_n[0 .. nseg) of `adam`, whose gradients earlier launches of
+  // the step finished and whose parameters no tile of this launch reads;
+  // side_book: the first side workgroup also does adam.state / adam.alpha
+  // bookkeeping.  Independent of fuse_adam (small kernel only).
+  // side_first: the side workgroups are blockIdx [0, side_adam) (a multiple
+  // of 8, so every tile keeps its XCD), dispatched ahead of the tiles.
+  int side_adam, side_book, side_first;
   RowGather rg;              // rg.ring != null: direct row gather (small kernel only)
 };
 

@@ -98,6 +98,23 @@ inline void fuse_adam(GemmBatch& gb, const AdamArgs& a, int nseg, const long* of
   for (int i = 0; i < nseg; ++i) { gb.seg_off[i] = off[i]; gb.seg_n[i] = n[i]; }
 }
 
+// Large-batch single-process step (split-K slabs, no fused epilogue Adam):
+// each group's Adam runs as side workgroups of a later GEMM launch that reads
+// none of the updated parameters (GemmBatch::side_adam) instead of its own
+// launch -- the critic's layer 1 + last layer beside its layer-0 dW, the
+// critic's layer 0 beside the -min Q dX to layer 1, the policy's layer 1 +
+// heads beside its layer-0 dW; only the policy's layer 0 keeps a launch.
+// OAC_SPLIT_ADAM=0: one Adam launch per group (A/B runs).
+inline bool split_adam_on(const SacPlan& p) {
+  static const bool v = [] { const char* e = getenv("OAC_SPLIT_ADAM"); return !e || atoi(e) != 0; }();
+  return v && p.cfg != 0 && p.c.world_size == 1 && !can_fuse_adam(p);
+}
+// Attach the ranges [off[i], off[i] + n[i]) of `a` to batch gb as side
+// workgroups when gb runs on gemm_bwdp; otherwise launch them now, one Adam
+// launch per range (before gb: every caller's ranges are already final).
+int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long* off,
+              const long* n, bool book, hipStream_t s);
+
 // particle trainer (particle_plan.hip)
 void particle_layout_workspace(SacPlan& p);
 int particle_run_step(SacPlan& p, int flags, hipStream_t s);

@@ -195,6 +195,54 @@ static void add_critic_l1(SacPlan& p, GemmBatch& gb) {
   add(gb, q_l1(p, p.W(W_H1Q2), q2, p.W(W_H2Q2), QV_Q2));
 }
 
+int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long* off,
+              const long* n, bool book, hipStream_t s) {
+  const int cfg = launch_cfg(p.cfg, gb);
+  if (cfg >= 9 && cfg <= 11 && nseg <= 2) {
+    // one float4 per thread, dispatched after the tiles (B=4096 SAC, same
+    // box: one Adam launch per group 3,429 steps/s; side blocks after the
+    // tiles, 32 per launch 3,186 -- the side work became the launch's tail --,
+    // 64 3,419, 128 3,508, one float4 per thread 3,485; ahead of the tiles
+    // 3,442); OAC_SIDE_BLOCKS forces a count, OAC_SIDE_FIRST=1 dispatches
+    // them ahead of the tiles
+    static const int forced = [] { const char* e = getenv("OAC_SIDE_BLOCKS"); return e ? atoi(e) : 0; }();
+    static const int first = [] { const char* e = getenv("OAC_SIDE_FIRST"); return e ? atoi(e) : 0; }();
+    long n4 = 0;
+    for (int i = 0; i < nseg; ++i) n4 += n[i] >> 2;
+    int blocks = forced > 0 ? forced : (int)std::min<long>(1024, (n4 + 255) / 256);
+    gb.side_adam = std::max(8, (blocks + 7) & ~7);
+    gb.side_first = first ? 1 : 0;
+    gb.side_book = book ? 1 : 0;
+    gb.adam = a;
+    gb.nseg = nseg;
+    for (int i = 0; i < nseg; ++i) { gb.seg_off[i] = off[i]; gb.seg_n[i] = n[i]; }
+    return 0;
+  }
+  for (int i = 0; i < nseg; ++i) {
+    AdamArgs r = a;
+    r.p += off[i]; r.g += off[i]; r.m += off[i]; r.v += off[i];
+    r.gslab += off[i];
+    if (r.target) r.target += off[i];
+    r.n = n[i];
+    r.no_book = (book && i == 0) ? 0 : 1;
+    TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(r, s)));
+    p.launches++;
+  }
+  return 0;
+}
+
+// policy_head workgroups per 16-row block: 64 hidden columns each at small
+// batch (more workgroups in flight); at large batch one workgroup takes the
+// whole hidden layer of both nets (4 (net, column tile) pairs per wave), so
+// the row block's heads are computed once and the 512 workgroups of 8 waves
+// (114 VGPRs: 4 waves per SIMD) run as a single round -- two chunks of 128
+// columns made 1,024 workgroups and two rounds (B=4096: 24.4 us)
+static int head_col_chunks(int B, int H) {
+  static const int forced = [] { const char* e = getenv("OAC_HEAD_CC"); return e ? atoi(e) : 0; }();
+  if (forced > 0) return forced;
+  return B >= 1024 ? std::max(1, (H + 255) / 256) : std::max(1, (H + 63) / 64);
+}
+
 static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool critic_done = false) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
@@ -258,7 +306,7 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
     // 64 hidden columns per workgroup at small batch (more workgroups in
     // flight); at large batch the fewest chunks the per-wave prefetch allows
     // (each chunk recomputes the row block's heads)
-    a.col_chunks = std::max(1, (H + (B >= 1024 ? 127 : 63)) / (B >= 1024 ? 128 : 64));
+    a.col_chunks = head_col_chunks(B, H);
     HeadSeg& s0 = a.seg[0];   // policy(obs; eps1) -> Q1/Q2(obs, a~)
     s0.h2 = p.W(W_H2P); s0.eps = p.E1(); s0.head = p.W(OAC_WS_HEAD1);
     s0.act = p.W(OAC_WS_ACT1); s0.stdv = p.W(W_STD1); s0.u = p.W(W_U1); s0.logp = p.W(OAC_WS_LOGP1);
@@ -287,7 +335,7 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
 // part 0: the whole phase; 1: the fresh-action critic forward only (layer 1 +
 // last layer: no alpha needed, so the data-parallel alpha all-reduce overlaps
 // it); 2: the rest (targets through the critic gradients)
-static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0) {
+static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool split = false) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -372,6 +420,11 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0) {
       const long off[2] = {(long)L.q_fc1_w, (long)(L.q_size + L.q_fc1_w)};
       const long n[2] = {(long)(L.q_size - L.q_fc1_w), (long)(L.q_size - L.q_fc1_w)};
       fuse_adam(gb, critic_adam(p, 0, c.auto_alpha ? p.alpha() : nullptr), 2, off, n);
+    } else if (split) {   // layer 1 + last layer of both critics (their gradients are final)
+      const long off[2] = {(long)L.q_fc1_w, (long)(L.q_size + L.q_fc1_w)};
+      const long n[2] = {(long)(L.q_size - L.q_fc1_w), (long)(L.q_size - L.q_fc1_w)};
+      if (side_adam(p, gb, critic_adam(p, 0, c.auto_alpha ? p.alpha() : nullptr), 2, off, n, true, s))
+        return 1;
     }
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -389,7 +442,8 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
 
 // prefetch: batch of the next step (its critic-side forward rides on this
 // step's policy-backward launches, small-batch path only), or null
-static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch = nullptr) {
+static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch = nullptr,
+                  bool split = false) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -409,6 +463,11 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
       add(gb, d);
     }
     if (prefetch) add_critic_l0(p, gb, prefetch);
+    if (split) {   // the critics' layer 0 (not read here; the dL/da launch reads it next)
+      const long off[2] = {0, (long)L.q_size};
+      const long n[2] = {(long)L.q_fc1_w, (long)L.q_fc1_w};
+      if (side_adam(p, gb, critic_adam(p, 0, nullptr), 2, off, n, false, s)) return 1;
+    }
     if (run_gemm(p, gb, s)) return 1;
   }
   if (p.cfg == 0 || head_bwd_fused_big()) {  // dL/da through both critics' action columns + head backward, one launch (small kernel)
@@ -466,6 +525,10 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
       const long off[1] = {(long)L.pol_fc1_w};
       const long n[1] = {(long)(L.pol_size - L.pol_fc1_w)};
       fuse_adam(gb, policy_adam(p, 0, nullptr), 1, off, n);
+    } else if (split) {   // the policy's layer 1 + heads (layer 0: the step's last launch)
+      const long off[1] = {(long)L.pol_fc1_w};
+      const long n[1] = {(long)(L.pol_size - L.pol_fc1_w)};
+      if (side_adam(p, gb, policy_adam(p, 0, nullptr), 1, off, n, false, s)) return 1;
     }
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -493,12 +556,16 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
   // issued inside the previous step's policy backward (small-batch path)
   const bool ahead = p.cfg == 0 && (flags & OAC_STEP_GATHER) && ahead_on;
   if (phase0(p, flags, s, gather_n, ahead && p.slot > 0)) return 1;
-  if (phase1(p, s, fused)) return 1;
-  if (!fused && phase2_adam(p, s, 0)) return 1;
+  const bool split = !fused && split_adam_on(p);
+  if (phase1(p, s, fused, 0, split)) return 1;
+  if (!fused && !split && phase2_adam(p, s, 0)) return 1;
   const bool pf = ahead && i + 1 < n && p.slot + 1 < kXSlots;
-  if (phase2(p, s, fused, pf ? p.W(OAC_WS_BATCH) + (long)(p.slot + 1) * c_batch_rows(p) : nullptr)) return 1;
+  if (phase2(p, s, fused, pf ? p.W(OAC_WS_BATCH) + (long)(p.slot + 1) * c_batch_rows(p) : nullptr,
+             split))
+    return 1;
   if (!fused) {
     AdamArgs a = policy_adam(p, 0, nullptr);
+    if (split) a.n = p.L.pol_fc1_w;   // layer 0; the rest ran beside the layer-0 dW
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
   }
