@@ -201,6 +201,7 @@ struct RowHead {
 struct ParticleTargetArgs {
   const float* q; const float* tq;      // [B, K] critic / target critic outputs
   RowHead th;                           // th.h set: tq computed here (into th.out)
+  RowHead qh;                           // qh.h set: q computed here (into qh.out)
   const float* batch; long ld_batch; int off_rew, off_term;
   float reward_scale, discount;
   int B, K;
@@ -233,6 +234,7 @@ hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s);
 struct GaussTargetArgs {
   const float* q; const float* tq;      // [B, 2] Q(obs, a), Q_target(next_obs, a') raw outputs
   RowHead th;                           // th.h set: tq computed here (into th.out)
+  RowHead qh;                           // qh.h set: q computed here (into qh.out)
   const float* batch; long ld_batch; int off_rew, off_term;
   float reward_scale, discount, std_init;
   float soft_prob;                      // std_soft_update_prob, < 0: off

@@ -68,7 +68,7 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
-  const int K = c.q_out, Dq = Do + Da;
+  const int Dq = Do + Da;
   float* X = p.W(OAC_WS_BATCH);
   const float* obs = X + c.off_obs;
   const float* nobs = X + c.off_next_obs;
@@ -113,22 +113,24 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
     add(gb, t_fwd(p.W(X_H1Q), H, B, H, q + L.q_fc1_w, H, H, p.W(X_H2Q), H, EPI_BIAS_RELU, q + L.q_fc1_b));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {
-    GemmBatch gb{};
-    add(gb, t_fwd(p.W(X_H2P), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD1), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
-    add(gb, t_fwd(p.W(X_H2P2), H, B, H, pol + L.pol_head_w, H, 2 * Da, p.W(OAC_WS_HEAD2), 2 * Da, EPI_BIAS, pol + L.pol_head_b));
-    add(gb, t_fwd(p.W(X_H2Q), H, B, H, q + L.q_last_w, H, K, p.W(OAC_WS_Q1), K, EPI_BIAS, q + L.q_last_b));
-    if (run_gemm(p, gb, s)) return 1;
-  }
-  {
-    PolicySampleArgs a;
+  {  // policy heads, tanh-Gaussian sample + log-prob (both batches), and the
+     // target critic's action columns on a' (next_obs batch) in one launch
+     // (head.hip); Q(obs, a)'s K-output last layer runs in the targets kernel
+    HeadArgs a;
     std::memset(&a, 0, sizeof(a));
-    a.seg[0] = {p.W(OAC_WS_HEAD1), p.W(OAC_WS_EPS2), p.W(OAC_WS_ACT1), p.W(X_STD1), p.W(X_U1),
-                p.W(OAC_WS_LOGP1), nullptr, 0};
-    a.seg[1] = {p.W(OAC_WS_HEAD2), p.W(OAC_WS_EPS1), p.W(OAC_WS_ACT2), p.W(X_STD2), p.W(X_U2),
-                p.W(OAC_WS_LOGP2), nullptr, 0};
-    a.B = B; a.act_dim = Da;
-    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_sample(a, 2, s)));
+    a.wh = pol + L.pol_head_w; a.bh = pol + L.pol_head_b; a.ld_wa = Dq;
+    a.B = B; a.H = H; a.Da = Da;
+    a.col_chunks = B >= 1024 ? std::max(1, (H + 255) / 256) : std::max(1, (H + 63) / 64);
+    HeadSeg& s0 = a.seg[0];   // policy(obs; eps2) (particle_trainer_oac.py:271-273)
+    s0.h2 = p.W(X_H2P); s0.eps = p.W(OAC_WS_EPS2); s0.head = p.W(OAC_WS_HEAD1);
+    s0.act = p.W(OAC_WS_ACT1); s0.stdv = p.W(X_STD1); s0.u = p.W(X_U1); s0.logp = p.W(OAC_WS_LOGP1);
+    s0.n_nets = 0;
+    HeadSeg& s1 = a.seg[1];   // policy(next_obs; eps1) -> TQ(next_obs, a') layer 0 (:193-202)
+    s1.h2 = p.W(X_H2P2); s1.eps = p.W(OAC_WS_EPS1); s1.head = p.W(OAC_WS_HEAD2);
+    s1.act = p.W(OAC_WS_ACT2); s1.stdv = p.W(X_STD2); s1.u = p.W(X_U2); s1.logp = p.W(OAC_WS_LOGP2);
+    s1.n_nets = 1;
+    s1.wa[0] = tq + L.q_fc0_w + Do; s1.pre[0] = p.W(X_PT); s1.h1[0] = p.W(X_H1T);
+    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head(a, 2, s)));
     p.launches++;
   }
   if (c.world_size > 1 && c.auto_alpha) {
@@ -147,15 +149,7 @@ static int pphase1(SacPlan& p, int flags, hipStream_t s, bool split = false) {
   float* X = p.W(OAC_WS_BATCH);
   const float* q = p.b.params + L.q1_base;
   const float* tq = p.b.targets;
-  {
-    GemmBatch gb{};
-    GemmTask t = t_fwd(p.W(OAC_WS_ACT2), Da, B, Da, tq + L.q_fc0_w + Do, Dq, H, p.W(X_H1T), H,
-                       EPI_ADD_RELU, nullptr);
-    t.aux = p.W(X_PT); t.ld_aux = H;
-    add(gb, t);
-    if (run_gemm(p, gb, s)) return 1;
-  }
-  {
+  {  // target critic layer 1 (its layer 0 finished in the head launch)
     GemmBatch gb{};
     add(gb, t_fwd(p.W(X_H1T), H, B, H, tq + L.q_fc1_w, H, H, p.W(X_H2T), H, EPI_BIAS_RELU, tq + L.q_fc1_b));
     if (run_gemm(p, gb, s)) return 1;
@@ -164,6 +158,7 @@ static int pphase1(SacPlan& p, int flags, hipStream_t s, bool split = false) {
     ParticleTargetArgs a;
     std::memset(&a, 0, sizeof(a));
     a.th = RowHead{p.W(X_H2T), tq + L.q_last_w, tq + L.q_last_b, p.W(OAC_WS_TQ1), H};
+    a.qh = RowHead{p.W(X_H2Q), q + L.q_last_w, q + L.q_last_b, p.W(OAC_WS_Q1), H};
     a.q = p.W(OAC_WS_Q1); a.tq = p.W(OAC_WS_TQ1); a.batch = X; a.ld_batch = RS;
     a.off_rew = c.off_rew; a.off_term = c.off_term; a.reward_scale = c.reward_scale;
     a.discount = c.discount; a.B = B; a.K = K;

@@ -269,18 +269,22 @@ __device__ __forceinline__ void row_heads(const RowHead& hd, int K, int B, int r
 }
 
 __global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArgs p) {
-  __shared__ RowHeadLds hs;
+  __shared__ RowHeadLds hs, qs;
   const int r0 = blockIdx.x * kRowBlock, r = r0 + threadIdx.x;
   const int K = p.K;
   if (p.th.h) {
     row_heads(p.th, K, p.B, r0, hs);
     __syncthreads();
   }
+  if (p.qh.h) {   // the critic's own last layer on (obs, a) (particle_trainer_oac.py:185-191)
+    row_heads(p.qh, K, p.B, r0, qs);
+    __syncthreads();
+  }
   if (threadIdx.x >= kRowBlock || r >= p.B) return;
   const float fK = (float)K;
   float q[kMaxHeads], t[kMaxHeads];
   int qi[kMaxHeads], tix[kMaxHeads];
-  load_row16(p.q + (long)r * K, K, q, qi);
+  load_row16(p.qh.h ? &qs.out[threadIdx.x][0] : p.q + (long)r * K, K, q, qi);
   load_row16(p.th.h ? &hs.out[threadIdx.x][0] : p.tq + (long)r * K, K, t, tix);
   sort16(q, qi);
   sort16(t, tix);
@@ -390,7 +394,7 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
 }
 
 hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s) {
-  if (a.K > kMaxHeads || !head_ok(a.th)) return hipErrorInvalidValue;
+  if (a.K > kMaxHeads || !head_ok(a.th) || !head_ok(a.qh)) return hipErrorInvalidValue;
   OAC_LAUNCH(particle_targets_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock), dim3(256), 0, s, a);
   return hipGetLastError();
 }
