@@ -220,6 +220,10 @@ struct ParticleMinArgs {
   RowHead hn;                           // hn.h set: qn computed here (into hn.out)
   float* gq;                            // [B, K] -1/B at the argmin head
   float* qmin;                          // [B]
+  // dh2 set (needs hn.h): the -min Q backward into the last hidden layer,
+  // dh2[r, n] = [h2[r, n] > 0] (-1/B) W_last[argmin_r, n] (the one nonzero
+  // term of gq . W_last) with h2 = hn.h, W_last = hn.w, n < hn.H
+  float* dh2;
   // alpha update (same as CriticTargetArgs)
   AlphaState* alpha; const StepState* state; const float* logp; float target_entropy;
   double lr, beta1, beta2, adam_eps; int world_size;

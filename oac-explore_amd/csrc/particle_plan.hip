@@ -232,13 +232,14 @@ static int pphase2(SacPlan& p, hipStream_t s, bool split = false) {
     a.qn = p.W(OAC_WS_QN1); a.B = B; a.K = K; a.gq = p.W(X_GQ); a.qmin = p.W(OAC_WS_QNEW);
     // the post-step critic's last layer on (obs, a~) runs in this kernel (row_heads)
     a.hn = RowHead{p.W(X_H2N), q + L.q_last_w, q + L.q_last_b, p.W(OAC_WS_QN1), H};
+    if ((H & 3) == 0) a.dh2 = p.W(X_DH2N);   // the dX launch into the last hidden layer, folded
     a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.state = p.state(); a.logp = p.W(OAC_WS_LOGP1);
     a.target_entropy = c.target_entropy; a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2;
     a.adam_eps = c.adam_eps; a.world_size = c.world_size;
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_particle_min(a, s)));
     p.launches++;
   }
-  {
+  if (H & 3) {   // (otherwise done by the min kernel)
     GemmBatch gb{};
     add(gb, t_dx(p.W(X_GQ), K, B, K, q + L.q_last_w, H, H, p.W(X_DH2N), H, p.W(X_H2N), H));
     if (run_gemm(p, gb, s)) return 1;
@@ -248,19 +249,17 @@ static int pphase2(SacPlan& p, hipStream_t s, bool split = false) {
     add(gb, t_dx(p.W(X_DH2N), H, B, H, q + L.q_fc1_w, H, H, p.W(X_DH1N), H, p.W(X_H1N), H));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {
+  {  // dL/da through the critic's action columns + the tanh-Gaussian head
+     // backward in the epilogue (EPI_HEAD_BWD, small kernel; one launch)
     GemmBatch gb{};
-    add(gb, t_dx(p.W(X_DH1N), H, B, H, q + L.q_fc0_w + Do, Dq, Da, p.W(X_DA), Da, nullptr, 0));
+    GemmTask t = t_dx(p.W(X_DH1N), H, B, H, q + L.q_fc0_w + Do, Dq, Da, p.W(X_DHEAD), 2 * Da,
+                      nullptr, 0);
+    t.epi = EPI_HEAD_BWD;
+    t.ex[0] = p.W(OAC_WS_ACT1); t.ex[1] = p.W(X_STD1); t.ex[2] = p.W(X_U1);
+    t.ex[3] = p.W(OAC_WS_EPS2); t.ex[4] = p.W(OAC_WS_HEAD1);
+    t.ex[5] = c.auto_alpha ? &p.alpha()->alpha : nullptr;
+    add(gb, t);
     if (run_gemm(p, gb, s)) return 1;
-  }
-  {
-    PolicyHeadBwdArgs a;
-    std::memset(&a, 0, sizeof(a));
-    a.da1 = p.W(X_DA); a.da2 = nullptr; a.act = p.W(OAC_WS_ACT1); a.stdv = p.W(X_STD1);
-    a.u = p.W(X_U1); a.eps = p.W(OAC_WS_EPS2); a.head = p.W(OAC_WS_HEAD1);
-    a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.B = B; a.act_dim = Da; a.dhead = p.W(X_DHEAD);
-    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head_backward(a, s)));
-    p.launches++;
   }
   {
     GemmBatch gb{};

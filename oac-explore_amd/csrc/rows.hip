@@ -380,17 +380,35 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
     row_heads(p.hn, K, p.B, r0, hs);
     __syncthreads();
   }
-  if (threadIdx.x >= kRowBlock || r >= p.B) return;
-  const float* qn = p.hn.h ? &hs.out[threadIdx.x][0] : p.qn + (long)r * K;
-  int best = 0;
-  float bv = qn[0];
-  for (int i = 1; i < K; ++i) {
-    const float x = qn[i];
-    if (x < bv) { bv = x; best = i; }
-  }
+  __shared__ int sbest[kRowBlock];
   const float invB = 1.f / (float)p.B;
-  for (int i = 0; i < K; ++i) p.gq[(long)r * K + i] = (i == best) ? -invB : 0.f;
-  p.qmin[r] = bv;
+  if (threadIdx.x < kRowBlock && r < p.B) {
+    const float* qn = p.hn.h ? &hs.out[threadIdx.x][0] : p.qn + (long)r * K;
+    int best = 0;
+    float bv = qn[0];
+    for (int i = 1; i < K; ++i) {
+      const float x = qn[i];
+      if (x < bv) { bv = x; best = i; }
+    }
+    for (int i = 0; i < K; ++i) p.gq[(long)r * K + i] = (i == best) ? -invB : 0.f;
+    p.qmin[r] = bv;
+    sbest[threadIdx.x] = best;
+  }
+  if (!p.dh2) return;
+  // -min Q backward into the last hidden layer (the dX launch it replaces
+  // summed gq[r, k] W[k, n] over k: one nonzero product, the rest +0)
+  __syncthreads();
+  const int H = p.hn.H, n4 = H >> 2;
+  for (int e = threadIdx.x; e < kRowBlock * n4; e += 256) {
+    const int rr = e / n4, c = 4 * (e - rr * n4), m = r0 + rr;
+    if (m >= p.B) continue;
+    const float4 h = *reinterpret_cast<const float4*>(p.hn.h + (long)m * H + c);
+    const float4 w = *reinterpret_cast<const float4*>(p.hn.w + (long)sbest[rr] * H + c);
+    float4 o;
+    o.x = h.x > 0.f ? -invB * w.x : 0.f; o.y = h.y > 0.f ? -invB * w.y : 0.f;
+    o.z = h.z > 0.f ? -invB * w.z : 0.f; o.w = h.w > 0.f ? -invB * w.w : 0.f;
+    *reinterpret_cast<float4*>(p.dh2 + (long)m * H + c) = o;
+  }
 }
 
 hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s) {
@@ -399,6 +417,7 @@ hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s) {
+  if (a.dh2 && (!a.hn.h || (a.hn.H & 3))) return hipErrorInvalidValue;
   if (a.K > kMaxHeads || !head_ok(a.hn)) return hipErrorInvalidValue;
   OAC_LAUNCH(particle_min_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock), dim3(256), 0, s, a);
   return hipGetLastError();
