@@ -95,7 +95,7 @@ static int dphase0(SacPlan& p, int flags, hipStream_t s) {
   if (flags & OAC_STEP_GATHER) {
     GatherArgs g;
     std::memset(&g, 0, sizeof(g));
-    g.replay = p.b.replay; g.row_stride = RS; g.idx = p.b.idx_ring; g.ring_slots = p.b.ring_slots;
+    g.replay = p.b.replay; g.row_stride = RS; g.idx = gather_idx(p, flags); g.ring_slots = p.b.ring_slots;
     g.out = X; g.B = B;
     g.seed = c.seed; g.state = p.state();
     TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_gather(g, s)));
@@ -103,7 +103,7 @@ static int dphase0(SacPlan& p, int flags, hipStream_t s) {
   }
   if ((flags & (OAC_STEP_GATHER | OAC_STEP_COUNTS)) == (OAC_STEP_GATHER | OAC_STEP_COUNTS) &&
       p.b.counts) {   // ring path of a counts=True trainer: this draw's counts on the device
-    CountsStepArgs ca{p.b.counts, p.b.count_tags, p.b.count_epoch, p.b.idx_ring, p.b.ring_slots,
+    CountsStepArgs ca{p.b.counts, p.b.count_tags, p.b.count_epoch, gather_idx(p, flags), p.b.ring_slots,
                       p.state(), c.batch, p.W(OAC_WS_COUNTS)};
     TIMED(p, K_GATHER, s, OAC_HIP_CHECK(launch_counts_step(ca, s)));
     p.launches++;

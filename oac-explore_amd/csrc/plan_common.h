@@ -40,6 +40,11 @@ struct PlanBase {
   // indices from it (no H2D copy, no gather launch); the chunk's completion
   // event is recorded at the next staging call, behind the step that read it
   bool rows_direct = false;
+  // host-read mode (the plan's own ring, not rows_direct: the large-batch SAC
+  // step and the particle / det trainers): an oac_sac_step_host_idx step's
+  // gather (and counts) launch reads the slot straight from the host ring
+  // (kStepHostIdx), so no H2D copy precedes the step's graph
+  bool idx_host = false;
   bool owns_host_ring = false;
   int pending_ev = -1;
   // per-launch small-GEMM geometry overrides (tuning experiments: env

@@ -98,6 +98,13 @@ inline void fuse_adam(GemmBatch& gb, const AdamArgs& a, int nseg, const long* of
   for (int i = 0; i < nseg; ++i) { gb.seg_off[i] = off[i]; gb.seg_n[i] = n[i]; }
 }
 
+// internal step flag (not in oac_amd.h): this step's indices are in the host
+// ring slot (PlanBase::idx_host), read there by the gather / counts launch
+constexpr int kStepHostIdx = 1 << 12;
+inline const int* gather_idx(const SacPlan& p, int flags) {
+  return ((flags & kStepHostIdx) && p.host_ring) ? p.host_ring : p.b.idx_ring;
+}
+
 // Large-batch single-process step (split-K slabs, no fused epilogue Adam):
 // each group's Adam runs as side workgroups of a later GEMM launch that reads
 // none of the updated parameters (GemmBatch::side_adam) instead of its own

@@ -143,7 +143,7 @@ static int gather_steps(SacPlan& p, int flags, int n, hipStream_t s) {
   const int B = c.batch, Da = c.act_dim;
   GatherArgs g;
   std::memset(&g, 0, sizeof(g));
-  g.replay = p.b.replay; g.row_stride = c.row_stride; g.idx = p.b.idx_ring; g.ring_slots = p.b.ring_slots;
+  g.replay = p.b.replay; g.row_stride = c.row_stride; g.idx = gather_idx(p, flags); g.ring_slots = p.b.ring_slots;
   g.out = p.W(OAC_WS_BATCH); g.B = (flags & OAC_STEP_GATHER) ? B : 0;
   g.n_steps = n; g.out_stride = (long)B * c.row_stride; g.eps_stride = (long)B * Da;
   if (flags & OAC_STEP_DEVICE_EPS) {
@@ -785,6 +785,7 @@ int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
   p.host_ring = nullptr;
   p.owns_host_ring = false;
   p.rows_direct = false;
+  p.idx_host = false;
   if (!pinned_ring) {   // the plan's own host-coherent ring
     int32_t* r = nullptr;
     OAC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&r), sizeof(int32_t) * (size_t)p.b.ring_slots * p.c.batch,
@@ -794,6 +795,8 @@ int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
     p.owns_host_ring = true;
     p.rows_direct = p.cfg == 0 && dropin_direct_on() && !has_target_policy(p.c.kind) &&
                     p.c.kind != OAC_KIND_PARTICLE;   // sac_plan's run_step / phase0 only
+    static const bool hostidx_on = [] { const char* e = getenv("OAC_HOSTIDX"); return !e || atoi(e) != 0; }();
+    p.idx_host = !p.rows_direct && hostidx_on;
     // not direct (large batch): the copy path still stages through this ring
     if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
     if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
@@ -805,7 +808,9 @@ int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
 
 int32_t* oac_sac_host_ring(oac_sac* h) { return h ? h->plan.host_ring : nullptr; }
 
-int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream) {
+// host_read: the step that follows reads the slot from the host ring (no H2D
+// copy); its chunk event is recorded behind that step, at the next staging call
+static int stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream, bool host_read) {
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
   if (!p.host_ring) { set_error("oac_sac_set_host_ring first"); return 1; }
@@ -813,7 +818,7 @@ int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* str
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   const int B = p.c.batch, S = p.b.ring_slots;
   const int slot = (int)(bc % S), ch = slot / kRingChunk;
-  if (p.rows_direct && p.pending_ev >= 0) {   // behind the step that read the chunk's last slot
+  if (p.pending_ev >= 0) {   // behind the step that read the chunk's last slot
     OAC_HIP_CHECK(hipEventRecord(p.ring_ev[p.pending_ev], s));
     p.ring_ev_set[p.pending_ev] = 1;
     p.pending_ev = -1;
@@ -831,7 +836,7 @@ int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* str
     }
     dst[i] = (int32_t)v;
   }
-  if (p.rows_direct) {   // the layer-0 launch reads the slot from host memory
+  if (host_read) {   // the step's first launch reads the slot from host memory
     if (slot % kRingChunk == kRingChunk - 1 || slot == S - 1) p.pending_ev = ch;
     return 0;
   }
@@ -844,9 +849,16 @@ int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* str
   return 0;
 }
 
+int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream) {
+  return stage_host_idx(h, idx, bc, stream, h && h->plan.rows_direct);
+}
+
 int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags, void* stream) {
-  if (oac_sac_stage_host_idx(h, idx, bc, stream)) return 1;
-  return oac_sac_step_n(h, flags | OAC_STEP_GATHER | OAC_STEP_USE_GRAPH, 1, stream);
+  if (!h) { set_error("null handle"); return 1; }
+  const bool hr = h->plan.idx_host;
+  if (stage_host_idx(h, idx, bc, stream, hr || h->plan.rows_direct)) return 1;
+  return oac_sac_step_n(h, flags | OAC_STEP_GATHER | OAC_STEP_USE_GRAPH | (hr ? kStepHostIdx : 0), 1,
+                        stream);
 }
 
 int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
