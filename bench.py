@@ -647,6 +647,9 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     if dp:
+        # the captured step graphs hold RCCL kernels: release them while the
+        # communicator is alive
+        tr.release_graphs()
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
 

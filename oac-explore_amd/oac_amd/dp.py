@@ -115,6 +115,14 @@ class _DataParallel:
             for t in (self.params, self.targets, self.alpha_state):
                 dist.broadcast(t, src=0, group=process_group)
 
+    def release_graphs(self):
+        """Drop the captured step graphs (they hold RCCL kernels of this
+        process group's communicator): call before destroy_process_group."""
+        torch.cuda.synchronize(self.device)
+        self._graphs.clear()
+        self._eager_seen.clear()
+        torch.cuda.synchronize(self.device)
+
     def _make_cfg(self, batch):
         c = super()._make_cfg(batch)
         c.world_size = self.world
