@@ -597,10 +597,10 @@ def main():
     out = None
     if rank == 0:
         roof = roofline_of(kt, FLOP_PER_SAMPLE, B, args.timing_steps)
-        # B >= 1024: per-launch choice among gemm_big_kernel (forward),
-        # gemm_grouped_kernel (backward) and gemm_small_kernel (narrow)
+        # B >= 1024: per-launch choice among gemm_fwd_kernel (forward),
+        # gemm_bwdp_kernel (backward) and gemm_small_kernel (narrow products)
         roof["kernel"] = ("gemm_small_kernel" if B < 1024 else
-                          "gemm launches (gemm_big/gemm_grouped/gemm_small)")
+                          "gemm launches (gemm_fwd / gemm_bwdp / gemm_small)")
         out = {
             "metric": "OAC gradient steps/sec, Humanoid-v2 dims, batch 256, 1->8 MI355X",
             "value": round(value, 2),
