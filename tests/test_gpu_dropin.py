@@ -80,3 +80,64 @@ def test_dropin_rejects_out_of_range_indices():
     bad = DeviceBatch(ra, host_indices=np.full(B, N + 5, dtype=np.int64))
     with pytest.raises(RuntimeError, match="outside the replay"):
         a.train(bad)
+
+
+# ------------------------------------------------ host-read index ring
+# The drop-in step of the large-batch SAC plan and of the particle / g-oac
+# trainers reads its indices straight from the pinned host ring in the gather
+# launch (oac_sac_step_host_idx, PlanBase::idx_host): no H2D copy before the
+# step graph.  It must equal the device-index path bit for bit across the
+# staging ring's wrap-around.
+def _kind_trainer(kind, dropin):
+    from fixtures_lib import goac_params
+    from gpu_helpers import producers, Space
+    Hh = 32
+    if kind == "sac_large":
+        from oac_amd import SACTrainer
+        pp, qp = producers(sac_params(Do, Da, [Hh, Hh], 3, pi_init_w=0.2, q_init_w=0.1))
+        tr = SACTrainer(pp, qp, action_space=Space(Da), discount=0.99, reward_scale=1.0,
+                        policy_lr=1e-3, qf_lr=1e-3, soft_target_tau=5e-3, device="cuda:0", seed=7)
+    elif kind == "goac":
+        from oac_amd import GaussianTrainer
+        from test_gpu_goac import goac_producers
+        pp, qp = goac_producers(goac_params(Do, Da, [Hh, Hh], 3, 0.0, 100.0, pi_init_w=0.2,
+                                            q_init_w=0.1))
+        tr = GaussianTrainer(pp, qp, action_space=Space(Da), policy_lr=1e-3, qf_lr=1e-3,
+                             soft_target_tau=5e-3, q_min=0.0, q_max=100.0, share_layers=True)
+    else:
+        from oac_amd import ParticleTrainerOAC
+        K = 5
+        pp, qp = producers(sac_params(Do, Da, [Hh, Hh], 3, q_out=K, pi_init_w=0.2,
+                                      q_last_bias=np.linspace(0.0, 50.0, K)),
+                           q_keys=("qf1", "qf2", "target_qf1", "target_qf2", "qf1", "target_qf1"))
+        tr = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Space(Da), policy_lr=1e-3,
+                                qf_lr=1e-3, soft_target_tau=5e-3, use_automatic_entropy_tuning=True,
+                                deterministic=False, q_min=0.0, q_max=50.0, share_layers=True)
+    tr._no_dropin = not dropin
+    return tr
+
+
+@pytest.mark.parametrize("kind", ["sac_large", "poac", "goac"])
+def test_host_read_dropin_equals_device_index_path(kind):
+    from oac_amd import ReplayBuffer
+    from gpu_helpers import Space
+    Bk, Nk, steps = (1024, 3000, 136) if kind == "sac_large" else (B, N, 140)
+
+    def run(dropin):
+        tr = _kind_trainer(kind, dropin)
+        rb = ReplayBuffer(Nk, Space(Do), Space(Da), device="cuda:0")
+        d = synthetic_transitions(Nk, Do, Da, seed=1)
+        rb.add_paths([dict(observations=d["observations"], actions=d["actions"],
+                           rewards=d["rewards"], next_observations=d["next_observations"],
+                           terminals=d["terminals"])])
+        np.random.seed(3)
+        for _ in range(steps):
+            batch = rb.random_batch(Bk)
+            batch["buffer"] = rb
+            tr.train(batch)
+        return tr
+    a, b = run(True), run(False)
+    assert a._n_train_steps_total == b._n_train_steps_total == steps
+    sa, sb = _state(a), _state(b)
+    assert np.isfinite(sa).all()
+    assert np.array_equal(sa, sb)
