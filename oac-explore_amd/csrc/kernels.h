@@ -202,6 +202,10 @@ struct ParticleTargetArgs {
   const float* q; const float* tq;      // [B, K] critic / target critic outputs
   RowHead th;                           // th.h set: tq computed here (into th.out)
   RowHead qh;                           // qh.h set: q computed here (into qh.out)
+  // dh2 set (needs qh.h): the critic backward into its last hidden layer,
+  // dh2[r, n] = [h2[r, n] > 0] sum_k dq[r, k] W_last[k, n] (h2 = qh.h,
+  // W_last = qh.w, n < qh.H): the rank-K dX launch it replaces
+  float* dh2;
   const float* batch; long ld_batch; int off_rew, off_term;
   float reward_scale, discount;
   int B, K;
@@ -239,6 +243,10 @@ struct GaussTargetArgs {
   const float* q; const float* tq;      // [B, 2] Q(obs, a), Q_target(next_obs, a') raw outputs
   RowHead th;                           // th.h set: tq computed here (into th.out)
   RowHead qh;                           // qh.h set: q computed here (into qh.out)
+  // dh2 set (needs qh.h): the critic backward into its last hidden layer,
+  // dh2[r, n] = [h2[r, n] > 0] sum_k dq[r, k] W_last[k, n] (h2 = qh.h,
+  // W_last = qh.w, n < qh.H): the rank-K dX launch it replaces
+  float* dh2;
   const float* batch; long ld_batch; int off_rew, off_term;
   float reward_scale, discount, std_init;
   float soft_prob;                      // std_soft_update_prob, < 0: off

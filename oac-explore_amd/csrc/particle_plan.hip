@@ -12,6 +12,7 @@
 //   -> min_K Q_new(obs, a~) [286-292] -> Adam(pi) [295-300] -> Polyak [320-324]
 // The policy forward on obs uses the pre-step policy (it is only updated at
 // the end), so it runs in the first forward stage with everything else.
+#include <cstdlib>
 #include <cstring>
 
 #include "../../include/oac_amd.h"
@@ -64,6 +65,13 @@ void particle_layout_workspace(SacPlan& p) {
 }
 
 // ------------------------------------------------------------------ phases
+// the critic's backward into its last hidden layer inside the targets kernel
+// (rank-K dX of the K-output head; OAC_DH2_TARGETS=0 keeps its GEMM launch)
+static bool dh2_in_targets(const SacPlan& p) {
+  static const bool v = [] { const char* e = getenv("OAC_DH2_TARGETS"); return !e || atoi(e) != 0; }();
+  return v && (p.c.hidden & 3) == 0;
+}
+
 static int pphase0(SacPlan& p, int flags, hipStream_t s) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
@@ -159,6 +167,7 @@ static int pphase1(SacPlan& p, int flags, hipStream_t s, bool split = false) {
     std::memset(&a, 0, sizeof(a));
     a.th = RowHead{p.W(X_H2T), tq + L.q_last_w, tq + L.q_last_b, p.W(OAC_WS_TQ1), H};
     a.qh = RowHead{p.W(X_H2Q), q + L.q_last_w, q + L.q_last_b, p.W(OAC_WS_Q1), H};
+    if (dh2_in_targets(p)) a.dh2 = p.W(X_DH2Q);   // the rank-K dX launch, folded
     a.q = p.W(OAC_WS_Q1); a.tq = p.W(OAC_WS_TQ1); a.batch = X; a.ld_batch = RS;
     a.off_rew = c.off_rew; a.off_term = c.off_term; a.reward_scale = c.reward_scale;
     a.discount = c.discount; a.B = B; a.K = K;
@@ -168,14 +177,20 @@ static int pphase1(SacPlan& p, int flags, hipStream_t s, bool split = false) {
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_particle_targets(a, s)));
     p.launches++;
   }
-  {  // last layer: dW_last slab and dh2 = (dq . W_last) * [h2 > 0]
-    GemmBatch gb{};
+  // last layer: dW_last slab and dh2 = (dq . W_last) * [h2 > 0]; with dh2
+  // from the targets kernel, dW_last rides in the layer-0 dW launch
+  const bool fold = dh2_in_targets(p);
+  GemmTask tl;
+  {
     float* gq = grad_q(p);
-    GemmTask tl = t_dw(p.W(X_DQ), K, K, B, p.W(X_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
-                 q_group(p), p.sp_ql);
+    tl = t_dw(p.W(X_DQ), K, K, B, p.W(X_H2Q), H, H, gq + L.q_last_w, gq + L.q_last_b,
+              q_group(p), p.sp_ql);
     // train_bias=False: no ones column, the frozen bias keeps a zero gradient
     // (Adam then leaves it, and its moments, exactly unchanged)
     if (c.freeze_q_bias) { tl.N = H; tl.b_ones = 0; tl.bias_grad = nullptr; }
+  }
+  if (!fold) {
+    GemmBatch gb{};
     add(gb, tl);
     add(gb, t_dx(p.W(X_DQ), K, B, K, q + L.q_last_w, H, H, p.W(X_DH2Q), H, p.W(X_H2Q), H));
     if (run_gemm(p, gb, s)) return 1;
@@ -193,6 +208,10 @@ static int pphase1(SacPlan& p, int flags, hipStream_t s, bool split = false) {
     float* gq = grad_q(p);
     add(gb, t_dw(p.W(X_DH1Q), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_fc0_w, gq + L.q_fc0_b,
                  q_group(p), p.sp_q0));
+    // the last layer's dW (M = K rows) beside the layer-0 dW (B=4096: 7.9 us,
+    // fewest workgroups of the backward launches; in the layer-1 launch it
+    // added 5.8 us)
+    if (fold) add(gb, tl);
     if (split) {   // the critic's layer 1 + last layer beside its layer-0 dW
       const long off[1] = {(long)L.q_fc1_w};
       const long n[1] = {(long)(L.q_size - L.q_fc1_w)};

@@ -268,8 +268,9 @@ __device__ __forceinline__ void row_heads(const RowHead& hd, int K, int B, int r
   }
 }
 
-__global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArgs p) {
-  __shared__ RowHeadLds hs, qs;
+__device__ __forceinline__ void particle_targets_rows(const ParticleTargetArgs& p, RowHeadLds& hs,
+                                                      RowHeadLds& qs,
+                                                      float (&sdq)[kRowBlock][kMaxHeads]) {
   const int r0 = blockIdx.x * kRowBlock, r = r0 + threadIdx.x;
   const int K = p.K;
   if (p.th.h) {
@@ -341,10 +342,40 @@ __global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArg
   for (int i = 0; i < kMaxHeads; ++i) {
     if (i < K) {
       const float d = q[i] - y[i];
+      const float g = __fmul_rn(g2 * d, invB);
       p.y[(long)r * K + i] = y[i];
       p.sqe[(long)r * K + i] = d * d;
-      p.dq[(long)r * K + qi[i]] = __fmul_rn(g2 * d, invB);
+      p.dq[(long)r * K + qi[i]] = g;
+      if (p.dh2) sdq[threadIdx.x][qi[i]] = g;
     }
+  }
+}
+
+// the targets kernel's row logic, then (p.dh2) the 16 rows' backward into
+// the last hidden layer by the whole block
+__global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArgs p) {
+  __shared__ RowHeadLds hs, qs;
+  __shared__ float sdq[kRowBlock][kMaxHeads];
+  const int r0 = blockIdx.x * kRowBlock;
+  particle_targets_rows(p, hs, qs, sdq);
+  if (!p.dh2) return;
+  __syncthreads();
+  const int K = p.K, H = p.qh.H, n4 = H >> 2;
+  for (int e = threadIdx.x; e < kRowBlock * n4; e += 256) {
+    const int rr = e / n4, c = 4 * (e - rr * n4), m = r0 + rr;
+    if (m >= p.B) continue;
+    const float4 h = *reinterpret_cast<const float4*>(p.qh.h + (long)m * H + c);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < K; ++k) {   // k order, as the GEMM's accumulation
+      const float4 w = *reinterpret_cast<const float4*>(p.qh.w + (long)k * H + c);
+      const float g = sdq[rr][k];
+      a.x = fmaf(g, w.x, a.x); a.y = fmaf(g, w.y, a.y);
+      a.z = fmaf(g, w.z, a.z); a.w = fmaf(g, w.w, a.w);
+    }
+    float4 o;
+    o.x = h.x > 0.f ? a.x : 0.f; o.y = h.y > 0.f ? a.y : 0.f;
+    o.z = h.z > 0.f ? a.z : 0.f; o.w = h.w > 0.f ? a.w : 0.f;
+    *reinterpret_cast<float4*>(p.dh2 + (long)m * H + c) = o;
   }
 }
 
@@ -413,6 +444,7 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
 
 hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s) {
   if (a.K > kMaxHeads || !head_ok(a.th) || !head_ok(a.qh)) return hipErrorInvalidValue;
+  if (a.dh2 && (!a.qh.h || (a.qh.H & 3))) return hipErrorInvalidValue;
   OAC_LAUNCH(particle_targets_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock), dim3(256), 0, s, a);
   return hipGetLastError();
 }
