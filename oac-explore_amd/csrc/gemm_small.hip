@@ -270,27 +270,6 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   // the direct gather's row index (host memory, the longest wait of the
   // launch) is requested before anything else
   const int arow = (t.a_rows && rows) ? rows[min(m0 + (lane & 31), t.M - 1)] : -1;
-  // EPI_BIAS_RANK_RELU: the rank-R operands of the tile (U rows m0.., V rows
-  // n0..) requested now so their latency hides behind the k loop; a direct-
-  // gather U row comes through this wave's own row index (lane r holds
-  // rows[m0 + r]) instead of a second host-memory read in the epilogue
-  constexpr int kUV = 2;                  // registers per thread (32 R <= 128 NW; else loaded late)
-  const int uv_it = t.epi == EPI_BIAS_RANK_RELU ? (32 * t.R + 64 * NW - 1) / (64 * NW) : 0;
-  float upf[kUV], vpf[kUV];
-  if (uv_it > 0 && uv_it <= kUV) {
-#pragma unroll
-    for (int it = 0; it < kUV; ++it) {
-      if (it < uv_it) {
-        const int e = threadIdx.x + it * 64 * NW;
-        const int r = min(e / t.R, 31), j = e - (e / t.R) * t.R;
-        const int ur = __shfl(arow, r);   // every lane active: wave-uniform trip count
-        const int mr = min(m0 + r, t.M - 1);
-        const bool ok = e < 32 * t.R;
-        upf[it] = ok ? t.U[(long)(t.a_rows ? ur : mr) * t.ldu + j] : 0.f;
-        vpf[it] = ok ? t.V[(long)min(n0 + r, t.N - 1) * t.ldv + j] : 0.f;
-      }
-    }
-  }
 
   EpiIn xin[PER];
 #pragma unroll
@@ -330,23 +309,11 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   if (t.epi == EPI_BIAS_RANK_RELU) {   // stage the rank-R operands (reusing the LDS)
     __syncthreads();
     const int Rp = t.R | 1;
-    if (uv_it <= kUV) {   // prefetched before the k loop
-#pragma unroll
-      for (int it = 0; it < kUV; ++it) {
-        const int e = threadIdx.x + it * 64 * NW;
-        if (it < uv_it && e < 32 * t.R) {
-          const int r = e / t.R, j = e - r * t.R;
-          lds_u[r * Rp + j] = upf[it];
-          lds_v[r * Rp + j] = vpf[it];
-        }
-      }
-    } else {
-      for (int e = threadIdx.x; e < 32 * t.R; e += 64 * NW) {
-        const int r = e / t.R, j = e % t.R;
-        const int mr = min(m0 + r, t.M - 1);
-        lds_u[r * Rp + j] = t.U[(long)(t.a_rows ? rows[mr] : mr) * t.ldu + j];
-        lds_v[r * Rp + j] = t.V[(long)min(n0 + r, t.N - 1) * t.ldv + j];
-      }
+    for (int e = threadIdx.x; e < 32 * t.R; e += 64 * NW) {
+      const int r = e / t.R, j = e % t.R;
+      const int mr = min(m0 + r, t.M - 1);
+      lds_u[r * Rp + j] = t.U[(long)(t.a_rows ? rows[mr] : mr) * t.ldu + j];
+      lds_v[r * Rp + j] = t.V[(long)min(n0 + r, t.N - 1) * t.ldv + j];
     }
     __syncthreads();
   }

@@ -66,7 +66,54 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
   const int l16 = lane & 15, g4 = lane >> 4;
   STAGE(0);
 
-  // ---- 0. prefetch what steps 1-3 read besides the head GEMM operands
+  // ---- 1a. head GEMM operands of the first k-chunks, issued FIRST: vmcnt
+  // retires loads in issue order, so with the step-3 prefetch below issued
+  // ahead of them the head MFMAs waited for the whole 32-KB prefetch too
+  typedef float floatx4 __attribute__((ext_vector_type(4)));
+  floatx4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+  constexpr int ntile = NT;
+  const float* arow = sg.h2 + (long)min(m0 + l16, B - 1) * H;
+  const float* brow[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) brow[t] = wh + (long)min(t * 16 + l16, D2 - 1) * H;
+  const int chunks = (H + 15) >> 4;
+  constexpr int kC = 2;                         // k-chunks in flight per wave
+  f4u xa[kC], xb[kC][4];
+  // branch-free (clamped k): a branch between these loads and their MFMAs
+  // makes the waitcnt pass assume the fewest loads in flight of any path
+  auto head_loads = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < kC; ++j) {
+      const int kb = min(16 * (c0 + j * kHeadWaves) + 4 * g4, H - 4);
+      xa[j] = *reinterpret_cast<const f4u*>(arow + kb);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+        if (t < ntile) xb[j][t] = *reinterpret_cast<const f4u*>(brow[t] + kb);
+    }
+  };
+  auto head_mfma = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < kC; ++j)
+      if (c0 + j * kHeadWaves < chunks) {
+        const int kb = 16 * (c0 + j * kHeadWaves) + 4 * g4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const bool kin = kb + c < H;
+          const float av = kin ? xa[j][c] : 0.f;
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (t < ntile) {
+              const float bv = (kin && t * 16 + l16 < D2) ? xb[j][t][c] : 0.f;
+              acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
+            }
+        }
+      }
+  };
+  head_loads(wave);   // chunk past the end: clamped, its MFMAs skipped
+
+  // ---- 0. prefetch what steps 2-3 read besides the head GEMM operands
   const int cols = (H + a.col_chunks - 1) / a.col_chunks;
   const int n_lo = chunk * cols;
   const int tiles = (cols + 15) / 16;
@@ -83,65 +130,29 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
   constexpr int kPairs = KP;                     // pairs per wave prefetched
   float bw_pf[kPairs][KS], pre_pf[kPairs][4];
 #pragma unroll
-  for (int q = 0; q < kPairs; ++q) {
+  for (int q = 0; q < kPairs; ++q) {   // branch-free: a pair past the end reads wh[0]
     const int pi = wave + q * kHeadWaves;
-    if (pi < pairs) {
-      const int net = pi / tiles;
-      const int n = n_lo + (pi % tiles) * 16 + l16;
-      const bool nv = n < H && n < n_lo + cols;
-      const float* wrow = sg.wa[net] + (long)(nv ? n : 0) * a.ld_wa;
+    const bool pv = pi < pairs;
+    const int net = pv ? pi / tiles : 0;
+    const int n = n_lo + (pi % tiles) * 16 + l16;
+    const bool nv = pv && n < H && n < n_lo + cols;
+    const float* wrow = pv ? sg.wa[net] + (long)(nv ? n : 0) * a.ld_wa : wh;
+    const float* prow = pv ? sg.pre[net] + (nv ? n : 0) : wh;
+    const long pld = pv ? (long)H : 0;
 #pragma unroll
-      for (int st = 0; st < KS; ++st) bw_pf[q][st] = wrow[min(4 * st + g4, Da - 1)];
+    for (int st = 0; st < KS; ++st) bw_pf[q][st] = wrow[pv ? min(4 * st + g4, Da - 1) : 0];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        pre_pf[q][r] = sg.pre[net][(long)min(m0 + 4 * g4 + r, B - 1) * H + (nv ? n : 0)];
-    }
+    for (int r = 0; r < 4; ++r) pre_pf[q][r] = prow[(long)min(m0 + 4 * g4 + r, B - 1) * pld];
   }
 
   STAGE_DRAIN(5);
-  // ---- 1. heads [mean | ls_raw] for 16 rows: up to 4 column tiles of 16
-  typedef float floatx4 __attribute__((ext_vector_type(4)));
-  floatx4 acc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
-  constexpr int ntile = NT;
-  {
-    const float* arow = sg.h2 + (long)min(m0 + l16, B - 1) * H;
-    const float* brow[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t) brow[t] = wh + (long)min(t * 16 + l16, D2 - 1) * H;
-    const int chunks = (H + 15) >> 4;
-    constexpr int kC = 2;                         // k-chunks in flight per wave
+  // ---- 1b. heads [mean | ls_raw] for 16 rows: up to 4 column tiles of 16
+  STAGE_DRAIN(6);
+  head_mfma(wave);
 #pragma unroll 1
-    for (int c0 = wave; c0 < chunks; c0 += kC * kHeadWaves) {
-      f4u xa[kC], xb[kC][4];
-#pragma unroll
-      for (int j = 0; j < kC; ++j)
-        if (c0 + j * kHeadWaves < chunks) {
-          const int kb = 16 * (c0 + j * kHeadWaves) + 4 * g4;
-          xa[j] = *reinterpret_cast<const f4u*>(arow + kb);
-#pragma unroll
-          for (int t = 0; t < 4; ++t)
-            if (t < ntile) xb[j][t] = *reinterpret_cast<const f4u*>(brow[t] + kb);
-        }
-      STAGE_DRAIN(6);
-#pragma unroll
-      for (int j = 0; j < kC; ++j)
-        if (c0 + j * kHeadWaves < chunks) {
-          const int kb = 16 * (c0 + j * kHeadWaves) + 4 * g4;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const bool kin = kb + c < H;
-            const float av = kin ? xa[j][c] : 0.f;
-#pragma unroll
-            for (int t = 0; t < 4; ++t)
-              if (t < ntile) {
-                const float bv = (kin && t * 16 + l16 < D2) ? xb[j][t][c] : 0.f;
-                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
-              }
-          }
-        }
-    }
+  for (int c0 = wave + kC * kHeadWaves; c0 < chunks; c0 += kC * kHeadWaves) {
+    head_loads(c0);
+    head_mfma(c0);
   }
   STAGE(1);
 #pragma unroll
