@@ -7,8 +7,8 @@ D=profiles/$R
 mkdir -p $D
 tail -1 gpurun_out/bench256.log > $D/bench_b256.json
 tail -1 gpurun_out/bench4096.log > $D/bench_b4096.json
-cp $(ls gpurun_out/prof_b256/*/*kernel_stats.csv) $D/b256_kernel_stats.csv
-cp $(ls gpurun_out/prof_b4096/*/*kernel_stats.csv) $D/b4096_kernel_stats.csv
+cp "$(ls -t gpurun_out/prof_b256/*/*kernel_stats.csv | head -1)" $D/b256_kernel_stats.csv
+cp "$(ls -t gpurun_out/prof_b4096/*/*kernel_stats.csv | head -1)" $D/b4096_kernel_stats.csv
 python3 tools/prof_summary.py gpurun_out/prof_b256 > $D/b256_gemm_avg.txt
 python3 tools/prof_summary.py gpurun_out/prof_b4096 > $D/b4096_gemm_avg.txt
 python3 tools/trace.py gpurun_out/prof_b256 ${NLAUNCH:-11} > $D/b256_step_trace.txt
