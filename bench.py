@@ -191,7 +191,7 @@ def ring_timing(tr, stream, rb, B, steps=640, n=64):
             "steps_per_launch": n}
 
 
-def poac_ant_leg(args, device, B=4096, steps=128, warmup=16, timing_steps=8):
+def poac_ant_leg(args, device, B=4096, steps=384, warmup=32, timing_steps=8):
     """BASELINE configs[4]: particle_trainer_oac.ParticleTrainer, K=10 shared
     critic heads, Ant-v2 dims (obs 111, act 8), 2x256, batch 4096, replay 1e6,
     on the drop-in loop."""
@@ -593,7 +593,7 @@ def main():
     if not args.no_extras and B != 4096:
         big = batch_leg("SAC/OAC trainer step, Humanoid-v2 dims, 2x256, batch 4096 per rank, "
                         "replay 1e6 (BASELINE configs[%d])" % (3 if world > 1 else 2),
-                        tr, rb, 4096, 96, 8, FLOP_PER_SAMPLE, world, device, rank=rank)
+                        tr, rb, 4096, 320, 32, FLOP_PER_SAMPLE, world, device, rank=rank)
     out = None
     if rank == 0:
         roof = roofline_of(kt, FLOP_PER_SAMPLE, B, args.timing_steps)
