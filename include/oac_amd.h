@@ -135,6 +135,9 @@ enum oac_ws_buffer {
   OAC_WS_Y, OAC_WS_SQE1, OAC_WS_SQE2, OAC_WS_QNEW,
   OAC_WS_COUNTS,                       /* [B] batch counts (ReplayBufferCount) for OAC_STEP_COUNTS */
   OAC_WS_HEAD3, OAC_WS_ACT3,           /* GAUSS, PARTICLE_UB: target_policy(obs) head and action */
+  OAC_WS_LOGP_PART,                    /* [ceil(B/16)] sum of (logp1 + target_entropy) per 16-row
+                                          block: the data-parallel alpha exchange (world_size > 1)
+                                          all-reduces this vector, the targets kernel sums it */
   OAC_WS_COUNT_PUBLIC
 };
 

@@ -65,6 +65,7 @@ void det_layout_workspace(SacPlan& p) {
   for (int id : {OAC_WS_Q1, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_Y, OAC_WS_SQE1}) set(id, B, K);
   set(OAC_WS_QNEW, B, 1);
   set(OAC_WS_COUNTS, B, 1);
+  set(OAC_WS_LOGP_PART, (B + 15) / 16, 1);
   for (int id = G_H1P; id <= G_H2T; ++id) set(id, B, H);
   for (int id : {G_DQ, G_GQ, G_GQ3}) set(id, B, K);
   for (int id : {G_DH2Q, G_DH1Q, G_PN, G_H1N, G_H2N, G_PN3, G_H1N3, G_H2N3, G_DH2N, G_DH1N,

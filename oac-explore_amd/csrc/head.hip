@@ -54,6 +54,7 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
   // one LDS array: reduction scratch, then the head tile and the actions
   constexpr int kRed = kHeadWaves * 4 * 4 * 64;   // waves x col tiles x regs x lanes
   __shared__ __attribute__((aligned(16))) float lds[kRed];
+  __shared__ float s_lp[kRows];   // per-row logp + te (HeadArgs::logp_part)
   const HeadSeg& sg = a.seg[blockIdx.y];
   const float* wh = sg.wh ? sg.wh : a.wh;
   const float* bh = sg.bh ? sg.bh : a.bh;
@@ -207,8 +208,16 @@ __global__ void __launch_bounds__(64 * kHeadWaves) policy_head_kernel(const Head
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) l += __shfl_xor(l, o, 32);
     if (j == 0 && m < B && chunk == 0 && !a.det) sg.logp[m] = l;
+    if (j == 0) s_lp[row] = m < B ? l + a.target_entropy : 0.f;
   }
   __syncthreads();
+  // data-parallel alpha: this row block's sum of (logp + te), rows in order
+  if (a.logp_part && blockIdx.y == 0 && chunk == 0 && !a.det && threadIdx.x == 0) {
+    float sum = 0.f;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) sum += s_lp[r];
+    a.logp_part[rb] = sum;
+  }
   STAGE(3);
 
   // ---- 3. critics' action columns: h1[m, n] = relu(P[m, n] + sum_j a[m, j] W[n, j])

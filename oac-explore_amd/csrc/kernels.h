@@ -64,6 +64,9 @@ struct HeadArgs {
   int B, H, Da;
   int col_chunks;                     // workgroups per 32-row block
   long long* stage_clock;             // tools/micro builds only (-DOAC_STAGE_CLOCK)
+  // non-null: segment 0's row blocks also write sum_rows (logp + te) of their
+  // 16 rows (rows in order) to logp_part[row block] (data-parallel alpha)
+  float* logp_part; float target_entropy;
 };
 hipError_t launch_policy_head(const HeadArgs& a, int nseg, hipStream_t s);
 
@@ -86,7 +89,8 @@ struct CriticTargetArgs {
   const float* logp1;                   // for the alpha gradient
   float target_entropy;
   double lr, beta1, beta2, adam_eps;    // alpha optimiser (policy_lr)
-  int world_size;                       // > 1: use alpha->sum (all-reduced)
+  int world_size;                       // > 1: use alpha->sum (all-reduced), or with
+  const float* logp_part; int n_logp_part;   // logp_part: the sum of these (all-reduced) partials
   float reward_scale, discount;
   int B;
   float* y; float* dq1; float* dq2; float* gq1; float* gq2; float* sqe1; float* sqe2;
@@ -231,6 +235,7 @@ struct ParticleMinArgs {
   // alpha update (same as CriticTargetArgs)
   AlphaState* alpha; const StepState* state; const float* logp; float target_entropy;
   double lr, beta1, beta2, adam_eps; int world_size;
+  const float* logp_part; int n_logp_part;   // world_size > 1: all-reduced partials (else alpha->sum)
 };
 hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s);
 hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s);

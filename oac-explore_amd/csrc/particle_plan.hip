@@ -49,6 +49,7 @@ void particle_layout_workspace(SacPlan& p) {
   for (int id : {OAC_WS_Q1, OAC_WS_QN1, OAC_WS_TQ1, OAC_WS_Y, OAC_WS_SQE1}) set(id, B, K);
   set(OAC_WS_QNEW, B, 1);
   set(OAC_WS_COUNTS, B, 1);
+  set(OAC_WS_LOGP_PART, (B + 15) / 16, 1);
   for (int id = X_H1P; id <= X_H2T; ++id) set(id, B, H);
   for (int id : {X_STD1, X_U1, X_STD2, X_U2, X_DA}) set(id, B, Da);
   set(X_DQ, B, K); set(X_GQ, B, K);
@@ -138,12 +139,10 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
     s1.act = p.W(OAC_WS_ACT2); s1.stdv = p.W(X_STD2); s1.u = p.W(X_U2); s1.logp = p.W(OAC_WS_LOGP2);
     s1.n_nets = 1;
     s1.wa[0] = tq + L.q_fc0_w + Do; s1.pre[0] = p.W(X_PT); s1.h1[0] = p.W(X_H1T);
+    if (c.world_size > 1 && c.auto_alpha) {   // the local alpha partials for the all-reduce
+      a.logp_part = p.W(OAC_WS_LOGP_PART); a.target_entropy = c.target_entropy;
+    }
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head(a, 2, s)));
-    p.launches++;
-  }
-  if (c.world_size > 1 && c.auto_alpha) {
-    LogpSumArgs a{p.W(OAC_WS_LOGP1), B, c.target_entropy, p.alpha()};
-    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_logp_sum(a, s)));
     p.launches++;
   }
   return 0;
@@ -255,6 +254,7 @@ static int pphase2(SacPlan& p, hipStream_t s, bool split = false) {
     a.alpha = c.auto_alpha ? p.alpha() : nullptr; a.state = p.state(); a.logp = p.W(OAC_WS_LOGP1);
     a.target_entropy = c.target_entropy; a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2;
     a.adam_eps = c.adam_eps; a.world_size = c.world_size;
+    if (c.world_size > 1) { a.logp_part = p.W(OAC_WS_LOGP_PART); a.n_logp_part = (B + 15) / 16; }
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_particle_min(a, s)));
     p.launches++;
   }

@@ -69,6 +69,24 @@ __device__ float block_logp_sum(const float* logp, int B, float te, float* red) 
   return sum;
 }
 
+// Data-parallel: the all-reduced per-row-block partials of the head launch
+// (HeadArgs::logp_part), summed by the whole block (one load per thread for
+// n <= blockDim, then the fixed tree of block_logp_sum); every block and
+// every thread gets the same value
+__device__ float block_part_sum(const float* part, int n, float* red) {
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  const float sum = red[0];
+  __syncthreads();
+  return sum;
+}
+
 // Data-parallel: local sum(logp + target_entropy) into alpha->sum (all-reduced
 // by the caller before phase 1).
 __global__ void __launch_bounds__(256) logp_sum_kernel(LogpSumArgs a) {
@@ -94,7 +112,9 @@ __global__ void __launch_bounds__(256) critic_targets_kernel(CriticTargetArgs p)
   if (p.alpha) {
     // every block computes the update identically; block 0 publishes next_*
     // (the critic Adam commits them), so no block reads what another writes
-    const float S = (p.world_size > 1) ? p.alpha->sum : logp_sum256(p.logp1, p.B, p.target_entropy, red);
+    const float S = (p.world_size > 1) ? (p.logp_part ? block_part_sum(p.logp_part, p.n_logp_part, red)
+                                                      : p.alpha->sum)
+                                       : logp_sum256(p.logp1, p.B, p.target_entropy, red);
     alpha = alpha_update(p, S, blockIdx.x == 0 && threadIdx.x == 0);
   }
   if (r >= p.B) return;
@@ -386,7 +406,8 @@ __global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArg
 __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
   __shared__ float red[256];
   if (p.alpha && blockIdx.x == 0) {
-    const float S = (p.world_size > 1) ? p.alpha->sum
+    const float S = (p.world_size > 1) ? (p.logp_part ? block_part_sum(p.logp_part, p.n_logp_part, red)
+                                                      : p.alpha->sum)
                                        : block_logp_sum(p.logp, p.B, p.target_entropy, red);
     if (threadIdx.x == 0) {
       AlphaState* as = p.alpha;

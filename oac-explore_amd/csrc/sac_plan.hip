@@ -87,6 +87,7 @@ static void layout_workspace(SacPlan& p) {
   for (int id : {OAC_WS_Q1, OAC_WS_Q2, OAC_WS_QN1, OAC_WS_QN2, OAC_WS_TQ1, OAC_WS_TQ2}) set(id, B, Q);
   for (int id : {OAC_WS_Y, OAC_WS_SQE1, OAC_WS_SQE2, OAC_WS_QNEW}) set(id, B, Q);
   set(OAC_WS_COUNTS, B, 1);   // unused by SAC (the reference SACTrainer ignores counts)
+  set(OAC_WS_LOGP_PART, (B + 15) / 16, 1);
   for (int id = W_H1P; id <= W_H2T2; ++id) set(id, B, H);
   for (int id : {W_STD1, W_U1, W_STD2, W_U2, W_DA1, W_DA2}) set(id, B, Da);
   for (int id : {W_DQ1, W_DQ2, W_GQ1, W_GQ2}) set(id, B, Q);
@@ -319,12 +320,10 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
     s1.n_nets = 2;
     s1.wa[0] = t1 + L.q_fc0_w + Do; s1.pre[0] = p.W(W_PT1); s1.h1[0] = p.W(W_H1T1);
     s1.wa[1] = t2 + L.q_fc0_w + Do; s1.pre[1] = p.W(W_PT2); s1.h1[1] = p.W(W_H1T2);
+    if (c.world_size > 1 && c.auto_alpha) {   // the local alpha partials for the all-reduce
+      a.logp_part = p.W(OAC_WS_LOGP_PART); a.target_entropy = c.target_entropy;
+    }
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_policy_head(a, 2, s)));
-    p.launches++;
-  }
-  if (c.world_size > 1 && c.auto_alpha) {  // local alpha partial for the all-reduce
-    LogpSumArgs a{p.W(OAC_WS_LOGP1), B, c.target_entropy, p.alpha()};
-    TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_logp_sum(a, s)));
     p.launches++;
   }
   return 0;
@@ -384,6 +383,7 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
     a.state = p.state(); a.logp1 = p.W(OAC_WS_LOGP1); a.target_entropy = c.target_entropy;
     a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.adam_eps = c.adam_eps;
     a.world_size = c.world_size;
+    if (c.world_size > 1) { a.logp_part = p.W(OAC_WS_LOGP_PART); a.n_logp_part = (B + 15) / 16; }
     a.reward_scale = c.reward_scale; a.discount = c.discount; a.B = B;
     a.y = p.W(OAC_WS_Y); a.dq1 = p.W(W_DQ1); a.dq2 = p.W(W_DQ2); a.gq1 = p.W(W_GQ1); a.gq2 = p.W(W_GQ2);
     a.sqe1 = p.W(OAC_WS_SQE1); a.sqe2 = p.W(OAC_WS_SQE2); a.qnew = p.W(OAC_WS_QNEW);

@@ -26,7 +26,7 @@ OAC_STEP_COUNTS = 8
 WS = {name: i for i, name in enumerate([
     "batch", "eps1", "eps2", "head1", "head2", "act1", "act2", "logp1", "logp2",
     "q1", "q2", "qn1", "qn2", "tq1", "tq2", "y", "sqe1", "sqe2", "qnew", "counts",
-    "head3", "act3"])}
+    "head3", "act3", "logp_part"])}
 
 
 class SacConfig(ctypes.Structure):

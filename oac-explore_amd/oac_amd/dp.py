@@ -7,7 +7,8 @@ this is the DP scheme the build adds.  Per step there are exactly three
 exchanges, at the points where the single-GPU step needs a whole-batch
 quantity, in the torch-1.4 order of trainer.py:139-210:
 
-  phase 0   forward, policy sample, local sum(logp + H)       -> all-reduce SUM (4 B)
+  phase 0   forward, policy sample, local sum(logp + H) as
+            per-16-row partials (the head launch)              -> all-reduce SUM (B/16 floats)
   phase 1   alpha update (global sum), TD target, critic grads -> all-reduce SUM (1.34 MB)
   phase 2   critic Adam (grads / world) + Polyak, policy grad
             through the post-step critics                       -> all-reduce SUM (0.68 MB)
@@ -78,7 +79,9 @@ class _GpuExecutor:
                                             _lib.stream_ptr(self.stream)))
 
     def alpha_sum(self):
-        return self.t.alpha_state[6:7]
+        # the head launch's per-16-row partials of sum(logp + target_entropy)
+        # (OAC_WS_LOGP_PART); the targets kernel sums the all-reduced vector
+        return self.plan.views["logp_part"].view(-1)
 
     def critic_grads(self):
         return self._crit
