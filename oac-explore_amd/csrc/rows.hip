@@ -288,18 +288,73 @@ __device__ __forceinline__ void row_heads(const RowHead& hd, int K, int B, int r
   }
 }
 
+// Two K-output heads of the same hidden width for the same 16 rows (the
+// targets kernel's target critic and critic): all loads of both issued
+// before the first MFMA, one LDS round.  Same per-head MFMA order as
+// row_heads.  H % 16 == 0 and H <= 256 (one k-batch per wave).
+__device__ __forceinline__ void row_heads2(const RowHead& h0, const RowHead& h1, int K, int B, int r0,
+                                           RowHeadLds& s0, RowHeadLds& s1) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int H = h0.H, chunks = H >> 4;
+  const long ra = (long)min(r0 + l16, B - 1) * H, rb = (long)min(l16, K - 1) * H;
+  const bool bv = l16 < K;
+  constexpr int kQ = 4;
+  f4a x0[kQ], w0[kQ], x1[kQ], w1[kQ];
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {   // unpredicated (clamped chunk): no branch before the MFMAs
+    const int kb = 16 * min(wave + 4 * q, chunks - 1) + 4 * g4;
+    x0[q] = *reinterpret_cast<const f4a*>(h0.h + ra + kb);
+    w0[q] = *reinterpret_cast<const f4a*>(h0.w + rb + kb);
+    x1[q] = *reinterpret_cast<const f4a*>(h1.h + ra + kb);
+    w1[q] = *reinterpret_cast<const f4a*>(h1.w + rb + kb);
+  }
+  floatx4 acc0 = floatx4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q)
+    if (wave + 4 * q < chunks) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x0[q][e], bv ? w0[q][e] : 0.f, acc0, 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x1[q][e], bv ? w1[q][e] : 0.f, acc1, 0, 0, 0);
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { s0.red[wave][r][lane] = acc0[r]; s1.red[wave][r][lane] = acc1[r]; }
+  __syncthreads();
+  const int r = threadIdx.x >> 6, l = threadIdx.x & 63;   // D reg r of lane l
+  const int row = 4 * (l >> 4) + r, col = l & 15;
+  if (col < K) {
+    const float v0 = ((s0.red[0][r][l] + s0.red[1][r][l]) + s0.red[2][r][l]) + s0.red[3][r][l];
+    const float v1 = ((s1.red[0][r][l] + s1.red[1][r][l]) + s1.red[2][r][l]) + s1.red[3][r][l];
+    const float o0 = v0 + h0.b[col], o1 = v1 + h1.b[col];
+    s0.out[row][col] = o0;
+    s1.out[row][col] = o1;
+    if (r0 + row < B) {
+      h0.out[(long)(r0 + row) * K + col] = o0;
+      h1.out[(long)(r0 + row) * K + col] = o1;
+    }
+  }
+}
+
 __device__ __forceinline__ void particle_targets_rows(const ParticleTargetArgs& p, RowHeadLds& hs,
                                                       RowHeadLds& qs,
                                                       float (&sdq)[kRowBlock][kMaxHeads]) {
   const int r0 = blockIdx.x * kRowBlock, r = r0 + threadIdx.x;
   const int K = p.K;
-  if (p.th.h) {
-    row_heads(p.th, K, p.B, r0, hs);
+  if (p.th.h && p.qh.h && p.th.H == p.qh.H && (p.th.H & 15) == 0 && p.th.H <= 256) {
+    row_heads2(p.th, p.qh, K, p.B, r0, hs, qs);   // both heads, loads issued together
     __syncthreads();
-  }
-  if (p.qh.h) {   // the critic's own last layer on (obs, a) (particle_trainer_oac.py:185-191)
-    row_heads(p.qh, K, p.B, r0, qs);
-    __syncthreads();
+  } else {
+    if (p.th.h) {
+      row_heads(p.th, K, p.B, r0, hs);
+      __syncthreads();
+    }
+    if (p.qh.h) {   // the critic's own last layer on (obs, a) (particle_trainer_oac.py:185-191)
+      row_heads(p.qh, K, p.B, r0, qs);
+      __syncthreads();
+    }
   }
   if (threadIdx.x >= kRowBlock || r >= p.B) return;
   const float fK = (float)K;
