@@ -245,33 +245,53 @@ __device__ __forceinline__ void row_heads(const RowHead& hd, int K, int B, int r
   const bool bv = l16 < K;
   floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
   const int chunks = (hd.H + 15) >> 4;
-  // up to 4 chunks per wave in flight (all of them for H <= 256): the loads
-  // of a batch are issued together, then its 16 MFMAs
-  constexpr int kQ = 4;
-#pragma unroll 1
-  for (int c0 = wave; c0 < chunks; c0 += 4 * kQ) {
-    float xa[kQ][4], xb[kQ][4];
+  if ((hd.H & 15) == 0 && hd.H <= 256) {
+    // one k-batch per wave, unpredicated (clamped chunk) loads: a per-lane
+    // branch between the loads and the MFMAs made them wait for every load
+    constexpr int kQ = 4;
+    f4a xa[kQ], xb[kQ];
 #pragma unroll
     for (int q = 0; q < kQ; ++q) {
-      const int kb = 16 * (c0 + 4 * q) + 4 * g4;
-      if (kb + 3 < hd.H) {
-        const f4a a = *reinterpret_cast<const f4a*>(arow + kb);
-        const f4a b = *reinterpret_cast<const f4a*>(brow + kb);
-        xa[q][0] = a.x; xa[q][1] = a.y; xa[q][2] = a.z; xa[q][3] = a.w;
-        xb[q][0] = b.x; xb[q][1] = b.y; xb[q][2] = b.z; xb[q][3] = b.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          xa[q][e] = kb + e < hd.H ? arow[kb + e] : 0.f;
-          xb[q][e] = kb + e < hd.H ? brow[kb + e] : 0.f;
-        }
-      }
+      const int kb = 16 * min(wave + 4 * q, chunks - 1) + 4 * g4;
+      xa[q] = *reinterpret_cast<const f4a*>(arow + kb);
+      xb[q] = *reinterpret_cast<const f4a*>(brow + kb);
     }
 #pragma unroll
     for (int q = 0; q < kQ; ++q)
+      if (wave + 4 * q < chunks) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[q][e], bv ? xb[q][e] : 0.f, acc, 0, 0, 0);
+        for (int e = 0; e < 4; ++e)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[q][e], bv ? xb[q][e] : 0.f, acc, 0, 0, 0);
+      }
+  } else {
+    // up to 4 chunks per wave in flight (all of them for H <= 256): the loads
+    // of a batch are issued together, then its 16 MFMAs
+    constexpr int kQ = 4;
+#pragma unroll 1
+    for (int c0 = wave; c0 < chunks; c0 += 4 * kQ) {
+      float xa[kQ][4], xb[kQ][4];
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) {
+        const int kb = 16 * (c0 + 4 * q) + 4 * g4;
+        if (kb + 3 < hd.H) {
+          const f4a a = *reinterpret_cast<const f4a*>(arow + kb);
+          const f4a b = *reinterpret_cast<const f4a*>(brow + kb);
+          xa[q][0] = a.x; xa[q][1] = a.y; xa[q][2] = a.z; xa[q][3] = a.w;
+          xb[q][0] = b.x; xb[q][1] = b.y; xb[q][2] = b.z; xb[q][3] = b.w;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            xa[q][e] = kb + e < hd.H ? arow[kb + e] : 0.f;
+            xb[q][e] = kb + e < hd.H ? brow[kb + e] : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kQ; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[q][e], bv ? xb[q][e] : 0.f, acc, 0, 0, 0);
+    }
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) sh.red[wave][r][lane] = acc[r];
