@@ -158,7 +158,7 @@ hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s) {
-  // 64 rows per block: the per-row work spreads over CUs (every block redoes
+  // 256 rows per block: the per-row work spreads over CUs (every block redoes
   // the 4-byte-per-row alpha reduction, which is cheap)
   OAC_LAUNCH(critic_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
   return hipGetLastError();
