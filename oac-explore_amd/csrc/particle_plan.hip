@@ -323,7 +323,10 @@ int particle_run_step(SacPlan& p, int flags, hipStream_t s) {
   // remaining Adam launches shrank by 0.5 us (4,336 -> 4,275 steps/s);
   // OAC_SPLIT_ADAM_POAC=1 turns it on
   static const bool poac_on = [] { const char* e = getenv("OAC_SPLIT_ADAM_POAC"); return e && atoi(e) != 0; }();
-  const bool split = poac_on && split_adam_on(p);
+  // (not with the last layer's dW in the layer-0 dW launch, dh2_in_targets:
+  // the side blocks would update the last layer while its gradient is
+  // still being written in the same launch)
+  const bool split = poac_on && split_adam_on(p) && !dh2_in_targets(p);
   if (pphase1(p, flags, s, split)) return 1;
   {
     AdamArgs a = critic_adam(p, 0, nullptr);   // alpha is updated after the critic step

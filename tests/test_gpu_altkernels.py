@@ -29,3 +29,27 @@ def test_alternative_large_batch_kernels_match_oracle(name):
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, f"{name}: rc {r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
     assert r.stdout.count("ok ") == 8, r.stdout
+
+
+def test_side_workgroup_adam_is_bitwise_the_adam_launch(tmp_path):
+    """Large-batch side-workgroup Adam (GemmBatch::side_adam; on for SAC, opt-in
+    for P-OAC) against one Adam launch per group, child processes: params,
+    targets and Adam moments bit for bit after three steps."""
+    import numpy as np
+    outs = {}
+    # P-OAC: the side path needs its last-layer dW out of the layer-0 dW
+    # launch (OAC_DH2_TARGETS=0); both runs use that launch layout
+    for name, env in {"side": {"OAC_SPLIT_ADAM": "1", "OAC_SPLIT_ADAM_POAC": "1",
+                               "OAC_DH2_TARGETS": "0"},
+                      "launch": {"OAC_SPLIT_ADAM": "0", "OAC_SPLIT_ADAM_POAC": "0",
+                                 "OAC_DH2_TARGETS": "0"}}.items():
+        out = str(tmp_path / f"{name}.npz")
+        r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "split_adam_check.py"), out],
+                           env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, f"{name}: rc {r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+        outs[name] = np.load(out)
+    a, b = outs["side"], outs["launch"]
+    assert sorted(a.files) == sorted(b.files) and len(a.files) == 16
+    for k in a.files:
+        assert np.isfinite(a[k]).all(), k
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
