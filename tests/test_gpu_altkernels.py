@@ -33,8 +33,9 @@ def test_alternative_large_batch_kernels_match_oracle(name):
 
 def test_side_workgroup_adam_is_bitwise_the_adam_launch(tmp_path):
     """Large-batch side-workgroup Adam (GemmBatch::side_adam; on for SAC, opt-in
-    for P-OAC) against one Adam launch per group, child processes: params,
-    targets and Adam moments bit for bit after three steps."""
+    for P-OAC) against one Adam launch per group, and the policy head's
+    column-chunk count, child processes: params, targets and Adam moments bit
+    for bit after three steps."""
     import numpy as np
     outs = {}
     # P-OAC: the side path needs its last-layer dW out of the layer-0 dW
@@ -42,14 +43,22 @@ def test_side_workgroup_adam_is_bitwise_the_adam_launch(tmp_path):
     for name, env in {"side": {"OAC_SPLIT_ADAM": "1", "OAC_SPLIT_ADAM_POAC": "1",
                                "OAC_DH2_TARGETS": "0"},
                       "launch": {"OAC_SPLIT_ADAM": "0", "OAC_SPLIT_ADAM_POAC": "0",
-                                 "OAC_DH2_TARGETS": "0"}}.items():
+                                 "OAC_DH2_TARGETS": "0"},
+                      # and the policy head on two 128-column chunks per row
+                      # block (recomputed heads, 2 pairs per wave): the same
+                      # arithmetic per output, so bitwise too
+                      "head_cc2": {"OAC_SPLIT_ADAM": "1", "OAC_SPLIT_ADAM_POAC": "1",
+                                   "OAC_DH2_TARGETS": "0", "OAC_HEAD_CC": "2"}}.items():
         out = str(tmp_path / f"{name}.npz")
         r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "split_adam_check.py"), out],
                            env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, f"{name}: rc {r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
         outs[name] = np.load(out)
-    a, b = outs["side"], outs["launch"]
-    assert sorted(a.files) == sorted(b.files) and len(a.files) == 16
-    for k in a.files:
-        assert np.isfinite(a[k]).all(), k
-        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    a = outs["side"]
+    assert len(a.files) == 16
+    for other in ("launch", "head_cc2"):
+        b = outs[other]
+        assert sorted(a.files) == sorted(b.files)
+        for k in a.files:
+            assert np.isfinite(a[k]).all(), k
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"{other}: {k}")
