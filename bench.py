@@ -28,6 +28,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "oac-explore_amd"))
 
 FLOP_PER_SAMPLE = 4_377_600        # algorithmic GEMM FLOPs per sample (SAC, Humanoid)
+# what the build's MFMAs execute per sample (SAC, Humanoid): the fresh-action
+# critics reuse the obs projection W0[:, :376] obs of Q(obs, a) / TQ(next_obs)
+# and add a rank-17 action update, so two 376 x 256 products per sample of the
+# 8d count are not executed (1,996,288 MAC against 2,188,800: 8.8 % fewer)
+EXEC_FLOP_PER_SAMPLE = 3_992_576
 FLOP_PER_SAMPLE_POAC_ANT = 1_792_512   # P-OAC K=10, Ant dims
 GATHER_BYTES_PER_SAMPLE = 3_081 + 4
 ADAM_BYTES_PER_STEP = 18_142_244
@@ -154,18 +159,96 @@ def dropin_run(tr, rb, B):
     return run
 
 
-def roofline_of(kt, flop_per_sample, B, n, traffic_key=None):
+def roofline_of(kt, flop_per_sample, B, n, traffic_key=None, exec_flop_per_sample=None):
+    """The dominant kernel family's roofline: ALGORITHMIC flops per launch
+    (SURVEY 8d per-sample figure x samples per step / GEMM launches per step)
+    over the average launch duration measured live with dispatch events
+    (kernel_timing: the begin->end interval of each launch, as rocprofv3's
+    kernel trace reports it; the same command under rocprofv3 is committed
+    in profiles/)."""
     gk = kt["gemm_grouped"]
     fpl = flop_per_sample * B * n / max(gk["launches"], 1)
     ach = fpl / (gk["avg_us"] * 1e-6) / 1e12
-    return {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4),
-            "traffic": load_traffic(traffic_key or B), "flops_per_launch": round(fpl),
-            "avg_launch_us": round(gk["avg_us"], 3), "launches_per_step": gk["launches"] / n}
+    out = {"bound": "mfma", "achieved": round(ach, 3), "peak": PEAK_FP32_TFLOPS,
+           "unit": "TFLOP/s", "frac": round(ach / PEAK_FP32_TFLOPS, 4),
+           "traffic": load_traffic(traffic_key or B), "flops_per_launch": round(fpl),
+           "avg_launch_us": round(gk["avg_us"], 3), "launches_per_step": gk["launches"] / n,
+           "duration_source": "hipExtLaunchKernel dispatch events, %d steps" % n}
+    if exec_flop_per_sample:
+        out["executed_flops_per_launch"] = round(exec_flop_per_sample * B * n / max(gk["launches"], 1))
+        out["note"] = ("numerator = SURVEY 8d algorithmic GEMM FLOPs; the MFMAs execute %.1f %% fewer "
+                       "(obs projections reused by the fresh-action critics)"
+                       % (100.0 * (1 - exec_flop_per_sample / flop_per_sample)))
+    return out
+
+
+def hbm_legs(kt, B, n):
+    """SURVEY 8d HBM sub-roofline of the step's own gather launches (the
+    materialised replay gather: B x (3,085 read + 3,081 written) bytes per
+    launch), from the same dispatch events as the GEMM roofline."""
+    out = {}
+    ga = kt["gather"]
+    if ga["launches"]:
+        gb = (GATHER_BYTES_PER_SAMPLE + 3_081) * B * n / ga["launches"]
+        rate = gb / (ga["avg_us"] * 1e-6) / 1e9
+        out["gather"] = {"GBps": round(rate, 1), "bytes_per_launch": round(gb),
+                         "avg_launch_us": round(ga["avg_us"], 3), "launches_per_step": ga["launches"] / n,
+                         "frac_of_hbm_peak": round(rate / PEAK_HBM_GBS, 4)}
+    return out
+
+
+def standalone_hbm(rb, device, B=4096, reps=50):
+    """SURVEY 8d "sub-kernels measured separately against HBM": the replay
+    gather (oac_replay_gather of B random rows of the resident 1e6-row replay,
+    B x (3,085 + 3,081) algorithmic bytes) and one SAC step's Adam + Polyak
+    (oac_adam_polyak over the critics' 333,826 parameters with their targets
+    and the policy's 171,043 without: 18,142,244 bytes), each as `reps`
+    back-to-back launches between torch events on the launching stream (so a
+    launch's time includes its share of the launch boundaries)."""
+    from oac_amd import _lib
+    L = _lib.lib()
+    sp = _lib.stream_ptr()
+    rs = np.random.RandomState(5)
+    idx = torch.from_numpy(rs.randint(0, rb._storage.shape[0], B).astype(np.int32)).to(device)
+    out = torch.empty(B, rb._storage.shape[1], device=device)
+
+    def ev_time(fn):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        b.synchronize()
+        return a.elapsed_time(b) * 1e3 / reps   # us per call
+
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    us_g = ev_time(lambda: _lib.check(L.oac_replay_gather(p(rb._storage), rb._storage.shape[1], p(idx),
+                                                          B, p(out), sp)))
+    nq, npol = 333_826, 171_043
+    bufs = [torch.zeros(n, device=device) for n in (nq, nq, nq, nq, nq, npol, npol, npol, npol)]
+    state = torch.zeros(16, dtype=torch.int64, device=device)
+    qp, qg, qm, qv, qt, pp_, pg, pm, pv = bufs
+
+    def adam():
+        _lib.check(L.oac_adam_polyak(p(qp), p(qg), p(qm), p(qv), nq, p(qt), 5e-3, 1, 3e-4, 0.9, 0.999,
+                                     1e-8, p(state), 0, sp))
+        _lib.check(L.oac_adam_polyak(p(pp_), p(pg), p(pm), p(pv), npol, None, 5e-3, 1, 3e-4, 0.9, 0.999,
+                                     1e-8, p(state), 1, sp))
+    us_a = ev_time(adam)
+    gbytes = (GATHER_BYTES_PER_SAMPLE + 3_081) * B
+    return {"gather": {"B": B, "bytes": gbytes, "us": round(us_g, 3),
+                       "GBps": round(gbytes / us_g / 1e3, 1),
+                       "frac_of_hbm_peak": round(gbytes / us_g / 1e3 / PEAK_HBM_GBS, 4)},
+            "adam_polyak": {"bytes": ADAM_BYTES_PER_STEP, "us": round(us_a, 3), "launches": 2,
+                            "GBps": round(ADAM_BYTES_PER_STEP / us_a / 1e3, 1),
+                            "frac_of_hbm_peak": round(ADAM_BYTES_PER_STEP / us_a / 1e3 / PEAK_HBM_GBS, 4)},
+            "method": "%d back-to-back launches between torch events on the launching stream" % reps}
 
 
 def batch_leg(name, tr, rb, B, steps, warmup, flop_per_sample, world, device, timing_steps=8,
-              rank=0, seed=101, traffic_key=None):
+              rank=0, seed=101, traffic_key=None, exec_flop_per_sample=None):
     """The drop-in loop at another batch size on the same trainer (every rank
     steps: at world > 1 this is the data-parallel step), with its own
     kernel timing and roofline."""
@@ -173,10 +256,93 @@ def batch_leg(name, tr, rb, B, steps, warmup, flop_per_sample, world, device, ti
     el = timed(dropin_run(tr, rb, B), steps, warmup, world, device)
     kt = kernel_timing(tr, rb, B, timing_steps)
     v = world * steps / el
-    return {"workload": name, "steps_per_s": round(v, 1), "ms_per_step": round(1e3 * el / steps, 4),
-            "samples_per_s": round(v * B, 1), "batch_per_rank": B, "steps": steps,
-            "step_roofline_frac": round(flop_per_sample * B * v / world / 1e12 / PEAK_FP32_TFLOPS, 4),
-            "roofline": roofline_of(kt, flop_per_sample, B, timing_steps, traffic_key)}
+    out = {"workload": name, "steps_per_s": round(v, 1), "ms_per_step": round(1e3 * el / steps, 4),
+           "samples_per_s": round(v * B, 1), "batch_per_rank": B, "steps": steps,
+           "step_roofline_frac": round(flop_per_sample * B * v / world / 1e12 / PEAK_FP32_TFLOPS, 4),
+           "roofline": roofline_of(kt, flop_per_sample, B, timing_steps, traffic_key,
+                                   exec_flop_per_sample),
+           "kernels": {k: {kk: round(vv, 4) if isinstance(vv, float) else vv for kk, vv in d.items()}
+                       for k, d in kt.items()}}
+    out.update(hbm_legs(kt, B, timing_steps))
+    return out
+
+
+def launch_breakdown(tr, rb, B, n=20, seed=4321):
+    """Per-launch device durations (us, median over n drop-in steps) of the
+    trainer's step, in issue order, with the kind of each launch (direct
+    launches with dispatch events; collectives are not kernels of the plan)."""
+    from oac_amd import _lib
+    capture = getattr(tr, "capture", None)
+    if capture is not None:
+        tr.capture = False
+    st = np.random.get_state()
+    np.random.seed(seed)
+    tr.train(rb.random_batch(B))
+    plan = tr._last_plan
+    L = _lib.lib()
+    torch.cuda.synchronize()
+    _lib.check(L.oac_sac_set_timing(plan.handle, 1))
+    ms = (ctypes.c_double * 4)()
+    cnt = (ctypes.c_int64 * 4)()
+    _lib.check(L.oac_sac_read_timing(plan.handle, ms, cnt, 4))   # reset
+    for _ in range(n):
+        tr.train(rb.random_batch(B))
+    torch.cuda.synchronize()
+    cap = 64 * n
+    t = (ctypes.c_double * cap)()
+    k = (ctypes.c_int * cap)()
+    m = L.oac_sac_read_launch_times(plan.handle, t, k, cap)
+    _lib.check(L.oac_sac_read_timing(plan.handle, ms, cnt, 4))
+    _lib.check(L.oac_sac_set_timing(plan.handle, 0))
+    np.random.set_state(st)
+    if capture is not None:
+        tr.capture = capture
+    per = m // n if m > 0 else 0
+    if per == 0:
+        return {}
+    arr = np.array(t[:per * n]).reshape(n, per) * 1e3
+    names = ["gemm", "row", "adam", "gather"]
+    return {"launches_per_step": per, "sum_us": round(float(np.median(arr, 0).sum()), 2),
+            "us": [round(float(x), 2) for x in np.median(arr, 0)],
+            "kinds": [names[k[i]] for i in range(per)]}
+
+
+def dp1_leg(args, rb, device, B, single_value, steps=640, warmup=64):
+    """The data-parallel step at ONE rank over RCCL (an in-process process
+    group of world size 1): the phase split, the separate critic / policy Adam
+    launches and the three all-reduces captured into the step graph, on the
+    same drop-in loop and replay as the headline -- what the DP structure
+    costs before any link latency."""
+    import datetime
+    import torch.distributed as dist
+    if dist.is_initialized():
+        return None
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=device,
+                            timeout=datetime.timedelta(seconds=120))
+    try:
+        import oac_amd
+        from oac_amd.dp import DataParallelSACTrainer
+        torch.manual_seed(0)
+        hid = [args.hidden, args.hidden]
+        pp = oac_amd.get_policy_producer(args.obs_dim, args.act_dim, hid, device=device)
+        qp = oac_amd.get_q_producer(args.obs_dim, args.act_dim, hid, device=device)
+        with DataParallelSACTrainer(pp, qp, action_space=Space(args.act_dim), discount=0.99,
+                                    reward_scale=1.0, policy_lr=3e-4, qf_lr=3e-4,
+                                    soft_target_tau=5e-3, target_update_period=1,
+                                    use_automatic_entropy_tuning=True, device=device, seed=2,
+                                    gemm_cfg=args.gemm_cfg) as tr:
+            np.random.seed(1)
+            el = timed(dropin_run(tr, rb, B), steps, warmup, 1, device)
+            assert torch.isfinite(tr.params).all().item(), "non-finite DP parameters"
+            lb = launch_breakdown(tr, rb, B)
+        v = steps / el
+        return {"steps_per_s": round(v, 1), "ms_per_step": round(1e3 * el / steps, 4),
+                "vs_single_process": round(v / single_value, 4), "batch": B, "steps": steps,
+                "backend": "nccl (RCCL), world_size 1", "launches": lb}
+    finally:
+        dist.destroy_process_group()
 
 
 def ring_timing(tr, stream, rb, B, steps=640, n=64):
@@ -260,10 +426,12 @@ def cpu_threads_all():
     return (min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n), n
 
 
-def cpu_baseline(args, runs=5, steps=150):
+def cpu_baseline(args, runs=5, steps=100, warmup=20, min_s=2.0):
     """The oracle's PyTorch-CPU restatement of the reference step (incl. the
-    host numpy gather + fp32 conversion), timed on this host's cores: median
-    of `runs` runs of `steps` steps at 1 thread (the reference launcher's
+    host numpy gather + fp32 conversion), timed on this host's cores with
+    BASELINE.md section 3's procedure, bounded: 20 warm-up steps, then the
+    median of `runs` runs of at least `steps` steps and at least `min_s`
+    seconds each, at 1 thread (the reference launcher's
     torch.set_num_threads(1), launcher_util.py:90) and at all cores."""
     sys.path.insert(0, ROOT)
     from oracle import sac_oracle as so
@@ -289,20 +457,23 @@ def cpu_baseline(args, runs=5, steps=150):
 
     def median_rate(threads):
         torch.set_num_threads(threads)
-        for _ in range(3):
+        for _ in range(warmup):
             step()
         rates = []
         for _ in range(runs):
+            k = 0
             t0 = time.perf_counter()
-            for _ in range(steps):
+            while k < steps or time.perf_counter() - t0 < min_s:
                 step()
-            rates.append(steps / (time.perf_counter() - t0))
+                k += 1
+            rates.append(k / (time.perf_counter() - t0))
         return float(np.median(rates)), [round(r, 2) for r in rates]
     one, one_runs = median_rate(1)
     T, aff = cpu_threads_all()
     allc, all_runs = median_rate(T)
     torch.set_num_threads(1)
-    sample = (f"median of {runs} runs x {steps} oracle SAC steps (Humanoid dims, 2x256, B={B}, "
+    sample = (f"{warmup} warm-up steps, then median of {runs} runs of >= {steps} steps and "
+              f">= {min_s:g} s of oracle SAC steps (Humanoid dims, 2x256, B={B}, "
               f"numpy f64 replay of {n} rows, torch CPU fp32)")
     return dict(value=round(one, 2), unit="grad-steps/s", cores=1, kind="port",
                 sample=sample + ", 1 thread", runs=one_runs,
@@ -342,15 +513,15 @@ def recipe_cpu_baseline(kind, args, steps=200):
         b["counts"] = counts[idx][:, None].copy()
         np.add.at(counts, np.unique(idx), 1)
         orc.step(b)
-    for _ in range(3):
+    for _ in range(20):
         step()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     dt = time.perf_counter() - t0
     return dict(value=round(steps / dt, 2), unit="grad-steps/s", cores=1, kind="port",
-                sample=f"{steps} oracle {kind} steps (Humanoid dims, 2x256, B={B}, counts, "
-                       f"torch CPU fp32, 1 thread)")
+                sample=f"20 warm-up steps, then {steps} oracle {kind} steps (Humanoid dims, 2x256, "
+                       f"B={B}, counts, torch CPU fp32, 1 thread)")
 
 
 def exploration_timing(tr, obs_dim, reps=200):
@@ -460,12 +631,36 @@ def _free_port():
     return port
 
 
+def visible_gpu_count():
+    """GPUs a rank would see, counted without the HIP runtime (the launcher
+    process must not initialise the GPU): the KFD topology's GPU nodes (a
+    nonzero simd_count), narrowed by ROCR_ / HIP_ / CUDA_VISIBLE_DEVICES.  An
+    unreadable topology falls back to torch.cuda.device_count()."""
+    import glob
+    n = 0
+    for path in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            with open(path) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    if n == 0:
+        return torch.cuda.device_count()
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip()]))
+    return n
+
+
 def launch_ranks(n, argv=None):
     """``bench.py --gpus N`` without a launcher: start N rank processes of this
     script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment,
-    rendezvous on 127.0.0.1) and return the worst exit code.  The parent never
-    touches the GPU (no torch.cuda call), so the ranks start on a clean
-    device; a rank that fails takes the others down."""
+    rendezvous on 127.0.0.1) and return the worst exit code.  The parent makes
+    no HIP call (the device count comes from the KFD topology), so the ranks
+    start on a clean device; a rank that fails takes the others down."""
     import subprocess
     argv = sys.argv[1:] if argv is None else argv
     port = _free_port()
@@ -512,9 +707,10 @@ def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # started as `python bench.py --gpus N` (no torchrun): become the launcher
+        ngpu = visible_gpu_count() if not args.selftest_launcher else args.gpus
         if not args.selftest_launcher and os.environ.get("OAC_BENCH_SAME_DEVICE") != "1" \
-                and torch.cuda.device_count() < args.gpus:
-            print(f"bench.py --gpus {args.gpus}: only {torch.cuda.device_count()} GPU(s) visible "
+                and ngpu < args.gpus:
+            print(f"bench.py --gpus {args.gpus}: only {ngpu} GPU(s) visible "
                   "(OAC_BENCH_SAME_DEVICE=1 OAC_BENCH_BACKEND=gloo rehearses N ranks on one GPU)",
                   file=sys.stderr)
             sys.exit(2)
@@ -537,10 +733,14 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         backend = os.environ.get("OAC_BENCH_BACKEND", "nccl")
+        # a finite timeout: a stuck collective ends the rank (non-zero exit)
+        # instead of running into the driver's limit
+        import datetime
+        tmo = datetime.timedelta(seconds=int(os.environ.get("OAC_BENCH_PG_TIMEOUT", "300")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
     B = args.batch
@@ -599,10 +799,12 @@ def main():
     if not args.no_extras and B != 4096:
         big = batch_leg("SAC/OAC trainer step, Humanoid-v2 dims, 2x256, batch 4096 per rank, "
                         "replay 1e6 (BASELINE configs[%d])" % (3 if world > 1 else 2),
-                        tr, rb, 4096, 320, 32, FLOP_PER_SAMPLE, world, device, rank=rank)
+                        tr, rb, 4096, 320, 32, FLOP_PER_SAMPLE, world, device, rank=rank,
+                        exec_flop_per_sample=EXEC_FLOP_PER_SAMPLE)
     out = None
     if rank == 0:
-        roof = roofline_of(kt, FLOP_PER_SAMPLE, B, args.timing_steps)
+        roof = roofline_of(kt, FLOP_PER_SAMPLE, B, args.timing_steps,
+                           exec_flop_per_sample=EXEC_FLOP_PER_SAMPLE)
         # B >= 1024: per-launch choice among gemm_fwd_kernel (forward),
         # gemm_bwdp_kernel (backward) and gemm_small_kernel (narrow products)
         roof["kernel"] = ("gemm_small_kernel" if B < 1024 else
@@ -634,14 +836,17 @@ def main():
         }
         if big is not None:
             out["b4096"] = big
-        ga, ad = kt["gather"], kt["adam"]
-        if ga["launches"]:
-            out["gather_GBps"] = round(GATHER_BYTES_PER_SAMPLE * B / (ga["avg_us"] * 1e-6) / 1e9, 1)
-        if ad["launches"]:
-            out["adam_GBps"] = round(ADAM_BYTES_PER_STEP * args.timing_steps / (ad["ms"] * 1e-3) / 1e9, 1)
+        out.update(hbm_legs(kt, B, args.timing_steps))
         if world == 1 and not args.no_extras:
+            out["launches"] = launch_breakdown(tr, rb, B)
+            out["hbm_subkernels"] = standalone_hbm(rb, device)
             if args.mode == "dropin":
                 out["ring"] = ring_timing(tr, stream, rb, B)
+                if not dp:
+                    try:
+                        out["dp1"] = dp1_leg(args, rb, device, B, value)
+                    except Exception as e:   # the headline stands without this leg
+                        out["dp1"] = {"error": repr(e)[:300]}
             out["exploration"] = exploration_timing(tr, args.obs_dim)
             out["poac_ant_b4096"] = poac_ant_leg(args, device)
             rbc = count_replay(args, device)
@@ -653,9 +858,9 @@ def main():
             out["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(out), flush=True)
     if dp:
-        # the captured step graphs hold RCCL kernels: release them while the
-        # communicator is alive
-        tr.release_graphs()
+        # the trainer's teardown (its captured step graphs hold RCCL kernels),
+        # then the process group
+        tr.close()
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
 

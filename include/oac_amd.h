@@ -185,8 +185,11 @@ int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags,
  * runs its phases and all-reduces on the same stream) */
 int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream);
 /* data-parallel split (config.world_size > 1): phase 0 = forward through the
- * policy sample and the local sum(logp + target_entropy) into alpha_state[6];
- * 1 = alpha update from the caller's all-reduced sum through the critic
+ * policy sample and the local sum(logp + target_entropy) as per-16-row
+ * partials into the workspace buffer OAC_WS_LOGP_PART (ceil(B / 16) floats):
+ * with auto-alpha on and world_size > 1 that vector is what the caller
+ * all-reduces (SUM) before phase 1 (the targets kernel adds its entries);
+ * 1 = alpha update from the caller's all-reduced partials through the critic
  * gradients (reduced into the grads arena); 2 = critic Adam + Polyak (after
  * the caller's critic-grad all-reduce, averaged) through the policy gradient
  * (grads arena); 3 = policy Adam + step advance (after the policy-grad

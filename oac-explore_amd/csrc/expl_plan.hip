@@ -105,6 +105,7 @@ static ExplFusedArgs expl_args(ExplPlan& p, const float* eps, float beta, float 
   a.nq = p.q2 ? 2 : 1; a.K = p.K;
   a.eps = eps; a.out = w + p.o_out; a.grad = w + p.o_grad;
   a.state = p.state; a.ticket = reinterpret_cast<unsigned*>(w + p.o_cnt);
+  a.fail = reinterpret_cast<unsigned*>(w + p.o_cnt + 1);
   a.seed = p.seed; a.beta_UB = beta; a.sqrt_2delta = (float)std::sqrt(2.0 * (double)delta);
   a.ub_index = p.ub_index;
   a.stage_clock = p.stage_clock;
@@ -155,16 +156,17 @@ static inline void cpu_relax() {
 #endif
 }
 
-// spin on the completion word; every ~4k polls ask the stream whether it
+// spin on the completion word (bits 0-30: the call's sequence number, bit 31:
+// a hand-off of the call timed out); every ~4k polls ask the stream whether it
 // failed (or finished without writing the word)
 static int expl_wait(ExplPlan& p, unsigned seq, hipStream_t s) {
   volatile unsigned* f = p.hc_done;
   unsigned polls = 0;
-  while (*f != seq) {
+  while ((*f & 0x7fffffffu) != seq) {
     cpu_relax();
     if ((++polls & 4095) == 0) {
       const hipError_t e = hipStreamQuery(s);
-      if (e == hipSuccess && *f != seq) {
+      if (e == hipSuccess && (*f & 0x7fffffffu) != seq) {
         set_error("exploration: the launch finished without its completion word");
         return 1;
       }
@@ -175,6 +177,11 @@ static int expl_wait(ExplPlan& p, unsigned seq, hipStream_t s) {
     }
   }
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  if (*f & 0x80000000u) {
+    set_error("exploration: an in-launch hand-off timed out (the workgroups of an observation's "
+              "group were not co-resident); the results are NaN");
+    return 1;
+  }
   return 0;
 }
 
@@ -333,7 +340,12 @@ int oac_expl_action_now(oac_expl* h, const float* eps, float beta_UB, float delt
   a.obs = p.hc_obs;
   a.out = p.hc_out;
   const bool split = expl_split_on() && !p.stage_clock;
-  if (split) { a.done = p.hc_done; a.done_seq = ++p.seq; }
+  if (split) {
+    p.seq = (p.seq + 1) & 0x7fffffffu;   // bit 31 of the word is the failure flag
+    if (p.seq == 0) p.seq = 1;           // 0 is the word's initial value
+    a.done = p.hc_done;
+    a.done_seq = p.seq;
+  }
   if (expl_launch(p, a, s)) return 1;
   if (!split) {   // the one-workgroup kernel (A/B runs, stage clocks) has no completion word
     OAC_HIP_CHECK(hipStreamSynchronize(s));

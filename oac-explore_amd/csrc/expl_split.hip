@@ -378,10 +378,14 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
     a.out[2 * nd + e] = sd;
     if (a.grad) a.grad[e] = g;
   }
+  // a timed-out hand-off of this group is reported through the call's fail
+  // word (and so through the completion word below)
+  if (t == 0 && !ok && a.fail)
+    __hip_atomic_fetch_or(a.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // the Philox counter advances once per call and the completion word (host
   // polling, oac_expl_action_now) is written once per call: the last group to
   // finish does both
-  if (!a.eps || a.done) {
+  if (!a.eps || a.done || a.fail) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (t == 0) {
@@ -393,10 +397,16 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         if (!a.eps) a.state->expl_counter = cnt_s + 1;
         __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned failed = 0;
+        if (a.fail) {   // every group's report precedes its ticket (release / acquire above)
+          failed = __hip_atomic_load(a.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.fail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (a.done) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          __hip_atomic_store(a.done, a.done_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(a.done, a.done_seq | (failed ? 0x80000000u : 0u), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
         }
       }
     }
@@ -423,7 +433,20 @@ size_t expl_split_lds_bytes(int Do, int Da, int H) {
   return sizeof(float) * expl_split_lds(Do, Da, H, 1024);
 }
 
-// group size for a launch of n_rows observations: the chip's 256 CUs shared
+// compute units of the current device (read once per process: one device per
+// process, as the trainer is built)
+int expl_device_cus() {
+  static const int v = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n < 1)
+      return 1;   // unknown: one workgroup per observation, no hand-offs
+    return n;
+  }();
+  return v;
+}
+
+// group size for a launch of n_rows observations: the device's CUs shared
 // out, at most kExplGroup (OAC_EXPL_GROUP overrides the cap: tuning runs)
 int expl_split_group(int n_rows) {
   static const int cap = [] {
@@ -431,7 +454,7 @@ int expl_split_group(int n_rows) {
     const int v = e ? atoi(e) : kExplGroup;
     return v < 1 ? 1 : (v > 64 ? 64 : v);
   }();
-  const int g = 256 / (n_rows < 1 ? 1 : n_rows);
+  const int g = expl_device_cus() / (n_rows < 1 ? 1 : n_rows);
   return g < 1 ? 1 : (g > cap ? cap : g);
 }
 
@@ -443,7 +466,8 @@ hipError_t launch_expl_split(const ExplFusedArgs& a, int row0, int n_rows, float
   const int nt = expl_split_threads();
   const int G = expl_split_group(n_rows);
   const long lds = expl_split_lds(a.Do, a.Da, a.H, nt);
-  const bool wt = G > 1 && (long)n_rows * G <= 256 && lds <= kWtLdsFloats;
+  // write-through hand-offs need every workgroup of the launch on a CU of its own
+  const bool wt = G > 1 && (long)n_rows * G <= expl_device_cus() && lds <= kWtLdsFloats;
   if (wt) {
     OAC_LAUNCH(oac_expl_split_kernel<true>, dim3(n_rows * G), dim3(nt), 0, s, a, row0, G, scratch);
   } else {

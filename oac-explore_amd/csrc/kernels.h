@@ -125,7 +125,10 @@ struct ExplFusedArgs {                  // expl_fused.hip: one workgroup per obs
   int ub_index;                         // K heads: >= 0 -> Q_UB = sorted head ub_index
                                         // (trainer.predict, particle_trainer_oac.py:147-167)
   long long* stage_clock;               // instrumentation (tools/expl_latency.py) or null
-  unsigned* done; unsigned done_seq;    // expl_split.hip: completion word (host-polled) or null
+  unsigned* done; unsigned done_seq;    // expl_split.hip: completion word (host-polled) or null;
+                                        // bit 31 of the word set: a hand-off of the call timed out
+  unsigned* fail;                       // zeroed device word: a group's timed-out hand-off (re-armed
+                                        // by the kernel that reports it)
 };
 size_t expl_fused_lds_bytes(int Do, int Da, int H);
 hipError_t launch_expl_fused(const ExplFusedArgs& a, hipStream_t s);

@@ -31,10 +31,14 @@ struct PlanBase {
   hipStream_t cap_stream = nullptr;   // capture stream (graphs launch on the caller's stream)
   int launches = 0;
   // drop-in host-index staging (oac_sac_set_host_ring): pinned [slots][B] int32,
-  // one completion event per 16-slot chunk
+  // one completion event per 16-slot chunk, recorded when staging leaves the
+  // chunk (behind every step enqueued so far, so behind all of the chunk's
+  // readers) and waited on when staging enters it again; last_bc is the
+  // batch counter of the previous staging call (-1: none since the ring was set)
   int32_t* host_ring = nullptr;
   std::vector<hipEvent_t> ring_ev;
   std::vector<char> ring_ev_set;
+  int64_t last_bc = -1;
   // direct mode (oac_sac_set_host_ring(NULL)): the ring is the plan's own
   // host-coherent allocation and the small-batch layer-0 launch reads the
   // indices from it (no H2D copy, no gather launch); the chunk's completion
@@ -46,7 +50,6 @@ struct PlanBase {
   // (kStepHostIdx), so no H2D copy precedes the step's graph
   bool idx_host = false;
   bool owns_host_ring = false;
-  int pending_ev = -1;
   // per-launch small-GEMM geometry overrides (tuning experiments: env
   // OAC_TUNE="launch:nw:gpw,..." read at plan creation; 0 = automatic)
   int tune_nw[64] = {0}, tune_gpw[64] = {0};

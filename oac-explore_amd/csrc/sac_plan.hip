@@ -780,7 +780,7 @@ int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
     p.ring_ev.push_back(e);
   }
   p.ring_ev_set.assign(nch, 0);
-  p.pending_ev = -1;
+  p.last_bc = -1;
   if (p.owns_host_ring && p.host_ring) (void)hipHostFree(p.host_ring);
   p.host_ring = nullptr;
   p.owns_host_ring = false;
@@ -809,22 +809,39 @@ int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
 int32_t* oac_sac_host_ring(oac_sac* h) { return h ? h->plan.host_ring : nullptr; }
 
 // host_read: the step that follows reads the slot from the host ring (no H2D
-// copy); its chunk event is recorded behind that step, at the next staging call
+// copy), else an H2D copy on the stream reads it.  Either way a slot's readers
+// are enqueued on `stream` after its staging call, so the event recorded at
+// the first staging call outside a chunk follows all of that chunk's readers;
+// entering the chunk again (one lap later) waits for it.  A batch counter that
+// does not advance by one (another path of the trainer stepped in between, or
+// a restore) drains every reader enqueued so far: the slots are then all free.
 static int stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream, bool host_read) {
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
   if (!p.host_ring) { set_error("oac_sac_set_host_ring first"); return 1; }
   if (bc < 0) { set_error("bad batch counter %lld", (long long)bc); return 1; }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  const int B = p.c.batch, S = p.b.ring_slots;
-  const int slot = (int)(bc % S), ch = slot / kRingChunk;
-  if (p.pending_ev >= 0) {   // behind the step that read the chunk's last slot
-    OAC_HIP_CHECK(hipEventRecord(p.ring_ev[p.pending_ev], s));
-    p.ring_ev_set[p.pending_ev] = 1;
-    p.pending_ev = -1;
+  const int B = p.c.batch, S = p.b.ring_slots, nch = S / kRingChunk;
+  const int slot = (int)(bc % S);
+  const int64_t chunk = bc / kRingChunk;   // absolute: a wrap onto the same slots is a new chunk
+  const int ch = (int)(chunk % nch);
+  if (p.last_bc >= 0) {
+    const int64_t last_chunk = p.last_bc / kRingChunk;
+    const int lch = (int)(last_chunk % nch);
+    if (bc != p.last_bc + 1) {
+      OAC_HIP_CHECK(hipEventRecord(p.ring_ev[lch], s));
+      OAC_HIP_CHECK(hipEventSynchronize(p.ring_ev[lch]));
+      std::fill(p.ring_ev_set.begin(), p.ring_ev_set.end(), 0);
+    } else if (chunk != last_chunk) {
+      OAC_HIP_CHECK(hipEventRecord(p.ring_ev[lch], s));
+      p.ring_ev_set[lch] = 1;
+    }
+    if (chunk != last_chunk && p.ring_ev_set[ch]) {
+      OAC_HIP_CHECK(hipEventSynchronize(p.ring_ev[ch]));
+      p.ring_ev_set[ch] = 0;
+    }
   }
-  // first slot of a chunk: the copies that read this chunk S steps ago are done
-  if (slot % kRingChunk == 0 && p.ring_ev_set[ch]) OAC_HIP_CHECK(hipEventSynchronize(p.ring_ev[ch]));
+  p.last_bc = bc;
   int32_t* dst = p.host_ring + (long)slot * B;
   const int64_t rows = p.b.replay_rows;
   for (int i = 0; i < B; ++i) {
@@ -836,16 +853,9 @@ static int stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stre
     }
     dst[i] = (int32_t)v;
   }
-  if (host_read) {   // the step's first launch reads the slot from host memory
-    if (slot % kRingChunk == kRingChunk - 1 || slot == S - 1) p.pending_ev = ch;
-    return 0;
-  }
+  if (host_read) return 0;   // the step's first launch reads the slot from host memory
   OAC_HIP_CHECK(hipMemcpyAsync(const_cast<int32_t*>(p.b.idx_ring) + (long)slot * B, dst,
                                sizeof(int32_t) * B, hipMemcpyHostToDevice, s));
-  if (slot % kRingChunk == kRingChunk - 1 || slot == S - 1) {
-    OAC_HIP_CHECK(hipEventRecord(p.ring_ev[ch], s));
-    p.ring_ev_set[ch] = 1;
-  }
   return 0;
 }
 

@@ -87,7 +87,7 @@ def _batch_actions(agent, obs, optimistic_exploration, kwargs, deterministic_pol
         if eps is not None:
             eps = np.asarray(eps, np.float32)
             if eps.ndim == 1:
-                eps = np.broadcast_to(eps, (n, eps.shape[0]))
+                eps = np.tile(eps, (n, 1))   # writable (torch.from_numpy of a view warns)
         kw.pop("deterministic", None)
         A, _ = get_optimistic_exploration_actions(obs, eps=eps, **kw)
         return A, [{} for _ in range(n)]

@@ -454,7 +454,8 @@ class ParticleOACOracle:
         self.n_steps += 1
         self.last = dict(grads=dict(policy=gp, qf=gq, log_alpha=g_la), qf_losses=losses,
                          qf_loss=losses.sum(), policy_loss=policy_loss, alpha=alpha,
-                         alpha_loss=alpha_loss, sorted_qs=sorted_qs, y=y)
+                         alpha_loss=alpha_loss, sorted_qs=sorted_qs, y=y, tq=tq,
+                         policy_mean=pf["mean"], policy_log_std=pf["log_std"])
         return self.last
 
 
@@ -486,7 +487,7 @@ class GaussianOACOracle:
     def __init__(self, params, obs_dim, act_dim, delta=0.95, q_min=0.0, q_max=100.0,
                  discount=0.99, reward_scale=1.0, policy_lr=3e-4, qf_lr=3e-4, tau=5e-3,
                  target_update_period=1, std_soft_update_prob=None, mean_update=False,
-                 train_bias=True, dtype=torch.float32):
+                 train_bias=True, next_policy=None, dtype=torch.float32):
         from scipy.stats import norm
         self.mean_update = mean_update
         self.train_bias = train_bias
@@ -494,6 +495,10 @@ class GaussianOACOracle:
         self.Do, self.Da = obs_dim, act_dim
         self.P = to_torch_params(params["policy"], dtype)
         self.TP = to_torch_params(params["target_policy"], dtype)
+        # use_target_policy (gaussian_trainer.py:154-158, particle_trainer.py:
+        # 150-154): the DDPG target network acts on next_obs; its soft update
+        # copies it onto itself (:385-387), so its weights never change
+        self.NP = None if next_policy is None else to_torch_params(next_policy, dtype)
         self.Q = to_torch_params(params["qf1"], dtype)
         self.T = to_torch_params(params["target_qf1"], dtype)
         self.z = float(norm.ppf(delta, loc=0, scale=1))          # gaussian_trainer.py:69
@@ -511,6 +516,14 @@ class GaussianOACOracle:
         self.phase1()
         self.phase2()
         return self.phase3()
+
+    def _next_policy(self):
+        """The policy acting on next_obs: target_policy with mean_update, else
+        the DDPG target network with use_target_policy, else the policy
+        (gaussian_trainer.py:194-205, particle_trainer.py:194-205)."""
+        if self.mean_update:
+            return self.TP
+        return self.NP if self.NP is not None else self.P
 
     @staticmethod
     def _flat(grads, order):
@@ -539,8 +552,7 @@ class GaussianOACOracle:
         B = S["B"] = obs.shape[0]
         c = S["c"] = q_forward(obs, act, self.Q)                     # :187
         q_preds, std_preds = c["q"][:, :1], torch.exp(c["q"][:, 1:2])
-        pf2 = policy_forward(nobs, self.TP if self.mean_update else self.P, None,
-                             deterministic=True)                      # :192-202
+        pf2 = policy_forward(nobs, self._next_policy(), None, deterministic=True)   # :192-202
         tq = q_forward(nobs, pf2["a"], self.T)["q"]                  # :204
         tq0, tstd = tq[:, :1], torch.exp(tq[:, 1:2])
         std_target = (1. - term) * self.discount * tstd              # :213
@@ -615,12 +627,12 @@ class ParticleUBOracle(GaussianOACOracle):
     def __init__(self, params, obs_dim, act_dim, K, delta_index, q_min=0.0, q_max=100.0,
                  discount=0.99, reward_scale=1.0, policy_lr=1e-3, qf_lr=1e-3, tau=5e-3,
                  target_update_period=1, std_soft_update_prob=None, mean_update=False,
-                 rescale=False, train_bias=True, dtype=torch.float32):
+                 rescale=False, train_bias=True, next_policy=None, dtype=torch.float32):
         super().__init__(params, obs_dim, act_dim, q_min=q_min, q_max=q_max, discount=discount,
                          reward_scale=reward_scale, policy_lr=policy_lr, qf_lr=qf_lr, tau=tau,
                          target_update_period=target_update_period,
                          std_soft_update_prob=std_soft_update_prob, mean_update=mean_update,
-                         train_bias=train_bias, dtype=dtype)
+                         train_bias=train_bias, next_policy=next_policy, dtype=dtype)
         self.K, self.delta_index = K, delta_index
         self.spread = (q_max - q_min) if rescale else None
 
@@ -636,8 +648,7 @@ class ParticleUBOracle(GaussianOACOracle):
         c = S["c"] = q_forward(obs, act, self.Q)                     # :190-195
         qs = c["q"].t()                                              # [K, B]
         sorted_qs, qs_idx = torch.sort(qs, dim=0)                    # :196
-        pf2 = policy_forward(nobs, self.TP if self.mean_update else self.P, None,
-                             deterministic=True)                      # :197-207
+        pf2 = policy_forward(nobs, self._next_policy(), None, deterministic=True)   # :197-207
         tq = q_forward(nobs, pf2["a"], self.T)["q"].t()              # :211-214
         tq_sorted, _ = torch.sort(tq, dim=0)                         # :215
         y = self.reward_scale * rew.t() + (1. - term.t()) * self.discount * tq_sorted   # :219-220

@@ -195,7 +195,7 @@ def _record_batch(rb, B):
 def gen_sac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=7,
             pi_init_w=1e-3, q_init_w=3e-3, auto_alpha=True, log_alpha0=0.0,
             discount=0.99, reward_scale=1.0, tau=5e-3, lr=3e-4, idx_seed=1,
-            eps_seed=2, full_s0=False):
+            eps_seed=2, full_s0=False, period=1):
     """full_s0: step 0's gradients and post-step parameters stored whole (not
     sampled) even at hidden 256, so the headline configs are checked
     element for element at 1e-5."""
@@ -203,7 +203,7 @@ def gen_sac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=7,
     torch.manual_seed(0)
     tr = SACTrainer(pp, qp, action_space=Box(-1, 1, (act_dim,)), discount=discount,
                     reward_scale=reward_scale, policy_lr=lr, qf_lr=lr,
-                    optimizer_class=Adam14, soft_target_tau=tau, target_update_period=1,
+                    optimizer_class=Adam14, soft_target_tau=tau, target_update_period=period,
                     use_automatic_entropy_tuning=auto_alpha)
     params = sac_params(obs_dim, act_dim, hidden, seed, pi_init_w=pi_init_w, q_init_w=q_init_w)
     load_sd(tr.policy, params["policy"])
@@ -219,7 +219,7 @@ def gen_sac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=7,
                 n_replay=n_replay, seed=seed, pi_init_w=pi_init_w, q_init_w=q_init_w,
                 auto_alpha=auto_alpha, log_alpha0=log_alpha0, discount=discount,
                 reward_scale=reward_scale, tau=tau, lr=lr, idx_seed=idx_seed,
-                eps_seed=eps_seed, target_entropy=-float(act_dim))
+                eps_seed=eps_seed, target_entropy=-float(act_dim), target_update_period=period)
     for s in range(steps):
         EPS_LOG.clear()
         batch, idx = _record_batch(rb, B)
@@ -257,13 +257,13 @@ def gen_sac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=7,
 # ------------------------------------------------------------- P-OAC runs
 def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=11,
              delta=0.95, q_min=0.0, q_max=500.0, discount=0.99, lr=3e-4, tau=5e-3,
-             idx_seed=1, eps_seed=2, pi_init_w=1e-3, counts=False, train_bias=True):
+             idx_seed=1, eps_seed=2, pi_init_w=1e-3, counts=False, train_bias=True, period=1):
     pp, qp = _producers(obs_dim, act_dim, hidden, q_out=K)
     torch.manual_seed(0)
     tr = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Box(-1, 1, (act_dim,)),
                             discount=discount, reward_scale=1.0, delta=delta,
                             policy_lr=lr, qf_lr=lr, optimizer_class=Adam14,
-                            soft_target_tau=tau, target_update_period=1,
+                            soft_target_tau=tau, target_update_period=period,
                             use_automatic_entropy_tuning=True, deterministic=False,
                             q_min=q_min, q_max=q_max, share_layers=True, counts=counts,
                             train_bias=train_bias)
@@ -282,7 +282,8 @@ def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=1
                 steps=steps, n_replay=n_replay, seed=seed, delta=delta, q_min=q_min,
                 q_max=q_max, discount=discount, lr=lr, tau=tau, idx_seed=idx_seed,
                 eps_seed=eps_seed, delta_index=int(tr.delta_index), pi_init_w=pi_init_w,
-                target_entropy=-float(act_dim), counts=counts, train_bias=train_bias)
+                target_entropy=-float(act_dim), counts=counts, train_bias=train_bias,
+                target_update_period=period)
     for s in range(steps):
         EPS_LOG.clear()
         batch, idx = _record_batch(rb, B)
@@ -731,6 +732,15 @@ def gen_det_snapshot(path, kind, obs_dim=11, act_dim=3, hidden=(32, 32), B=16, s
     print(f"{os.path.basename(path)}: {os.path.getsize(path) / 1e3:.0f} KB")
 
 
+def gen_period():
+    """target_update_period = 2 (trainer/trainer.py:215, particle_trainer_oac.py:
+    320): Polyak only on even steps; tau 0.1 so the skipped updates show."""
+    save("sac_period2", *gen_sac("sac_period2", 11, 3, [32, 32], 16, 4, 300, True, tau=0.1,
+                                 lr=1e-3, pi_init_w=0.2, q_init_w=0.1, period=2))
+    save("poac_period2", *gen_poac("poac_period2", 11, 3, [32, 32], 5, 16, 4, 300, True,
+                                   tau=0.1, lr=1e-3, q_max=50.0, period=2))
+
+
 def save(name, meta, out):
     import json
     out = dict(out)
@@ -753,6 +763,9 @@ def gen_tpn():
 
 def main():
     torch.set_num_threads(8)
+    if len(sys.argv) > 1 and sys.argv[1] == "period":
+        gen_period()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "sac_snapshot":
         gen_sac_snapshot(os.path.join(HERE, "sac_snapshot.pt"))
         return

@@ -38,7 +38,8 @@ def sac_trainer_for(meta, params=None, **kw):
     pp, qp = producers(params)
     tr = SACTrainer(pp, qp, action_space=Space(meta["act_dim"]), discount=meta["discount"],
                     reward_scale=meta["reward_scale"], policy_lr=meta["lr"], qf_lr=meta["lr"],
-                    soft_target_tau=meta["tau"], target_update_period=1,
+                    soft_target_tau=meta["tau"],
+                    target_update_period=meta.get("target_update_period", 1),
                     use_automatic_entropy_tuning=meta["auto_alpha"], **kw)
     if meta["auto_alpha"]:
         tr.log_alpha.fill_(meta["log_alpha0"])

@@ -154,7 +154,7 @@ def _ring_run(tr, n_calls, n_steps):
     return torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy()
 
 
-def _nccl_worker(port, q):
+def _nccl_worker(port, q, teardown="close"):
     import faulthandler
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -171,21 +171,29 @@ def _nccl_worker(port, q):
     assert tr.capture
     got = _ring_run(tr, 4, 4)          # call 1 eager, calls 2.. captured (RCCL inside the graph)
     n_graphs = len(tr._graphs)
-    dist.destroy_process_group()
     q.put((got, n_graphs))
+    if teardown == "close":
+        # the trainer's own teardown, then the process group: destroying the
+        # group under live graphs (they hold RCCL kernels) aborted the process
+        tr.close()
+        assert not tr._graphs
+        dist.destroy_process_group()
+    # "atexit": neither -- the trainer's atexit hook releases the graphs
 
 
-def test_dp_rccl_graph_capture_single_rank_equals_single_gpu():
+@pytest.mark.parametrize("teardown", ["close", "atexit"])
+def test_dp_rccl_graph_capture_single_rank_equals_single_gpu(teardown):
     """The captured data-parallel step (phases + RCCL all-reduces in one
     hipGraph, 4 steps per replay) on one rank equals the single-GPU trainer on
-    the same device index stream."""
+    the same device index stream, and the process exits cleanly through the
+    trainer's teardown (explicit close(), or its atexit hook)."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    p = ctx.Process(target=_nccl_worker, args=(port, q))
+    p = ctx.Process(target=_nccl_worker, args=(port, q, teardown))
     p.start()
     p.join(timeout=150)
     assert p.exitcode == 0, p.exitcode

@@ -141,3 +141,37 @@ def test_host_read_dropin_equals_device_index_path(kind):
     sa, sb = _state(a), _state(b)
     assert np.isfinite(sa).all()
     assert np.array_equal(sa, sb)
+
+
+def test_host_read_dropin_mixed_paths_across_ring_wrap():
+    """The large-batch drop-in step (host-read index ring) interleaved with the
+    device-ring path: each ring call advances the batch counter by 3, so the
+    following drop-in steps start mid-chunk and the staging ring wraps (more
+    than 128 staged slots).  A slot must never be rewritten while a queued step
+    still reads it: bitwise equal to the device-index path."""
+    from oac_amd import DeviceIndexStream, ReplayBuffer
+    from gpu_helpers import Space
+    Bk, Nk = 1024, 3000
+
+    def run(dropin):
+        tr = _kind_trainer("sac_large", dropin)
+        rb = ReplayBuffer(Nk, Space(Do), Space(Da), device="cuda:0")
+        d = synthetic_transitions(Nk, Do, Da, seed=1)
+        rb.add_paths([dict(observations=d["observations"], actions=d["actions"],
+                           rewards=d["rewards"], next_observations=d["next_observations"],
+                           terminals=d["terminals"])])
+        np.random.seed(5)
+        for seg, n in enumerate((37, 61, 45, 50)):
+            for _ in range(n):
+                batch = rb.random_batch(Bk)
+                batch["buffer"] = rb
+                tr.train(batch)
+            st = DeviceIndexStream(rb, Bk, chunk=3, seed=4 + seg)
+            st.before_step(3)
+            tr.train_from_ring(rb._storage, st.ring, st.slots, Bk, n_steps=3)
+        return tr
+    a, b = run(True), run(False)
+    assert a._n_train_steps_total == b._n_train_steps_total == 193 + 12
+    sa, sb = _state(a), _state(b)
+    assert np.isfinite(sa).all()
+    assert np.array_equal(sa, sb)

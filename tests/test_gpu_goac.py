@@ -7,6 +7,7 @@ import pytest
 import torch
 
 import parity
+import test_oracle_golden as tog
 from fixtures_lib import PARAM_ORDER_POLICY, PARAM_ORDER_Q, goac_params
 from gpu_helpers import Space, StateDictModule, batch_from, module_tensors
 
@@ -78,9 +79,12 @@ def test_goac_step_matches_reference_golden(name):
                 errs[key], _ = parity.compare_post(g, key, gk, t.cpu().numpy(), meta["lr"])
         for k, v in tr.get_diagnostics().items():
             errs[f"s{s}/stat/{k}"] = parity.stat_err(v, g, f"s{s}/stat/{k}")
-    bad = {k: v for k, v in errs.items() if v > (parity.TOL if k.startswith("s0/") else 1e-4)}
+    # every step under the noise-derived gate (max(1e-5, 3x the reference's
+    # own fp32 distance from the float64 oracle, per key))
+    noise = tog.goac_errors(meta, g, tog.make_goac_oracle(meta, torch.float64, g=g))
+    bad = tog.gated(errs, noise)
     print(name, "worst", sorted(errs.items(), key=lambda kv: -kv[1])[:3])
-    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1])[:10]
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
 
 
 def test_goac_stats_keys_match_reference_order():

@@ -12,7 +12,7 @@ from oracle import sac_oracle as so
 pytestmark = pytest.mark.gpu
 
 SAC_FIXTURES = ["sac_small", "sac_stress", "sac_noalpha", "sac_riverswim", "sac_humanoid",
-                "sac_humanoid_b4096"]
+                "sac_humanoid_b4096", "sac_period2"]
 
 
 def _oracle_noise(meta, g):

@@ -11,7 +11,7 @@ from oracle import sac_oracle as so
 from oracle.mt_oracle import MT
 
 SAC_FIXTURES = ["sac_small", "sac_stress", "sac_noalpha", "sac_riverswim", "sac_humanoid",
-                "sac_humanoid_b4096"]
+                "sac_humanoid_b4096", "sac_period2"]
 
 
 def test_randint_oracle_matches_numpy_golden():
@@ -35,7 +35,8 @@ def make_sac_oracle(meta, dtype=torch.float32):
     return so.SACOracle(params, meta["obs_dim"], meta["act_dim"], discount=meta["discount"],
                         reward_scale=meta["reward_scale"], policy_lr=meta["lr"],
                         qf_lr=meta["lr"], tau=meta["tau"], auto_alpha=meta["auto_alpha"],
-                        log_alpha0=meta["log_alpha0"], dtype=dtype)
+                        log_alpha0=meta["log_alpha0"],
+                        target_update_period=meta.get("target_update_period", 1), dtype=dtype)
 
 
 def sac_errors(meta, g, orc, steps=None):
@@ -78,48 +79,116 @@ def test_sac_oracle_matches_reference_golden(name):
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
 
 
-def test_poac_oracle_matches_reference_golden():
-    for name in ("poac_small", "poac_ant", "poac_counts", "poac_nobias"):
-        meta, g = parity.load(name)
-        params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
-                            q_out=meta["K"], q_last_bias=np.linspace(meta["q_min"], meta["q_max"],
-                                                                      meta["K"]),
-                            pi_init_w=meta["pi_init_w"])
-        orc = so.ParticleOACOracle(params, meta["obs_dim"], meta["act_dim"], meta["K"],
-                                   discount=meta["discount"], policy_lr=meta["lr"],
-                                   qf_lr=meta["lr"], tau=meta["tau"],
-                                   train_bias=meta.get("train_bias", True))
-        errs = {}
-        for s in range(meta["steps"]):
-            b = build_batch(meta, g[f"s{s}/idx"])
-            if meta.get("counts"):
-                b["counts"] = g[f"s{s}/counts"][:, None]
-            out = orc.step(b, g[f"s{s}/eps1"], g[f"s{s}/eps2"])
-            for grp, order in (("policy", PARAM_ORDER_POLICY), ("qf", PARAM_ORDER_Q)):
-                for pn in order:
-                    key = f"s{s}/grad/{grp}/{pn}"
-                    errs[key] = parity.compare(g, key, out["grads"][grp][pn].numpy())
-            errs[f"s{s}/grad/log_alpha"] = parity.rel_err(out["grads"]["log_alpha"].numpy(),
-                                                          g[f"s{s}/grad/log_alpha"])
-            for grp, params_ in (("policy", orc.P), ("qf", orc.Q), ("tf", orc.T)):
-                for pn, t in params_.items():
-                    key = f"s{s}/post/{grp}/{pn}"
-                    gk = f"s{s}/grad/{grp}/{pn}" if s == 0 and grp != "tf" else None
-                    errs[key], _ = parity.compare_post(g, key, gk, t.numpy(), meta["lr"])
-            for i in range(meta["K"]):
-                k = f"s{s}/stat/QF{i} Loss"
-                errs[k] = parity.rel_err(out["qf_losses"][i].item(), g[k])
-        bad = {k: v for k, v in errs.items()
-               if v > (parity.TOL if k.startswith("s0/") else 1e-4)}
-        assert not bad, (name, sorted(bad.items(), key=lambda kv: -kv[1])[:10])
+def stats_of(name, x):
+    """create_stats_ordered_dict (utils/eval_util.py:70-110): Mean, Std
+    (population), Max, Min of an array."""
+    x = np.asarray(x.detach().numpy() if torch.is_tensor(x) else x, np.float64)
+    return {f"{name} Mean": x.mean(), f"{name} Std": x.std(), f"{name} Max": x.max(),
+            f"{name} Min": x.min()}
 
 
-GOAC_FIXTURES = ["goac_small", "goac_counts", "goac_soft", "goac_humanoid", "goac_nobias"]
-GOAC_STATS = ("QF mean", "QF std", "QF Loss", "STD Loss", "Q Target Mean", "Q STD Target Mean",
-              "Policy Loss", "Policy mu Mean", "Policy log std Mean")
+# integer counts of the sorted heads (exact on both sides; not a float statistic)
+COUNT_STATS = ("QF Unordered", "QF target Undordered")
 
 
-def make_goac_oracle(meta, dtype=torch.float32):
+def stat_errors(s, g, st):
+    """{key: err} for every float statistic of step s the fixture holds."""
+    errs = {}
+    for k in g:
+        if not k.startswith(f"s{s}/stat/"):
+            continue
+        name = k[len(f"s{s}/stat/"):]
+        if name in COUNT_STATS:
+            continue
+        assert name in st, (k, "statistic not restated by the oracle")
+        errs[k] = parity.stat_err(float(st[name]), g, k)
+    return errs
+
+
+POAC_FIXTURES = ["poac_small", "poac_ant", "poac_counts", "poac_nobias", "poac_period2"]
+
+
+def make_poac_oracle(meta, dtype=torch.float32):
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                        q_out=meta["K"], q_last_bias=np.linspace(meta["q_min"], meta["q_max"],
+                                                                  meta["K"]),
+                        pi_init_w=meta["pi_init_w"])
+    return so.ParticleOACOracle(params, meta["obs_dim"], meta["act_dim"], meta["K"],
+                                discount=meta["discount"], policy_lr=meta["lr"],
+                                qf_lr=meta["lr"], tau=meta["tau"],
+                                target_update_period=meta.get("target_update_period", 1),
+                                train_bias=meta.get("train_bias", True), dtype=dtype)
+
+
+def poac_stats(meta, out):
+    """particle_trainer_oac.py:335-362."""
+    qs = out["sorted_qs"].detach().numpy().astype(np.float64)
+    st = {"QF mean": np.mean(qs, axis=0).mean(), "QF std": np.std(qs, axis=0).mean()}
+    for i in range(meta["K"]):
+        st[f"QF{i} Loss"] = float(out["qf_losses"][i])
+        st.update(stats_of(f"Q{i}Predictions", out["sorted_qs"][i]))
+        st.update(stats_of(f"Q{i}Targets", out["tq"][i]))
+    st["Policy Loss"] = float(out["policy_loss"])
+    st.update(stats_of("Policy mu", out["policy_mean"]))
+    st.update(stats_of("Policy log std", out["policy_log_std"]))
+    return st
+
+
+def poac_errors(meta, g, orc):
+    """Run the P-OAC oracle through the fixture's steps; return {key: err}
+    over gradients, log-alpha, post-step parameters and statistics."""
+    errs = {}
+    for s in range(meta["steps"]):
+        b = build_batch(meta, g[f"s{s}/idx"])
+        if meta.get("counts"):
+            b["counts"] = g[f"s{s}/counts"][:, None]
+        out = orc.step(b, g[f"s{s}/eps1"], g[f"s{s}/eps2"])
+        for grp, order in (("policy", PARAM_ORDER_POLICY), ("qf", PARAM_ORDER_Q)):
+            for pn in order:
+                key = f"s{s}/grad/{grp}/{pn}"
+                errs[key] = parity.compare(g, key, out["grads"][grp][pn].numpy())
+        errs[f"s{s}/grad/log_alpha"] = parity.rel_err(out["grads"]["log_alpha"].numpy(),
+                                                      g[f"s{s}/grad/log_alpha"])
+        errs[f"s{s}/post/log_alpha"] = parity.rel_err(orc.log_alpha.numpy(),
+                                                      g[f"s{s}/post/log_alpha"])
+        for grp, params_ in (("policy", orc.P), ("qf", orc.Q), ("tf", orc.T)):
+            for pn, t in params_.items():
+                key = f"s{s}/post/{grp}/{pn}"
+                gk = f"s{s}/grad/{grp}/{pn}" if s == 0 and grp != "tf" else None
+                errs[key], _ = parity.compare_post(g, key, gk, t.numpy(), meta["lr"])
+        errs.update(stat_errors(s, g, poac_stats(meta, out)))
+    return errs
+
+
+def gated(errs, noise):
+    """The keys whose error exceeds the noise-derived gate (parity.gate)."""
+    return {k: (v, noise.get(k, 0.0)) for k, v in errs.items()
+            if v > parity.gate(k, noise.get(k, 0.0))}
+
+
+@pytest.mark.parametrize("name", POAC_FIXTURES)
+def test_poac_oracle_matches_reference_golden(name):
+    """particle_trainer_oac.ParticleTrainer restatement vs the reference's own
+    run, every step under the noise-derived gate (max(1e-5, 3x the
+    reference's own fp32 distance from the float64 oracle))."""
+    meta, g = parity.load(name)
+    errs = poac_errors(meta, g, make_poac_oracle(meta))
+    noise = poac_errors(meta, g, make_poac_oracle(meta, torch.float64))
+    bad = gated(errs, noise)
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
+
+
+GOAC_FIXTURES = ["goac_small", "goac_counts", "goac_soft", "goac_humanoid", "goac_nobias",
+                 "goac_tpn"]
+
+
+def next_policy_of(g):
+    """use_target_policy fixtures: the DDPG target network's weights."""
+    tpn = {k[4:]: v for k, v in g.items() if k.startswith("tpn/")}
+    return tpn or None
+
+
+def make_goac_oracle(meta, dtype=torch.float32, g=None):
     params = goac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
                          meta["q_min"], meta["q_max"], pi_init_w=meta["pi_init_w"],
                          q_init_w=meta["q_init_w"])
@@ -128,10 +197,28 @@ def make_goac_oracle(meta, dtype=torch.float32):
                                 discount=meta["discount"], policy_lr=meta["lr"],
                                 qf_lr=meta["lr"], tau=meta["tau"],
                                 std_soft_update_prob=meta["soft"],
-                                train_bias=meta.get("train_bias", True), dtype=dtype)
+                                train_bias=meta.get("train_bias", True),
+                                next_policy=next_policy_of(g) if g is not None else None,
+                                dtype=dtype)
 
 
-def goac_errors(meta, g, orc):
+def goac_stats(out):
+    """gaussian_trainer.py:400-436 ('Policy mu / log std' describe the target
+    policy: the variable is reassigned by its forward)."""
+    st = {"QF mean": float(out["q_preds"].mean()), "QF std": float(out["std_preds"].mean()),
+          "QF Loss": float(out["q_loss"])}
+    st.update(stats_of("Q Predictions", out["q_preds"]))
+    st.update(stats_of("Q Target", out["q_target"]))
+    st["STD Loss"] = float(out["std_loss"])
+    st.update(stats_of("Q STD Predictions", out["std_preds"]))
+    st.update(stats_of("Q STD Target", out["std_target"]))
+    st["Policy Loss"] = float(out["upper_bound"].mean())
+    st.update(stats_of("Policy mu", out["target_head"]["mean"]))
+    st.update(stats_of("Policy log std", out["target_head"]["log_std"]))
+    return st
+
+
+def det_errors(meta, g, orc, stats_fn):
     errs = {}
     for s in range(meta["steps"]):
         b = build_batch(meta, g[f"s{s}/idx"])
@@ -148,34 +235,29 @@ def goac_errors(meta, g, orc):
                 key = f"s{s}/post/{grp}/{pn}"
                 gk = f"s{s}/grad/{grp}/{pn}" if s == 0 and grp != "tf" else None
                 errs[key], _ = parity.compare_post(g, key, gk, t.numpy(), meta["lr"])
-        Da = meta["act_dim"]
-        th = out["target_head"]
-        st = {"QF mean": out["q_preds"].mean(), "QF std": out["std_preds"].mean(),
-              "QF Loss": out["q_loss"], "STD Loss": out["std_loss"],
-              "Q Target Mean": out["q_target"].mean(),
-              "Q STD Target Mean": out["std_target"].mean(),
-              "Policy Loss": out["upper_bound"].mean(), "Policy mu Mean": th["mean"].mean(),
-              "Policy log std Mean": th["log_std"].mean()}
-        for k in GOAC_STATS:
-            errs[f"s{s}/stat/{k}"] = parity.stat_err(float(st[k]), g, f"s{s}/stat/{k}")
+        errs.update(stat_errors(s, g, stats_fn(meta, out)))
     return errs
+
+
+def goac_errors(meta, g, orc):
+    return det_errors(meta, g, orc, lambda meta, out: goac_stats(out))
 
 
 @pytest.mark.parametrize("name", GOAC_FIXTURES)
 def test_goac_oracle_matches_reference_golden(name):
     """GaussianTrainer (g-oac) restatement vs the reference's own run."""
     meta, g = parity.load(name)
-    errs = goac_errors(meta, g, make_goac_oracle(meta))
-    noise = goac_errors(meta, g, make_goac_oracle(meta, torch.float64))
-    bad = {k: (v, noise[k]) for k, v in errs.items() if v > parity.gate(k, noise[k])}
+    errs = goac_errors(meta, g, make_goac_oracle(meta, g=g))
+    noise = goac_errors(meta, g, make_goac_oracle(meta, torch.float64, g=g))
+    bad = gated(errs, noise)
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
 
 
 PTRAIN_FIXTURES = ["ptrain_small", "ptrain_counts", "ptrain_soft_rescale", "ptrain_mean_update",
-                   "ptrain_humanoid", "ptrain_nobias"]
+                   "ptrain_humanoid", "ptrain_nobias", "ptrain_tpn"]
 
 
-def make_ptrain_oracle(meta, dtype=torch.float32):
+def make_ptrain_oracle(meta, dtype=torch.float32, g=None):
     params = ptrain_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
                            meta["K"], meta["q_min"], meta["q_max"], pi_init_w=meta["pi_init_w"],
                            q_init_w=meta["q_init_w"])
@@ -184,35 +266,28 @@ def make_ptrain_oracle(meta, dtype=torch.float32):
                                discount=meta["discount"], policy_lr=meta["lr"], qf_lr=meta["lr"],
                                tau=meta["tau"], std_soft_update_prob=meta["soft"],
                                mean_update=meta["mean_update"], rescale=meta["rescale"],
-                               train_bias=meta.get("train_bias", True), dtype=dtype)
+                               train_bias=meta.get("train_bias", True),
+                               next_policy=next_policy_of(g) if g is not None else None,
+                               dtype=dtype)
+
+
+def ptrain_stats(meta, out):
+    """particle_trainer.py:403-432."""
+    qs = out["sorted_qs"].detach().numpy().astype(np.float64)
+    st = {"QF mean": np.mean(qs, axis=0).mean(), "QF std": np.std(qs, axis=0).mean(),
+          "Q Loss": float(out["qf_loss"])}
+    for i in range(meta["K"]):
+        st[f"QF{i} Loss"] = float(out["qf_losses"][i])
+        st.update(stats_of(f"Q{i}Predictions", out["sorted_qs"][i]))
+        st.update(stats_of(f"Q{i}Targets", out["tq"][i]))
+    st["Policy Loss"] = float(out["upper_bound"].mean())
+    st.update(stats_of("Policy mu", out["target_head"]["mean"]))
+    st.update(stats_of("Policy log std", out["target_head"]["log_std"]))
+    return st
 
 
 def ptrain_errors(meta, g, orc):
-    errs = {}
-    for s in range(meta["steps"]):
-        b = build_batch(meta, g[f"s{s}/idx"])
-        if meta["counts"]:
-            b["counts"] = g[f"s{s}/counts"][:, None]
-        out = orc.step(b)
-        for grp in ("policy", "target_policy", "qf"):
-            for pn in (PARAM_ORDER_Q if grp == "qf" else PARAM_ORDER_POLICY):
-                key = f"s{s}/grad/{grp}/{pn}"
-                errs[key] = parity.compare(g, key, out["grads"][grp][pn].numpy())
-        for grp, params_ in (("policy", orc.P), ("target_policy", orc.TP), ("qf", orc.Q),
-                             ("tf", orc.T)):
-            for pn, t in params_.items():
-                key = f"s{s}/post/{grp}/{pn}"
-                gk = f"s{s}/grad/{grp}/{pn}" if s == 0 and grp != "tf" else None
-                errs[key], _ = parity.compare_post(g, key, gk, t.numpy(), meta["lr"])
-        th = out["target_head"]
-        st = {"Q Loss": out["qf_loss"], "Policy Loss": out["upper_bound"].mean(),
-              "Policy mu Mean": th["mean"].mean(), "Policy log std Mean": th["log_std"].mean(),
-              "QF mean": out["sorted_qs"].mean()}
-        for i in range(meta["K"]):
-            st[f"QF{i} Loss"] = out["qf_losses"][i]
-        for k, v in st.items():
-            errs[f"s{s}/stat/{k}"] = parity.stat_err(float(v), g, f"s{s}/stat/{k}")
-    return errs
+    return det_errors(meta, g, orc, ptrain_stats)
 
 
 @pytest.mark.parametrize("name", PTRAIN_FIXTURES)
@@ -220,9 +295,9 @@ def test_ptrain_oracle_matches_reference_golden(name):
     """p-oac ParticleTrainer (particle_trainer.py) restatement vs the
     reference's own run."""
     meta, g = parity.load(name)
-    errs = ptrain_errors(meta, g, make_ptrain_oracle(meta))
-    noise = ptrain_errors(meta, g, make_ptrain_oracle(meta, torch.float64))
-    bad = {k: (v, noise[k]) for k, v in errs.items() if v > parity.gate(k, noise[k])}
+    errs = ptrain_errors(meta, g, make_ptrain_oracle(meta, g=g))
+    noise = ptrain_errors(meta, g, make_ptrain_oracle(meta, torch.float64, g=g))
+    bad = gated(errs, noise)
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
 
 
