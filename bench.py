@@ -174,6 +174,12 @@ def roofline_of(kt, flop_per_sample, B, n, traffic_key=None, exec_flop_per_sampl
            "traffic": load_traffic(traffic_key or B), "flops_per_launch": round(fpl),
            "avg_launch_us": round(gk["avg_us"], 3), "launches_per_step": gk["launches"] / n,
            "duration_source": "hipExtLaunchKernel dispatch events, %d steps" % n}
+    prof = rocprof_gemm_avg(traffic_key or B)
+    if prof is not None:   # the same figure from the committed rocprofv3 statistics
+        us, path = prof
+        a2 = fpl / (us * 1e-6) / 1e12
+        out["rocprof"] = {"avg_launch_us": us, "achieved": round(a2, 3),
+                          "frac": round(a2 / PEAK_FP32_TFLOPS, 4), "source": path}
     if exec_flop_per_sample:
         out["executed_flops_per_launch"] = round(exec_flop_per_sample * B * n / max(gk["launches"], 1))
         out["note"] = ("numerator = SURVEY 8d algorithmic GEMM FLOPs; the MFMAs execute %.1f %% fewer "
@@ -226,7 +232,9 @@ def standalone_hbm(rb, device, B=4096, reps=50):
     p = lambda t: ctypes.c_void_p(t.data_ptr())
     us_g = ev_time(lambda: _lib.check(L.oac_replay_gather(p(rb._storage), rb._storage.shape[1], p(idx),
                                                           B, p(out), sp)))
-    nq, npol = 333_826, 171_043
+    # the arenas' 16-byte padding: 333,828 / 171,044 floats (the bytes below
+    # stay SURVEY 8d's unpadded count)
+    nq, npol = 333_828, 171_044
     bufs = [torch.zeros(n, device=device) for n in (nq, nq, nq, nq, nq, npol, npol, npol, npol)]
     state = torch.zeros(16, dtype=torch.int64, device=device)
     qp, qg, qm, qv, qt, pp_, pg, pm, pv = bufs
@@ -328,19 +336,26 @@ def dp1_leg(args, rb, device, B, single_value, steps=640, warmup=64):
         hid = [args.hidden, args.hidden]
         pp = oac_amd.get_policy_producer(args.obs_dim, args.act_dim, hid, device=device)
         qp = oac_amd.get_q_producer(args.obs_dim, args.act_dim, hid, device=device)
-        with DataParallelSACTrainer(pp, qp, action_space=Space(args.act_dim), discount=0.99,
-                                    reward_scale=1.0, policy_lr=3e-4, qf_lr=3e-4,
-                                    soft_target_tau=5e-3, target_update_period=1,
-                                    use_automatic_entropy_tuning=True, device=device, seed=2,
-                                    gemm_cfg=args.gemm_cfg) as tr:
-            np.random.seed(1)
-            el = timed(dropin_run(tr, rb, B), steps, warmup, 1, device)
-            assert torch.isfinite(tr.params).all().item(), "non-finite DP parameters"
-            lb = launch_breakdown(tr, rb, B)
-        v = steps / el
-        return {"steps_per_s": round(v, 1), "ms_per_step": round(1e3 * el / steps, 4),
-                "vs_single_process": round(v / single_value, 4), "batch": B, "steps": steps,
-                "backend": "nccl (RCCL), world_size 1", "launches": lb}
+        out = {"batch": B, "steps": steps, "backend": "nccl (RCCL), world_size 1"}
+        for force in (False, True):
+            with DataParallelSACTrainer(pp, qp, action_space=Space(args.act_dim), discount=0.99,
+                                        reward_scale=1.0, policy_lr=3e-4, qf_lr=3e-4,
+                                        soft_target_tau=5e-3, target_update_period=1,
+                                        use_automatic_entropy_tuning=True, device=device, seed=2,
+                                        gemm_cfg=args.gemm_cfg, force_collectives=force) as tr:
+                np.random.seed(1)
+                el = timed(dropin_run(tr, rb, B), steps, warmup, 1, device)
+                assert torch.isfinite(tr.params).all().item(), "non-finite DP parameters"
+                lb = launch_breakdown(tr, rb, B) if not force else None
+            v = steps / el
+            leg = {"steps_per_s": round(v, 1), "ms_per_step": round(1e3 * el / steps, 4),
+                   "vs_single_process": round(v / single_value, 4)}
+            if force:   # the three all-reduces issued through RCCL although world size is 1
+                out["with_rccl_allreduces"] = leg
+            else:       # the phase split itself (at world size 1 the sums are identities)
+                out.update(leg)
+                out["launches"] = lb
+        return out
     finally:
         dist.destroy_process_group()
 
@@ -610,6 +625,21 @@ def recipe_timing(kind, args, device, rb, steps=640, warmup=64, n=64):
 def _launches(tr):
     from oac_amd import _lib
     return _lib.lib().oac_sac_launch_count(tr._last_plan.handle)
+
+
+def rocprof_gemm_avg(key, round_dir="r03"):
+    """(average GEMM launch us, path) from the committed rocprofv3 summary of
+    this workload (tools/prof_summary.py output), or None."""
+    path = os.path.join("profiles", round_dir, {256: "b256", 4096: "b4096"}.get(key, str(key))
+                        + "_gemm_avg.txt")
+    try:
+        with open(os.path.join(ROOT, path)) as f:
+            for line in f:
+                if line.startswith("GEMM kernel (all instances)"):
+                    return float(line.rsplit("avg", 1)[1].split()[0]), path
+    except OSError:
+        pass
+    return None
 
 
 def load_traffic(B):

@@ -112,11 +112,16 @@ class _DataParallel:
     graph replay instead of ~20 host-issued launches and collectives
     (``capture=False`` keeps every step eager)."""
 
-    def __init__(self, *args, process_group=None, capture=None, **kwargs):
+    def __init__(self, *args, process_group=None, capture=None, force_collectives=False,
+                 **kwargs):
         if not dist.is_initialized():
             raise RuntimeError("DataParallelSACTrainer needs torch.distributed initialised")
         self.pg = process_group
         self.world = dist.get_world_size(process_group)
+        # a sum over one rank is the identity: at world size 1 the exchanges
+        # are skipped (force_collectives=True issues them anyway: what the
+        # collective library's captured calls cost, for measurement)
+        self._collectives = self.world > 1 or force_collectives
         self.capture = (dist.get_backend(process_group) == "nccl") if capture is None else capture
         # the alpha exchange beside the fresh-action critic forward (RCCL only:
         # with gloo the collective is a host call and there is nothing to
@@ -172,7 +177,8 @@ class _DataParallel:
         return c
 
     def _all_reduce(self, t):
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+        if self._collectives:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
 
     def _all_reduce_async(self, t):
         """The all-reduce on a side stream forked from the current one; the

@@ -72,8 +72,9 @@ def _trainer(dp, kind="sac"):
     from oac_amd.dp import DataParallelSACTrainer
     pp, qp = producers(sac_params(Do, Da, [H, H], 3, pi_init_w=0.2, q_init_w=0.1))
     cls = DataParallelSACTrainer if dp else SACTrainer
+    kw = dict(force_collectives=True) if dp == "rccl1" else {}
     return cls(pp, qp, action_space=Space(Da), discount=0.99, reward_scale=1.0, policy_lr=1e-3,
-               qf_lr=1e-3, soft_target_tau=5e-3, use_automatic_entropy_tuning=True)
+               qf_lr=1e-3, soft_target_tau=5e-3, use_automatic_entropy_tuning=True, **kw)
 
 
 def _with_counts(batch, step):
@@ -167,7 +168,7 @@ def _nccl_worker(port, q, teardown="close"):
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    tr = _trainer(True)
+    tr = _trainer("rccl1")   # the all-reduces issued through RCCL although world size is 1
     assert tr.capture
     got = _ring_run(tr, 4, 4)          # call 1 eager, calls 2.. captured (RCCL inside the graph)
     n_graphs = len(tr._graphs)
