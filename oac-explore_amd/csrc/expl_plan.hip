@@ -80,7 +80,7 @@ static void expl_layout(ExplPlan& p) {
   p.o_grad = take(N * p.Da);
   p.o_cnt = take(2);
   // expl_split.hip: published vectors + hand-off counters of the groups of one launch
-  p.o_split = take((int64_t)std::min(N, (int64_t)kExplRows) * expl_split_scratch_floats(p.H));
+  p.o_split = take((int64_t)std::min(N, (int64_t)kExplRows) * expl_split_scratch_floats(p.H, p.Da));
   p.total = o + 64;
 }
 

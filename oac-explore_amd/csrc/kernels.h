@@ -139,7 +139,7 @@ constexpr int kExplRows = 256;
 int expl_split_group(int n_rows);
 int expl_split_threads();
 size_t expl_split_lds_bytes(int Do, int Da, int H);
-long expl_split_scratch_floats(int H);
+long expl_split_scratch_floats(int H, int Da);
 hipError_t launch_expl_split(const ExplFusedArgs& a, int row0, int n_rows, float* scratch,
                              hipStream_t s);
 
