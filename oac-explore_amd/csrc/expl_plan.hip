@@ -47,7 +47,6 @@ struct ExplPlan {
   // optional pinned host staging (oac_expl_set_host_io): uploads / downloads
   // captured into the graph
   const float* host_obs = nullptr; float* host_out = nullptr;
-  long long* stage_clock = nullptr;   // instrumentation: per-stage wall clock of row 0
   // oac_expl_action_now: host-coherent observation rows [N, Do + Da], results
   // [3][N][Da] and completion word (hipHostMalloc, allocated on first use)
   float* hc_obs = nullptr; float* hc_out = nullptr; unsigned* hc_done = nullptr;
@@ -80,14 +79,8 @@ static void expl_layout(ExplPlan& p) {
   p.o_grad = take(N * p.Da);
   p.o_cnt = take(2);
   // expl_split.hip: published vectors + hand-off counters of the groups of one launch
-  p.o_split = take((int64_t)std::min(N, (int64_t)kExplRows) * expl_split_scratch_floats(p.H, p.Da));
+  p.o_split = take((int64_t)std::min(N, (int64_t)kExplRows) * expl_split_scratch_floats(p.H));
   p.total = o + 64;
-}
-
-// OAC_EXPL_SPLIT=0: the one-workgroup-per-observation kernel (expl_fused.hip)
-static bool expl_split_on() {
-  static const bool v = [] { const char* e = getenv("OAC_EXPL_SPLIT"); return !e || atoi(e) != 0; }();
-  return v;
 }
 
 static ExplFusedArgs expl_args(ExplPlan& p, const float* eps, float beta, float delta) {
@@ -108,17 +101,12 @@ static ExplFusedArgs expl_args(ExplPlan& p, const float* eps, float beta, float 
   a.fail = reinterpret_cast<unsigned*>(w + p.o_cnt + 1);
   a.seed = p.seed; a.beta_UB = beta; a.sqrt_2delta = (float)std::sqrt(2.0 * (double)delta);
   a.ub_index = p.ub_index;
-  a.stage_clock = p.stage_clock;
   return a;
 }
 
 static int expl_launch(ExplPlan& p, const ExplFusedArgs& a, hipStream_t s) {
-  if (expl_split_on() && !p.stage_clock) {
-    for (int row0 = 0; row0 < p.N; row0 += kExplRows)
-      OAC_HIP_CHECK(launch_expl_split(a, row0, std::min(kExplRows, p.N - row0), p.ws + p.o_split, s));
-  } else {
-    OAC_HIP_CHECK(launch_expl_fused(a, s));
-  }
+  for (int row0 = 0; row0 < p.N; row0 += kExplRows)
+    OAC_HIP_CHECK(launch_expl_split(a, row0, std::min(kExplRows, p.N - row0), p.ws + p.o_split, s));
   return 0;
 }
 
@@ -215,8 +203,8 @@ int oac_expl_create_batch(int n_obs, int obs_dim, int act_dim, int hidden, const
   }
   if (act_dim < 1 || act_dim > 63) { set_error("act_dim must be in [1, 63]"); return 1; }
   if (n_obs < 1 || n_obs > 65536) { set_error("n_obs must be in [1, 65536]"); return 1; }
-  if (expl_fused_lds_bytes(obs_dim, act_dim, hidden) > 64 * 1024) {
-    set_error("exploration: obs_dim + 8 * hidden too large for one workgroup's LDS");
+  if (expl_split_lds_bytes(obs_dim, act_dim, hidden) > 64 * 1024) {
+    set_error("exploration: obs_dim + 4 * hidden too large for one workgroup's LDS");
     return 1;
   }
   oac_expl* h = new oac_expl();
@@ -339,28 +327,12 @@ int oac_expl_action_now(oac_expl* h, const float* eps, float beta_UB, float delt
   ExplFusedArgs a = expl_args(p, eps, beta_UB, delta);
   a.obs = p.hc_obs;
   a.out = p.hc_out;
-  const bool split = expl_split_on() && !p.stage_clock;
-  if (split) {
-    p.seq = (p.seq + 1) & 0x7fffffffu;   // bit 31 of the word is the failure flag
-    if (p.seq == 0) p.seq = 1;           // 0 is the word's initial value
-    a.done = p.hc_done;
-    a.done_seq = p.seq;
-  }
+  p.seq = (p.seq + 1) & 0x7fffffffu;   // bit 31 of the word is the failure flag
+  if (p.seq == 0) p.seq = 1;           // 0 is the word's initial value
+  a.done = p.hc_done;
+  a.done_seq = p.seq;
   if (expl_launch(p, a, s)) return 1;
-  if (!split) {   // the one-workgroup kernel (A/B runs, stage clocks) has no completion word
-    OAC_HIP_CHECK(hipStreamSynchronize(s));
-    return 0;
-  }
   return expl_wait(p, a.done_seq, s);
-}
-
-// instrumentation hook (tools/expl_latency.py; not in include/oac_amd.h):
-// device buffer of >= 16 int64 stage stamps of row 0's workgroup, or NULL
-int oac_expl_debug_stage_clock(oac_expl* h, long long* dev_buf) {
-  if (!h) return 1;
-  h->p.stage_clock = dev_buf;
-  h->p.drop_graphs();
-  return 0;
 }
 
 const float* oac_expl_outputs(oac_expl* h) { return h ? h->p.ws + h->p.o_out : nullptr; }

@@ -338,29 +338,11 @@ __global__ void __launch_bounds__(256) gemm_grouped_kernel(const GemmBatch batch
   }
 }
 
-// LDS-tiled kernel for the large-batch stages (cfg 1); cfg 0 is the
-// latency-optimised register-direct kernel of gemm_small.hip.  Tile variants
-// (OAC_LDS_TILE, read once): 0 = 64x64x32 (32x32 per wave), 1 = 128x128x16
-// (64x64 per wave), 2 = 128x64x32 (64x32 per wave), 3 = 64x128x32 (32x64 per
-// wave).  The k order of every accumulator is the same in all of them, so
-// they are bitwise interchangeable.
+// LDS-tiled kernel (cfg 1, 64x64x32 tiles, 32x32 per wave): the fallback for
+// large-batch products the pipelined kernels do not take; cfg 0 is the
+// latency-optimised kernel of gemm_small.hip.  (128x128 / 128x64 / 64x128 /
+// 64x64x16 variants measured 0.6-1.02x and were retired.)
 using CfgLarge = GemmCfg<64, 64, 32, 2, 2, 1>;
-using CfgL1 = GemmCfg<128, 128, 16, 2, 2, 1>;
-using CfgL2 = GemmCfg<128, 64, 32, 2, 2, 1>;
-using CfgL3 = GemmCfg<64, 128, 32, 2, 2, 1>;
-using CfgL4 = GemmCfg<64, 64, 16, 2, 2, 1>;
-using CfgL5 = GemmCfg<64, 32, 32, 2, 1, 2>;
-
-static int lds_variant() {
-  static int v = [] {
-    const char* e = getenv("OAC_LDS_TILE");
-    const int x = e ? atoi(e) : 0;
-    return (x >= 0 && x <= 5) ? x : 0;
-  }();
-  return v;
-}
-static int lds_tile_m() { const int v = lds_variant(); return v == 1 || v == 2 ? 128 : 64; }
-static int lds_tile_n() { const int v = lds_variant(); return v == 1 || v == 3 ? 128 : v == 5 ? 32 : 64; }
 
 // cfg 2: the register-direct kernel of gemm_big.hip (128 x 128 workgroup tiles)
 // cfg 3: the same kernel with the backward tile (dX / dW batches)
@@ -368,12 +350,6 @@ int gemm_big_tile_m(bool bwd);
 int gemm_big_tile_n(bool bwd);
 hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s, bool bwd);
 
-// cfg 4: the LDS-staged kernel of gemm_lds.hip (64 x 64 workgroup tiles)
-hipError_t gemm_lds_launch(const GemmBatch& b, hipStream_t s);
-int gemm_lds_tile_m();
-int gemm_lds_tile_n();
-
-hipError_t gemm_bwd_launch(const GemmBatch& b, hipStream_t s);
 hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s);
 int gemm_fwd_tile_m(int cfg);
 int gemm_fwd_tile_n(int cfg);
@@ -384,15 +360,13 @@ int gemm_bwdp_tile_n(int cfg);
 
 int gemm_tile_m(int cfg) {
   if (cfg >= 9) return gemm_bwdp_tile_m(cfg);
-  if (cfg == 5) return 64;
   if (cfg >= 6) return gemm_fwd_tile_m(cfg);
-  return cfg == 0 ? 32 : cfg == 4 ? gemm_lds_tile_m() : cfg >= 2 ? gemm_big_tile_m(cfg == 3) : lds_tile_m();
+  return cfg == 0 ? 32 : cfg >= 2 ? gemm_big_tile_m(cfg == 3) : 64;
 }
 int gemm_tile_n(int cfg) {
   if (cfg >= 9) return gemm_bwdp_tile_n(cfg);
-  if (cfg == 5) return 64;
   if (cfg >= 6) return gemm_fwd_tile_n(cfg);
-  return cfg == 0 ? 32 : cfg == 4 ? gemm_lds_tile_n() : cfg >= 2 ? gemm_big_tile_n(cfg == 3) : lds_tile_n();
+  return cfg == 0 ? 32 : cfg >= 2 ? gemm_big_tile_n(cfg == 3) : 64;
 }
 
 void gemm_small_finalize(GemmBatch& b);
@@ -413,7 +387,6 @@ void gemm_batch_finalize(GemmBatch& b, int cfg) {
     t.tiles_n = tn;
     if (t.ksplit < 1) t.ksplit = 1;
     tiles += tm * tn * t.ksplit;
-    if (cfg == 5) tiles = (tiles + 7) & ~7;   // gemm_bwd.hip: XCD-aligned block ranges
   }
   b.total_tiles = tiles;
 }
@@ -428,19 +401,10 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
     // the width-1 head dot: small kernel, the register-direct one (cfg 2 / 3) or gemm_fwd (6-8)
     if (b.t[i].epi == EPI_BIAS_RELU_DOT && cfg != 2 && cfg != 3 && (cfg < 6 || cfg > 8)) return hipErrorInvalidValue;
   }
-  if (cfg == 4) return gemm_lds_launch(b, s);
-  if (cfg == 5) return gemm_bwd_launch(b, s);
   if (cfg >= 9) return gemm_bwdp_launch(b, cfg, s);
   if (cfg >= 6) return gemm_fwd_launch(b, cfg, s);
   if (cfg >= 2) return gemm_big_launch(b, s, cfg == 3);
-  switch (lds_variant()) {
-    case 1: OAC_LAUNCH(gemm_grouped_kernel<CfgL1>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-    case 2: OAC_LAUNCH(gemm_grouped_kernel<CfgL2>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-    case 3: OAC_LAUNCH(gemm_grouped_kernel<CfgL3>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-    case 4: OAC_LAUNCH(gemm_grouped_kernel<CfgL4>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-    case 5: OAC_LAUNCH(gemm_grouped_kernel<CfgL5>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-    default: OAC_LAUNCH(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b); break;
-  }
+  OAC_LAUNCH(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b);
   return hipGetLastError();
 }
 

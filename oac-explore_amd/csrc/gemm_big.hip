@@ -183,26 +183,11 @@ gemm_big_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
 // wave block (32 WM) x (32 WN), default 64 x 32 (workgroup 128 x 64): at
 // B=4096, 1,828 steps/s against 1,827 for 32 x 64, 1,775 for 64 x 64 and 1,741
 // for 32 x 32; 3 k-groups in flight instead of 2 changed nothing (+-1 %).
-// OAC_BIG_TILE="WM,WN" selects another instantiation (tuning experiments)
-// Backward batches (dX / dW, cfg 3) default to 32 x 32 wave blocks (64 x 64
+// Backward batches (dX / dW, cfg 3) use 32 x 32 wave blocks (64 x 64
 // workgroups): at B=4096 their products are 256 wide, and the 4x larger
 // grid hides the per-wave operand latency better than the larger blocks do.
-// OAC_BIG_TILE / OAC_BIG_BWD_TILE="WM,WN" select other instantiations.
-static int tile_env(const char* name, int which, int dflt) {
-  const char* e = getenv(name);
-  if (!e) return dflt;
-  if (which == 0) return atoi(e);
-  const char* c = strchr(e, ',');
-  return c ? atoi(c + 1) : dflt;
-}
-static int big_wm(bool bwd) {
-  static const int f = tile_env("OAC_BIG_TILE", 0, 2), b = tile_env("OAC_BIG_BWD_TILE", 0, 1);
-  return bwd ? b : f;
-}
-static int big_wn(bool bwd) {
-  static const int f = tile_env("OAC_BIG_TILE", 1, 1), b = tile_env("OAC_BIG_BWD_TILE", 1, 1);
-  return bwd ? b : f;
-}
+static int big_wm(bool bwd) { return bwd ? 1 : 2; }
+static int big_wn(bool bwd) { (void)bwd; return 1; }
 int gemm_big_tile_m(bool bwd) { return 64 * big_wm(bwd); }
 int gemm_big_tile_n(bool bwd) { return 64 * big_wn(bwd); }
 
@@ -217,15 +202,13 @@ hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s, bool bwd) {
   }
   int tb[8];
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
-  static const int pf_bwd = tile_env("OAC_BIG_BWD_PF", 0, 3), pf_fwd = tile_env("OAC_BIG_PF", 0, 2);
-  const int pf = bwd ? pf_bwd : pf_fwd;
+  const int pf = bwd ? 3 : 2;   // k-groups in flight
 #define OAC_BIG(WM_, WN_, PF_) \
   if (big_wm(bwd) == WM_ && big_wn(bwd) == WN_ && pf == PF_) { \
     OAC_LAUNCH((gemm_big_kernel<WM_, WN_, PF_>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, \
                tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
     return hipGetLastError(); }
-  OAC_BIG(2, 1, 2) OAC_BIG(1, 1, 3) OAC_BIG(2, 1, 3) OAC_BIG(1, 2, 2) OAC_BIG(1, 2, 3)
-  OAC_BIG(1, 1, 2) OAC_BIG(2, 2, 2) OAC_BIG(1, 1, 4)
+  OAC_BIG(2, 1, 2) OAC_BIG(1, 1, 3)
 #undef OAC_BIG
   return hipErrorInvalidValue;
 }

@@ -107,7 +107,7 @@ struct PolicyHeadBwdArgs {
 };
 
 
-struct ExplFusedArgs {                  // expl_fused.hip: one workgroup per observation
+struct ExplFusedArgs {                  // expl_split.hip: the exploration action
   const float* obs; long ld_obs;        // [N, ld_obs] observation rows
   const float* pol; const float* q[2];  // parameter blocks (oac_sac_layout offsets below)
   long p_fc0_w, p_fc0_b, p_fc1_w, p_fc1_b, p_head_w, p_head_b;
@@ -124,14 +124,11 @@ struct ExplFusedArgs {                  // expl_fused.hip: one workgroup per obs
   float beta_UB, sqrt_2delta;
   int ub_index;                         // K heads: >= 0 -> Q_UB = sorted head ub_index
                                         // (trainer.predict, particle_trainer_oac.py:147-167)
-  long long* stage_clock;               // instrumentation (tools/expl_latency.py) or null
   unsigned* done; unsigned done_seq;    // expl_split.hip: completion word (host-polled) or null;
                                         // bit 31 of the word set: a hand-off of the call timed out
   unsigned* fail;                       // zeroed device word: a group's timed-out hand-off (re-armed
                                         // by the kernel that reports it)
 };
-size_t expl_fused_lds_bytes(int Do, int Da, int H);
-hipError_t launch_expl_fused(const ExplFusedArgs& a, hipStream_t s);
 // expl_split.hip: one observation per group of expl_split_group(rows) <=
 // kExplGroup workgroups; a launch carries at most kExplRows observations
 constexpr int kExplGroup = 32;
@@ -139,7 +136,7 @@ constexpr int kExplRows = 256;
 int expl_split_group(int n_rows);
 int expl_split_threads();
 size_t expl_split_lds_bytes(int Do, int Da, int H);
-long expl_split_scratch_floats(int H, int Da);
+long expl_split_scratch_floats(int H);
 hipError_t launch_expl_split(const ExplFusedArgs& a, int row0, int n_rows, float* scratch,
                              hipStream_t s);
 

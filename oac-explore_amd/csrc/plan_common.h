@@ -50,9 +50,6 @@ struct PlanBase {
   // (kStepHostIdx), so no H2D copy precedes the step's graph
   bool idx_host = false;
   bool owns_host_ring = false;
-  // per-launch small-GEMM geometry overrides (tuning experiments: env
-  // OAC_TUNE="launch:nw:gpw,..." read at plan creation; 0 = automatic)
-  int tune_nw[64] = {0}, tune_gpw[64] = {0};
   // HIP-event kernel timing (bench instrumentation; never inside a graph)
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -63,12 +60,11 @@ struct PlanBase {
 };
 
 static inline Split choose_split(int K, int tiles, int cfg) {
-  const int bk = (cfg == 0 || cfg == 4) ? 64 : 32;   // cfg 4: whole LDS stages (32 or 64 deep)
+  const int bk = cfg == 0 ? 64 : 32;
   int S = 1;
   if (K >= 512) {
     int want = (512 + tiles - 1) / tiles;
-    static const int kmin = [] { const char* e = getenv("OAC_SPLIT_KMIN"); return e ? atoi(e) : 128; }();
-    int maxS = K / (cfg == 0 ? 256 : kmin);
+    int maxS = K / (cfg == 0 ? 256 : 128);
     S = want < maxS ? want : maxS;
     if (S < 1) S = 1;
   }
@@ -177,50 +173,21 @@ static inline int tock(PlanBase& p, int kind, int i, hipStream_t s) {
     if (tock(p, kind, _t, s)) return 1;  \
   } while (0)
 
-static inline void read_tuning(PlanBase& p) {
-  const char* e = getenv("OAC_TUNE");
-  while (e && *e) {
-    int i = 0, nw = 0, g = 0, used = 0;
-    if (sscanf(e, "%d:%d:%d%n", &i, &nw, &g, &used) != 3) break;
-    if (i >= 0 && i < 64) { p.tune_nw[i] = nw; p.tune_gpw[i] = g; }
-    e += used;
-    if (*e == ',') ++e;
-  }
-}
 
 // The register-direct kernel (gemm_big.hip) runs the large-batch products
-// with N >= 64: forward batches as cfg 2 (64x32 wave blocks; B=4096 layer 0
-// 115 -> 80 us, layer 1 64 -> 40 us against the LDS kernel) and backward
-// batches -- dX / dW, batch-major operands, one dword load per lane and k --
-// as cfg 3 (32x32 wave blocks: step 2,044 -> 2,209 steps/s).  Narrow outputs
-// go to the small-batch kernel, the rest to the LDS kernel (cfg 1).
-// OAC_BIG_BWD=0 keeps the backward batches on the LDS kernel (A/B runs).
-static inline bool big_bwd() {
-  static const bool v = [] { const char* e = getenv("OAC_BIG_BWD"); return !e || atoi(e) != 0; }();
-  return v;
-}
+// the pipelined kernels below do not take, with N >= 64: forward batches as
+// cfg 2 (64x32 wave blocks) and backward batches -- dX / dW, batch-major
+// operands, one dword load per lane and k -- as cfg 3 (32x32 wave blocks).
+// Narrow outputs go to the small-batch kernel, the rest to the LDS kernel
+// (cfg 1).  (The register-staged LDS kernels of round 2, gemm_lds.hip / cfg 4,
+// and gemm_bwd.hip / cfg 5, were slower in every geometry and are retired to
+// tools/micro/retired.)
+static inline int large_batch_cfg() { return 2; }
 
-// Large-batch default: the register-direct kernel (gemm_big.hip, cfg 2 / 3).
-// OAC_LDS2=1 selects the LDS-staged kernel (gemm_lds.hip, cfg 4) instead: at
-// B=4096 the SAC step ran 1,943 / 1,925 / 1,721 / 2,044 steps/s with its
-// 64x64 / 128x64 / 64x64-KD64 / 64x128 tiles (OAC_LDS_GEOM 0-3) against 2,303
-// on the register-direct pair (tools/gpu_geom.sh; every variant parity-green).
-static inline int large_batch_cfg() {
-  static const int v = [] { const char* e = getenv("OAC_LDS2"); return (e && atoi(e) != 0) ? 4 : 2; }();
-  return v;
-}
-bool gemm_lds_supports(const GemmBatch& b);
-
-// forward batches with fewer 128x64 tiles than this run on 64x64 tiles
-// (OAC_SMALL_FWD=<tiles>; 0: always 128x64).  configs[4] P-OAC (single N = 256
-// products at B=4096: 128 tiles) 2,872 -> 3,105 / 3,132 / 3,174 steps/s at 256 /
-// 512 / 1024; the SAC step 2,473 -> 2,475 / 2,476 / 2,301 (its 512- and
-// 768-tile layer launches must stay on 128x64)
-static inline int small_fwd_tiles() {
-  static const int v = [] { const char* e = getenv("OAC_SMALL_FWD"); return e ? atoi(e) : 512; }();
-  return v;
-}
-bool gemm_bwd_supports(const GemmBatch& b);
+// a forward batch with fewer 128x64 tiles than this runs on the register-
+// direct kernel's 64x64 tiles (cfg 3) when the pipelined kernel does not take
+// it: twice the workgroups (configs[4]: single N = 256 products at B=4096)
+constexpr int kSmallFwdTiles = 512;
 bool gemm_fwd_supports(const GemmBatch& b);
 
 // Forward batches at large batch go to gemm_fwd.hip (LDS-DMA pipelined
@@ -252,17 +219,10 @@ static inline int fwd2_cfg(const GemmBatch& gb) {
   return c8 < c7 ? 8 : 7;
 }
 
-// Backward batches at large batch go to gemm_bwd.hip (cfg 5: float2 fetch of
-// the batch-major operands, K split over the workgroup's waves); OAC_BWD2=0
-// keeps them on the register-direct kernel (cfg 3) for A/B runs.
-static inline bool bwd2_on() {
-  static const bool v = [] { const char* e = getenv("OAC_BWD2"); return !e || atoi(e) != 0; }();
-  return v;
-}
-
 // Backward batches at large batch go to gemm_bwdp.hip (LDS-DMA pipelined,
 // cfg 9 = 128x64 tiles, 10 = 64x64 when 128x64 leaves CUs idle);
-// OAC_BWDP=0 keeps them on gemm_bwd.hip / the register-direct kernel.
+// OAC_BWDP=0 keeps them on the register-direct kernel (A/B parity runs,
+// tests/test_gpu_altkernels.py).
 bool gemm_bwdp_supports(const GemmBatch& b);
 static inline bool bwdp_on() {
   static const bool v = [] { const char* e = getenv("OAC_BWDP"); return !e || atoi(e) != 0; }();
@@ -281,13 +241,6 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
   if (cfg == 0) return 0;
   for (int i = 0; i < gb.ntasks; ++i)   // the fused head backward exists on the small kernel only
     if (gb.t[i].epi == EPI_HEAD_BWD) return 0;
-  if (cfg == 4) {
-    bool narrow = !gb.fuse_adam;
-    for (int i = 0; i < gb.ntasks && narrow; ++i)
-      narrow = gb.t[i].N <= 32 && gb.t[i].ksplit <= 1 && gb.t[i].K2 == 0;
-    if (narrow) return 0;
-    return gemm_lds_supports(gb) ? 4 : 1;
-  }
   // narrow products at large batch (width-1 critic heads, dL/da with N = act
   // dim): a 64-wide LDS tile computes 1-17 useful columns over 8 barriered K
   // blocks; the small-batch kernel's 32x32 tiles with K split over waves
@@ -297,20 +250,7 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     narrow = gb.t[i].N <= 32 && gb.t[i].ksplit <= 1 && gb.t[i].K2 == 0;
   if (narrow) return 0;
   if (cfg != 2) return cfg;
-  {  // OAC_NARROWM_SMALL=1: a batch of narrow-row dW products (M <= 32: the
-     // head's 2 Da, a K-output critic's last layer) with short-K dX products
-     // only on the small kernel's 32-row tiles.  Measured (same box, B=4096):
-     // SAC 3,277 -> 3,274, configs[4] 4,077 -> 4,023 steps/s -- off by default
-    static const int nm = [] { const char* e = getenv("OAC_NARROWM_SMALL"); return e ? atoi(e) : 0; }();
-    bool nar = nm != 0 && !gb.fuse_adam;
-    for (int i = 0; i < gb.ntasks && nar; ++i) {
-      const GemmTask& t = gb.t[i];
-      const bool dw = t.epi == EPI_GRAD && !t.a_kc && t.M <= 32;
-      const bool dx = t.a_kc && !t.b_kc && t.K < 64 && t.ksplit <= 1;
-      nar = (dw || dx) && t.K2 == 0 && (t.ksplit <= 1 || t.kchunk % 64 == 0);
-    }
-    if (nar) return 0;
-  }
+  // (narrow-row dW batches on the small kernel measured -1 % at B=4096 and were dropped)
   if (fwd2_on()) {
     bool all_fwd = true;
     for (int i = 0; i < gb.ntasks; ++i)
@@ -321,25 +261,10 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     // a dX with a short K (the head's 2 Da, a K-output critic's K) rides
     // along with its batch's dW (same-box A/B, B=4096: SAC 3,276 -> 3,310,
     // configs[4] 4,106 -> 4,200 steps/s against keeping those batches on the
-    // register-direct kernel; OAC_BWDP_SHORT=0 restores that)
-    bool all_bwd = true, short_dx = false;
-    for (int i = 0; i < gb.ntasks; ++i) {
-      all_bwd = all_bwd && !gb.t[i].b_kc;
-      short_dx = short_dx || (gb.t[i].a_kc && gb.t[i].K < 64);
-    }
-    static const bool short_ok = [] { const char* e = getenv("OAC_BWDP_SHORT"); return !e || atoi(e) != 0; }();
-    if (all_bwd && (!short_dx || short_ok) && gemm_bwdp_supports(gb)) return bwdp_cfg(gb);
-  }
-  if (bwd2_on() && big_bwd()) {
-    // a dX with a short K (the head's 2 Da, the K-output critic's K) leaves
-    // gemm_bwd's K-split waves idle and its epilogue to two waves: those
-    // launches stay on the register-direct kernel (cfg 3)
-    bool all_bwd = true, short_dx = false;
-    for (int i = 0; i < gb.ntasks; ++i) {
-      all_bwd = all_bwd && !gb.t[i].b_kc;
-      short_dx = short_dx || (gb.t[i].a_kc && gb.t[i].K < 64);
-    }
-    if (all_bwd && !short_dx && gemm_bwd_supports(gb)) return 5;
+    // register-direct kernel)
+    bool all_bwd = true;
+    for (int i = 0; i < gb.ntasks; ++i) all_bwd = all_bwd && !gb.t[i].b_kc;
+    if (all_bwd && gemm_bwdp_supports(gb)) return bwdp_cfg(gb);
   }
   // a width-1 head riding on a layer-1 epilogue (EPI_BIAS_RELU_DOT) exists on
   // the small and register-direct kernels only: a batch the register-direct
@@ -349,7 +274,7 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
   for (int i = 0; i < gb.ntasks; ++i) {
     const GemmTask& t = gb.t[i];
     const bool fwd = t.a_kc && t.b_kc && t.a_mode == A_PLAIN;
-    const bool bwd = !t.b_kc && big_bwd();   // dX / dW products (register-direct, gemm_big.hip)
+    const bool bwd = !t.b_kc;   // dX / dW products (register-direct, gemm_big.hip)
     if (!(fwd || bwd) || t.N < 64 || t.K2 > 0 || t.epi == EPI_HEAD_BWD || gb.fuse_adam)
       return dot ? 0 : 1;
     any_bwd |= bwd;
@@ -364,7 +289,7 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
     int tiles = 0;
     for (int i = 0; i < gb.ntasks; ++i)
       tiles += ((gb.t[i].M + 127) / 128) * ((gb.t[i].N + 63) / 64) * std::max(1, gb.t[i].ksplit);
-    if (tiles < small_fwd_tiles()) return 3;
+    if (tiles < kSmallFwdTiles) return 3;
   }
   return any_bwd ? 3 : 2;
 }
@@ -372,10 +297,6 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
 static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {
   const int cfg = launch_cfg(p.cfg, gb);
   gemm_batch_finalize(gb, cfg);
-  if (p.launches < 64 && p.tune_nw[p.launches] > 0) {
-    gb.force_nw = p.tune_nw[p.launches];
-    gb.force_gpw = p.tune_gpw[p.launches];
-  }
   static const bool dbg = getenv("OAC_DEBUG_CFG") != nullptr;
   if (dbg) {
     fprintf(stderr, "launch %d cfg %d tiles %d:", p.launches, cfg, gb.total_tiles);

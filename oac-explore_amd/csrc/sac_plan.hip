@@ -109,23 +109,13 @@ static void layout_workspace(SacPlan& p) {
 //          sample (+ alpha update when world_size == 1)
 // The width-1 critic heads ride on the layer-1 epilogue (EPI_BIAS_RELU_DOT;
 // critic_targets adds the per-32-column partials): on the small-batch kernel
-// and, since round 2, on the large-batch register-direct kernel (two N = 1
-// launches fewer at B=4096; OAC_QDOT_BIG=0 keeps them)
-static bool qdot_big() {
-  static const bool v = [] { const char* e = getenv("OAC_QDOT_BIG"); return !e || atoi(e) != 0; }();
-  return v;
-}
-// the large-batch step runs dL/da + the tanh-Gaussian head backward as one
-// small-kernel launch too (the dL/da product is 17 wide; its epilogue is the
-// head backward) instead of a GEMM launch and a row launch; OAC_HEADBWD_BIG=0
-// keeps the two
-static bool head_bwd_fused_big() {
-  static const bool v = [] { const char* e = getenv("OAC_HEADBWD_BIG"); return !e || atoi(e) != 0; }();
-  return v;
-}
+// and, since round 2, on the large-batch kernels (two N = 1 launches fewer at
+// B=4096).  The large-batch step also runs dL/da + the tanh-Gaussian head
+// backward as one small-kernel launch (the dL/da product is 17 wide; its
+// epilogue is the head backward) instead of a GEMM launch and a row launch.
+static bool head_bwd_fused_big() { return true; }
 static bool qdot(const SacPlan& p) {
-  return (p.cfg == 0 || (p.cfg == 2 && qdot_big())) && p.c.q_out == 1 &&
-         (p.c.hidden + 31) / 32 <= 16;
+  return (p.cfg == 0 || p.cfg == 2) && p.c.q_out == 1 && (p.c.hidden + 31) / 32 <= 16;
 }
 static GemmTask q_l1(SacPlan& p, const float* in, const float* net, float* out, int qv) {
   const oac_sac_config& c = p.c;
@@ -204,15 +194,12 @@ int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long
     // box: one Adam launch per group 3,429 steps/s; side blocks after the
     // tiles, 32 per launch 3,186 -- the side work became the launch's tail --,
     // 64 3,419, 128 3,508, one float4 per thread 3,485; ahead of the tiles
-    // 3,442); OAC_SIDE_BLOCKS forces a count, OAC_SIDE_FIRST=1 dispatches
-    // them ahead of the tiles
-    static const int forced = [] { const char* e = getenv("OAC_SIDE_BLOCKS"); return e ? atoi(e) : 0; }();
-    static const int first = [] { const char* e = getenv("OAC_SIDE_FIRST"); return e ? atoi(e) : 0; }();
+    // 3,442)
     long n4 = 0;
     for (int i = 0; i < nseg; ++i) n4 += n[i] >> 2;
-    int blocks = forced > 0 ? forced : (int)std::min<long>(1024, (n4 + 255) / 256);
+    const int blocks = (int)std::min<long>(1024, (n4 + 255) / 256);
     gb.side_adam = std::max(8, (blocks + 7) & ~7);
-    gb.side_first = first ? 1 : 0;
+    gb.side_first = 0;
     gb.side_book = book ? 1 : 0;
     gb.adam = a;
     gb.nseg = nseg;
@@ -539,22 +526,14 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
 // slot 0 (one launch per kXSlots steps), step i uses slot i % kXSlots
 static long c_batch_rows(const SacPlan& p) { return (long)p.c.batch * p.c.row_stride; }
 
-// OAC_STEP_FUSE / OAC_STEP_AHEAD = 0 switch off the fused optimizer epilogue /
-// the next-step critic prefetch (A/B measurements)
-static bool env_on(const char* name) {
-  const char* e = getenv(name);
-  return !e || atoi(e) != 0;
-}
-
 static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) {
-  static const bool fuse_on = env_on("OAC_STEP_FUSE"), ahead_on = env_on("OAC_STEP_AHEAD");
   p.launches = 0;
-  const bool fused = can_fuse_adam(p) && fuse_on;
+  const bool fused = can_fuse_adam(p);
   p.slot = i % kXSlots;
   const int gather_n = p.slot == 0 ? std::min(kXSlots, n - i) : 0;
   // steps after the first of a gather batch had their critic-side forward
   // issued inside the previous step's policy backward (small-batch path)
-  const bool ahead = p.cfg == 0 && (flags & OAC_STEP_GATHER) && ahead_on;
+  const bool ahead = p.cfg == 0 && (flags & OAC_STEP_GATHER);
   if (phase0(p, flags, s, gather_n, ahead && p.slot > 0)) return 1;
   const bool split = !fused && split_adam_on(p);
   if (phase1(p, s, fused, 0, split)) return 1;
@@ -650,7 +629,7 @@ static void plan_splits(SacPlan& p) {
     int v[5] = {0, 0, 0, 0, 0};
     sscanf(e, "%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4]);
     Split* sp[5] = {&p.sp_q1, &p.sp_q0, &p.sp_ph, &p.sp_p1, &p.sp_p0};
-    const int bk = (p.cfg == 0 || p.cfg == 4) ? 64 : 32;
+    const int bk = p.cfg == 0 ? 64 : 32;
     for (int i = 0; i < 5; ++i)
       if (v[i] > 0) {
         int kc = (c.batch + v[i] - 1) / v[i];
@@ -688,7 +667,6 @@ int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_s
   else if (has_target_policy(p.c.kind)) det_layout_workspace(p);
   else layout_workspace(p);
   p.b = *bufs;
-  read_tuning(p);
   *out = h;
   return 0;
 }
@@ -759,12 +737,6 @@ int oac_sac_step(oac_sac* h, int flags, void* stream) { return oac_sac_step_n(h,
 
 static constexpr int kRingChunk = 16;
 
-// direct mode needs the small-batch kernel (cfg 0); OAC_DROPIN_DIRECT=0 keeps
-// the H2D copy + gather launch (A/B runs)
-static bool dropin_direct_on() {
-  static const bool v = [] { const char* e = getenv("OAC_DROPIN_DIRECT"); return !e || atoi(e) != 0; }();
-  return v;
-}
 
 int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
   if (!h) { set_error("null handle"); return 1; }
@@ -793,10 +765,10 @@ int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
     std::memset(r, 0, sizeof(int32_t) * (size_t)p.b.ring_slots * p.c.batch);
     p.host_ring = r;
     p.owns_host_ring = true;
-    p.rows_direct = p.cfg == 0 && dropin_direct_on() && !has_target_policy(p.c.kind) &&
+    // direct mode needs the small-batch kernel (cfg 0)
+    p.rows_direct = p.cfg == 0 && !has_target_policy(p.c.kind) &&
                     p.c.kind != OAC_KIND_PARTICLE;   // sac_plan's run_step / phase0 only
-    static const bool hostidx_on = [] { const char* e = getenv("OAC_HOSTIDX"); return !e || atoi(e) != 0; }();
-    p.idx_host = !p.rows_direct && hostidx_on;
+    p.idx_host = !p.rows_direct;
     // not direct (large batch): the copy path still stages through this ring
     if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
     if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }

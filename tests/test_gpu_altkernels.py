@@ -1,7 +1,7 @@
 """The large-batch kernels the default per-launch choice does not pick
 (plan_common.h launch_cfg), each in a child process whose environment forces
 it: the register-direct forward / backward GEMMs (OAC_FWD2=0 OAC_BWDP=0:
-gemm_big.hip, gemm_bwd.hip), the pipelined forward on 128x128 tiles with a
+gemm_big.hip), the pipelined forward on 128x128 tiles with a
 3-stage ring (OAC_FWD2_TILE=128,128) and the pipelined backward on 128x64 /
 128x128 tiles (OAC_BWDP_CFG=9 / 11), and the step-structure fallbacks
 (OAC_SPLIT_ADAM=0, OAC_DH2_TARGETS=0).  Each runs the ragged large-batch parity

@@ -72,20 +72,6 @@ def main():
     t_kernel = bench(launch)
     check(L.oac_expl_host_staging(e.handle, ctypes.byref(po), ctypes.byref(pr)))
     check(L.oac_expl_set_host_io(e.handle, po, pr))
-    clk = torch.zeros(16, dtype=torch.int64, device=dev)
-    fn = L.oac_expl_debug_stage_clock
-    fn.argtypes, fn.restype = [ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int
-    fn(e.handle, ctypes.c_void_p(clk.data_ptr()))
-    for _ in range(20):
-        launch()
-    c = clk.cpu().numpy()
-    names = ["load", "pol L0", "pol L1", "head+tanh", "Q L0", "Q L1+last+seed", "dh2/dh1",
-             "da", "final"]
-    print({n: round((c[i + 1] - c[i]) / 100.0, 2) for i, n in enumerate(names[:-1])},
-          "(us, 100 MHz wall clock)")
-    print("head matvec+sync", (c[9] - c[2]) / 100.0, "tanh+sync", (c[3] - c[9]) / 100.0,
-          "Q1 L0", (c[10] - c[3]) / 100.0, "Q2 L0+sync", (c[4] - c[10]) / 100.0)
-    fn(e.handle, None)
     print({"full_call_us": round(full, 1), "full_call_graph_us": round(full_graph, 1),
            "action_now_us": round(t_now, 1), "call_64obs_us": round(t64, 1), "graph_with_host_io_sync_us": round(t_launch, 1),
            "graph_device_only_sync_us": round(t_kernel, 1),
