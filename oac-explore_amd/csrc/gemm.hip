@@ -393,7 +393,7 @@ void gemm_batch_finalize(GemmBatch& b, int cfg) {
 
 hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   if (b.total_tiles <= 0) return hipSuccess;
-  if (b.side_adam > 0 && (cfg < 9 || cfg > 11)) return hipErrorInvalidValue;   // side Adam: gemm_bwdp only
+  if (b.side_adam > 0 && (cfg < 9 || cfg > 12)) return hipErrorInvalidValue;   // side Adam: gemm_bwdp only
   if (cfg == 0) return gemm_small_launch(b, s);
   if (b.fuse_adam) return hipErrorInvalidValue;   // fused optimizer: small-batch kernel only
   for (int i = 0; i < b.ntasks; ++i) {             // dual products / head backward: small kernel

@@ -37,12 +37,13 @@ enum PKind { PK_KC = 0, PK_KC_R1 = 1, PK_MN = 2, PK_MN_R1 = 3 };
 
 constexpr int kVec = 1024;   // LDS floats for a rank-1 factor indexed by k
 
-template <int BM, int BN>
+template <int BM, int BN, int NB = kFBuf>
 struct BwdG {
   static constexpr int WM = BM / 64, WN = BN / 64;
   static constexpr int PA = BM / 32, PB = BN / 32;   // LDS-DMA instructions per wave and stage
   static constexpr int LPW = PA + PB;
   static constexpr int STAGE = (BM + BN) * kFK;
+  static constexpr int LDS = NB * STAGE + kVec;      // ring of NB stages + the rank-1 vector
 };
 
 // one operand's LDS-DMA sources.  KC: ROWS x 32 k, 8 rows per instruction,
@@ -110,11 +111,11 @@ __device__ __forceinline__ float f4c(const float4& v, int c) {
 
 // acc += A . B over k in [k_lo, k_hi) for one workgroup tile; bsum: row sums
 // of A (the dW ones column) when ones
-template <int BM, int BN, int AK>
+template <int BM, int BN, int AK, int NB>
 __device__ __forceinline__ void bwdp_pipe(const GemmTask& t, int m0, int n0, int nx, int k_lo,
                                           int k_hi, bool ones, float* lds, float* vec,
                                           floatx16 (&acc)[BM / 64][BN / 64], float (&bsum)[BM / 64]) {
-  using G = BwdG<BM, BN>;
+  using G = BwdG<BM, BN, NB>;
   constexpr int WM = G::WM, WN = G::WN;
   constexpr bool AKC = AK == PK_KC || AK == PK_KC_R1;
   constexpr bool AR1 = AK == PK_KC_R1 || AK == PK_MN_R1;
@@ -122,6 +123,20 @@ __device__ __forceinline__ void bwdp_pipe(const GemmTask& t, int m0, int n0, int
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int kb0 = k_lo & ~7;
   const int nst = (k_hi - kb0 + kFK - 1) / kFK;
+  PSrc<AKC, BM> sa;
+  PSrc<false, BN> sb;
+  sa.init(AR1 ? t.a_mask : t.A, AR1 ? t.ld_mask : t.lda, m0, t.M, wave, lane);
+  sb.init(t.B, t.ldb, n0, nx, wave, lane);
+  const int ar = (wave >> 1) * (BM / 2) + l32, br = (wave & 1) * (BN / 2) + l32;
+  // the ring's first two stages are in flight before the rank-1 factors are
+  // requested, so their round trips overlap (the factors' waits also cover
+  // the two stages: both were issued before them)
+  sa.issue(kb0, k_hi, lds, wave);
+  sb.issue(kb0, k_hi, lds + BM * kFK, wave);
+  if (NB == 3 && nst > 1) {
+    sa.issue(kb0 + kFK, k_hi, lds + G::STAGE, wave);
+    sb.issue(kb0 + kFK, k_hi, lds + G::STAGE + BM * kFK, wave);
+  }
   // rank-1 factors: the one indexed by k into LDS (kb0-relative), the one
   // indexed by the output row into registers
   float fm[WM];
@@ -138,37 +153,28 @@ __device__ __forceinline__ void bwdp_pipe(const GemmTask& t, int m0, int n0, int
 #pragma unroll
     for (int i = 0; i < WM; ++i) {
       fm[i] = fr[min(m0 + (wave >> 1) * (BM / 2) + 32 * i + l32, t.M - 1)];
-      // consumed here, so the compiler's wait for these loads comes before the
-      // first LDS-DMA (a wait inside the pipeline would drain it)
-      asm volatile("" ::"v"(fm[i]));
+      asm volatile("" ::"v"(fm[i]));   // consumed here: the wait stays out of the loop
     }
-    __syncthreads();   // no LDS-DMA in flight yet: a plain barrier
+    // every wave's DMA and factor loads done (the compiler does not count
+    // the DMA) and its vec stores in LDS, then vec is complete for all
+    wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    raw_barrier();
   }
   PIPE_CLK(1);
-  PSrc<AKC, BM> sa;
-  PSrc<false, BN> sb;
-  sa.init(AR1 ? t.a_mask : t.A, AR1 ? t.ld_mask : t.lda, m0, t.M, wave, lane);
-  sb.init(t.B, t.ldb, n0, nx, wave, lane);
-  const int ar = (wave >> 1) * (BM / 2) + l32, br = (wave & 1) * (BN / 2) + l32;
-  sa.issue(kb0, k_hi, lds, wave);
-  sb.issue(kb0, k_hi, lds + BM * kFK, wave);
-  if (nst > 1) {
-    sa.issue(kb0 + kFK, k_hi, lds + G::STAGE, wave);
-    sb.issue(kb0 + kFK, k_hi, lds + G::STAGE + BM * kFK, wave);
-  }
 #pragma unroll 1
   for (int st = 0; st < nst; ++st) {
-    if (st + 1 < nst) wait_vm<G::LPW>();
+    if (NB == 3 && st + 1 < nst) wait_vm<G::LPW>();
     else wait_vm<0>();
     raw_barrier();   // stage st landed for every wave; stage st - 1 is read by all
     PIPE_CLK(2 + st);
-    if (st + 2 < nst) {
-      float* nb = lds + ((st + 2) % kFBuf) * G::STAGE;
-      sa.issue(kb0 + (st + 2) * kFK, k_hi, nb, wave);
-      sb.issue(kb0 + (st + 2) * kFK, k_hi, nb + BM * kFK, wave);
+    if (st + NB - 1 < nst) {
+      float* nb = lds + ((st + NB - 1) % NB) * G::STAGE;
+      sa.issue(kb0 + (st + NB - 1) * kFK, k_hi, nb, wave);
+      sb.issue(kb0 + (st + NB - 1) * kFK, k_hi, nb + BM * kFK, wave);
     }
     const int kst = kb0 + st * kFK;
-    const float* as = lds + (st % kFBuf) * G::STAGE;
+    const float* as = lds + (st % NB) * G::STAGE;
     const float* bs = as + BM * kFK;
     const bool mask = kst < k_lo || kst + kFK > k_hi;
     // the whole stage's fragments first (one LDS round trip per stage, not
@@ -230,9 +236,9 @@ __device__ __forceinline__ void bwdp_pipe(const GemmTask& t, int m0, int n0, int
 
 constexpr unsigned kEpiBwd = (1u << EPI_STORE) | (1u << EPI_MASK) | (1u << EPI_GRAD);
 
-template <int BM, int BN, int AK>
+template <int BM, int BN, int AK, int NB>
 __device__ __forceinline__ void bwdp_tile(const GemmBatch& batch, int ti, int local, float* lds) {
-  using G = BwdG<BM, BN>;
+  using G = BwdG<BM, BN, NB>;
   constexpr int WM = G::WM, WN = G::WN;
   GemmTask t = batch.t[ti];
   int k_lo = 0, k_hi = t.K;
@@ -263,7 +269,7 @@ __device__ __forceinline__ void bwdp_tile(const GemmBatch& batch, int ti, int lo
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   }
   PIPE_CLK(0);
-  bwdp_pipe<BM, BN, AK>(t, m0, n0, nx, k_lo, k_hi, ones, lds, lds + kFBuf * G::STAGE, acc, bsum);
+  bwdp_pipe<BM, BN, AK, NB>(t, m0, n0, nx, k_lo, k_hi, ones, lds, lds + NB * G::STAGE, acc, bsum);
   PIPE_CLK(29);
   if (grad_ones) {
     t.N = nx;
@@ -283,11 +289,11 @@ __device__ __forceinline__ void bwdp_tile(const GemmBatch& batch, int ti, int lo
   PIPE_CLK(31);
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int NB>
 __global__ void __launch_bounds__(256)
 gemm_bwdp_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                  const GemmBatch batch) {
-  __shared__ __attribute__((aligned(16))) float lds[kFBuf * BwdG<BM, BN>::STAGE + kVec];
+  __shared__ __attribute__((aligned(16))) float lds[BwdG<BM, BN, NB>::LDS];
   if (batch.publish && blockIdx.x == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
   const int side0 = batch.side_first ? 0 : total_tiles;   // side workgroups: the flat Adam
@@ -306,10 +312,10 @@ gemm_bwdp_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, i
   const int local = bid - t.tile_begin;
   const int ak = (t.a_kc ? PK_KC : PK_MN) + (t.a_mode == A_RANK1_MASK ? 1 : 0);
   switch (ak) {
-    case PK_KC: bwdp_tile<BM, BN, PK_KC>(batch, ti, local, lds); break;
-    case PK_KC_R1: bwdp_tile<BM, BN, PK_KC_R1>(batch, ti, local, lds); break;
-    case PK_MN: bwdp_tile<BM, BN, PK_MN>(batch, ti, local, lds); break;
-    default: bwdp_tile<BM, BN, PK_MN_R1>(batch, ti, local, lds); break;
+    case PK_KC: bwdp_tile<BM, BN, PK_KC, NB>(batch, ti, local, lds); break;
+    case PK_KC_R1: bwdp_tile<BM, BN, PK_KC_R1, NB>(batch, ti, local, lds); break;
+    case PK_MN: bwdp_tile<BM, BN, PK_MN, NB>(batch, ti, local, lds); break;
+    default: bwdp_tile<BM, BN, PK_MN_R1, NB>(batch, ti, local, lds); break;
   }
 }
 
@@ -332,7 +338,7 @@ bool gemm_bwdp_supports(const GemmBatch& b) {
   return true;
 }
 
-int gemm_bwdp_tile_m(int cfg) { return cfg == 10 ? 64 : 128; }
+int gemm_bwdp_tile_m(int cfg) { return cfg == 10 || cfg == 12 ? 64 : 128; }
 int gemm_bwdp_tile_n(int cfg) { return cfg == 11 ? 128 : 64; }
 
 hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s) {
@@ -340,12 +346,13 @@ hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   if (!gemm_bwdp_supports(b)) return hipErrorInvalidValue;
   int tb[8];
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
-#define OAC_BWDP(C_, BM_, BN_) \
+#define OAC_BWDP(C_, BM_, BN_, NB_) \
   if (cfg == C_) { \
-    OAC_LAUNCH((gemm_bwdp_kernel<BM_, BN_>), dim3(b.total_tiles + b.side_adam), dim3(256), 0, s, b.total_tiles, \
+    OAC_LAUNCH((gemm_bwdp_kernel<BM_, BN_, NB_>), dim3(b.total_tiles + b.side_adam), dim3(256), 0, s, b.total_tiles, \
                tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
     return hipGetLastError(); }
-  OAC_BWDP(9, 128, 64) OAC_BWDP(10, 64, 64) OAC_BWDP(11, 128, 128)
+  // cfg 12: 64x64 tiles on a 2-stage ring (36 KB of LDS: four workgroups per CU)
+  OAC_BWDP(9, 128, 64, 3) OAC_BWDP(10, 64, 64, 3) OAC_BWDP(11, 128, 128, 3) OAC_BWDP(12, 64, 64, 2)
 #undef OAC_BWDP
   return hipErrorInvalidValue;
 }

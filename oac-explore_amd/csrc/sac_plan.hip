@@ -189,7 +189,7 @@ static void add_critic_l1(SacPlan& p, GemmBatch& gb) {
 int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long* off,
               const long* n, bool book, hipStream_t s) {
   const int cfg = launch_cfg(p.cfg, gb);
-  if (cfg >= 9 && cfg <= 11 && nseg <= 2) {
+  if (cfg >= 9 && cfg <= 12 && nseg <= 2) {
     // one float4 per thread, dispatched after the tiles (B=4096 SAC, same
     // box: one Adam launch per group 3,429 steps/s; side blocks after the
     // tiles, 32 per launch 3,186 -- the side work became the launch's tail --,

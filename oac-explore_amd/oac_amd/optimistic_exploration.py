@@ -11,6 +11,7 @@ sequence, each row exactly as a single call.  ``policy`` must be the policy of a
 (its parameters live in the trainer's HBM arena, which the kernels read in
 place); there is no torch/CPU fallback.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -69,11 +70,43 @@ def get_optimistic_exploration_action(ob_np, policy=None, qfs=None, trainer=None
         raise NotImplementedError("the deterministic OAC variant is unreachable from rollout() "
                                   "(SURVEY 8a quirk Q7) and not implemented")
     assert np.ndim(ob_np) == 1
+    if eps is None and not return_info and not _USE_GRAPH:
+        return _action_now(ob_np, policy, qfs, trainer, hyper_params), {}
     t = _owner(policy, qfs, trainer, hyper_params)
     a, info = _actions(t, np.asarray(ob_np)[None, :], hyper_params,
                        None if eps is None else np.asarray(eps, np.float32)[None, :], return_info,
                        trainer is not None)
     return a[0], {k: v[0] for k, v in info.items()}
+
+
+# the per-environment-step call (path_collector.py:219-220) validates the same
+# (policy, qfs, trainer, share_layers) every step: the owner check is cached
+# (strong references, so an id is never reused while its entry lives)
+_OWNERS = {}
+
+
+def _action_now(ob_np, policy, qfs, trainer, hyper_params):
+    """The single-observation Philox call on its shortest host path: cached
+    owner validation, the raw current-stream handle, one C call."""
+    share = bool(hyper_params.get("share_layers", False))
+    key = (id(policy), id(trainer), None if qfs is None else tuple(map(id, qfs)), share)
+    ent = _OWNERS.get(key)
+    if ent is None or ent[0] is not policy or ent[1] is not trainer:
+        t = _owner(policy, qfs, trainer, hyper_params)
+        if len(_OWNERS) > 16:
+            _OWNERS.clear()
+        ent = _OWNERS[key] = (policy, trainer, tuple(qfs) if qfs is not None else None, t)
+    t = ent[3]
+    e = t._expl_handle(1)
+    L = _lib.lib()
+    if t.layout.q2_base < 0:   # K heads: mean + beta std, or trainer.predict's sorted head
+        check(L.oac_expl_set_ub_index(e.handle, int(t.delta_index) if trainer is not None else -1))
+    e.obs_np[0, :t.obs_dim] = ob_np                   # float64 observation -> fp32 row
+    s = torch._C._cuda_getCurrentRawStream(t.device.index if t.device.index is not None else
+                                           torch.cuda.current_device())
+    check(L.oac_expl_action_now(e.handle, None, float(hyper_params["beta_UB"]),
+                                float(hyper_params["delta"]), ctypes.c_void_p(s)))
+    return e.out_np[0, 0].copy()
 
 
 def get_optimistic_exploration_actions(obs_np, policy=None, qfs=None, trainer=None,

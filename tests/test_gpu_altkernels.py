@@ -3,7 +3,7 @@
 it: the register-direct forward / backward GEMMs (OAC_FWD2=0 OAC_BWDP=0:
 gemm_big.hip), the pipelined forward on 128x128 tiles with a
 3-stage ring (OAC_FWD2_TILE=128,128) and the pipelined backward on 128x64 /
-128x128 tiles (OAC_BWDP_CFG=9 / 11), and the step-structure fallbacks
+128x128 tiles or 64x64 on a 3-stage ring (OAC_BWDP_CFG=9 / 11 / 10), and the step-structure fallbacks
 (OAC_SPLIT_ADAM=0, OAC_DH2_TARGETS=0).  Each runs the ragged large-batch parity
 cases (tests/alt_kernels_check.py) against the fp32 CPU oracle at 1e-5."""
 import os
@@ -20,6 +20,8 @@ VARIANTS = {
     "register_direct": {"OAC_FWD2": "0", "OAC_BWDP": "0"},
     "fwd_128x128_bwd_128x64": {"OAC_FWD2_TILE": "128,128", "OAC_BWDP_CFG": "9"},
     "fwd_64x64_nb3_bwd_128x128": {"OAC_FWD2_TILE": "64,64", "OAC_FWD2_NB": "3", "OAC_BWDP_CFG": "11"},
+    # the backward 64x64 tiles on the 3-stage ring (the default is the 2-stage one, cfg 12)
+    "bwd_64x64_nb3": {"OAC_BWDP_CFG": "10"},
     # the step-structure fallbacks: one Adam launch per group, the P-OAC
     # rank-K dX as its own GEMM launch
     "adam_launches_dh2_gemm": {"OAC_SPLIT_ADAM": "0", "OAC_DH2_TARGETS": "0"},
