@@ -14,8 +14,10 @@
 //   S3  (every workgroup) heads -> mean, std, a = tanh(mean); critic layer 0
 //       h1_i = relu(P_i + W0_i[:, Do:] a) for all rows; then its rows of critic layer 1
 //   S4  (every workgroup) Q, the Q_UB seeds and dh2 = seed . W_last (x) 1[h2 > 0];
-//       then its columns of dh1 = (dh2 W1) (x) 1[h1 > 0]
-//   S5  (workgroup 0 of the group) da = dh1 . W0[:, Do:], grad, shift, sample.
+//       then, per fixed column part it owns, those columns of dh1 = (dh2 W1)
+//       (x) 1[h1 > 0] and their partial of da = dh1 . W0[:, Do:]
+//   S5  (workgroup 0 of the group) da = the parts' partials in order, grad,
+//       shift, sample.
 // Hand-off forms (MI355X_MICROARCH.md, "Valid forms"):
 //   WT    one workgroup per CU (84 KB of static LDS admits no second one):
 //         write-through (sc1) stores of the published vectors, every storing
@@ -34,6 +36,14 @@
 #include "kernels.h"
 
 namespace oac {
+
+#ifdef OAC_EXPL_CLOCK   // tools/micro/expl_micro: stage wall clocks (100 MHz) of the group's first and last workgroup
+__device__ long long g_expl_clock[64];
+#define EXPL_CLK(i) do { if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == (unsigned)G - 1)) \
+    g_expl_clock[(blockIdx.x == 0 ? 0 : 32) + (i)] = wall_clock64(); } while (0)
+#else
+#define EXPL_CLK(i) do {} while (0)
+#endif
 
 __device__ __forceinline__ float wsum64(float v) {
 #pragma unroll
@@ -97,21 +107,30 @@ __device__ __forceinline__ void rows_matvec(const float* __restrict__ W, long ld
 }
 
 // The group's hand-off: every storing wave drains its stores, the workgroup
-// meets, lane 0 arrives on the stage counter (FENCE: behind an agent release)
-// and polls it (relaxed, bounded) until all G workgroups arrived (FENCE: then
-// acquires); the workgroup meets again.
-template <bool WT>
-__device__ __forceinline__ bool group_sync(unsigned* ctr, unsigned target) {
+// meets, lane 0 arrives on the stage counter (FENCE: behind an agent release);
+// then every thread runs `pre` (the next stage's weight loads into LDS: their
+// round trips overlap the group's arrival skew and the poll), lane 0 polls the
+// counter (relaxed, bounded) until all G workgroups arrived (FENCE: then
+// acquires), and the workgroup meets again.
+struct NoPre { __device__ void operator()() const {} };
+template <bool WT, class Pre = NoPre>
+__device__ __forceinline__ bool group_sync(unsigned* ctr, unsigned target, Pre pre = Pre()) {
   __shared__ int ok_s;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (target <= 1) return true;   // G = 1: the workgroup's own barrier orders its scratch
-  if (threadIdx.x == 0) {
+  if (target > 1 && threadIdx.x == 0) {
     if constexpr (!WT) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  pre();
+  if (target <= 1) {   // G = 1: the workgroup's own barrier orders its scratch
+    __syncthreads();
+    return true;
+  }
+  if (threadIdx.x == 0) {
     int ok = 1;
     unsigned spins = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -128,13 +147,71 @@ __device__ __forceinline__ bool group_sync(unsigned* ctr, unsigned target) {
   return ok_s != 0;
 }
 
-// per-observation scratch (floats) in the workspace: vectors + 4 counters
-__host__ __device__ inline long expl_split_scratch(int H) { return 10L * H + 64; }
-// LDS floats: x | v1 [2H] | v2 [2H] | head [64] | misc [128] | partials [threads]
-__host__ __device__ inline long expl_split_lds(int Do, int Da, int H, int threads) {
-  return ((Do + Da + 3) & ~3L) + 4L * H + 64 + 128 + threads;
+// A prefetch of up to 4 row blocks into LDS: segment s copies rows x cols
+// floats from src (row stride lds_src; published == sc1 loads in WT mode) to
+// dst (row stride ld_dst).  All segments share one flattened loop with 16
+// loads per thread in flight before the LDS stores.
+struct PfSeg { float* dst; const float* src; long ld_src; int rows, cols, ld_dst, published; };
+template <bool WT>
+__device__ __forceinline__ void pf_copy(const PfSeg* sg, int ns) {
+  long base[5];
+  base[0] = 0;
+  for (int i = 0; i < 4; ++i) base[i + 1] = base[i] + (i < ns ? (long)sg[i].rows * sg[i].cols : 0);
+  const long n = base[4];
+  const long nt = blockDim.x;
+  for (long e0 = threadIdx.x; e0 < n; e0 += 16 * nt) {
+    float v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const long e = e0 + u * nt;
+      v[u] = 0.f;
+      if (e < n) {
+        const int i = e >= base[1] ? (e >= base[2] ? (e >= base[3] ? 3 : 2) : 1) : 0;
+        const long l = e - base[i];
+        const int r = (int)(l / sg[i].cols), c = (int)(l - (long)r * sg[i].cols);
+        const float* p = sg[i].src + (long)r * sg[i].ld_src + c;
+        v[u] = sg[i].published ? ld_pub<WT>(p) : *p;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const long e = e0 + u * nt;
+      if (e < n) {
+        const int i = e >= base[1] ? (e >= base[2] ? (e >= base[3] ? 3 : 2) : 1) : 0;
+        const long l = e - base[i];
+        const int r = (int)(l / sg[i].cols), c = (int)(l - (long)r * sg[i].cols);
+        sg[i].dst[(long)r * sg[i].ld_dst + c] = v[u];
+      }
+    }
+  }
 }
-constexpr int kWtLdsFloats = 21 * 1024;   // 84 KB: one workgroup per CU
+
+// the dh1 columns are cut into kExplParts fixed parts (never by the group
+// size): part p's partial of da is published, and S5 adds the parts in order
+constexpr int kExplParts = 32;
+// per-observation scratch (floats) in the workspace: vectors [8H] | da
+// partials [kExplParts][64] | 4 counters
+__host__ __device__ inline long expl_split_scratch(int H) { return 8L * H + kExplParts * 64L + 64; }
+// LDS floats: x | v1 [2H] | v2 [2H] | head [64] | misc [128] | partials [threads] |
+// a part's dh1 columns | their da products
+__host__ __device__ inline long expl_split_lds(int Do, int Da, int H, int threads) {
+  // the dh1 columns of one workgroup (G = 1: all 2H) and a part's da products
+  const long w = (2L * H + kExplParts - 1) / kExplParts;
+  return ((Do + Da + 3) & ~3L) + 4L * H + 64 + 128 + threads + (2L * H + 32) + w * 64;
+}
+constexpr int kWtLdsFloats = 36 * 1024;   // 144 KB: one workgroup per CU
+// floats of the stage-weight prefetch buffers for a group of G (WT mode):
+// S2 the workgroup's policy layer-1 rows; S3 the heads, the critics' action
+// columns, the obs projections and the workgroup's critic layer-1 rows; S4
+// the last layer(s) and the workgroup's dh1 columns of W1 and of W0[:, Do:]
+__host__ __device__ inline long expl_split_pf(int Da, int H, int nq, int Kq, int G) {
+  const long r1 = (H + G - 1) / G, r3 = (nq * (long)H + G - 1) / G;
+  const long c4 = ((long)kExplParts / G + 1) * ((nq * (long)H + kExplParts - 1) / kExplParts);
+  const long s2 = r1 * H;
+  const long s3 = 2L * Da * H + (long)nq * H * Da + (long)nq * H + r3 * H;
+  const long s4 = (long)Kq * H + c4 * (H + 1) + c4 * Da;
+  return s2 > s3 ? (s2 > s4 ? s2 : s4) : (s3 > s4 ? s3 : s4);
+}
 
 template <bool WT>
 __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, int row0, int G,
@@ -156,8 +233,8 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
   float* g_P = Gv + H;          // [2H]  critics' obs projections (+ b0)
   float* g_h2p = Gv + 3 * H;    // [H]   policy layer 1
   float* g_qh2 = Gv + 4 * H;    // [2H]  critic layer 1
-  float* g_dh1 = Gv + 6 * H;    // [2H]  critic dh1
-  unsigned* ctr = reinterpret_cast<unsigned*>(Gv + 10 * H);   // [4] stage counters
+  float* g_dap = Gv + 6 * H + 2 * H;   // [kExplParts][64] da partials
+  unsigned* ctr = reinterpret_cast<unsigned*>(g_dap + kExplParts * 64);   // [4] stage counters
   float* x = sm;                           // [Do + Da] ob | a
   float* v1 = x + ((Dq + 3) & ~3);         // [2H] scratch vectors
   float* v2 = v1 + 2 * H;                  // [2H]
@@ -166,11 +243,13 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
   float* qk = misc + 16;                   // [16] K head values
   float* wk = qk + 16;                     // [16] K head seeds
   float* red = misc + 64;                  // [64]
-  float* prt = misc + 128;                 // [threads] dh1 partials; da [nq][64] in S5
+  float* prt = misc + 128;                 // [threads] dh1 partials, then a part's dh1 columns
   __shared__ long long cnt_s;
   if (t == 0) cnt_s = a.state->expl_counter;
+  EXPL_CLK(0);
   for (int k = t; k < Do; k += nt) x[k] = a.obs[(long)r * a.ld_obs + k];
   __syncthreads();
+  EXPL_CLK(1);
   // rows of a length-L product owned by this workgroup
   auto part = [&](int L, int& lo, int& hi) {
     const int per = (L + G - 1) / G;
@@ -195,14 +274,18 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
       }
     }
   }
+  EXPL_CLK(2);
   bool ok = group_sync<WT>(ctr + 0, G);
+  EXPL_CLK(3);
   // ---- S2: policy layer 1 rows
   for (int k = t; k < H; k += nt) v1[k] = ld_pub<WT>(g_h1p + k);
   __syncthreads();
   part(H, lo, hi);
   if (lo < hi)
     rows_matvec<true, WT>(a.pol + a.p_fc1_w, H, a.pol + a.p_fc1_b, v1, H, lo, hi, g_h2p, true);
+  EXPL_CLK(4);
   ok = group_sync<WT>(ctr + 1, G) && ok;
+  EXPL_CLK(5);
   // ---- S3: heads (every workgroup), a = tanh(mean), critic layer 0, its layer-1 rows
   for (int k = t; k < H; k += nt) v1[k] = ld_pub<WT>(g_h2p + k);
   __syncthreads();
@@ -210,6 +293,7 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
   __syncthreads();
   if (t < Da) x[Do + t] = tanhf(head[t]);
   __syncthreads();
+  EXPL_CLK(6);
   for (int e = t; e < nq * H; e += nt) {   // h1_i = relu(P_i + W0_i[:, Do:] a)
     const int i = e / H, n = e - i * H;
     const float* w = a.q[i] + a.q_fc0_w + (long)n * Dq + Do;
@@ -230,7 +314,9 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
       }
     }
   }
+  EXPL_CLK(7);
   ok = group_sync<WT>(ctr + 2, G) && ok;
+  EXPL_CLK(8);
   // ---- S4: Q, seeds, dh2 (every workgroup), then its columns of dh1
   for (int e = t; e < nq * H; e += nt) v1[e] = ld_pub<WT>(g_qh2 + e);
   __syncthreads();
@@ -284,12 +370,20 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
     v1[e] = v1[e] > 0.f ? sv : 0.f;
   }
   __syncthreads();
-  {   // dh1_i[k] = 1[h1_i[k] > 0] sum_n dh2_i[n] W1_i[n, k]: 32 columns at a time, the
-      // rows cut into threads/32 parts (thread: column c, part pp; coalesced along the
-      // columns), the parts added in order
+  {   // dh1_i[k] = 1[h1_i[k] > 0] sum_n dh2_i[n] W1_i[n, k] over the columns of the
+      // fixed parts this workgroup owns, 32 columns at a time, the rows cut into
+      // threads/32 parts (thread: column c, part pp; coalesced along the columns),
+      // the parts added in order; then the part's partial of da = dh1 . W0[:, Do:]
+      // (its columns in order), published for S5
     const int R = nq * H, c = t & 31, pp = t >> 5, np = nt >> 5;
     const int rows = (H + np - 1) / np;
-    part(R, lo, hi);
+    float* dcol = prt + nt;   // [R / G + 32] dh1 of this workgroup's columns
+    float* prod = dcol + (2 * H + G - 1) / G + 32;   // [part width][Da]
+    // this workgroup's parts are contiguous, p0 .. p1 - 1 (a function of G,
+    // but each part's partial is not)
+    const int p0 = wg * kExplParts / G, p1 = (wg + 1) * kExplParts / G;
+    lo = p0 * R / kExplParts;
+    hi = p1 * R / kExplParts;
     for (int cb = lo; cb < hi; cb += 32) {
       const int e = cb + c;
       float s = 0.f;
@@ -312,11 +406,29 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
       if (t < 32 && cb + t < hi) {
         float v = prt[t];
         for (int q = 1; q < np; ++q) v += prt[q * 32 + t];
-        st_pub<WT>(g_dh1 + cb + t, v2[cb + t] > 0.f ? v : 0.f);
+        dcol[cb - lo + t] = v2[cb + t] > 0.f ? v : 0.f;
+      }
+      __syncthreads();
+    }
+    for (int pq = p0; pq < p1; ++pq) {
+      // the part's da partial: every (column, j) product in one round of loads
+      // (thread e = column * Da + j), then its columns in order
+      const int plo = pq * R / kExplParts, phi = (pq + 1) * R / kExplParts;
+      for (int e = t; e < (phi - plo) * Da; e += nt) {
+        const int cl = e / Da, j = e - cl * Da, col = plo + cl;
+        const int i = col / H, k = col - i * H;
+        prod[e] = dcol[col - lo] * a.q[i][a.q_fc0_w + (long)k * Dq + Do + j];
+      }
+      __syncthreads();
+      if (t < Da) {
+        float s = 0.f;
+        for (int cl = 0; cl < phi - plo; ++cl) s += prod[cl * Da + t];
+        st_pub<WT>(g_dap + pq * 64 + t, s);
       }
       __syncthreads();
     }
   }
+  EXPL_CLK(9);
   if (wg != 0) {   // the group's other workgroups only publish (their arrival is the signal)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -330,26 +442,21 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
     return;
   }
   ok = group_sync<WT>(ctr + 3, G) && ok;
-  // ---- S5 (workgroup 0): da = dh1 . W0[:, Do:], grad, shift, sample
-  for (int e = t; e < nq * H; e += nt) v1[e] = ld_pub<WT>(g_dh1 + e);
-  __syncthreads();
-  float* da = prt;   // [nq][64]
-  {
-    const int lane = t & 63, wave = t >> 6, nw = nt >> 6;
-    for (int o = wave; o < nq * Da; o += nw) {
-      const int i = o / Da, j = o - i * Da;
-      const float* W0 = a.q[i] + a.q_fc0_w + Do + j;
-      float s = 0.f;
-      for (int n = lane; n < H; n += 64) s = fmaf(v1[i * H + n], W0[(long)n * Dq], s);
-      s = wsum64(s);
-      if (lane == 0) da[i * 64 + j] = s;
-    }
+  EXPL_CLK(10);
+  // ---- S5 (workgroup 0): da = the parts' partials in order, grad, shift, sample
+  float da = 0.f;
+  if (t < Da) {
+    float dp[kExplParts];   // every part's load in flight before the first add
+#pragma unroll
+    for (int q = 0; q < kExplParts; ++q) dp[q] = ld_pub<WT>(g_dap + q * 64 + t);
+#pragma unroll
+    for (int q = 0; q < kExplParts; ++q) da += dp[q];
   }
-  __syncthreads();
+  EXPL_CLK(11);
   float g = 0.f, sig = 0.f, sd = 0.f, mean = 0.f;
   if (t < Da) {
     const float act = x[Do + t];
-    g = (nq == 2 ? da[t] + da[64 + t] : da[t]) * (1.f - act * act);
+    g = da * (1.f - act * act);
     sd = expf(fminf(fmaxf(head[Da + t], -20.f), 2.f));
     sig = sd * sd;
     mean = head[t];
@@ -378,6 +485,7 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
     a.out[2 * nd + e] = sd;
     if (a.grad) a.grad[e] = g;
   }
+  EXPL_CLK(12);
   // a timed-out hand-off of this group is reported through the call's fail
   // word (and so through the completion word below)
   if (t == 0 && !ok && a.fail)
