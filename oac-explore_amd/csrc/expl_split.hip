@@ -107,30 +107,24 @@ __device__ __forceinline__ void rows_matvec(const float* __restrict__ W, long ld
 }
 
 // The group's hand-off: every storing wave drains its stores, the workgroup
-// meets, lane 0 arrives on the stage counter (FENCE: behind an agent release);
-// then every thread runs `pre` (the next stage's weight loads into LDS: their
-// round trips overlap the group's arrival skew and the poll), lane 0 polls the
-// counter (relaxed, bounded) until all G workgroups arrived (FENCE: then
+// meets, lane 0 arrives on the stage counter (FENCE: behind an agent release),
+// polls it (relaxed, bounded) until all G workgroups arrived (FENCE: then
 // acquires), and the workgroup meets again.
-struct NoPre { __device__ void operator()() const {} };
-template <bool WT, class Pre = NoPre>
-__device__ __forceinline__ bool group_sync(unsigned* ctr, unsigned target, Pre pre = Pre()) {
+template <bool WT>
+__device__ __forceinline__ bool group_sync(unsigned* ctr, unsigned target) {
   __shared__ int ok_s;
+  if (target <= 1) {   // G = 1: the workgroup's own barrier orders its scratch
+    __syncthreads();
+    return true;
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (target > 1 && threadIdx.x == 0) {
+  if (threadIdx.x == 0) {
     if constexpr (!WT) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  pre();
-  if (target <= 1) {   // G = 1: the workgroup's own barrier orders its scratch
-    __syncthreads();
-    return true;
-  }
-  if (threadIdx.x == 0) {
     int ok = 1;
     unsigned spins = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -147,45 +141,6 @@ __device__ __forceinline__ bool group_sync(unsigned* ctr, unsigned target, Pre p
   return ok_s != 0;
 }
 
-// A prefetch of up to 4 row blocks into LDS: segment s copies rows x cols
-// floats from src (row stride lds_src; published == sc1 loads in WT mode) to
-// dst (row stride ld_dst).  All segments share one flattened loop with 16
-// loads per thread in flight before the LDS stores.
-struct PfSeg { float* dst; const float* src; long ld_src; int rows, cols, ld_dst, published; };
-template <bool WT>
-__device__ __forceinline__ void pf_copy(const PfSeg* sg, int ns) {
-  long base[5];
-  base[0] = 0;
-  for (int i = 0; i < 4; ++i) base[i + 1] = base[i] + (i < ns ? (long)sg[i].rows * sg[i].cols : 0);
-  const long n = base[4];
-  const long nt = blockDim.x;
-  for (long e0 = threadIdx.x; e0 < n; e0 += 16 * nt) {
-    float v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const long e = e0 + u * nt;
-      v[u] = 0.f;
-      if (e < n) {
-        const int i = e >= base[1] ? (e >= base[2] ? (e >= base[3] ? 3 : 2) : 1) : 0;
-        const long l = e - base[i];
-        const int r = (int)(l / sg[i].cols), c = (int)(l - (long)r * sg[i].cols);
-        const float* p = sg[i].src + (long)r * sg[i].ld_src + c;
-        v[u] = sg[i].published ? ld_pub<WT>(p) : *p;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const long e = e0 + u * nt;
-      if (e < n) {
-        const int i = e >= base[1] ? (e >= base[2] ? (e >= base[3] ? 3 : 2) : 1) : 0;
-        const long l = e - base[i];
-        const int r = (int)(l / sg[i].cols), c = (int)(l - (long)r * sg[i].cols);
-        sg[i].dst[(long)r * sg[i].ld_dst + c] = v[u];
-      }
-    }
-  }
-}
-
 // the dh1 columns are cut into kExplParts fixed parts (never by the group
 // size): part p's partial of da is published, and S5 adds the parts in order
 constexpr int kExplParts = 32;
@@ -199,20 +154,7 @@ __host__ __device__ inline long expl_split_lds(int Do, int Da, int H, int thread
   const long w = (2L * H + kExplParts - 1) / kExplParts;
   return ((Do + Da + 3) & ~3L) + 4L * H + 64 + 128 + threads + (2L * H + 32) + w * 64;
 }
-constexpr int kWtLdsFloats = 36 * 1024;   // 144 KB: one workgroup per CU
-// floats of the stage-weight prefetch buffers for a group of G (WT mode):
-// S2 the workgroup's policy layer-1 rows; S3 the heads, the critics' action
-// columns, the obs projections and the workgroup's critic layer-1 rows; S4
-// the last layer(s) and the workgroup's dh1 columns of W1 and of W0[:, Do:]
-__host__ __device__ inline long expl_split_pf(int Da, int H, int nq, int Kq, int G) {
-  const long r1 = (H + G - 1) / G, r3 = (nq * (long)H + G - 1) / G;
-  const long c4 = ((long)kExplParts / G + 1) * ((nq * (long)H + kExplParts - 1) / kExplParts);
-  const long s2 = r1 * H;
-  const long s3 = 2L * Da * H + (long)nq * H * Da + (long)nq * H + r3 * H;
-  const long s4 = (long)Kq * H + c4 * (H + 1) + c4 * Da;
-  return s2 > s3 ? (s2 > s4 ? s2 : s4) : (s3 > s4 ? s3 : s4);
-}
-
+constexpr int kWtLdsFloats = 21 * 1024;   // 84 KB: one workgroup per CU
 template <bool WT>
 __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, int row0, int G,
                                                               float* scratch) {
@@ -228,6 +170,11 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
   const int gi = blockIdx.x / G, wg = blockIdx.x - gi * G;
   const int r = row0 + gi, t = threadIdx.x, nt = blockDim.x;
   const int nq = a.nq, KQ = a.K;
+  // the critics' parameter blocks in registers: a.q[i] with i per lane would be
+  // a vector load from the argument segment (and a wait) per use
+  const float* const q0p = a.q[0];
+  const float* const q1p = a.q[1];
+  auto Qp = [&](int i) { return i == 0 ? q0p : q1p; };
   float* Gv = scratch + (long)gi * expl_split_scratch(H);   // group's published vectors
   float* g_h1p = Gv;            // [H]   policy layer 0
   float* g_P = Gv + H;          // [2H]  critics' obs projections (+ b0)
@@ -268,7 +215,7 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
       const int b0 = (1 + i) * H, b1 = b0 + H;
       const int l = max(lo, b0), h = min(hi, b1);
       if (l < h) {
-        const float* q = a.q[i];
+        const float* q = Qp(i);
         rows_matvec<true, WT>(q + a.q_fc0_w, Dq, q + a.q_fc0_b, x, Do, l - b0, h - b0,
                               g_P + i * H, false);
       }
@@ -287,7 +234,9 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
   ok = group_sync<WT>(ctr + 1, G) && ok;
   EXPL_CLK(5);
   // ---- S3: heads (every workgroup), a = tanh(mean), critic layer 0, its layer-1 rows
+  // the published h2 and P_i: one round of loads
   for (int k = t; k < H; k += nt) v1[k] = ld_pub<WT>(g_h2p + k);
+  for (int e = t; e < nq * H; e += nt) v2[e] = ld_pub<WT>(g_P + e);
   __syncthreads();
   rows_matvec<false, WT>(a.pol + a.p_head_w, H, a.pol + a.p_head_b, v1, H, 0, 2 * Da, head, false);
   __syncthreads();
@@ -296,8 +245,8 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
   EXPL_CLK(6);
   for (int e = t; e < nq * H; e += nt) {   // h1_i = relu(P_i + W0_i[:, Do:] a)
     const int i = e / H, n = e - i * H;
-    const float* w = a.q[i] + a.q_fc0_w + (long)n * Dq + Do;
-    float s = ld_pub<WT>(g_P + e);
+    const float* w = Qp(i) + a.q_fc0_w + (long)n * Dq + Do;
+    float s = v2[e];
     for (int j = 0; j < Da; ++j) s = fmaf(w[j], x[Do + j], s);
     v2[e] = fmaxf(s, 0.f);
   }
@@ -308,7 +257,7 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
     for (int i = 0; i < nq; ++i) {
       const int l = max(lo, i * H), h = min(hi, (i + 1) * H);
       if (l < h) {
-        const float* q = a.q[i];
+        const float* q = Qp(i);
         rows_matvec<true, WT>(q + a.q_fc1_w, H, q + a.q_fc1_b, v2 + i * H, H, l - i * H,
                               h - i * H, g_qh2 + i * H, true);
       }
@@ -323,14 +272,14 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
   if (nq == 2) {
     const int wave = t >> 6, lane = t & 63;
     if (wave < 2) {
-      const float* q = a.q[wave];
+      const float* q = Qp(wave);
       float s = 0.f;
       for (int k = lane; k < H; k += 64) s = fmaf(q[a.q_last_w + k], v1[wave * H + k], s);
       s = wsum64(s);
       if (lane == 0) misc[wave] = s + q[a.q_last_b];
     }
   } else {
-    rows_matvec<false, WT>(a.q[0] + a.q_last_w, H, a.q[0] + a.q_last_b, v1, H, 0, KQ, qk, false);
+    rows_matvec<false, WT>(Qp(0) + a.q_last_w, H, Qp(0) + a.q_last_b, v1, H, 0, KQ, qk, false);
   }
   __syncthreads();
   if (t == 0) {
@@ -362,10 +311,10 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
     const int i = e / H, n = e - i * H;
     float sv;
     if (nq == 2) {
-      sv = misc[2 + i] * a.q[i][a.q_last_w + n];
+      sv = misc[2 + i] * Qp(i)[a.q_last_w + n];
     } else {
       sv = 0.f;
-      for (int k = 0; k < KQ; ++k) sv = fmaf(wk[k], a.q[0][a.q_last_w + (long)k * H + n], sv);
+      for (int k = 0; k < KQ; ++k) sv = fmaf(wk[k], Qp(0)[a.q_last_w + (long)k * H + n], sv);
     }
     v1[e] = v1[e] > 0.f ? sv : 0.f;
   }
@@ -389,7 +338,7 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
       float s = 0.f;
       if (e < hi) {
         const int i = e / H, k = e - i * H;
-        const float* W1 = a.q[i] + a.q_fc1_w + k;
+        const float* W1 = Qp(i) + a.q_fc1_w + k;
         const float* g = v1 + i * H;
         const int n_lo = min(H, pp * rows), n_hi = min(H, n_lo + rows);
         for (int n0 = n_lo; n0 < n_hi; n0 += 16) {
@@ -417,7 +366,7 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
       for (int e = t; e < (phi - plo) * Da; e += nt) {
         const int cl = e / Da, j = e - cl * Da, col = plo + cl;
         const int i = col / H, k = col - i * H;
-        prod[e] = dcol[col - lo] * a.q[i][a.q_fc0_w + (long)k * Dq + Do + j];
+        prod[e] = dcol[col - lo] * Qp(i)[a.q_fc0_w + (long)k * Dq + Do + j];
       }
       __syncthreads();
       if (t < Da) {

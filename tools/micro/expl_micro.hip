@@ -69,7 +69,16 @@ int main(int argc, char** argv) {
     a.done_seq = (unsigned)(c + 1);
     const auto t0 = std::chrono::steady_clock::now();
     CK(launch_expl_split(a, 0, 1, ws + 4096, s));
-    while (*(volatile unsigned*)done != a.done_seq) {}
+    // bounded: a failed call (bit 31) or a faulted launch ends the run
+    while ((*(volatile unsigned*)done & 0x7fffffffu) != a.done_seq) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2) ||
+          hipStreamQuery(s) != hipErrorNotReady) {
+        if ((*(volatile unsigned*)done & 0x7fffffffu) == a.done_seq) break;
+        printf("call %d: no completion (stream %s)\n", c, hipGetErrorString(hipStreamQuery(s)));
+        return 1;
+      }
+    }
+    if (*(volatile unsigned*)done & 0x80000000u) { printf("call %d: hand-off timed out\n", c); return 1; }
     const auto t1 = std::chrono::steady_clock::now();
     CK(hipStreamSynchronize(s));
     wall.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
