@@ -64,28 +64,71 @@ __device__ __forceinline__ float ld_pub(const float* p) {
   else return *p;
 }
 
+// The first pass of a wave's rows (its first RW rows, k < 64 U) and their
+// bias, loaded ahead -- during the hand-off before the stage -- by rows_pre
+// and used by rows_matvec in place of those loads (the same values, the same
+// order: the result is bitwise the same).
+constexpr int kRW = 4, kRU = 4;
+struct RowsPre { float wv[kRW][kRU]; float b; };
+__device__ __forceinline__ void rows_pre(const float* __restrict__ W, long ldw,
+                                         const float* __restrict__ b, int K, int n_lo, int n_hi,
+                                         RowsPre& p) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n0 = n_lo + wave * kRW;
+  if (n0 >= n_hi) return;
+#pragma unroll
+  for (int u = 0; u < kRU; ++u) {
+    const int k = u * 64 + lane, kc = k < K ? k : K - 1;
+#pragma unroll
+    for (int r = 0; r < kRW; ++r) p.wv[r][u] = W[(long)min(n0 + r, n_hi - 1) * ldw + kc];
+  }
+  p.b = b ? b[min(n0 + (lane < kRW ? lane : 0), n_hi - 1)] : 0.f;
+}
+
 // y[n] = act(W[n, :K] . x + b[n]) for n in [n_lo, n_hi): one wave per row,
 // RW rows of loads in flight, lanes along k (fixed-order butterfly sum).
-// PUB: y is a published vector (global), else LDS.
+// PUB: y is a published vector (global), else LDS.  pre: the wave's first
+// pass, loaded ahead (rows_pre), or null.
 template <bool PUB, bool WT>
 __device__ __forceinline__ void rows_matvec(const float* __restrict__ W, long ldw,
                                             const float* __restrict__ b, const float* x, int K,
-                                            int n_lo, int n_hi, float* y, bool relu) {
-  constexpr int RW = 4, U = 4;
+                                            int n_lo, int n_hi, float* y, bool relu,
+                                            const RowsPre* pre = nullptr) {
+  constexpr int RW = kRW, U = kRU;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // (read up front: a select between pre's and W's addresses would keep pre in memory)
+  float pw[RW][U], pb = 0.f;
+  if (pre) {
+    pb = pre->b;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < RW; ++r) pw[r][u] = pre->wv[r][u];
+  }
   for (int n0 = n_lo + wave * RW; n0 < n_hi; n0 += nw * RW) {
+    const bool first = pre && n0 == n_lo + wave * RW;
     float acc[RW];
 #pragma unroll
     for (int r = 0; r < RW; ++r) acc[r] = 0.f;
     for (int kb = 0; kb < K; kb += 64 * U) {
       float wv[RW][U], xv[U];
+      if (first && kb == 0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int r = 0; r < RW; ++r) wv[r][u] = pw[r][u];
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int kc = min(kb + u * 64 + lane, K - 1);
+#pragma unroll
+          for (int r = 0; r < RW; ++r) wv[r][u] = W[(long)min(n0 + r, n_hi - 1) * ldw + kc];
+        }
+      }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int k = kb + u * 64 + lane;
-        const int kc = k < K ? k : K - 1;
-        xv[u] = k < K ? x[kc] : 0.f;
-#pragma unroll
-        for (int r = 0; r < RW; ++r) wv[r][u] = W[(long)min(n0 + r, n_hi - 1) * ldw + kc];
+        xv[u] = k < K ? x[k < K ? k : K - 1] : 0.f;
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -98,7 +141,7 @@ __device__ __forceinline__ void rows_matvec(const float* __restrict__ W, long ld
       float v = acc[0];
 #pragma unroll
       for (int r = 1; r < RW; ++r) v = lane == r ? acc[r] : v;
-      v += b ? b[n0 + lane] : 0.f;
+      v += first ? pb : (b ? b[n0 + lane] : 0.f);
       v = relu ? fmaxf(v, 0.f) : v;
       if constexpr (PUB) st_pub<WT>(y + n0 + lane, v);
       else y[n0 + lane] = v;
@@ -106,26 +149,37 @@ __device__ __forceinline__ void rows_matvec(const float* __restrict__ W, long ld
   }
 }
 
-// The group's hand-off: every storing wave drains its stores, the workgroup
-// meets, lane 0 arrives on the stage counter (FENCE: behind an agent release),
-// polls it (relaxed, bounded) until all G workgroups arrived (FENCE: then
-// acquires), and the workgroup meets again.
+// The group's hand-off, in two halves so that the next stage's weight loads
+// can be issued between them (their round trips then overlap the group's
+// arrival skew and the poll).  group_arrive: every storing wave drains its
+// stores, the workgroup meets, the last wave's lane 0 arrives on the stage
+// counter (FENCE: behind an agent release).  group_wait: that lane polls the
+// counter (relaxed, bounded) until all G workgroups arrived (FENCE: then
+// acquires), and the workgroup meets again.  G = 1: the workgroup's own
+// barriers order its scratch.  The last wave issues no loads ahead.
 template <bool WT>
-__device__ __forceinline__ bool group_sync(unsigned* ctr, unsigned target) {
-  __shared__ int ok_s;
-  if (target <= 1) {   // G = 1: the workgroup's own barrier orders its scratch
-    __syncthreads();
-    return true;
-  }
+__device__ __forceinline__ void group_arrive(unsigned* ctr, unsigned target) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  // (the polling wave arrives too: a wave with the add in flight waits for it
+  // before its next loads)
+  if (target > 1 && threadIdx.x == blockDim.x - 64) {
     if constexpr (!WT) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int ok = 1;
+  }
+}
+template <bool WT>
+__device__ __forceinline__ bool group_wait(unsigned* ctr, unsigned target) {
+  __shared__ int ok_s;
+  if (target <= 1) {
+    __syncthreads();
+    return true;
+  }
+  if (threadIdx.x == blockDim.x - 64) {   // (vmcnt is in order: a poll behind loads
+    int ok = 1;                            // ahead would wait for them)
     unsigned spins = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
       __builtin_amdgcn_s_sleep(1);
@@ -139,6 +193,11 @@ __device__ __forceinline__ bool group_sync(unsigned* ctr, unsigned target) {
   }
   __syncthreads();
   return ok_s != 0;
+}
+template <bool WT>
+__device__ __forceinline__ bool group_sync(unsigned* ctr, unsigned target) {
+  group_arrive<WT>(ctr, target);
+  return group_wait<WT>(ctr, target);
 }
 
 // the dh1 columns are cut into kExplParts fixed parts (never by the group
@@ -190,51 +249,61 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
   float* qk = misc + 16;                   // [16] K head values
   float* wk = qk + 16;                     // [16] K head seeds
   float* red = misc + 64;                  // [64]
-  float* prt = misc + 128;                 // [threads] dh1 partials, then a part's dh1 columns
+  float* prt = misc + 128;                 // [threads] dh1 partials
   __shared__ long long cnt_s;
   if (t == 0) cnt_s = a.state->expl_counter;
-  EXPL_CLK(0);
-  for (int k = t; k < Do; k += nt) x[k] = a.obs[(long)r * a.ld_obs + k];
-  __syncthreads();
-  EXPL_CLK(1);
   // rows of a length-L product owned by this workgroup
   auto part = [&](int L, int& lo, int& hi) {
     const int per = (L + G - 1) / G;
     lo = min(L, wg * per);
     hi = min(L, lo + per);
   };
-  int lo, hi;
+  // the part [l, h) of rows [b0, b0 + L) within the range [lo, hi)
+  auto clip = [](int lo, int hi, int b0, int L, int& l, int& h) {
+    l = max(lo, b0) - b0;
+    h = min(hi, b0 + L) - b0;
+  };
+  int lo1, hi1, lo2, hi2, lo3, hi3;
+  part((1 + nq) * H, lo1, hi1);
+  part(H, lo2, hi2);
+  part(nq * H, lo3, hi3);
+  const int e01 = min(hi1, H);   // S1 policy rows [lo1, e01)
+  // S2's and S4's first weight loads are issued ahead, during the hand-off
+  // before the stage (the group's arrival skew and the poll), into registers:
+  // the stage then starts on its published inputs' round trip alone.  (S3's
+  // -- heads, W0_i[:, Do:], its layer-1 rows, ~47 loads per wave -- made
+  // hand-off 1 longer by more than they saved.)
+  RowsPre pre;
+  EXPL_CLK(0);
+  for (int k = t; k < Do; k += nt) x[k] = a.obs[(long)r * a.ld_obs + k];
+  __syncthreads();
+  EXPL_CLK(1);
   // ---- S1: policy layer 0 | critic obs projections (3H or 2H rows)
-  {
-    const int R = (1 + nq) * H;
-    part(R, lo, hi);
-    const int e0 = min(hi, H);   // policy rows [lo, e0)
-    if (lo < e0)
-      rows_matvec<true, WT>(a.pol + a.p_fc0_w, Do, a.pol + a.p_fc0_b, x, Do, lo, e0, g_h1p, true);
-    for (int i = 0; i < nq; ++i) {
-      const int b0 = (1 + i) * H, b1 = b0 + H;
-      const int l = max(lo, b0), h = min(hi, b1);
-      if (l < h) {
-        const float* q = Qp(i);
-        rows_matvec<true, WT>(q + a.q_fc0_w, Dq, q + a.q_fc0_b, x, Do, l - b0, h - b0,
-                              g_P + i * H, false);
-      }
+  if (lo1 < e01)
+    rows_matvec<true, WT>(a.pol + a.p_fc0_w, Do, a.pol + a.p_fc0_b, x, Do, lo1, e01, g_h1p, true);
+  for (int i = 0; i < nq; ++i) {
+    int l, h;
+    clip(lo1, hi1, (1 + i) * H, H, l, h);
+    if (l < h) {
+      const float* q = Qp(i);
+      rows_matvec<true, WT>(q + a.q_fc0_w, Dq, q + a.q_fc0_b, x, Do, l, h, g_P + i * H, false);
     }
   }
   EXPL_CLK(2);
-  bool ok = group_sync<WT>(ctr + 0, G);
+  group_arrive<WT>(ctr + 0, G);
+  if (lo2 < hi2) rows_pre(a.pol + a.p_fc1_w, H, a.pol + a.p_fc1_b, H, lo2, hi2, pre);
+  bool ok = group_wait<WT>(ctr + 0, G);
   EXPL_CLK(3);
   // ---- S2: policy layer 1 rows
   for (int k = t; k < H; k += nt) v1[k] = ld_pub<WT>(g_h1p + k);
   __syncthreads();
-  part(H, lo, hi);
-  if (lo < hi)
-    rows_matvec<true, WT>(a.pol + a.p_fc1_w, H, a.pol + a.p_fc1_b, v1, H, lo, hi, g_h2p, true);
+  if (lo2 < hi2)
+    rows_matvec<true, WT>(a.pol + a.p_fc1_w, H, a.pol + a.p_fc1_b, v1, H, lo2, hi2, g_h2p, true, &pre);
   EXPL_CLK(4);
   ok = group_sync<WT>(ctr + 1, G) && ok;
   EXPL_CLK(5);
   // ---- S3: heads (every workgroup), a = tanh(mean), critic layer 0, its layer-1 rows
-  // the published h2 and P_i: one round of loads
+  // (the published h2 and P_i: one round of loads)
   for (int k = t; k < H; k += nt) v1[k] = ld_pub<WT>(g_h2p + k);
   for (int e = t; e < nq * H; e += nt) v2[e] = ld_pub<WT>(g_P + e);
   __syncthreads();
@@ -251,20 +320,56 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
     v2[e] = fmaxf(s, 0.f);
   }
   __syncthreads();
-  {
-    const int R = nq * H;
-    part(R, lo, hi);
-    for (int i = 0; i < nq; ++i) {
-      const int l = max(lo, i * H), h = min(hi, (i + 1) * H);
-      if (l < h) {
-        const float* q = Qp(i);
-        rows_matvec<true, WT>(q + a.q_fc1_w, H, q + a.q_fc1_b, v2 + i * H, H, l - i * H,
-                              h - i * H, g_qh2 + i * H, true);
-      }
+  for (int i = 0; i < nq; ++i) {
+    int l, h;
+    clip(lo3, hi3, i * H, H, l, h);
+    if (l < h) {
+      const float* q = Qp(i);
+      rows_matvec<true, WT>(q + a.q_fc1_w, H, q + a.q_fc1_b, v2 + i * H, H, l, h, g_qh2 + i * H, true);
     }
   }
   EXPL_CLK(7);
-  ok = group_sync<WT>(ctr + 2, G) && ok;
+  // S4 ahead: the last layers (Q dot: waves 0 and 1; dh2: this thread's
+  // element), the first column block's rows of W1 and the first part's
+  // (column, j) elements of W0_i[:, Do:]
+  const int R4 = nq * H, c4 = t & 31, pp4 = t >> 5, np4 = nt >> 5;
+  const int rows4 = (H + np4 - 1) / np4;
+  // this workgroup's parts are contiguous, p0 .. p1 - 1 (a function of G,
+  // but each part's partial is not)
+  const int p0 = wg * kExplParts / G, p1 = (wg + 1) * kExplParts / G;
+  const int lo4 = p0 * R4 / kExplParts, hi4 = p1 * R4 / kExplParts;
+  const bool pre_q = nq == 2 && H <= 64 * kRU && R4 <= nt;
+  const bool pre_c = rows4 <= 16 && t < nt - 64;   // (per thread: not the polling wave)
+  float wq[kRU], qb = 0.f, wd = 0.f, w1[16], wda = 0.f;
+  group_arrive<WT>(ctr + 2, G);
+  if (pre_q) {
+    const int wave = t >> 6, lane = t & 63;
+    if (wave < 2) {
+      const float* q = Qp(wave);
+#pragma unroll
+      for (int u = 0; u < kRU; ++u) wq[u] = q[a.q_last_w + min(lane + 64 * u, H - 1)];
+      qb = q[a.q_last_b];
+    }
+    if (t < R4) {
+      const int i = t / H;
+      wd = Qp(i)[a.q_last_w + (t - i * H)];
+    }
+  }
+  const int e = lo4 + c4;
+  if (pre_c && e < hi4) {
+    const int i = e / H, k = e - i * H;
+    const float* W1 = Qp(i) + a.q_fc1_w + k;
+    const int n_lo = min(H, pp4 * rows4), n_hi = min(H, n_lo + rows4);
+#pragma unroll
+    for (int u = 0; u < 16; ++u) w1[u] = W1[(long)max(0, min(n_lo + u, n_hi - 1)) * H];
+  }
+  const int plo = p0 * R4 / kExplParts, phi = (p0 + 1) * R4 / kExplParts;
+  if (p0 < p1 && t < (phi - plo) * Da) {
+    const int cl = t / Da, j = t - cl * Da, col = plo + cl;
+    const int i = col / H, k = col - i * H;
+    wda = Qp(i)[a.q_fc0_w + (long)k * Dq + Do + j];
+  }
+  ok = group_wait<WT>(ctr + 2, G) && ok;
   EXPL_CLK(8);
   // ---- S4: Q, seeds, dh2 (every workgroup), then its columns of dh1
   for (int e = t; e < nq * H; e += nt) v1[e] = ld_pub<WT>(g_qh2 + e);
@@ -274,9 +379,15 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
     if (wave < 2) {
       const float* q = Qp(wave);
       float s = 0.f;
-      for (int k = lane; k < H; k += 64) s = fmaf(q[a.q_last_w + k], v1[wave * H + k], s);
+      if (pre_q) {
+#pragma unroll
+        for (int u = 0; u < kRU; ++u)
+          if (lane + 64 * u < H) s = fmaf(wq[u], v1[wave * H + lane + 64 * u], s);
+      } else {
+        for (int k = lane; k < H; k += 64) s = fmaf(q[a.q_last_w + k], v1[wave * H + k], s);
+      }
       s = wsum64(s);
-      if (lane == 0) misc[wave] = s + q[a.q_last_b];
+      if (lane == 0) misc[wave] = s + (pre_q ? qb : q[a.q_last_b]);
     }
   } else {
     rows_matvec<false, WT>(Qp(0) + a.q_last_w, H, Qp(0) + a.q_last_b, v1, H, 0, KQ, qk, false);
@@ -307,16 +418,21 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
     }
   }
   __syncthreads();
-  for (int e = t; e < nq * H; e += nt) {   // dh2 (in v1)
-    const int i = e / H, n = e - i * H;
-    float sv;
-    if (nq == 2) {
-      sv = misc[2 + i] * Qp(i)[a.q_last_w + n];
-    } else {
-      sv = 0.f;
-      for (int k = 0; k < KQ; ++k) sv = fmaf(wk[k], Qp(0)[a.q_last_w + (long)k * H + n], sv);
+  if (pre_q) {   // dh2 (in v1)
+    const int i = t / H;
+    if (t < R4) v1[t] = v1[t] > 0.f ? misc[2 + i] * wd : 0.f;
+  } else {
+    for (int e = t; e < R4; e += nt) {
+      const int i = e / H, n = e - i * H;
+      float sv;
+      if (nq == 2) {
+        sv = misc[2 + i] * Qp(i)[a.q_last_w + n];
+      } else {
+        sv = 0.f;
+        for (int k = 0; k < KQ; ++k) sv = fmaf(wk[k], Qp(0)[a.q_last_w + (long)k * H + n], sv);
+      }
+      v1[e] = v1[e] > 0.f ? sv : 0.f;
     }
-    v1[e] = v1[e] > 0.f ? sv : 0.f;
   }
   __syncthreads();
   {   // dh1_i[k] = 1[h1_i[k] > 0] sum_n dh2_i[n] W1_i[n, k] over the columns of the
@@ -324,49 +440,48 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
       // threads/32 parts (thread: column c, part pp; coalesced along the columns),
       // the parts added in order; then the part's partial of da = dh1 . W0[:, Do:]
       // (its columns in order), published for S5
-    const int R = nq * H, c = t & 31, pp = t >> 5, np = nt >> 5;
-    const int rows = (H + np - 1) / np;
     float* dcol = prt + nt;   // [R / G + 32] dh1 of this workgroup's columns
     float* prod = dcol + (2 * H + G - 1) / G + 32;   // [part width][Da]
-    // this workgroup's parts are contiguous, p0 .. p1 - 1 (a function of G,
-    // but each part's partial is not)
-    const int p0 = wg * kExplParts / G, p1 = (wg + 1) * kExplParts / G;
-    lo = p0 * R / kExplParts;
-    hi = p1 * R / kExplParts;
-    for (int cb = lo; cb < hi; cb += 32) {
-      const int e = cb + c;
+    for (int cb = lo4; cb < hi4; cb += 32) {
+      const int e = cb + c4;
       float s = 0.f;
-      if (e < hi) {
+      if (e < hi4) {
         const int i = e / H, k = e - i * H;
         const float* W1 = Qp(i) + a.q_fc1_w + k;
         const float* g = v1 + i * H;
-        const int n_lo = min(H, pp * rows), n_hi = min(H, n_lo + rows);
+        const int n_lo = min(H, pp4 * rows4), n_hi = min(H, n_lo + rows4);
         for (int n0 = n_lo; n0 < n_hi; n0 += 16) {
           float w[16];
+          if (pre_c && cb == lo4) {
 #pragma unroll
-          for (int u = 0; u < 16; ++u) w[u] = W1[(long)min(n0 + u, n_hi - 1) * H];
+            for (int u = 0; u < 16; ++u) w[u] = w1[u];
+          } else {
+#pragma unroll
+            for (int u = 0; u < 16; ++u) w[u] = W1[(long)min(n0 + u, n_hi - 1) * H];
+          }
 #pragma unroll
           for (int u = 0; u < 16; ++u)
             if (n0 + u < n_hi) s = fmaf(g[n0 + u], w[u], s);
         }
       }
-      prt[pp * 32 + c] = s;
+      prt[pp4 * 32 + c4] = s;
       __syncthreads();
-      if (t < 32 && cb + t < hi) {
+      if (t < 32 && cb + t < hi4) {
         float v = prt[t];
-        for (int q = 1; q < np; ++q) v += prt[q * 32 + t];
-        dcol[cb - lo + t] = v2[cb + t] > 0.f ? v : 0.f;
+        for (int q = 1; q < np4; ++q) v += prt[q * 32 + t];
+        dcol[cb - lo4 + t] = v2[cb + t] > 0.f ? v : 0.f;
       }
       __syncthreads();
     }
     for (int pq = p0; pq < p1; ++pq) {
       // the part's da partial: every (column, j) product in one round of loads
       // (thread e = column * Da + j), then its columns in order
-      const int plo = pq * R / kExplParts, phi = (pq + 1) * R / kExplParts;
+      const int plo = pq * R4 / kExplParts, phi = (pq + 1) * R4 / kExplParts;
       for (int e = t; e < (phi - plo) * Da; e += nt) {
         const int cl = e / Da, j = e - cl * Da, col = plo + cl;
         const int i = col / H, k = col - i * H;
-        prod[e] = dcol[col - lo] * Qp(i)[a.q_fc0_w + (long)k * Dq + Do + j];
+        const float w = pq == p0 && e == t ? wda : Qp(i)[a.q_fc0_w + (long)k * Dq + Do + j];
+        prod[e] = dcol[col - lo4] * w;
       }
       __syncthreads();
       if (t < Da) {
