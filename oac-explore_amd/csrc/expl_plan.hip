@@ -331,7 +331,13 @@ int oac_expl_action_now(oac_expl* h, const float* eps, float beta_UB, float delt
   if (p.seq == 0) p.seq = 1;           // 0 is the word's initial value
   a.done = p.hc_done;
   a.done_seq = p.seq;
-  if (expl_launch(p, a, s)) return 1;
+  if (p.N == 1 && p.Do <= kExplObsArg) {   // one observation: it travels in the arguments
+    ExplObsArg o;
+    std::memcpy(o.v, p.hc_obs, sizeof(float) * p.Do);
+    OAC_HIP_CHECK(launch_expl_split_obs(a, o, p.ws + p.o_split, s));
+  } else if (expl_launch(p, a, s)) {
+    return 1;
+  }
   return expl_wait(p, a.done_seq, s);
 }
 

@@ -214,9 +214,10 @@ __host__ __device__ inline long expl_split_lds(int Do, int Da, int H, int thread
   return ((Do + Da + 3) & ~3L) + 4L * H + 64 + 128 + threads + (2L * H + 32) + w * 64;
 }
 constexpr int kWtLdsFloats = 21 * 1024;   // 84 KB: one workgroup per CU
-template <bool WT>
+// OBS: the (single) observation is the argument `oa` (launch_expl_split_obs)
+template <bool WT, bool OBS>
 __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, int row0, int G,
-                                                              float* scratch) {
+                                                              float* scratch, ExplObsArg oa) {
   float* sm;
   if constexpr (WT) {
     __shared__ __attribute__((aligned(16))) float sm_wt[kWtLdsFloats];
@@ -275,7 +276,11 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
   // hand-off 1 longer by more than they saved.)
   RowsPre pre;
   EXPL_CLK(0);
-  for (int k = t; k < Do; k += nt) x[k] = a.obs[(long)r * a.ld_obs + k];
+  if constexpr (OBS) {
+    for (int k = t; k < Do; k += nt) x[k] = oa.v[k];
+  } else {
+    for (int k = t; k < Do; k += nt) x[k] = a.obs[(long)r * a.ld_obs + k];
+  }
   __syncthreads();
   EXPL_CLK(1);
   // ---- S1: policy layer 0 | critic obs projections (3H or 2H rows)
@@ -627,13 +632,27 @@ hipError_t launch_expl_split(const ExplFusedArgs& a, int row0, int n_rows, float
   const long lds = expl_split_lds(a.Do, a.Da, a.H, nt);
   // write-through hand-offs need every workgroup of the launch on a CU of its own
   const bool wt = G > 1 && (long)n_rows * G <= expl_device_cus() && lds <= kWtLdsFloats;
+  static const ExplObsArg none{};   // (unread)
   if (wt) {
-    OAC_LAUNCH(oac_expl_split_kernel<true>, dim3(n_rows * G), dim3(nt), 0, s, a, row0, G, scratch);
+    OAC_LAUNCH((oac_expl_split_kernel<true, false>), dim3(n_rows * G), dim3(nt), 0, s, a, row0, G,
+               scratch, none);
   } else {
     if (lds * sizeof(float) > 64 * 1024) return hipErrorInvalidValue;
-    OAC_LAUNCH(oac_expl_split_kernel<false>, dim3(n_rows * G), dim3(nt), lds * sizeof(float), s, a,
-               row0, G, scratch);
+    OAC_LAUNCH((oac_expl_split_kernel<false, false>), dim3(n_rows * G), dim3(nt), lds * sizeof(float),
+               s, a, row0, G, scratch, none);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_expl_split_obs(const ExplFusedArgs& a, const ExplObsArg& obs, float* scratch,
+                                 hipStream_t s) {
+  if (a.n != 1 || a.Do > kExplObsArg || a.Da < 1 || a.Da > 63 || a.H < 1 || a.K > 16)
+    return hipErrorInvalidValue;
+  const int nt = expl_split_threads();
+  const int G = expl_split_group(1);
+  const long lds = expl_split_lds(a.Do, a.Da, a.H, nt);
+  if (!(G > 1 && G <= expl_device_cus() && lds <= kWtLdsFloats)) return launch_expl_split(a, 0, 1, scratch, s);
+  OAC_LAUNCH((oac_expl_split_kernel<true, true>), dim3(G), dim3(nt), 0, s, a, 0, G, scratch, obs);
   return hipGetLastError();
 }
 

@@ -139,6 +139,13 @@ size_t expl_split_lds_bytes(int Do, int Da, int H);
 long expl_split_scratch_floats(int H);
 hipError_t launch_expl_split(const ExplFusedArgs& a, int row0, int n_rows, float* scratch,
                              hipStream_t s);
+// the single-observation call with the observation inside the kernel
+// arguments (the argument segment is written with the launch: no read of the
+// host-coherent row from the kernel), Do <= kExplObsArg
+constexpr int kExplObsArg = 512;
+struct ExplObsArg { float v[kExplObsArg]; };
+hipError_t launch_expl_split_obs(const ExplFusedArgs& a, const ExplObsArg& obs, float* scratch,
+                                 hipStream_t s);
 
 // row-wise network evaluation off the gradient step (mlp_eval.hip)
 struct MlpEvalArgs {

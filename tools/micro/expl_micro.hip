@@ -4,7 +4,7 @@
 // outputs in host-coherent memory, the host polling the completion word).
 // Prints the per-stage wall clock of the group's first and last workgroup
 // (100 MHz counter, median over the calls) and the host wall per call.
-// Build: tools/micro/Makefile.  Run: tools/micro/expl_micro [calls]
+// Build: tools/micro/Makefile.  Run: tools/micro/expl_micro [calls] [obs in arguments 0|1]
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <chrono>
@@ -31,6 +31,7 @@ static float* dev_rand(size_t n, unsigned seed, float scale) {
 
 int main(int argc, char** argv) {
   const int calls = argc > 1 ? atoi(argv[1]) : 200;
+  const bool obs_arg = argc > 2 && atoi(argv[2]) != 0;   // the observation in the arguments
   const int Do = 376, Da = 17, H = 256, Dq = Do + Da;
   // parameter blocks: policy [fc0 | fc1 | head], critics [fc0 | fc1 | last]
   const long p0w = 0, p0b = p0w + (long)H * Do, p1w = p0b + H, p1b = p1w + (long)H * H,
@@ -68,7 +69,13 @@ int main(int argc, char** argv) {
   for (int c = 0; c < calls; ++c) {
     a.done_seq = (unsigned)(c + 1);
     const auto t0 = std::chrono::steady_clock::now();
-    CK(launch_expl_split(a, 0, 1, ws + 4096, s));
+    if (obs_arg) {
+      ExplObsArg o;
+      memcpy(o.v, obs, sizeof(float) * Do);
+      CK(launch_expl_split_obs(a, o, ws + 4096, s));
+    } else {
+      CK(launch_expl_split(a, 0, 1, ws + 4096, s));
+    }
     // bounded: a failed call (bit 31) or a faulted launch ends the run
     while ((*(volatile unsigned*)done & 0x7fffffffu) != a.done_seq) {
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2) ||
@@ -92,7 +99,7 @@ int main(int argc, char** argv) {
   const char* names[13] = {"start", "obs read", "S1 compute", "hand-off 0", "S2 compute", "hand-off 1",
                            "heads+tanh", "S3 rest", "hand-off 2", "S4 compute", "hand-off 3",
                            "S5 da", "S5 rest"};
-  printf("group of %d workgroups; host wall per call %.1f us (median of %d)\n", G, medd(wall), calls);
+  printf("obs %s; group of %d workgroups; host wall per call %.1f us (median of %d)\n", obs_arg ? "in arguments" : "host row", G, medd(wall), calls);
   printf("stage (us, from workgroup 0's start; median): wg0 / last wg\n");
   std::vector<long long> base = clk[0];
   {
