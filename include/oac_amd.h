@@ -184,6 +184,14 @@ int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags,
 /* the staging + H2D copy of step_host_idx alone (the data-parallel step then
  * runs its phases and all-reduces on the same stream) */
 int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream);
+/* the data-parallel drop-in step as one call (rl_algorithm.py:160-167 at
+ * world_size > 1): the caller captures one step -- the phases below and its
+ * collectives -- into a graph on its own collective library and hands the
+ * instantiated graph (hipGraphExec_t) to the handle; oac_sac_step_host_idx
+ * then stages the indices and launches that graph on `stream`, exactly as the
+ * single-process step launches its own.  NULL detaches it (the caller still
+ * owns the graph and destroys it after the last step that launched it). */
+int oac_sac_set_step_graph(oac_sac* h, void* graph_exec);
 /* data-parallel split (config.world_size > 1): phase 0 = forward through the
  * policy sample and the local sum(logp + target_entropy) as per-16-row
  * partials into the workspace buffer OAC_WS_LOGP_PART (ceil(B / 16) floats):

@@ -29,6 +29,8 @@ struct PlanBase {
   int graph_flags = -1;
   int graph_n = 0;          // steps captured in the graph
   hipStream_t cap_stream = nullptr;   // capture stream (graphs launch on the caller's stream)
+  // the caller's captured data-parallel step (oac_sac_set_step_graph; not owned)
+  hipGraphExec_t ext_exec = nullptr;
   int launches = 0;
   // drop-in host-index staging (oac_sac_set_host_ring): pinned [slots][B] int32,
   // one completion event per 16-slot chunk, recorded when staging leaves the

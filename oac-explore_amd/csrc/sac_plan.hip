@@ -835,8 +835,20 @@ int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* str
   return stage_host_idx(h, idx, bc, stream, h && h->plan.rows_direct);
 }
 
+int oac_sac_set_step_graph(oac_sac* h, void* graph_exec) {
+  if (!h) { set_error("null handle"); return 1; }
+  h->plan.ext_exec = reinterpret_cast<hipGraphExec_t>(graph_exec);
+  return 0;
+}
+
 int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags, void* stream) {
   if (!h) { set_error("null handle"); return 1; }
+  SacPlan& p = h->plan;
+  if (p.ext_exec) {   // the caller's captured step (phases + collectives)
+    if (stage_host_idx(h, idx, bc, stream, p.rows_direct)) return 1;
+    OAC_HIP_CHECK(hipGraphLaunch(p.ext_exec, reinterpret_cast<hipStream_t>(stream)));
+    return 0;
+  }
   const bool hr = h->plan.idx_host;
   if (stage_host_idx(h, idx, bc, stream, hr || h->plan.rows_direct)) return 1;
   return oac_sac_step_n(h, flags | OAC_STEP_GATHER | OAC_STEP_USE_GRAPH | (hr ? kStepHostIdx : 0), 1,

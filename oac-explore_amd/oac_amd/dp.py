@@ -130,6 +130,7 @@ class _DataParallel:
         self._overlap = (dist.get_backend(process_group) == "nccl" and self.world > 1
                          and os.environ.get("OAC_DP_OVERLAP", "1") != "0")
         self._graphs, self._eager_seen = {}, set()
+        self._attached = {}   # plan handles a captured step graph is attached to
         self._closed = False
         super().__init__(*args, **kwargs)
         # make sure every rank starts from rank 0's state
@@ -149,6 +150,9 @@ class _DataParallel:
         if not self._graphs and not self._eager_seen:
             return
         torch.cuda.synchronize(self.device)
+        for h in self._attached.values():   # the handles launch the step graphs: detach first
+            check(_lib.lib().oac_sac_set_step_graph(h, None))
+        self._attached.clear()
         self._graphs.clear()
         self._eager_seen.clear()
         torch.cuda.synchronize(self.device)
@@ -202,9 +206,14 @@ class _DataParallel:
 
     def _train_host_indices(self, dbatch):
         """The drop-in call (random_batch + train per step) at world > 1: this
-        rank's host-drawn indices are staged into the pinned ring and copied to
-        the device index ring on the trainer stream, then the captured
-        one-step data-parallel graph (phases + the three all-reduces) runs."""
+        rank's host-drawn indices are staged into the plan's ring, then the
+        one-step data-parallel graph (phases + the three all-reduces) runs.
+        The first call runs eager, the second captures; from then on the
+        captured graph is attached to the handle and a call is one library
+        call (staging + graph launch on torch's current stream), as in the
+        single-process step -- through torch's replay and the stream hop the
+        Python-side call cost ~40 us per step (B=256 at one rank: 7,294 ->
+        10,183 steps/s against 10,488 single-process)."""
         plan = self._dropin_plan(dbatch)
         if self._bc_mirror is None:
             torch.cuda.current_stream(self.device).wait_stream(self.stream)
@@ -213,6 +222,25 @@ class _DataParallel:
         if idx.dtype != np.int64 or not idx.flags.c_contiguous:
             idx = np.ascontiguousarray(idx, dtype=np.int64)
         bc = self._bc_mirror
+        key = (id(plan), _lib.OAC_STEP_GATHER | _lib.OAC_STEP_DEVICE_EPS, 1)
+        if self.capture and key in self._graphs and not self._closed:
+            # the captured step attached to the handle: staging + one graph
+            # launch on torch's current stream in one library call, as the
+            # single-process drop-in step (no stream hop, no replay prologue)
+            if plan.handle.value not in self._attached:
+                check(_lib.lib().oac_sac_set_step_graph(
+                    plan.handle, ctypes.c_void_p(self._graphs[key].raw_cuda_graph_exec())))
+                self._attached[plan.handle.value] = plan.handle
+            check(_lib.lib().oac_sac_step_host_idx(
+                plan.handle, ctypes.c_void_p(idx.ctypes.data), bc, 0,
+                _lib.stream_ptr(torch.cuda.current_stream(self.device))))
+            self._bc_mirror = bc + 1
+            self._last_plan = plan
+            if self._need_to_update_eval_statistics:
+                self._need_to_update_eval_statistics = False
+                self._fill_eval_statistics(plan)
+            self._n_train_steps_total += 1
+            return
 
         def stage(sp):
             check(_lib.lib().oac_sac_stage_host_idx(plan.handle, ctypes.c_void_p(idx.ctypes.data),

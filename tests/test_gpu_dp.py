@@ -350,6 +350,62 @@ def _dropin_worker(rank, world, port, q, dropin):
     dist.destroy_process_group()
 
 
+def _dropin_loop(tr, seed=1, steps=140):
+    from oac_amd import ReplayBuffer
+    from gpu_helpers import Space
+    rb = ReplayBuffer(500, Space(Do), Space(Da), device="cuda:0")
+    d = synthetic_transitions(500, Do, Da, seed=0)
+    rb.add_paths([dict(observations=d["observations"], actions=d["actions"],
+                       rewards=d["rewards"], next_observations=d["next_observations"],
+                       terminals=d["terminals"])])
+    np.random.seed(seed)
+    for _ in range(steps):        # past the 128-slot staging ring
+        b = rb.random_batch(BL)
+        b["buffer"] = rb
+        tr.train(b)
+    torch.cuda.synchronize()
+    return torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy()
+
+
+def _nccl_dropin_worker(port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    tr = _trainer("rccl1")   # the all-reduces issued through RCCL although world size is 1
+    got = _dropin_loop(tr)
+    q.put((got, len(tr._attached)))
+    tr.close()
+    assert not tr._attached
+    dist.destroy_process_group()
+
+
+def test_dp_rccl_dropin_step_graph_equals_single_gpu():
+    """The drop-in loop on the data-parallel trainer over RCCL (one rank): from
+    the third call on, the captured step (phases + RCCL all-reduces) is
+    attached to the handle and each train() is one library call (staging +
+    graph launch); 140 steps across the staging ring's wrap equal the
+    single-process drop-in step."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    p = ctx.Process(target=_nccl_dropin_worker, args=(port, q))
+    p.start()
+    p.join(timeout=150)
+    assert p.exitcode == 0, p.exitcode
+    got, n_attached = q.get()
+    assert n_attached == 1
+    want = _dropin_loop(_trainer(False))
+    assert parity.rel_err(got, want) < 1e-6, parity.rel_err(got, want)
+
+
 def test_dp_dropin_loop_equals_device_index_path():
     """rl_algorithm.py:160-167 on every rank (own replay shard, own numpy
     seed): the staged host-index path equals the device-index path."""
