@@ -3,6 +3,11 @@
 // /root/reference/optimistic_exploration.py:14-109): twin critics, or one K-head critic with mean + beta std or the trainer_UB
 // sorted head).
 //
+// Two kernels: oac_expl_twin_kernel (further down) takes twin critics -- the
+// SAC / OAC trainers' exploration -- with one polled hand-off and one
+// last-arrival; oac_expl_split_kernel below takes every call (the K-head
+// critic of share_layers, dims past the twin kernel's budget) with four.
+//
 // The round-1 kernel (one workgroup per observation, tools/micro/retired/
 // expl_fused.hip) streamed the row's 2.7 MB of weights (Humanoid dims) through
 // one CU at 45-110 GB/s per layer: ~59 us of a ~100 us call.  Here the
@@ -45,10 +50,25 @@ __device__ long long g_expl_clock[64];
 #define EXPL_CLK(i) do {} while (0)
 #endif
 
+// Sum over the 64 lanes of a wave, in every lane: DPP adds within each row of
+// 16 lanes (pairs, quads, mirrored halves, mirrored rows), then the four row
+// sums read out in lane order -- a fixed order, and no LDS-crossbar round
+// trip per step (the xor butterfly's ds_bpermute took ~6 of them).
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float wsum64(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = dpp_add<0xB1>(v);    // quad_perm [1,0,3,2]
+  v = dpp_add<0x4E>(v);    // quad_perm [2,3,0,1]
+  v = dpp_add<0x141>(v);   // row_half_mirror
+  v = dpp_add<0x140>(v);   // row_mirror
+  const int vi = __float_as_int(v);   // (the builtin is int-typed: move bits, not values)
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(vi, 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(vi, 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(vi, 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(vi, 48));
+  return (r0 + r1) + (r2 + r3);
 }
 
 // published-vector traffic of the group (global scratch)
@@ -88,14 +108,16 @@ __device__ __forceinline__ void rows_pre(const float* __restrict__ W, long ldw,
 // y[n] = act(W[n, :K] . x + b[n]) for n in [n_lo, n_hi): one wave per row,
 // RW rows of loads in flight, lanes along k (fixed-order butterfly sum).
 // PUB: y is a published vector (global), else LDS.  pre: the wave's first
-// pass, loaded ahead (rows_pre), or null.
+// pass, loaded ahead (rows_pre), or null.  wave0: the wave that takes the
+// first rows (a second product placed on the waves the first left idle).
 template <bool PUB, bool WT>
 __device__ __forceinline__ void rows_matvec(const float* __restrict__ W, long ldw,
                                             const float* __restrict__ b, const float* x, int K,
                                             int n_lo, int n_hi, float* y, bool relu,
-                                            const RowsPre* pre = nullptr) {
+                                            const RowsPre* pre = nullptr, int wave0 = 0) {
   constexpr int RW = kRW, U = kRU;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int wave = ((threadIdx.x >> 6) - wave0 % nw + nw) % nw;
   // (read up front: a select between pre's and W's addresses would keep pre in memory)
   float pw[RW][U], pb = 0.f;
   if (pre) {
@@ -203,9 +225,16 @@ __device__ __forceinline__ bool group_sync(unsigned* ctr, unsigned target) {
 // the dh1 columns are cut into kExplParts fixed parts (never by the group
 // size): part p's partial of da is published, and S5 adds the parts in order
 constexpr int kExplParts = 32;
-// per-observation scratch (floats) in the workspace: vectors [8H] | da
-// partials [kExplParts][64] | 4 counters
-__host__ __device__ inline long expl_split_scratch(int H) { return 8L * H + kExplParts * 64L + 64; }
+// the twin-critic kernel's fixed parts (oac_expl_twin_kernel below)
+constexpr int kTwinParts = 32;
+// per-observation scratch (floats) in the workspace, the larger of the two
+// kernels' layouts: here vectors [8H] | da partials [kExplParts][64] | 4
+// counters; the twin kernel's [2][kTwinParts][H] partials | [2H] | [64] | counters
+__host__ __device__ inline long expl_split_scratch(int H) {
+  const long split = 8L * H + kExplParts * 64L + 64;
+  const long twin = 2L * kTwinParts * H + 2L * H + 128;
+  return split > twin ? split : twin;
+}
 // LDS floats: x | v1 [2H] | v2 [2H] | head [64] | misc [128] | partials [threads] |
 // a part's dh1 columns | their da products
 __host__ __device__ inline long expl_split_lds(int Do, int Da, int H, int threads) {
@@ -590,6 +619,489 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
   }
 }
 
+// ---------------------------------------------------------------------------
+// Twin critics (nq = 2, K = 1; the SAC / OAC trainers): the same action with
+// one polled hand-off and one arrival instead of four hand-offs.  Two
+// rewrites make that possible, both exact in real arithmetic:
+//  * policy layer 1 from partial sums: the group's fixed parts of the policy's
+//    hidden layer 0 (part p = rows [pH/32, (p+1)H/32), owned whole by one
+//    workgroup) publish z_p = W1[:, part] h1[part] for all H outputs, so the
+//    consumers of layer 1 add 32 partials instead of waiting for a hand-off
+//    of h1 and another of h2;
+//  * the Q_UB gradient through critic layer 1 with the seed factored out:
+//    dh1_i = seed_i (sum_n W_last_i[n] [h2_i[n] > 0] W1_i[n, :]) (x) [h1_i > 0]
+//    and seed_i = 1/2 +- beta |.|' depends only on sign(Q1 - Q2); so the
+//    parts of critic layer 1's rows (16 per critic) publish their Q partial
+//    W_last . h2 and their seed-free u_p = sum_{n in part} ... W1_i[n, :]
+//    with the rows, and the workgroup whose arrival comes last reads the
+//    partials and finishes alone (seeds, dh1, da, shift, sample).
+//   S1  policy layer 0 rows of the workgroup's parts, their z_p; the critic
+//       obs projections P_i of its parts      -> hand-off A (polled)
+//   S2  (every workgroup) h2 = relu(b1 + sum_p z_p), heads, a = tanh(mean),
+//       critic layer 0 h1_i = relu(P_i + W0_i[:, Do:] a); its parts of
+//       critic layer 1: Q partials and u_p   -> arrival B (the last one goes on)
+//   S3  (the last arrival) Q_i, seeds, dh1, da, grad, shift, sample.
+// Every sum runs over fixed parts or fixed lanes in a fixed order, so a row of
+// a batched call is bitwise the same row of a single-observation call.
+constexpr int kTwinZW = 8;   // policy rows per part held in registers (H <= 8 * kTwinParts)
+constexpr int kTwinW0 = 9;   // W0_i[:, Do:] elements per thread in flight (2 H Da <= 9 x 1024)
+__host__ __device__ inline long expl_twin_lds(int Do, int Da, int H, int threads) {
+  return ((Do + Da + 3) & ~3L) + 4L * H + 64 + 128 + 2L * H * Da + (long)(threads / 64) * H;
+}
+// the twin kernel takes the call: twin critics, dims within its register and LDS budget
+static bool expl_twin_ok(const ExplFusedArgs& a, int threads, bool wt) {
+  if (a.nq != 2 || a.K != 1 || a.H < 1 || a.H > 64 * kRU || a.H > kTwinZW * kTwinParts ||
+      (a.H + kTwinParts / 2 - 1) / (kTwinParts / 2) > threads / 64 || 2 * a.Da > 64 || 2 * a.H > threads || a.Do > 512 ||
+      2L * a.H * a.Da > (long)kTwinW0 * threads)
+    return false;
+  const long lds = expl_twin_lds(a.Do, a.Da, a.H, threads);
+  return wt ? lds <= kWtLdsFloats : lds * (long)sizeof(float) <= 64 * 1024;
+}
+
+#ifdef OAC_EXPL_CLOCK   // S3 runs on the last arrival, whichever workgroup that is
+#define EXPL_CLK3(i) do { if (threadIdx.x == 0) g_expl_clock[i] = wall_clock64(); } while (0)
+#else
+#define EXPL_CLK3(i) do {} while (0)
+#endif
+
+template <bool WT, bool OBS>
+__global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, int row0, int G,
+                                                             float* scratch, ExplObsArg oa) {
+  float* sm;
+  if constexpr (WT) {
+    __shared__ __attribute__((aligned(16))) float sm_wt[kWtLdsFloats];
+    sm = sm_wt;
+  } else {
+    extern __shared__ __attribute__((aligned(16))) float sm_dyn[];
+    sm = sm_dyn;
+  }
+  constexpr int NP = kTwinParts, NPQ = kTwinParts / 2;
+  const int Do = a.Do, Da = a.Da, H = a.H, Dq = Do + Da;
+  const int gi = blockIdx.x / G, wg = blockIdx.x - gi * G;
+  const int r = row0 + gi, t = threadIdx.x, nt = blockDim.x;
+  const int lane = t & 63, wave = t >> 6, nw = nt >> 6;
+  const float* const q0p = a.q[0];
+  const float* const q1p = a.q[1];
+  auto Qp = [&](int i) { return i == 0 ? q0p : q1p; };
+  const float* pol = a.pol;
+  float* Gv = scratch + (long)gi * expl_split_scratch(H);
+  float* g_z = Gv;                         // [NP][H] policy layer-1 partials
+  float* g_u = g_z + (long)NP * H;         // [NP][H] seed-free dh1 partials (parts of 2H rows)
+  float* g_P = g_u + (long)NP * H;         // [2H]    critic obs projections (+ b0)
+  float* g_q = g_P + 2 * H;                // [NP]    Q partials
+  unsigned* ctr = reinterpret_cast<unsigned*>(g_q + 64);   // [2] hand-off A, arrival B
+  float* x = sm;                           // [Dq] ob | a
+  float* h1p = x + ((Dq + 3) & ~3);        // [H]  policy layer 0 (this workgroup's rows)
+  float* h2p = h1p + H;                    // [H]  policy layer 1
+  float* h1q = h2p + H;                    // [2H] P_i, then critic layer 0
+  float* head = h1q + 2 * H;               // [64] mean | raw log std
+  float* misc = head + 64;                 // [128] Q, seeds, norm, row Q terms, da
+  float* qrow = misc + 16;                 // [<= 48] per-row Q terms of a part
+  float* red = misc + 64;                  // [64] da, then g^2 sigma
+  float* w0a = misc + 128;                 // [2H][Da] W0_i[:, Do:]
+  float* ctb = w0a + 2L * H * Da;          // [nw][H] per-row u terms; S3: dh1 [2H]
+  __shared__ long long cnt_s;
+  if (t == 0) cnt_s = a.state->expl_counter;
+  const int p0 = wg * NP / G, p1 = (wg + 1) * NP / G;   // this workgroup's parts
+  // ---- ahead of everything: the weights of S1's first rows and of z.  The
+  // S1 rows of this workgroup form one list -- its policy layer-0 rows
+  // [rp0, rp1), then its obs-projection rows [rq0, rq1) over both critics;
+  // wave w takes list rows 2w, 2w + 1 (+ 2 nw ...), lanes along k, every k of
+  // a row in flight at once (Do <= 512).  The sum order is rows_matvec's
+  // (k ascending per lane, then the butterfly), so the values are the same.
+  const int rp0 = p0 * H / NP, rp1 = p1 * H / NP;
+  const int rq0 = p0 * 2 * H / NP, rq1 = p1 * 2 * H / NP;
+  const int npol = rp1 - rp0, n_s1 = npol + (rq1 - rq0);
+  auto s1_src = [&](int l, const float*& w, const float*& bias) {
+    if (l < npol) {
+      w = pol + a.p_fc0_w + (long)(rp0 + l) * Do;
+      bias = pol + a.p_fc0_b + rp0 + l;
+    } else {
+      const int rr = rq0 + l - npol, i = rr >= H ? 1 : 0, n = rr - i * H;
+      w = Qp(i) + a.q_fc0_w + (long)n * Dq;
+      bias = Qp(i) + a.q_fc0_b + n;
+    }
+  };
+  constexpr int U1 = 8;
+  float s1w[2][U1], s1b[2];
+  if (n_s1 > 0) {   // (clamped rows: unconditional loads keep the wait counts exact)
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const float *w, *bias;
+      s1_src(min(2 * wave + rr, n_s1 - 1), w, bias);
+#pragma unroll
+      for (int u = 0; u < U1; ++u) s1w[rr][u] = w[min(lane + 64 * u, Do - 1)];
+      s1b[rr] = *bias;
+    }
+  }
+  const int zs = nt / H, zm = t % H, zslot = t / H;
+  const float* W1p = pol + a.p_fc1_w;
+  float zw[kTwinZW];
+  {
+    const int p = p0 + zslot;
+    const int n0 = p * H / NP, n1 = (p + 1) * H / NP;
+    if (zslot < zs && p < p1 && n1 > n0) {
+#pragma unroll
+      for (int u = 0; u < kTwinZW; ++u) zw[u] = W1p[(long)zm * H + min(n0 + u, n1 - 1)];
+    }
+  }
+  EXPL_CLK(0);
+  if constexpr (OBS) {
+    for (int k = t; k < Do; k += nt) x[k] = oa.v[k];
+  } else {
+    for (int k = t; k < Do; k += nt) x[k] = a.obs[(long)r * a.ld_obs + k];
+  }
+  __syncthreads();
+  EXPL_CLK(1);
+  // ---- S1: policy layer 0 rows (LDS) and the obs-projection rows (published)
+  for (int l0 = 2 * wave; l0 < n_s1; l0 += 2 * nw) {
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      const int l = l0 + rr;
+      if (l >= n_s1) break;
+      const float *w, *bias;
+      s1_src(l, w, bias);
+      float acc = 0.f;
+#pragma unroll
+      for (int u = 0; u < U1; ++u) {
+        const int k = lane + 64 * u;
+        const float wv = l0 == 2 * wave ? s1w[rr][u] : w[min(k, Do - 1)];
+        acc = fmaf(wv, k < Do ? x[k] : 0.f, acc);
+      }
+      acc = wsum64(acc) + (l0 == 2 * wave ? s1b[rr] : *bias);
+      if (lane == 0) {
+        if (l < npol) h1p[rp0 + l] = fmaxf(acc, 0.f);
+        else st_pub<WT>(g_P + rq0 + l - npol, acc);
+      }
+    }
+  }
+  __syncthreads();
+  // z_p[m] = sum_{n in part p} W1[m, n] h1[n], n ascending, for every output m
+  for (int pb = p0; pb < p1; pb += zs) {
+    const int p = pb + zslot;
+    if (zslot < zs && p < p1) {
+      const int n0 = p * H / NP, n1 = (p + 1) * H / NP;
+      float s = 0.f;
+#pragma unroll
+      for (int u = 0; u < kTwinZW; ++u)
+        if (n0 + u < n1) s = fmaf(pb == p0 ? zw[u] : W1p[(long)zm * H + n0 + u], h1p[n0 + u], s);
+      st_pub<WT>(g_z + (long)p * H + zm, s);
+    }
+  }
+  EXPL_CLK(2);
+  group_arrive<WT>(ctr + 0, G);
+  // ahead, during the hand-off: the heads' rows, W0_i[:, Do:] into LDS, the
+  // layer-1 bias, and the first critic part's W1 row of each wave
+  RowsPre preh;
+  // (every wave: the polling wave is past the heads' rows and loads nothing;
+  // a pointer chosen per wave would keep preh in scratch)
+  rows_pre(pol + a.p_head_w, H, pol + a.p_head_b, H, 0, 2 * Da, preh);
+  const float b1v = t < H ? pol[a.p_fc1_b + t] : 0.f;
+  int ci = 0, ra = 0, rb = 0;   // the first critic part: critic ci, rows [ra, rb)
+  float w1r[kRU], b1q = 0.f, wlq = 0.f;
+  if (p0 < p1) {
+    ci = p0 / NPQ;
+    ra = (p0 % NPQ) * H / NPQ;
+    rb = (p0 % NPQ + 1) * H / NPQ;
+    if (wave < rb - ra) {   // (the polling wave too: its first poll waits these out, inside the hand-off)
+      const float* q = Qp(ci);
+      const int n = ra + wave;
+#pragma unroll
+      for (int u = 0; u < kRU; ++u) w1r[u] = q[a.q_fc1_w + (long)n * H + min(lane + 64 * u, H - 1)];
+      b1q = q[a.q_fc1_b + n];
+      wlq = q[a.q_last_w + n];
+    }
+  }
+  // W0_i[:, Do:] element e = t + u * threads (u < kTwinW0) of the [2H][Da]
+  // image: its source, stepped without a division per element
+  const int n0a = 2 * H * Da;
+  const float* wsrc[kTwinW0];
+  {
+    const int ers = t / Da, ej = t - ers * Da;           // row (over both critics), column
+    const int drow = nt / Da, dj = nt - drow * Da;
+    int rw = ers, jj = ej;
+#pragma unroll
+    for (int u = 0; u < kTwinW0; ++u) {
+      const int rr = min(rw, 2 * H - 1), i = rr >= H ? 1 : 0;
+      wsrc[u] = Qp(i) + a.q_fc0_w + (long)(rr - i * H) * Dq + Do + (rw < 2 * H ? jj : 0);
+      rw += drow; jj += dj;
+      if (jj >= Da) { jj -= Da; ++rw; }
+    }
+  }
+  bool ok = group_wait<WT>(ctr + 0, G);
+  EXPL_CLK(3);
+  // ---- S2 (every workgroup): policy layer 1 from the parts' partials (H <=
+  // threads: one output per thread) and P; W0_i[:, Do:] requested behind them
+  // (into LDS after the heads; every load in flight before the first store;
+  // expl_twin_ok: at most kTwinW0 per thread)
+  // (loads unconditional, clamped: a branch between a load and its use makes
+  // the wait count assume no load in flight)
+  float zz[NP];
+  const int tz = min(t, H - 1);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) zz[p] = ld_pub<WT>(g_z + (long)p * H + tz);
+  const float pv = ld_pub<WT>(g_P + min(t, 2 * H - 1));
+  float wt[kTwinW0];
+#pragma unroll
+  for (int u = 0; u < kTwinW0; ++u) wt[u] = *wsrc[u];
+  if (t < H) {
+    float s = zz[0];
+#pragma unroll
+    for (int p = 1; p < NP; ++p) s += zz[p];
+    h2p[t] = fmaxf(s + b1v, 0.f);
+  }
+  if (t < 2 * H) h1q[t] = pv;
+  __syncthreads();
+  EXPL_CLK(4);
+  rows_matvec<false, WT>(pol + a.p_head_w, H, pol + a.p_head_b, h2p, H, 0, 2 * Da, head, false,
+                         &preh);
+  __syncthreads();
+  if (t < Da) x[Do + t] = tanhf(head[t]);
+#pragma unroll
+  for (int u = 0; u < kTwinW0; ++u)
+    if (t + u * nt < n0a) w0a[t + u * nt] = wt[u];
+  __syncthreads();
+  EXPL_CLK(5);
+  for (int e = t; e < 2 * H; e += nt) {   // h1_i = relu(P_i + W0_i[:, Do:] a) (Da <= 32)
+    float wa[32], av[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      wa[j] = j < Da ? w0a[(long)e * Da + j] : 0.f;
+      av[j] = j < Da ? x[Do + j] : 0.f;
+    }
+    float s = h1q[e];
+#pragma unroll
+    for (int j = 0; j < 32; ++j)
+      if (j < Da) s = fmaf(wa[j], av[j], s);
+    h1q[e] = fmaxf(s, 0.f);
+  }
+  __syncthreads();
+  EXPL_CLK(6);
+  // critic layer 1 rows of the parts: one wave per row (lanes along k), the
+  // row's Q term W_last[n] h2[n] and its u term c_n W1[n, :] (c_n = W_last[n]
+  // [h2[n] > 0]); per part the terms are summed in row order
+  for (int p = p0; p < p1; ++p) {
+    const int i = p / NPQ, na = (p % NPQ) * H / NPQ, nb = (p % NPQ + 1) * H / NPQ;
+    const float* q = Qp(i);
+    if (wave < nb - na) {
+      const int n = na + wave;
+      float wv[kRU];
+      float bq, wl;
+      if (p == p0) {
+#pragma unroll
+        for (int u = 0; u < kRU; ++u) wv[u] = w1r[u];
+        bq = b1q; wl = wlq;
+      } else {
+#pragma unroll
+        for (int u = 0; u < kRU; ++u) wv[u] = q[a.q_fc1_w + (long)n * H + min(lane + 64 * u, H - 1)];
+        bq = q[a.q_fc1_b + n]; wl = q[a.q_last_w + n];
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int u = 0; u < kRU; ++u)
+        if (lane + 64 * u < H) s = fmaf(wv[u], h1q[i * H + lane + 64 * u], s);
+      s = wsum64(s);
+      const float h2 = fmaxf(s + bq, 0.f);
+      const float c = h2 > 0.f ? wl : 0.f;
+#pragma unroll
+      for (int u = 0; u < kRU; ++u)
+        if (lane + 64 * u < H) ctb[(long)wave * H + lane + 64 * u] = c * wv[u];
+      if (lane == 0) qrow[wave] = wl * h2;
+    }
+    __syncthreads();
+    // (rows of a part <= 16: every LDS read before the first add; an empty
+    // part publishes zeros)
+    for (int k = t; k < H; k += nt) {
+      float cc[16];
+#pragma unroll
+      for (int w = 0; w < 16; ++w) cc[w] = w < nb - na ? ctb[(long)w * H + k] : 0.f;
+      float s = cc[0];
+#pragma unroll
+      for (int w = 1; w < 16; ++w)
+        if (w < nb - na) s += cc[w];
+      st_pub<WT>(g_u + (long)p * H + k, s);
+    }
+    if (t == nt - 64) {   // (a wave without u columns when H <= nt - 64)
+      float cc[16];
+#pragma unroll
+      for (int w = 0; w < 16; ++w) cc[w] = w < nb - na ? qrow[w] : 0.f;
+      float s = cc[0];
+#pragma unroll
+      for (int w = 1; w < 16; ++w)
+        if (w < nb - na) s += cc[w];
+      st_pub<WT>(g_q + p, s);
+    }
+    __syncthreads();
+  }
+  EXPL_CLK(7);
+  // ---- arrival B: the last workgroup of the group goes on to S3.  The add
+  // carries this workgroup's hand-off failure in bit 16, so the last arrival
+  // learns every member's from the value its add returns.
+  if (t == 0 && !ok && a.fail)   // a timed-out hand-off of this workgroup: reported
+    __hip_atomic_fetch_or(a.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ unsigned arr_s;
+  if (t == 0) {
+    unsigned prev = 0;
+    if (G > 1) {
+      if constexpr (!WT) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      prev = __hip_atomic_fetch_add(ctr + 1, ok ? 1u : 0x10001u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (!WT) {
+        if ((prev & 0xffffu) == (unsigned)G - 1) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+      }
+    }
+    arr_s = prev;
+  }
+  __syncthreads();
+  const unsigned arrived = arr_s;
+  if ((arrived & 0xffffu) != (unsigned)G - 1) return;
+  const bool others_failed = (arrived >> 16) != 0;
+  EXPL_CLK3(8);
+  // ---- S3 (the last arrival): Q_i, seeds, dh1, da
+  if (t == 0 && G > 1) {   // every member is past both hand-offs: re-arm
+    __hip_atomic_store(ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // Q partials in wave 0 (lane p: part p; critic p / 16), the u sums on every
+  // thread below 2H (the critic's parts in order)
+  const float qv = wave == 0 ? ld_pub<WT>(g_q + (lane & (NP - 1))) : 0.f;
+  const float blast = wave == 0 ? Qp(lane >= NPQ ? 1 : 0)[a.q_last_b] : 0.f;
+  {
+    const int e = min(t, 2 * H - 1), i = e >= H ? 1 : 0, k = e - i * H;
+    float uu[NPQ];
+#pragma unroll
+    for (int p = 0; p < NPQ; ++p) uu[p] = ld_pub<WT>(g_u + (long)(i * NPQ + p) * H + k);
+    float su = uu[0];
+#pragma unroll
+    for (int p = 1; p < NPQ; ++p) su += uu[p];
+    if (t < 2 * H) ctb[t] = su;
+  }
+  if (wave == 0) {   // Q_i: a fixed butterfly over the critic's 16 parts, then the bias
+    float q = qv;
+#pragma unroll
+    for (int o = NPQ / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    q += blast;
+    const float q0 = __shfl(q, 0, 64), q1 = __shfl(q, NPQ, 64);
+    if (lane == 0) {
+      misc[0] = q0; misc[1] = q1;
+      // Q_UB = (Q1+Q2)/2 + beta |Q1-Q2|/2: d|x|/dx = sign(x) (0 at 0)
+      const float d = q0 - q1;
+      const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+      const float hb = a.beta_UB / 2.f;
+      misc[2] = 0.5f + hb * sg;
+      misc[3] = 0.5f - hb * sg;
+    }
+  }
+  __syncthreads();
+  for (int e = t; e < 2 * H; e += nt) ctb[e] = h1q[e] > 0.f ? misc[2 + e / H] * ctb[e] : 0.f;
+  __syncthreads();
+  EXPL_CLK3(9);
+  {   // da[j] = sum_e dh1[e] W0a[e, j]: one half-wave per j (Da <= 32), lanes along e
+    const int hw = t >> 5, l32 = t & 31;
+    if (hw < Da) {
+      const int j = hw;
+      float cv[16], wv[16];                 // (2H <= 512: every LDS read before the first FMA)
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int e = l32 + 32 * u;
+        cv[u] = e < 2 * H ? ctb[e] : 0.f;
+        wv[u] = e < 2 * H ? w0a[(long)e * Da + j] : 0.f;
+      }
+      float sj = 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) sj = fmaf(cv[u], wv[u], sj);
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) sj += __shfl_xor(sj, o, 32);
+      if (l32 == 0) red[j] = sj;
+    }
+  }
+  __syncthreads();
+  EXPL_CLK3(10);
+  // grad, shift, sample: wave 0 (Da <= 32), the norm as a wave sum
+  if (wave != 0) return;
+  float g = 0.f, sig = 0.f, sd = 0.f, mean = 0.f;
+  if (lane < Da) {
+    const float act = x[Do + lane];
+    g = red[lane] * (1.f - act * act);
+    sd = expf(fminf(fmaxf(head[Da + lane], -20.f), 2.f));
+    sig = sd * sd;
+    mean = head[lane];
+  }
+  const float nrm = sqrtf(wsum64(lane < Da ? g * g * sig : 0.f)) + 10e-6f;
+  // the call's only group with a host-polled completion word: the outputs
+  // (host memory) as system-scope stores, drained, then the word -- no ticket
+  const bool solo = a.n == 1 && a.done;
+  if (lane < Da) {
+    const long e = (long)r * Da + lane;
+    const float mu_C = (a.sqrt_2delta * (sig * g)) / nrm;
+    const float mu_E = mean + mu_C;
+    const float ev = a.eps ? a.eps[e]
+                           : philox_normal(a.seed, (unsigned long long)cnt_s, 3u, (unsigned)(r * Da + lane));
+    const long nd = (long)a.n * Da;
+    const float nan = __int_as_float(0x7fc00000);
+    const float o0 = ok ? tanhf(__fadd_rn(__fmul_rn(ev, sd), mu_E)) : nan, o1 = ok ? mu_E : nan;
+    if (solo) {
+      __hip_atomic_store(a.out + e, o0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.out + nd + e, o1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(a.out + 2 * nd + e, sd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {
+      a.out[e] = o0;
+      a.out[nd + e] = o1;
+      a.out[2 * nd + e] = sd;
+    }
+    if (a.grad) a.grad[e] = g;
+  }
+  if (solo) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      if (!a.eps) a.state->expl_counter = cnt_s + 1;
+      const unsigned failed = (!ok || others_failed) ? 1u : 0u;   // (the arrival told)
+      if (failed && a.fail) __hip_atomic_store(a.fail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.done, a.done_seq | (failed ? 0x80000000u : 0u), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    EXPL_CLK3(11);
+    return;
+  }
+  EXPL_CLK3(11);
+  if (t == 0 && !ok && a.fail)
+    __hip_atomic_fetch_or(a.fail, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the Philox counter and the completion word: the last group to finish
+  if (!a.eps || a.done || a.fail) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (wave 0 alone from here)
+    if (t == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system: the outputs may be host memory
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned prev =
+          __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == (unsigned)a.n - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        if (!a.eps) a.state->expl_counter = cnt_s + 1;
+        __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned failed = 0;
+        if (a.fail) {
+          failed = __hip_atomic_load(a.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.fail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (a.done) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_store(a.done, a.done_seq | (failed ? 0x80000000u : 0u), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
+  }
+}
+
 long expl_split_scratch_floats(int H) { return expl_split_scratch(H); }
 
 // threads per workgroup: 1024.  Humanoid, one observation, host wall per call
@@ -622,6 +1134,9 @@ int expl_split_group(int n_rows) {
   return g < 1 ? 1 : (g > kExplGroup ? kExplGroup : g);
 }
 
+// the twin-critic kernel off (tools/micro/expl_micro's A/B against the split kernel)
+bool g_expl_twin_off = false;
+
 // rows [row0, row0 + n_rows) of the call, one group of G workgroups each
 hipError_t launch_expl_split(const ExplFusedArgs& a, int row0, int n_rows, float* scratch,
                              hipStream_t s) {
@@ -629,10 +1144,21 @@ hipError_t launch_expl_split(const ExplFusedArgs& a, int row0, int n_rows, float
     return hipErrorInvalidValue;
   const int nt = expl_split_threads();
   const int G = expl_split_group(n_rows);
-  const long lds = expl_split_lds(a.Do, a.Da, a.H, nt);
-  // write-through hand-offs need every workgroup of the launch on a CU of its own
-  const bool wt = G > 1 && (long)n_rows * G <= expl_device_cus() && lds <= kWtLdsFloats;
   static const ExplObsArg none{};   // (unread)
+  // write-through hand-offs need every workgroup of the launch on a CU of its own
+  const bool own_cu = G > 1 && (long)n_rows * G <= expl_device_cus();
+  if (!g_expl_twin_off && expl_twin_ok(a, nt, own_cu)) {
+    if (own_cu) {
+      OAC_LAUNCH((oac_expl_twin_kernel<true, false>), dim3(n_rows * G), dim3(nt), 0, s, a, row0, G,
+                 scratch, none);
+    } else {
+      OAC_LAUNCH((oac_expl_twin_kernel<false, false>), dim3(n_rows * G), dim3(nt),
+                 expl_twin_lds(a.Do, a.Da, a.H, nt) * sizeof(float), s, a, row0, G, scratch, none);
+    }
+    return hipGetLastError();
+  }
+  const long lds = expl_split_lds(a.Do, a.Da, a.H, nt);
+  const bool wt = own_cu && lds <= kWtLdsFloats;
   if (wt) {
     OAC_LAUNCH((oac_expl_split_kernel<true, false>), dim3(n_rows * G), dim3(nt), 0, s, a, row0, G,
                scratch, none);
@@ -650,8 +1176,13 @@ hipError_t launch_expl_split_obs(const ExplFusedArgs& a, const ExplObsArg& obs, 
     return hipErrorInvalidValue;
   const int nt = expl_split_threads();
   const int G = expl_split_group(1);
+  const bool own_cu = G > 1 && G <= expl_device_cus();
+  if (own_cu && !g_expl_twin_off && expl_twin_ok(a, nt, true)) {
+    OAC_LAUNCH((oac_expl_twin_kernel<true, true>), dim3(G), dim3(nt), 0, s, a, 0, G, scratch, obs);
+    return hipGetLastError();
+  }
   const long lds = expl_split_lds(a.Do, a.Da, a.H, nt);
-  if (!(G > 1 && G <= expl_device_cus() && lds <= kWtLdsFloats)) return launch_expl_split(a, 0, 1, scratch, s);
+  if (!(own_cu && lds <= kWtLdsFloats)) return launch_expl_split(a, 0, 1, scratch, s);
   OAC_LAUNCH((oac_expl_split_kernel<true, true>), dim3(G), dim3(nt), 0, s, a, 0, G, scratch, obs);
   return hipGetLastError();
 }

@@ -77,10 +77,14 @@ static inline Split choose_split(int K, int tiles, int cfg) {
 }
 
 // split-K of a dW on gemm_bwdp.hip (64x64 tiles over the N - 1 real columns):
-// about 768 workgroups per gradient kind (three per CU), chunks of >= 256
-// batch rows.  B=4096 SAC step (OAC_SPLITS sweep): critic layer 0 13, the
-// rest 16 splits -- 3,225 steps/s against 3,108 with the register-direct
-// kernel's splits (19 / 16 / 32).
+// about 768 workgroups per gradient kind, chunks of >= 256 batch rows.  B=4096
+// SAC step (OAC_SPLITS sweep): critic layer 0 13, the rest 16 splits -- 3,225
+// steps/s against 3,108 with the register-direct kernel's splits (19 / 16 /
+// 32).  (Sizing each dW for the slots its launch's dX tiles and side blocks
+// leave -- critic layer 1 12 splits, one round of 992 workgroups instead of
+// 1,152; layer 0 15; policy layer 0 32 -- measured slower on every one of
+// those launches, round 3: 33.9 -> 34.7, 26.0 -> 29.8, 15.2 -> 16.0 us; the
+// per-workgroup prologue / epilogue and slab traffic outweigh the tail.)
 static inline Split choose_split_pipe(int K, int tiles) {
   tiles = std::max(1, tiles);
   int S = std::max(1, std::min(K / 256, 768 / tiles));

@@ -410,8 +410,10 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
     } else if (split) {   // layer 1 + last layer of both critics (their gradients are final)
       const long off[2] = {(long)L.q_fc1_w, (long)(L.q_size + L.q_fc1_w)};
       const long n[2] = {(long)(L.q_size - L.q_fc1_w), (long)(L.q_size - L.q_fc1_w)};
-      if (side_adam(p, gb, critic_adam(p, 0, c.auto_alpha ? p.alpha() : nullptr), 2, off, n, true, s))
-        return 1;
+      // (a range reads the slabs its own dW tasks wrote: the rest are zeros)
+      AdamArgs a = critic_adam(p, 0, c.auto_alpha ? p.alpha() : nullptr);
+      a.S = std::max(p.sp_q1.S, p.sp_ql.S);
+      if (side_adam(p, gb, a, 2, off, n, true, s)) return 1;
     }
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -453,7 +455,9 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     if (split) {   // the critics' layer 0 (not read here; the dL/da launch reads it next)
       const long off[2] = {0, (long)L.q_size};
       const long n[2] = {(long)L.q_fc1_w, (long)L.q_fc1_w};
-      if (side_adam(p, gb, critic_adam(p, 0, nullptr), 2, off, n, false, s)) return 1;
+      AdamArgs a = critic_adam(p, 0, nullptr);
+      a.S = p.sp_q0.S;
+      if (side_adam(p, gb, a, 2, off, n, false, s)) return 1;
     }
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -515,7 +519,9 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     } else if (split) {   // the policy's layer 1 + heads (layer 0: the step's last launch)
       const long off[1] = {(long)L.pol_fc1_w};
       const long n[1] = {(long)(L.pol_size - L.pol_fc1_w)};
-      if (side_adam(p, gb, policy_adam(p, 0, nullptr), 1, off, n, false, s)) return 1;
+      AdamArgs a = policy_adam(p, 0, nullptr);
+      a.S = std::max(p.sp_p1.S, p.sp_ph.S);
+      if (side_adam(p, gb, a, 1, off, n, false, s)) return 1;
     }
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -544,7 +550,7 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
     return 1;
   if (!fused) {
     AdamArgs a = policy_adam(p, 0, nullptr);
-    if (split) a.n = p.L.pol_fc1_w;   // layer 0; the rest ran beside the layer-0 dW
+    if (split) { a.n = p.L.pol_fc1_w; a.S = p.sp_p0.S; }   // layer 0; the rest ran beside the layer-0 dW
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
   }
@@ -620,6 +626,11 @@ static void plan_splits(SacPlan& p) {
     p.sp_q1 = choose_split_pipe(c.batch, nq * (t64(H, H) + t64(c.q_out, H)));
     p.sp_ql = p.sp_q1;
     p.sp_q0 = choose_split_pipe(c.batch, nq * t64(H, Dq));
+    // the particle trainer's K-output last-layer dW rides in the layer-0 dW
+    // launch (particle_plan.hip, hidden % 4 == 0): the same chunks as the
+    // layer-0 dW, so neither is that launch's tail (configs[4]: 16 splits of
+    // 256 rows beside layer 0's 32 of 128 made it 13.5 us, the same 32: 9.9)
+    if (c.kind == OAC_KIND_PARTICLE && (H & 3) == 0) p.sp_ql = p.sp_q0;
     // (the head dW rides with the short-K dh2 product: register-direct kernel, sp_ph as is)
     p.sp_p1 = choose_split_pipe(c.batch, t64(H, H));
     p.sp_p0 = choose_split_pipe(c.batch, t64(H, Do));

@@ -5,6 +5,7 @@
 // Prints the per-stage wall clock of the group's first and last workgroup
 // (100 MHz counter, median over the calls) and the host wall per call.
 // Build: tools/micro/Makefile.  Run: tools/micro/expl_micro [calls] [obs in arguments 0|1]
+//   [split kernel 0|1: the four-hand-off kernel instead of the twin-critic one]
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <chrono>
@@ -14,7 +15,7 @@
 #include <vector>
 #include "../../oac-explore_amd/csrc/expl_split.hip"
 
-namespace oac { thread_local ExtTiming g_ext_timing; }
+namespace oac { thread_local ExtTiming g_ext_timing; extern bool g_expl_twin_off; }
 using namespace oac;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
@@ -32,6 +33,8 @@ static float* dev_rand(size_t n, unsigned seed, float scale) {
 int main(int argc, char** argv) {
   const int calls = argc > 1 ? atoi(argv[1]) : 200;
   const bool obs_arg = argc > 2 && atoi(argv[2]) != 0;   // the observation in the arguments
+  const bool split = argc > 3 && atoi(argv[3]) != 0;     // the four-hand-off kernel
+  g_expl_twin_off = split;
   const int Do = 376, Da = 17, H = 256, Dq = Do + Da;
   // parameter blocks: policy [fc0 | fc1 | head], critics [fc0 | fc1 | last]
   const long p0w = 0, p0b = p0w + (long)H * Do, p1w = p0b + H, p1b = p1w + (long)H * H,
@@ -96,10 +99,15 @@ int main(int argc, char** argv) {
   }
   auto med = [](std::vector<long long> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
   auto medd = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
-  const char* names[13] = {"start", "obs read", "S1 compute", "hand-off 0", "S2 compute", "hand-off 1",
-                           "heads+tanh", "S3 rest", "hand-off 2", "S4 compute", "hand-off 3",
-                           "S5 da", "S5 rest"};
-  printf("obs %s; group of %d workgroups; host wall per call %.1f us (median of %d)\n", obs_arg ? "in arguments" : "host row", G, medd(wall), calls);
+  const char* names_split[13] = {"start", "obs read", "S1 compute", "hand-off 0", "S2 compute", "hand-off 1",
+                                 "heads+tanh", "S3 rest", "hand-off 2", "S4 compute", "hand-off 3",
+                                 "S5 da", "S5 rest"};
+  const char* names_twin[13] = {"start", "obs read", "S1 + z", "hand-off A", "h2 sums", "heads+tanh",
+                                "critic L0", "critic L1+u", "arrival B", "S3 sums", "S3 da", "S3 rest", "-"};
+  const char* const* names = split ? names_split : names_twin;
+  const int last_both = split ? 9 : 7, n_st = split ? 12 : 11;
+  printf("%s kernel; obs %s; group of %d workgroups; host wall per call %.1f us (median of %d)\n",
+         split ? "split" : "twin", obs_arg ? "in arguments" : "host row", G, medd(wall), calls);
   printf("stage (us, from workgroup 0's start; median): wg0 / last wg\n");
   std::vector<long long> base = clk[0];
   {
@@ -107,14 +115,14 @@ int main(int argc, char** argv) {
     for (size_t c = 0; c < base.size(); ++c) d1.push_back(clk[32][c] - base[c]);
     printf("  %-12s %6.2f  %6.2f\n", "start", 0.0, med(d1) / 100.0);
   }
-  for (int i = 1; i <= 12; ++i) {
+  for (int i = 1; i <= n_st; ++i) {
     std::vector<long long> d0, d1;
     for (size_t c = 0; c < base.size(); ++c) {
       d0.push_back(clk[i][c] - base[c]);
       d1.push_back(clk[32 + i][c] - base[c]);
     }
     printf("  %-12s %6.2f  %6.2f\n", names[i], med(d0) / 100.0,
-           (i <= 9 ? med(d1) / 100.0 : 0.0));
+           (i <= last_both ? med(d1) / 100.0 : 0.0));
   }
   return 0;
 }
