@@ -50,6 +50,8 @@ struct ExplPlan {
   // oac_expl_action_now: host-coherent observation rows [N, Do + Da], results
   // [3][N][Da] and completion word (hipHostMalloc, allocated on first use)
   float* hc_obs = nullptr; float* hc_out = nullptr; unsigned* hc_done = nullptr;
+  // single-observation calls: the outputs as tagged granules (ExplFusedArgs::tags)
+  unsigned long long* hc_tag = nullptr;
   unsigned seq = 0;
   hipStream_t cap_stream = nullptr;   // graph capture (the graphs launch on the caller's stream)
   // captured call graphs by (eps slot, beta_UB, delta, ub_index): alternating
@@ -132,6 +134,9 @@ static int expl_host_alloc(ExplPlan& p) {
   OAC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p.hc_out),
                               sizeof(float) * 3 * (size_t)p.N * p.Da, fl));
   OAC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p.hc_done), 64, fl));
+  OAC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p.hc_tag),
+                              sizeof(unsigned long long) * 3 * (size_t)p.N * p.Da, fl));
+  std::memset(p.hc_tag, 0, sizeof(unsigned long long) * 3 * (size_t)p.N * p.Da);
   std::memset(p.hc_obs, 0, sizeof(float) * (size_t)p.N * (p.Do + p.Da));
   std::memset(p.hc_out, 0, sizeof(float) * 3 * (size_t)p.N * p.Da);
   *p.hc_done = p.seq;
@@ -166,6 +171,45 @@ static int expl_wait(ExplPlan& p, unsigned seq, hipStream_t s) {
   }
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
   if (*f & 0x80000000u) {
+    set_error("exploration: an in-launch hand-off timed out (the workgroups of an observation's "
+              "group were not co-resident); the results are NaN");
+    return 1;
+  }
+  return 0;
+}
+
+// the single-observation call's tagged granules: spin until every one carries
+// this call's sequence number (8-byte granules arrive whole, in any order),
+// then unpack the values into the float outputs
+static int expl_wait_tags(ExplPlan& p, unsigned seq, hipStream_t s) {
+  const int n = 3 * p.Da;
+  volatile unsigned long long* g = p.hc_tag;
+  unsigned polls = 0;
+  for (int i = 0; i < n; ++i) {
+    while (((unsigned)(g[i] >> 32) & 0x7fffffffu) != seq) {
+      cpu_relax();
+      if ((++polls & 4095) == 0) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess && ((unsigned)(g[i] >> 32) & 0x7fffffffu) != seq) {
+          set_error("exploration: the launch finished without its outputs");
+          return 1;
+        }
+        if (e != hipSuccess && e != hipErrorNotReady) {
+          set_error("exploration: %s", hipGetErrorString(e));
+          return 1;
+        }
+      }
+    }
+  }
+  __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  bool failed = false;
+  for (int i = 0; i < n; ++i) {
+    const unsigned long long w = g[i];
+    failed |= (w >> 63) != 0;
+    const unsigned bits = (unsigned)w;
+    std::memcpy(p.hc_out + i, &bits, sizeof(float));
+  }
+  if (failed) {
     set_error("exploration: an in-launch hand-off timed out (the workgroups of an observation's "
               "group were not co-resident); the results are NaN");
     return 1;
@@ -260,6 +304,7 @@ int oac_expl_destroy(oac_expl* h) {
   if (h->p.hc_obs) (void)hipHostFree(h->p.hc_obs);
   if (h->p.hc_out) (void)hipHostFree(h->p.hc_out);
   if (h->p.hc_done) (void)hipHostFree(h->p.hc_done);
+  if (h->p.hc_tag) (void)hipHostFree(h->p.hc_tag);
   delete h;
   return 0;
 }
@@ -331,13 +376,14 @@ int oac_expl_action_now(oac_expl* h, const float* eps, float beta_UB, float delt
   if (p.seq == 0) p.seq = 1;           // 0 is the word's initial value
   a.done = p.hc_done;
   a.done_seq = p.seq;
-  if (p.N == 1 && p.Do <= kExplObsArg) {   // one observation: it travels in the arguments
-    ExplObsArg o;
+  if (p.N == 1 && p.Do <= kExplObsArg) {   // one observation: it travels in the arguments,
+    ExplObsArg o;                            // the outputs come back as tagged granules
     std::memcpy(o.v, p.hc_obs, sizeof(float) * p.Do);
+    a.tags = p.hc_tag;
     OAC_HIP_CHECK(launch_expl_split_obs(a, o, p.ws + p.o_split, s));
-  } else if (expl_launch(p, a, s)) {
-    return 1;
+    return expl_wait_tags(p, a.done_seq, s);
   }
+  if (expl_launch(p, a, s)) return 1;
   return expl_wait(p, a.done_seq, s);
 }
 

@@ -71,6 +71,12 @@ __device__ __forceinline__ float wsum64(float v) {
   return (r0 + r1) + (r2 + r3);
 }
 
+// one output of a single-observation call as a tagged granule (ExplFusedArgs::tags)
+__device__ __forceinline__ void put_tagged(unsigned long long* g, float v, unsigned tag) {
+  const unsigned long long w = (unsigned long long)__float_as_uint(v) | ((unsigned long long)tag << 32);
+  __hip_atomic_store(g, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // published-vector traffic of the group (global scratch)
 template <bool WT>
 __device__ __forceinline__ void st_pub(float* p, float v) {
@@ -569,6 +575,24 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
       for (int c = 0; c < 4; ++c) __hip_atomic_store(ctr + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
+  if (a.n == 1 && a.tags) {   // tagged granules (ExplFusedArgs::tags): no drain, no word
+    unsigned tag = a.done_seq | (ok ? 0u : 0x80000000u);
+    if (t < Da) {
+      const float mu_C = (a.sqrt_2delta * (sig * g)) / misc[4];
+      const float mu_E = mean + mu_C;
+      const float ev = a.eps ? a.eps[t] : philox_normal(a.seed, (unsigned long long)cnt_s, 3u, (unsigned)t);
+      const float nan = __int_as_float(0x7fc00000);
+      put_tagged(a.tags + t, ok ? tanhf(__fadd_rn(__fmul_rn(ev, sd), mu_E)) : nan, tag);
+      put_tagged(a.tags + Da + t, ok ? mu_E : nan, tag);
+      put_tagged(a.tags + 2 * Da + t, sd, tag);
+      if (a.grad) a.grad[t] = g;
+    }
+    if (t == 0) {
+      if (!a.eps) a.state->expl_counter = cnt_s + 1;
+      if (!ok && a.fail) __hip_atomic_store(a.fail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   if (t < Da) {
     const long e = (long)r * Da + t;
     const float mu_C = (a.sqrt_2delta * (sig * g)) / misc[4];
@@ -862,17 +886,9 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
     if (t + u * nt < n0a) w0a[t + u * nt] = wt[u];
   __syncthreads();
   EXPL_CLK(5);
-  for (int e = t; e < 2 * H; e += nt) {   // h1_i = relu(P_i + W0_i[:, Do:] a) (Da <= 32)
-    float wa[32], av[32];
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      wa[j] = j < Da ? w0a[(long)e * Da + j] : 0.f;
-      av[j] = j < Da ? x[Do + j] : 0.f;
-    }
+  for (int e = t; e < 2 * H; e += nt) {   // h1_i = relu(P_i + W0_i[:, Do:] a)
     float s = h1q[e];
-#pragma unroll
-    for (int j = 0; j < 32; ++j)
-      if (j < Da) s = fmaf(wa[j], av[j], s);
+    for (int j = 0; j < Da; ++j) s = fmaf(w0a[(long)e * Da + j], x[Do + j], s);
     h1q[e] = fmaxf(s, 0.f);
   }
   __syncthreads();
@@ -1039,6 +1055,27 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
   // the call's only group with a host-polled completion word: the outputs
   // (host memory) as system-scope stores, drained, then the word -- no ticket
   const bool solo = a.n == 1 && a.done;
+  if (a.n == 1 && a.tags) {   // tagged granules: no store drain, no completion word
+    const unsigned tag = a.done_seq | ((!ok || others_failed) ? 0x80000000u : 0u);
+    if (lane < Da) {
+      const float mu_C = (a.sqrt_2delta * (sig * g)) / nrm;
+      const float mu_E = mean + mu_C;
+      const float ev = a.eps ? a.eps[lane]
+                             : philox_normal(a.seed, (unsigned long long)cnt_s, 3u, (unsigned)lane);
+      const float nan = __int_as_float(0x7fc00000);
+      put_tagged(a.tags + lane, ok ? tanhf(__fadd_rn(__fmul_rn(ev, sd), mu_E)) : nan, tag);
+      put_tagged(a.tags + Da + lane, ok ? mu_E : nan, tag);
+      put_tagged(a.tags + 2 * Da + lane, sd, tag);
+      if (a.grad) a.grad[lane] = g;
+    }
+    if (lane == 0) {
+      if (!a.eps) a.state->expl_counter = cnt_s + 1;
+      if ((!ok || others_failed) && a.fail)
+        __hip_atomic_store(a.fail, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    EXPL_CLK3(11);
+    return;
+  }
   if (lane < Da) {
     const long e = (long)r * Da + lane;
     const float mu_C = (a.sqrt_2delta * (sig * g)) / nrm;

@@ -90,10 +90,13 @@ __device__ __forceinline__ void fwd_stage(const float* as, const float* bs, cons
 // past k_hi is fetched from the stage's first chunk instead (always in the
 // row); the chunk that straddles k_hi reads up to 3 floats past it (every
 // operand buffer is followed by >= 8 readable floats, gemm_operand.h).
+// rows: null, or A row m is buffer row rows[m] (the direct gather: the step's
+// index slot)
 template <int BM, int BN, int NB>
 __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const float* B, long ldb,
                                          int N, int k_lo, int k_hi, int m0, int n0, float* lds,
-                                         floatx16 (&acc)[BM / 64][BN / 64]) {
+                                         floatx16 (&acc)[BM / 64][BN / 64],
+                                         const int* rows = nullptr) {
   using G = FwdG<BM, BN>;
   constexpr int WM = G::WM, WN = G::WN, PA = G::PA, PB = G::PB;
   const int kb0 = k_lo & ~7;
@@ -111,7 +114,8 @@ __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const 
   for (int q = 0; q < PA; ++q) {
     const int r = 8 * (wave * PA + q) + (lane >> 3);
     ca[q] = 4 * ((lane & 7) ^ (r & 7));
-    sa[q] = A + (long)min(m0 + r, M - 1) * lda;
+    const int m = min(m0 + r, M - 1);
+    sa[q] = A + (long)(rows ? rows[m] : m) * lda;
   }
 #pragma unroll
   for (int q = 0; q < PB; ++q) {
@@ -163,6 +167,46 @@ __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const 
   }
 }
 
+// Side workgroup sb of nsb (256 threads) of a direct-gather step's forward
+// launches (GemmBatch::rg, blocks > 0): with rg.out, its rows of the step's
+// batch (row r = 4 sb + wave + 4 nsb k) copied from the replay through the
+// index slot -- the gather launch's copy, for the step's later readers --;
+// with rg.eps1, its share of the step's Philox eps.  A wave's row indices are
+// loaded together, and a row's float4s all in flight before its stores.
+__device__ __forceinline__ void fwd_gather_side(const RowGather& g, int sb, int nsb) {
+  const long long bc = g.state->batch_counter;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long n4 = g.row_stride >> 2;   // <= 256 (oac_sac row layouts: checked at launch)
+  constexpr int KR = 8;
+  const int* rows = g.out ? g.ring + (long)(bc % g.slots) * g.B : nullptr;
+  for (int r0 = 4 * sb + wave; rows && r0 < g.B; r0 += 4 * nsb * KR) {
+    int src_row[KR];
+#pragma unroll
+    for (int k = 0; k < KR; ++k) src_row[k] = rows[min(r0 + 4 * nsb * k, g.B - 1)];
+#pragma unroll 1
+    for (int k = 0; k < KR; ++k) {
+      const int r = r0 + 4 * nsb * k;
+      if (r >= g.B) break;
+      const float4* src = reinterpret_cast<const float4*>(g.replay) + (long)src_row[k] * n4;
+      float4* dst = reinterpret_cast<float4*>(g.out) + (long)r * n4;
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long i = lane + 64 * u;
+        v[u] = src[i < n4 ? i : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (lane + 64 * u < n4) dst[lane + 64 * u] = v[u];
+    }
+  }
+  if (!g.eps1) return;
+  for (int e = sb * 256 + threadIdx.x; e < g.n_eps; e += nsb * 256) {
+    g.eps1[e] = philox_normal(g.seed, (unsigned long long)bc, 1u, (unsigned)e);
+    g.eps2[e] = philox_normal(g.seed, (unsigned long long)bc, 2u, (unsigned)e);
+  }
+}
+
 template <int BM, int BN, int NB>
 __global__ void __launch_bounds__(256)
 gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
@@ -172,8 +216,15 @@ gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
   __shared__ __attribute__((aligned(16))) float lds[NB * G::STAGE];
   if (batch.publish && blockIdx.x == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
-  const int bid = xcd_tile(blockIdx.x, gridDim.x);
-  if (bid >= total_tiles) return;   // grid == total_tiles: never taken
+  if ((int)blockIdx.x >= total_tiles) {   // side workgroups of a direct gather (GemmBatch::rg)
+    fwd_gather_side(batch.rg, blockIdx.x - total_tiles, gridDim.x - total_tiles);
+    return;
+  }
+  const int bid = xcd_tile(blockIdx.x, total_tiles);
+  // the direct gather's index slot (the A rows of the a_rows tasks)
+  const int* rows = batch.rg.ring && batch.rg.slots > 0
+                        ? batch.rg.ring + (long)(batch.rg.state->batch_counter % batch.rg.slots) * batch.rg.B
+                        : nullptr;
   int ti = 0;
   ti = bid >= tb1 ? 1 : ti; ti = bid >= tb2 ? 2 : ti; ti = bid >= tb3 ? 3 : ti;
   ti = bid >= tb4 ? 4 : ti; ti = bid >= tb5 ? 5 : ti; ti = bid >= tb6 ? 6 : ti;
@@ -193,13 +244,14 @@ gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
   PIPE_CLK(0);
-  fwd_pipe<BM, BN, NB>(t.A, t.lda, t.M, t.B, t.ldb, t.N, 0, t.K, m0, n0, lds, acc);
+  const int* arows = t.a_rows ? rows : nullptr;
+  fwd_pipe<BM, BN, NB>(t.A, t.lda, t.M, t.B, t.ldb, t.N, 0, t.K, m0, n0, lds, acc, arows);
   PIPE_CLK(29);
   rd_epilogue<WM, WN, kEpiFwd>(t, mw, nw, acc, false);
   PIPE_CLK(30);
   if (t.epi == EPI_BIAS_RANK_RELU) {   // + U V^T on the same accumulators (gemm_big.hip)
     if (t.U == t.A + t.K && t.ldu == t.lda && t.V == t.B + t.K && t.ldv == t.ldb)
-      fwd_pipe<BM, BN, NB>(t.A, t.lda, t.M, t.B, t.ldb, t.N, t.K, t.K + t.R, m0, n0, lds, acc);
+      fwd_pipe<BM, BN, NB>(t.A, t.lda, t.M, t.B, t.ldb, t.N, t.K, t.K + t.R, m0, n0, lds, acc, arows);
     else
       fwd_pipe<BM, BN, NB>(t.U, t.ldu, t.M, t.V, t.ldv, t.N, 0, t.R, m0, n0, lds, acc);
     epi_dispatch<WM, WN, EPI_BIAS_RANK_RELU>(t, mw, nw, acc, true);
@@ -208,12 +260,19 @@ gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
 }
 
 // forward batches this kernel takes: both operands k-contiguous, plain A, no
-// split, no second product, the forward epilogues of the register-direct kernel
+// split, no second product, the forward epilogues of the register-direct
+// kernel; a_rows tasks (the direct gather) with the batch's RowGather, whose
+// rank-R columns (if any) continue the same rows
 bool gemm_fwd_supports(const GemmBatch& b) {
   if (b.fuse_adam || b.ntasks < 1) return false;
+  if (b.rg.blocks > 0 && !b.rg.state) return false;
+  if ((b.rg.ring || b.rg.out) &&
+      (!b.rg.ring || !b.rg.state || b.rg.slots < 1 || b.rg.row_stride % 4 || b.rg.row_stride / 4 > 256))
+    return false;
   for (int i = 0; i < b.ntasks; ++i) {
     const GemmTask& t = b.t[i];
-    if (!t.a_kc || !t.b_kc || t.a_mode != A_PLAIN || t.ksplit > 1 || t.K2 > 0 || t.a_rows) return false;
+    if (!t.a_kc || !t.b_kc || t.a_mode != A_PLAIN || t.ksplit > 1 || t.K2 > 0) return false;
+    if (t.a_rows && (!b.rg.ring || (t.epi == EPI_BIAS_RANK_RELU && t.U != t.A + t.K))) return false;
     if (t.epi != EPI_STORE && t.epi != EPI_BIAS && t.epi != EPI_BIAS_RELU &&
         t.epi != EPI_BIAS_RANK_RELU && t.epi != EPI_BIAS_RELU_DOT)
       return false;
@@ -254,9 +313,10 @@ hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   // register-bound to one workgroup per CU either way); OAC_FWD2_NB forces one
   static const int nb_env = [] { const char* e = getenv("OAC_FWD2_NB"); return e ? atoi(e) : 0; }();
   const int nb = (nb_env == 2 || nb_env == 3) ? nb_env : (bm == 128 && bn == 64) ? 2 : 3;
+  const int grid = b.total_tiles + b.rg.blocks;
 #define OAC_FWD(BM_, BN_, NB_) \
   if (bm == BM_ && bn == BN_ && nb == NB_) { \
-    OAC_LAUNCH((gemm_fwd_kernel<BM_, BN_, NB_>), dim3(b.total_tiles), dim3(256), 0, s, b.total_tiles, \
+    OAC_LAUNCH((gemm_fwd_kernel<BM_, BN_, NB_>), dim3(grid), dim3(256), 0, s, b.total_tiles, \
                tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
     return hipGetLastError(); }
   OAC_FWD(128, 128, 3) OAC_FWD(128, 64, 3) OAC_FWD(64, 128, 3) OAC_FWD(64, 64, 3)

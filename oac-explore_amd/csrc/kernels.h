@@ -128,6 +128,10 @@ struct ExplFusedArgs {                  // expl_split.hip: the exploration actio
                                         // bit 31 of the word set: a hand-off of the call timed out
   unsigned* fail;                       // zeroed device word: a group's timed-out hand-off (re-armed
                                         // by the kernel that reports it)
+  // non-null with n == 1 (oac_expl_action_now): the outputs as [3][Da] tagged
+  // 8-byte granules {value bits, done_seq | failed << 31} in host memory, in
+  // place of the drained outputs + completion word (no wait for the stores)
+  unsigned long long* tags;
 };
 // expl_split.hip: one observation per group of expl_split_group(rows) <=
 // kExplGroup workgroups; a launch carries at most kExplRows observations

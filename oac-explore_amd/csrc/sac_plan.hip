@@ -231,6 +231,13 @@ static int head_col_chunks(int B, int H) {
   return B >= 1024 ? std::max(1, (H + 255) / 256) : std::max(1, (H + 63) / 64);
 }
 
+// the large-batch SAC step can gather directly (phase0): every layer-0
+// product on the LDS-DMA forward kernel, rows that kernel's side copy takes
+static bool big_direct_ok(const SacPlan& p) {
+  return p.c.kind == OAC_KIND_SAC && p.cfg == 2 && fwd2_on() && p.c.hidden >= 64 &&
+         p.c.row_stride % 4 == 0 && p.c.row_stride / 4 <= 256;
+}
+
 static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool critic_done = false) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
@@ -241,7 +248,13 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
   // host-written index slot and its side blocks do the gather's copy + eps
   const bool direct = p.rows_direct && p.cfg == 0 && gather_n == 1 && !critic_done &&
                       (flags & OAC_STEP_GATHER) && p.b.ring_slots > 0;
-  if (!direct && gather_n > 0 && (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS)))
+  // the same at large batch: the LDS-DMA forward kernel stages layer 0's rows
+  // straight from the replay through the step's index slot, and side
+  // workgroups of that launch copy the batch and draw eps (gemm_fwd.hip;
+  // the conditions keep every layer-0 product on that kernel)
+  const bool direct_big = !direct && big_direct_ok(p) && gather_n == 1 && !critic_done &&
+                          (flags & OAC_STEP_GATHER) && p.b.ring_slots > 0;
+  if (!direct && !direct_big && gather_n > 0 && (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS)))
     if (gather_steps(p, flags, gather_n, s)) return 1;
   const float* pol = p.b.params;
   const float* q1 = p.b.params + L.q1_base;
@@ -251,12 +264,19 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
   {  // layer 0: policy(obs), policy(next_obs), critic obs-projections
     GemmBatch gb{};
     gb.publish = p.state(); gb.pub_beta1 = c.beta1; gb.pub_beta2 = c.beta2;   // step's Adam constants
-    const float* R0 = direct ? p.b.replay : X;   // rows base: the replay (indexed) or the batch
+    const float* R0 = (direct || direct_big) ? p.b.replay : X;   // rows base: the replay (indexed) or the batch
     add(gb, t_fwd(R0 + c.off_obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
     add(gb, t_fwd(R0 + c.off_next_obs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(W_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
     if (!critic_done) {
       add_critic_l0(p, gb, R0);
       add_target_l0(p, gb, R0);
+    }
+    p.direct_big = direct_big;
+    p.direct_ring = gather_idx(p, flags);
+    if (direct_big) {   // every layer-0 product reads its rows through the index slot
+      for (int i = 0; i < gb.ntasks; ++i) gb.t[i].a_rows = 1;
+      RowGather& g = gb.rg;
+      g.ring = gather_idx(p, flags); g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
     }
     if (direct) {
       for (int i = 0; i < gb.ntasks; ++i) gb.t[i].a_rows = 1;
@@ -278,6 +298,11 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
     add(gb, t_fwd(p.W(W_H1P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_H2P), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
     add(gb, t_fwd(p.W(W_H1P2), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_H2P2), H, EPI_BIAS_RELU, pol + L.pol_fc1_b));
     if (!critic_done) add_critic_l1(p, gb);
+    if (direct_big && (flags & OAC_STEP_DEVICE_EPS)) {   // the step's eps: side workgroups
+      RowGather& g = gb.rg;                               // (2 tiles per CU: a slot is free)
+      g.state = p.state(); g.eps1 = p.E1(); g.eps2 = p.E2(); g.n_eps = B * Da; g.seed = c.seed;
+      g.blocks = 256;
+    }
     if (run_gemm(p, gb, s)) return 1;
   }
   if (!qdot(p)) {  // q1/q2 predictions (the small-batch path has them from layer 1)
@@ -338,6 +363,12 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
     const int outs[4] = {W_H2N1, W_H2N2, W_H2T1, W_H2T2};
     const int qv[4] = {QV_QN1, QV_QN2, QV_TQ1, QV_TQ2};
     for (int i = 0; i < 4; ++i) add(gb, q_l1(p, p.W(ins[i]), nets[i], p.W(outs[i]), qv[i]));
+    if (p.direct_big) {   // the direct-gather step's batch copy (its first reader is the
+      RowGather& g = gb.rg;   // targets kernel next): side workgroups in the free slot per CU
+      g.ring = p.direct_ring; g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
+      g.replay = p.b.replay; g.row_stride = RS; g.out = X;
+      g.blocks = 256;
+    }
     if (run_gemm(p, gb, s)) return 1;
   }
   if (part != 2 && !qdot(p)) {  // last layer
@@ -779,7 +810,10 @@ int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
     // direct mode needs the small-batch kernel (cfg 0)
     p.rows_direct = p.cfg == 0 && !has_target_policy(p.c.kind) &&
                     p.c.kind != OAC_KIND_PARTICLE;   // sac_plan's run_step / phase0 only
-    p.idx_host = !p.rows_direct;
+    // (a direct large-batch step's 768 layer-0 tiles would each read their
+    // rows' indices across the host link: its slot is copied to the device
+    // ring instead, one H2D copy ahead of the step)
+    p.idx_host = !p.rows_direct && !big_direct_ok(p);
     // not direct (large batch): the copy path still stages through this ring
     if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
     if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }

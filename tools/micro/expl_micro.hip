@@ -49,6 +49,9 @@ int main(int argc, char** argv) {
   CK(hipHostMalloc((void**)&obs, sizeof(float) * (Do + Da), fl));
   CK(hipHostMalloc((void**)&out, sizeof(float) * 3 * Da, fl));
   CK(hipHostMalloc((void**)&done, 64, fl));
+  unsigned long long* tags;   // the single call's outputs as tagged granules (oac_expl_action_now)
+  CK(hipHostMalloc((void**)&tags, sizeof(unsigned long long) * 3 * Da, fl));
+  memset(tags, 0, sizeof(unsigned long long) * 3 * Da);
   for (int k = 0; k < Do; ++k) obs[k] = (float)((k * 37) % 101) / 101.f - 0.5f;
   *done = 0;
   const long scr = expl_split_scratch_floats(H);
@@ -64,7 +67,7 @@ int main(int argc, char** argv) {
   a.q_fc0_w = q0w; a.q_fc0_b = q0b; a.q_fc1_w = q1w; a.q_fc1_b = q1b; a.q_last_w = qlw; a.q_last_b = qlb;
   a.Do = Do; a.Da = Da; a.H = H; a.n = 1; a.nq = 2; a.K = 1;
   a.eps = nullptr; a.out = out; a.grad = grad; a.state = st; a.ticket = words; a.fail = words + 1;
-  a.seed = 7; a.beta_UB = 4.66f; a.sqrt_2delta = 6.86f; a.ub_index = -1; a.done = done;
+  a.seed = 7; a.beta_UB = 4.66f; a.sqrt_2delta = 6.86f; a.ub_index = -1; a.done = done; a.tags = tags;
   hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   const int G = expl_split_group(1);
   std::vector<std::vector<long long>> clk(64);
@@ -80,15 +83,18 @@ int main(int argc, char** argv) {
       CK(launch_expl_split(a, 0, 1, ws + 4096, s));
     }
     // bounded: a failed call (bit 31) or a faulted launch ends the run
-    while ((*(volatile unsigned*)done & 0x7fffffffu) != a.done_seq) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2) ||
-          hipStreamQuery(s) != hipErrorNotReady) {
-        if ((*(volatile unsigned*)done & 0x7fffffffu) == a.done_seq) break;
-        printf("call %d: no completion (stream %s)\n", c, hipGetErrorString(hipStreamQuery(s)));
-        return 1;
+    for (int i = 0; i < 3 * Da; ++i) {
+      volatile unsigned long long* g = tags + i;
+      while (((unsigned)(*g >> 32) & 0x7fffffffu) != a.done_seq) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2) ||
+            hipStreamQuery(s) != hipErrorNotReady) {
+          if (((unsigned)(*g >> 32) & 0x7fffffffu) == a.done_seq) break;
+          printf("call %d: no completion (stream %s)\n", c, hipGetErrorString(hipStreamQuery(s)));
+          return 1;
+        }
       }
+      if (*g >> 63) { printf("call %d: hand-off timed out\n", c); return 1; }
     }
-    if (*(volatile unsigned*)done & 0x80000000u) { printf("call %d: hand-off timed out\n", c); return 1; }
     const auto t1 = std::chrono::steady_clock::now();
     CK(hipStreamSynchronize(s));
     wall.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
