@@ -1166,9 +1166,12 @@ int expl_device_cus() {
 
 // group size for a launch of n_rows observations: the device's CUs shared
 // out, at most kExplGroup
+// (tools/micro/expl_micro's group-size sweep lowers it)
+int g_expl_group_cap = kExplGroup;
 int expl_split_group(int n_rows) {
   const int g = expl_device_cus() / (n_rows < 1 ? 1 : n_rows);
-  return g < 1 ? 1 : (g > kExplGroup ? kExplGroup : g);
+  const int cap = g_expl_group_cap;
+  return g < 1 ? 1 : (g > cap ? cap : g);
 }
 
 // the twin-critic kernel off (tools/micro/expl_micro's A/B against the split kernel)

@@ -126,6 +126,18 @@ inline bool split_adam_on(const SacPlan& p) {
 int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long* off,
               const long* n, bool book, hipStream_t s);
 
+// a large-batch SAC step can gather directly (sac_plan phase0): every layer-0
+// product on the LDS-DMA forward kernel, reading its rows from the replay
+// through the index slot; eps and the batch copy from side workgroups of
+// later forward launches.  (The same for the P-OAC step measured neutral at
+// configs[4]: 18 -> 17 launches, 185.3 -> 184.3 us of launches, 203.9 us per
+// step either way -- its short-K layer 0 took the index round trips, +3.2 us;
+// not kept.)
+inline bool big_direct_ok(const SacPlan& p) {
+  return p.c.kind == OAC_KIND_SAC && p.cfg == 2 && fwd2_on() && p.c.hidden >= 64 &&
+         p.c.row_stride % 4 == 0 && p.c.row_stride / 4 <= 256;
+}
+
 // particle trainer (particle_plan.hip)
 void particle_layout_workspace(SacPlan& p);
 int particle_run_step(SacPlan& p, int flags, hipStream_t s);

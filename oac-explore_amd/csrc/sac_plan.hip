@@ -231,13 +231,6 @@ static int head_col_chunks(int B, int H) {
   return B >= 1024 ? std::max(1, (H + 255) / 256) : std::max(1, (H + 63) / 64);
 }
 
-// the large-batch SAC step can gather directly (phase0): every layer-0
-// product on the LDS-DMA forward kernel, rows that kernel's side copy takes
-static bool big_direct_ok(const SacPlan& p) {
-  return p.c.kind == OAC_KIND_SAC && p.cfg == 2 && fwd2_on() && p.c.hidden >= 64 &&
-         p.c.row_stride % 4 == 0 && p.c.row_stride / 4 <= 256;
-}
-
 static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool critic_done = false) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;

@@ -5,7 +5,7 @@
 // Prints the per-stage wall clock of the group's first and last workgroup
 // (100 MHz counter, median over the calls) and the host wall per call.
 // Build: tools/micro/Makefile.  Run: tools/micro/expl_micro [calls] [obs in arguments 0|1]
-//   [split kernel 0|1: the four-hand-off kernel instead of the twin-critic one]
+//   [split kernel 0|1: the four-hand-off kernel instead of the twin-critic one] [group cap]
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <chrono>
@@ -15,7 +15,7 @@
 #include <vector>
 #include "../../oac-explore_amd/csrc/expl_split.hip"
 
-namespace oac { thread_local ExtTiming g_ext_timing; extern bool g_expl_twin_off; }
+namespace oac { thread_local ExtTiming g_ext_timing; extern bool g_expl_twin_off; extern int g_expl_group_cap; }
 using namespace oac;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
@@ -35,6 +35,7 @@ int main(int argc, char** argv) {
   const bool obs_arg = argc > 2 && atoi(argv[2]) != 0;   // the observation in the arguments
   const bool split = argc > 3 && atoi(argv[3]) != 0;     // the four-hand-off kernel
   g_expl_twin_off = split;
+  if (argc > 4) g_expl_group_cap = atoi(argv[4]);   // group-size sweep
   const int Do = 376, Da = 17, H = 256, Dq = Do + Da;
   // parameter blocks: policy [fc0 | fc1 | head], critics [fc0 | fc1 | last]
   const long p0w = 0, p0b = p0w + (long)H * Do, p1w = p0b + H, p1b = p1w + (long)H * H,
