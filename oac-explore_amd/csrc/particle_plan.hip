@@ -148,7 +148,7 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
   return 0;
 }
 
-static int pphase1(SacPlan& p, int flags, hipStream_t s, bool split = false) {
+static int pphase1(SacPlan& p, int flags, hipStream_t s) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -211,18 +211,13 @@ static int pphase1(SacPlan& p, int flags, hipStream_t s, bool split = false) {
     // fewest workgroups of the backward launches; in the layer-1 launch it
     // added 5.8 us)
     if (fold) add(gb, tl);
-    if (split) {   // the critic's layer 1 + last layer beside its layer-0 dW
-      const long off[1] = {(long)L.q_fc1_w};
-      const long n[1] = {(long)(L.q_size - L.q_fc1_w)};
-      if (side_adam(p, gb, critic_adam(p, 0, nullptr), 1, off, n, true, s)) return 1;
-    }
     if (run_gemm(p, gb, s)) return 1;
   }
   return 0;
 }
 
 // critic Adam done; post-step critic forward on (obs, a~), alpha, policy grads
-static int pphase2(SacPlan& p, hipStream_t s, bool split = false) {
+static int pphase2(SacPlan& p, hipStream_t s) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -301,11 +296,6 @@ static int pphase2(SacPlan& p, hipStream_t s, bool split = false) {
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(X_DH1P), H, H, B, X + c.off_obs, RS, Do, gp + L.pol_fc0_w, gp + L.pol_fc0_b,
                  L.pol_size, p.sp_p0));
-    if (split) {   // the policy's layer 1 + heads beside its layer-0 dW
-      const long off[1] = {(long)L.pol_fc1_w};
-      const long n[1] = {(long)(L.pol_size - L.pol_fc1_w)};
-      if (side_adam(p, gb, policy_adam(p, 0, nullptr), 1, off, n, false, s)) return 1;
-    }
     if (run_gemm(p, gb, s)) return 1;
   }
   return 0;
@@ -314,30 +304,22 @@ static int pphase2(SacPlan& p, hipStream_t s, bool split = false) {
 int particle_run_step(SacPlan& p, int flags, hipStream_t s) {
   p.launches = 0;
   if (pphase0(p, flags, s)) return 1;
-  // split_adam_on: the critic's layer 1 + last layer and the policy's layer 1
-  // + heads run as side workgroups of the layer-0 dW launches; the layer-0
-  // ranges keep their launches (the post-step critic forward reads the
-  // critic's layer 0 next; the policy's is the step's last update)
-  // Off by default here: configs[4]'s layer-0 dW launches are short (7.7
-  // us; 111 obs dims), the side work lengthened each by ~2.6 us while the
-  // remaining Adam launches shrank by 0.5 us (4,336 -> 4,275 steps/s);
-  // OAC_SPLIT_ADAM_POAC=1 turns it on
-  static const bool poac_on = [] { const char* e = getenv("OAC_SPLIT_ADAM_POAC"); return e && atoi(e) != 0; }();
-  // (not with the last layer's dW in the layer-0 dW launch, dh2_in_targets:
-  // the side blocks would update the last layer while its gradient is
-  // still being written in the same launch)
-  const bool split = poac_on && split_adam_on(p) && !dh2_in_targets(p);
-  if (pphase1(p, flags, s, split)) return 1;
+  // One Adam launch per group here.  (Side-workgroup Adam, as the SAC step
+  // runs it, measured slower at configs[4] -- its layer-0 dW launches are short
+  // (7.7 us; 111 obs dims): the side work lengthened each by ~2.6 us while the
+  // remaining Adam launches shrank by 0.5 us, 4,336 -> 4,275 steps/s -- and
+  // with the last layer's dW in the layer-0 dW launch the side blocks would
+  // update that layer while its gradient is still being written; the switch
+  // that kept it for A/B runs is gone.)
+  if (pphase1(p, flags, s)) return 1;
   {
     AdamArgs a = critic_adam(p, 0, nullptr);   // alpha is updated after the critic step
-    if (split) { a.n = p.L.q_fc1_w; a.no_book = 1; }
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
   }
-  if (pphase2(p, s, split)) return 1;
+  if (pphase2(p, s)) return 1;
   {
     AdamArgs a = policy_adam(p, 0, p.c.auto_alpha ? p.alpha() : nullptr);
-    if (split) a.n = p.L.pol_fc1_w;
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
   }

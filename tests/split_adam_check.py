@@ -2,7 +2,7 @@
 steps (B = 1100, hidden 48 / 80) of SACTrainer and ParticleTrainerOAC with
 fixed batches and eps; the trainers' params / targets / Adam moments are
 written to the .npz path given on the command line.  The parent compares the
-side-workgroup Adam (OAC_SPLIT_ADAM / OAC_SPLIT_ADAM_POAC) against one Adam
+side-workgroup Adam (OAC_SPLIT_ADAM, the SAC step) against one Adam
 launch per group: the same adam_flat_elem on the same slabs, so bit for bit."""
 import os
 import sys

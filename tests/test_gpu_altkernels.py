@@ -38,23 +38,20 @@ def test_alternative_large_batch_kernels_match_oracle(name):
 
 
 def test_side_workgroup_adam_is_bitwise_the_adam_launch(tmp_path):
-    """Large-batch side-workgroup Adam (GemmBatch::side_adam; on for SAC, opt-in
-    for P-OAC) against one Adam launch per group, and the policy head's
-    column-chunk count, child processes: params, targets and Adam moments bit
-    for bit after three steps."""
+    """Large-batch side-workgroup Adam (GemmBatch::side_adam; the SAC step)
+    against one Adam launch per group, and the policy head's column-chunk
+    count, child processes: params, targets and Adam moments bit for bit after
+    three steps (the P-OAC step, one Adam launch per group either way, rides
+    along as a control)."""
     import numpy as np
     outs = {}
-    # P-OAC: the side path needs its last-layer dW out of the layer-0 dW
-    # launch (OAC_DH2_TARGETS=0); both runs use that launch layout
-    for name, env in {"side": {"OAC_SPLIT_ADAM": "1", "OAC_SPLIT_ADAM_POAC": "1",
-                               "OAC_DH2_TARGETS": "0"},
-                      "launch": {"OAC_SPLIT_ADAM": "0", "OAC_SPLIT_ADAM_POAC": "0",
-                                 "OAC_DH2_TARGETS": "0"},
+    for name, env in {"side": {"OAC_SPLIT_ADAM": "1", "OAC_DH2_TARGETS": "0"},
+                      "launch": {"OAC_SPLIT_ADAM": "0", "OAC_DH2_TARGETS": "0"},
                       # and the policy head on two 128-column chunks per row
                       # block (recomputed heads, 2 pairs per wave): the same
                       # arithmetic per output, so bitwise too
-                      "head_cc2": {"OAC_SPLIT_ADAM": "1", "OAC_SPLIT_ADAM_POAC": "1",
-                                   "OAC_DH2_TARGETS": "0", "OAC_HEAD_CC": "2"}}.items():
+                      "head_cc2": {"OAC_SPLIT_ADAM": "1", "OAC_DH2_TARGETS": "0",
+                                   "OAC_HEAD_CC": "2"}}.items():
         out = str(tmp_path / f"{name}.npz")
         r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "split_adam_check.py"), out],
                            env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
