@@ -197,6 +197,8 @@ struct SmallLds {
   static constexpr int N = RED > 2 * 32 * 65 ? RED : 2 * 32 * 65;   // reused for the epilogue operands
 };
 
+constexpr int kGatherU = 4;   // float4s per lane of a side block's row copy (rows <= 1 KB)
+
 template <int NW, int GPW>
 __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int publish, int tb1,
                                                  int tb2, int tb3, int tb4, int tb5, int tb6,
@@ -212,21 +214,31 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     rows = batch.rg.ring + (long)(bc % batch.rg.slots) * batch.rg.B;
   }
   if (bid >= total_tiles + batch.adam_blocks) {   // side blocks: the batch copy and the eps draws
+    // one wave per row: the row's index is one read of the host slot per
+    // wave (every lane the same word), the row's float4s all in flight before
+    // their stores; then the eps
     const RowGather& g = batch.rg;
-    const long n4 = g.row_stride >> 2, nrow = (long)g.B * n4;
-    const long stride = (long)g.blocks * 64 * NW;
+    const int sb = bid - total_tiles - batch.adam_blocks;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const long n4 = g.row_stride >> 2;
+    const int nwv = g.blocks * NW;
     const float4* src = reinterpret_cast<const float4*>(g.replay);
     float4* dst = reinterpret_cast<float4*>(g.out);
-    for (long i = (long)(bid - total_tiles - batch.adam_blocks) * 64 * NW + threadIdx.x;
-         i < nrow + (g.eps1 ? g.n_eps : 0); i += stride) {
-      if (i < nrow) {
-        const long r = i / n4, c = i - r * n4;
-        dst[r * n4 + c] = src[(long)rows[r] * n4 + c];
-      } else {
-        const unsigned e = (unsigned)(i - nrow);
-        g.eps1[e] = philox_normal(g.seed, (unsigned long long)bc, 1u, e);
-        g.eps2[e] = philox_normal(g.seed, (unsigned long long)bc, 2u, e);
+    for (int r = sb * NW + wave; r < g.B; r += nwv) {
+      const long sr = rows[r];
+      float4 v[kGatherU];
+#pragma unroll
+      for (int u = 0; u < kGatherU; ++u) {
+        const long c = lane + 64 * u;
+        v[u] = src[sr * n4 + (c < n4 ? c : 0)];
       }
+#pragma unroll
+      for (int u = 0; u < kGatherU; ++u)
+        if (lane + 64 * u < n4) dst[(long)r * n4 + lane + 64 * u] = v[u];
+    }
+    for (int e = sb * 64 * NW + threadIdx.x; g.eps1 && e < g.n_eps; e += g.blocks * 64 * NW) {
+      g.eps1[e] = philox_normal(g.seed, (unsigned long long)bc, 1u, (unsigned)e);
+      g.eps2[e] = philox_normal(g.seed, (unsigned long long)bc, 2u, (unsigned)e);
     }
     return;
   }
@@ -267,9 +279,16 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   GS_STAGE(1);
-  // the direct gather's row index (host memory, the longest wait of the
-  // launch) is requested before anything else
-  const int arow = (t.a_rows && rows) ? rows[min(m0 + (lane & 31), t.M - 1)] : -1;
+  // the direct gather's row indices (host memory, the longest wait of the
+  // launch): one read of the tile's 32 by wave 0, handed to the other waves
+  // through LDS -- one host request per workgroup, not one per wave
+  int arow = -1;
+  if (t.a_rows && rows) {
+    __shared__ int tile_rows[32];
+    if (wave == 0 && lane < 32) tile_rows[lane] = rows[min(m0 + lane, t.M - 1)];
+    __syncthreads();
+    arow = tile_rows[lane & 31];
+  }
 
   EpiIn xin[PER];
 #pragma unroll

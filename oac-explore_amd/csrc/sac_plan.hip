@@ -280,9 +280,8 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
         g.eps1 = p.E1(); g.eps2 = p.E2(); g.n_eps = B * Da;
       }
       g.seed = c.seed;
-      // enough workgroups that each thread moves ~4 float4 of rows / eps
-      const long items = (long)B * (RS / 4) + (g.eps1 ? g.n_eps : 0);
-      g.blocks = (int)std::min<long>(64, std::max<long>(1, (items + 4095) / 4096));
+      // a wave per row (>= 8 waves per workgroup), the eps on the same threads
+      g.blocks = std::max(1, (B + 7) / 8);
     }
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -802,7 +801,8 @@ int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
     p.owns_host_ring = true;
     // direct mode needs the small-batch kernel (cfg 0)
     p.rows_direct = p.cfg == 0 && !has_target_policy(p.c.kind) &&
-                    p.c.kind != OAC_KIND_PARTICLE;   // sac_plan's run_step / phase0 only
+                    p.c.kind != OAC_KIND_PARTICLE &&   // sac_plan's run_step / phase0 only
+                    p.c.row_stride / 4 <= 64 * 4;      // a side wave's row copy (gemm_small.hip)
     // (a direct large-batch step's 768 layer-0 tiles would each read their
     // rows' indices across the host link: its slot is copied to the device
     // ring instead, one H2D copy ahead of the step)
