@@ -95,6 +95,11 @@ struct CriticTargetArgs {
   int B;
   float* y; float* dq1; float* dq2; float* gq1; float* gq2; float* sqe1; float* sqe2;
   float* qnew;
+  // large batch (wl_h2[0] set): the critics' last-layer dW in split-K slab
+  // form, slab s = the sum over rows [256 s, 256 s + 256) -- the rows of
+  // block s -- of dq_i[m] h2_i[m, :] (and of dq_i[m] for the bias), computed
+  // here (grid.y = wl_H / 32 column groups) instead of as 64-row GEMM tiles
+  const float* wl_h2[2]; float* wl_g[2]; float* wl_gb[2]; long wl_slab_stride; int wl_H;
 };
 
 struct PolicyHeadBwdArgs {

@@ -108,6 +108,18 @@ __global__ void __launch_bounds__(256) critic_targets_kernel(CriticTargetArgs p)
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   TargetRowIn x;
   target_row_load(p, min(r, p.B - 1), x);
+  // last-layer dW (p.wl_h2): thread t owns column 32 blockIdx.y + (t & 31) of
+  // critic (t >> 5) & 1 over the 64 rows 64 (t >> 6) .. + 63 of this block;
+  // those h2 values are requested with the row's inputs
+  const bool wl = p.wl_h2[0] != nullptr;
+  const int t = threadIdx.x, wi = (t >> 5) & 1, wpart = t >> 6;
+  const int wn = blockIdx.y * 32 + (t & 31);
+  float h2v[64];
+  if (wl) {
+    const float* hp = (wi ? p.wl_h2[1] : p.wl_h2[0]) + (long)(blockIdx.x * 256 + 64 * wpart) * p.wl_H + wn;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) h2v[j] = hp[(long)j * p.wl_H];
+  }
   float alpha = 0.f;
   if (p.alpha) {
     // every block computes the update identically; block 0 publishes next_*
@@ -115,11 +127,50 @@ __global__ void __launch_bounds__(256) critic_targets_kernel(CriticTargetArgs p)
     const float S = (p.world_size > 1) ? (p.logp_part ? block_part_sum(p.logp_part, p.n_logp_part, red)
                                                       : p.alpha->sum)
                                        : logp_sum256(p.logp1, p.B, p.target_entropy, red);
-    alpha = alpha_update(p, S, blockIdx.x == 0 && threadIdx.x == 0);
+    alpha = alpha_update(p, S, blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0);
   }
-  if (r >= p.B) return;
+  if (!wl) {
+    if (r >= p.B) return;
+    float dq1, dq2;
+    target_row(p, r, x, alpha, true, dq1, dq2);
+    return;
+  }
+  // (wl: B % 256 == 0, every thread has a row; column group 0 writes the rows)
+  __shared__ float sdq[2][256];
+  __shared__ float spart[4][65];
+  __shared__ float sbias[2][4];
   float dq1, dq2;
-  target_row(p, r, x, alpha, true, dq1, dq2);
+  target_row(p, r, x, alpha, blockIdx.y == 0, dq1, dq2);
+  sdq[0][t] = dq1;
+  sdq[1][t] = dq2;
+  __syncthreads();
+  {
+    float s = 0.f;   // rows in order within the 64-row part
+#pragma unroll
+    for (int j = 0; j < 64; ++j) s = fmaf(sdq[wi][64 * wpart + j], h2v[j], s);
+    spart[wpart][wi * 32 + (t & 31)] = s;
+  }
+  if (blockIdx.y == 0 && t < 8) {   // the bias: sum of dq_i over the part
+    const int bi = t >> 2, bp = t & 3;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) s += sdq[bi][64 * bp + j];
+    sbias[bi][bp] = s;
+  }
+  __syncthreads();
+  const long so = (long)blockIdx.x * p.wl_slab_stride;   // this block's slab
+  if (t < 64) {   // parts in order
+    float s = spart[0][t];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) s += spart[q][t];
+    ((t >> 5) ? p.wl_g[1] : p.wl_g[0])[so + blockIdx.y * 32 + (t & 31)] = s;
+  } else if (blockIdx.y == 0 && t < 66) {
+    const int bi = t - 64;
+    float s = sbias[bi][0];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) s += sbias[bi][q];
+    (bi ? p.wl_gb[1] : p.wl_gb[0])[so] = s;
+  }
 }
 
 // --------------------------------------------------------------------------
@@ -160,7 +211,11 @@ hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s) {
 hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s) {
   // 256 rows per block: the per-row work spreads over CUs (every block redoes
   // the 4-byte-per-row alpha reduction, which is cheap)
-  OAC_LAUNCH(critic_targets_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  if (a.wl_h2[0] && (a.B % 256 || a.wl_H % 32 || !a.wl_h2[1] || !a.wl_g[0] || !a.wl_g[1] ||
+                    !a.wl_gb[0] || !a.wl_gb[1]))
+    return hipErrorInvalidValue;
+  OAC_LAUNCH(critic_targets_kernel, dim3((a.B + 255) / 256, a.wl_h2[0] ? a.wl_H / 32 : 1), dim3(256), 0,
+             s, a);
   return hipGetLastError();
 }
 hipError_t launch_policy_head_backward(const PolicyHeadBwdArgs& a, hipStream_t s) {

@@ -333,6 +333,20 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
   return 0;
 }
 
+// Large-batch SAC: the width-1 last layers' dW as slabs of the targets kernel
+// (one 256-row block per split) instead of 64-row GEMM tiles with one useful
+// row -- the critic layer-1 backward launch keeps 1,024 workgroups (one round
+// at four per CU) instead of 1,152: B=4096 34.1 -> 27.5 us for that launch
+// (At B=256 the same, with layer 1's bias gradient -- the small kernel's ones
+// column tiles -- also from the targets kernel, made the layer-1 backward one
+// round of 256 tiles, 8.0 -> 5.6 us, but the targets launch 5.3 -> 8.3-9.1
+// us: eight blocks each redoing the row math and the h2 pass; not kept.)
+static bool wl_in_targets(const SacPlan& p) {
+  const oac_sac_config& c = p.c;
+  return c.kind == OAC_KIND_SAC && c.q_out == 1 && p.cfg == 2 && bwdp_on() &&
+         p.sp_ql.kchunk == 256 && p.sp_ql.S * 256 == c.batch && c.hidden % 32 == 0;
+}
+
 // phase 1: fresh-action critics, TD target, critic gradients (split-K slabs);
 // fused: the critic Adam + Polyak runs inside the layer-0 gradient launch
 // part 0: the whole phase; 1: the fresh-action critic forward only (layer 1 +
@@ -397,6 +411,16 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
     a.reward_scale = c.reward_scale; a.discount = c.discount; a.B = B;
     a.y = p.W(OAC_WS_Y); a.dq1 = p.W(W_DQ1); a.dq2 = p.W(W_DQ2); a.gq1 = p.W(W_GQ1); a.gq2 = p.W(W_GQ2);
     a.sqe1 = p.W(OAC_WS_SQE1); a.sqe2 = p.W(OAC_WS_SQE2); a.qnew = p.W(OAC_WS_QNEW);
+    if (wl_in_targets(p)) {   // the last-layer dW slabs (the rows of block s = split s)
+      float* gq = grad_q(p);
+      const int h2[2] = {W_H2Q1, W_H2Q2};
+      for (int i = 0; i < 2; ++i) {
+        a.wl_h2[i] = p.W(h2[i]);
+        a.wl_g[i] = gq + i * L.q_size + L.q_last_w;
+        a.wl_gb[i] = gq + i * L.q_size + L.q_last_b;
+      }
+      a.wl_slab_stride = q_group(p); a.wl_H = H;
+    }
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_critic_targets(a, s)));
     p.launches++;
   }
@@ -412,7 +436,8 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
       GemmTask t = t_dw(nullptr, 0, H, B, p.W(h1[i]), H, H, g + L.q_fc1_w, g + L.q_fc1_b, gs, p.sp_q1);
       set_rank1(t, p.W(dq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
       add(gb, t);
-      add(gb, t_dw(p.W(dq[i]), 1, 1, B, p.W(h2[i]), H, H, g + L.q_last_w, g + L.q_last_b, gs, p.sp_ql));
+      if (!wl_in_targets(p))   // (else the targets kernel wrote these slabs)
+        add(gb, t_dw(p.W(dq[i]), 1, 1, B, p.W(h2[i]), H, H, g + L.q_last_w, g + L.q_last_b, gs, p.sp_ql));
       GemmTask d = t_dx(nullptr, 0, B, H, qs[i] + L.q_fc1_w, H, H, p.W(dh1[i]), H, p.W(h1[i]), H);
       set_rank1(d, p.W(dq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
       add(gb, d);
