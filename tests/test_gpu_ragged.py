@@ -39,6 +39,18 @@ def _compare(tr, groups, want):
 
 @pytest.mark.parametrize("Do,Da,H,B", SHAPES)
 def test_sac_ragged(Do, Da, H, B):
+    _sac_case(Do, Da, H, B)
+
+
+# large batch with B a multiple of 256 and hidden % 32 == 0: the critics'
+# last-layer dW is written as split-K slabs by the targets kernel
+# (critic_targets_kernel, rows.hip; 2-8 row blocks x 2-8 column groups)
+@pytest.mark.parametrize("Do,Da,H,B", [(11, 3, 64, 1024), (7, 5, 96, 2048), (376, 17, 256, 1024)])
+def test_sac_last_layer_slabs_in_targets(Do, Da, H, B):
+    _sac_case(Do, Da, H, B)
+
+
+def _sac_case(Do, Da, H, B):
     from oac_amd import SACTrainer
     from oracle import sac_oracle as so
     params = sac_params(Do, Da, [H, H], 3, pi_init_w=0.2, q_init_w=0.1)
