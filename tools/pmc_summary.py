@@ -22,6 +22,9 @@ R = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "gpurun_out")
 def load(kind):
     files = glob.glob(os.path.join(R, f"pmc_{tag}_{kind}", "**", "*counter_collection.csv"),
                       recursive=True)
+    # the newest pass only: gpurun merges every call's output into the same
+    # directory, so earlier runs' files (other process ids) sit beside it
+    files = [max(files, key=os.path.getmtime)] if files else []
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in files:
         for row in csv.DictReader(open(f)):
