@@ -337,12 +337,17 @@ def dp1_leg(args, rb, device, B, single_value, steps=640, warmup=64):
         pp = oac_amd.get_policy_producer(args.obs_dim, args.act_dim, hid, device=device)
         qp = oac_amd.get_q_producer(args.obs_dim, args.act_dim, hid, device=device)
         out = {"batch": B, "steps": steps, "backend": "nccl (RCCL), world_size 1"}
-        for force in (False, True):
+        # (collectives, overlap): the phase split alone; the three all-reduces
+        # issued through RCCL although world size is 1; and the schedule an
+        # N > 1 run executes -- phases 4 / 5 with the alpha all-reduce on a
+        # forked side stream captured into the step graph
+        for force, ovl in ((False, False), (True, False), (True, True)):
             with DataParallelSACTrainer(pp, qp, action_space=Space(args.act_dim), discount=0.99,
                                         reward_scale=1.0, policy_lr=3e-4, qf_lr=3e-4,
                                         soft_target_tau=5e-3, target_update_period=1,
                                         use_automatic_entropy_tuning=True, device=device, seed=2,
-                                        gemm_cfg=args.gemm_cfg, force_collectives=force) as tr:
+                                        gemm_cfg=args.gemm_cfg, force_collectives=force,
+                                        force_overlap=ovl) as tr:
                 np.random.seed(1)
                 el = timed(dropin_run(tr, rb, B), steps, warmup, 1, device)
                 assert torch.isfinite(tr.params).all().item(), "non-finite DP parameters"
@@ -350,7 +355,9 @@ def dp1_leg(args, rb, device, B, single_value, steps=640, warmup=64):
             v = steps / el
             leg = {"steps_per_s": round(v, 1), "ms_per_step": round(1e3 * el / steps, 4),
                    "vs_single_process": round(v / single_value, 4)}
-            if force:   # the three all-reduces issued through RCCL although world size is 1
+            if ovl:
+                out["with_rccl_allreduces_overlap_schedule"] = leg
+            elif force:
                 out["with_rccl_allreduces"] = leg
             else:       # the phase split itself (at world size 1 the sums are identities)
                 out.update(leg)

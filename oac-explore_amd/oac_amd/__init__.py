@@ -7,7 +7,7 @@ Drop-in replacements for the reference's hot-path interfaces:
   GaussianTrainer                    trainer/gaussian_trainer.py (g-oac, share_layers)
   get_optimistic_exploration_action  optimistic_exploration.py
   ReplayBuffer, ReplayBufferCount    replay_buffer.py
-  rollout, vec_rollout               path_collector.py rollout (vec_: N envs, one call per step)
+  vec_rollout                        path_collector.py rollout over N envs, one call per step
 backed by liboac_amd.so (hand-written HIP for gfx950 behind a C ABI).
 """
 from ._lib import lib, LIB_PATH  # noqa: F401
@@ -20,4 +20,4 @@ from .optimistic_exploration import (get_optimistic_exploration_action,  # noqa:
                                      get_optimistic_exploration_actions)
 from .producers import get_policy_producer, get_q_producer  # noqa: F401
 from .networks import MakeDeterministic  # noqa: F401
-from .rollout import rollout, vec_rollout  # noqa: F401
+from .rollout import vec_rollout  # noqa: F401

@@ -113,7 +113,7 @@ class _DataParallel:
     (``capture=False`` keeps every step eager)."""
 
     def __init__(self, *args, process_group=None, capture=None, force_collectives=False,
-                 **kwargs):
+                 force_overlap=False, **kwargs):
         if not dist.is_initialized():
             raise RuntimeError("DataParallelSACTrainer needs torch.distributed initialised")
         self.pg = process_group
@@ -126,9 +126,15 @@ class _DataParallel:
         # the alpha exchange beside the fresh-action critic forward (RCCL only:
         # with gloo the collective is a host call and there is nothing to
         # overlap; at one rank the all-reduce has no link latency to hide and
-        # the fork / join alone cost ~3.7 us per step)
-        self._overlap = (dist.get_backend(process_group) == "nccl" and self.world > 1
-                         and os.environ.get("OAC_DP_OVERLAP", "1") != "0")
+        # the fork / join alone cost ~3.7 us per step).  force_overlap=True
+        # runs the split schedule anyway -- phase "1a", the alpha exchange,
+        # phase "1b" (library phases 4 / 5) -- so the code the world > 1 RCCL
+        # step executes can be tested at world size 1 (RCCL: the forked-stream
+        # all-reduce captured into the step graph) and over gloo (a
+        # synchronous all-reduce between the two halves)
+        self._nccl = dist.get_backend(process_group) == "nccl"
+        self._overlap = force_overlap or (self._nccl and self.world > 1
+                                          and os.environ.get("OAC_DP_OVERLAP", "1") != "0")
         self._graphs, self._eager_seen = {}, set()
         self._attached = {}   # plan handles a captured step graph is attached to
         self._closed = False
@@ -189,13 +195,16 @@ class _DataParallel:
         returned join makes the current stream wait for it (captured into the
         step graph as a fork / join, so the exchange overlaps the work issued
         between the fork and the join)."""
+        if not self._nccl:   # gloo: a host-side collective, nothing runs beside it
+            self._all_reduce(t)
+            return lambda: None
         cur = torch.cuda.current_stream(self.device)
         if getattr(self, "_side", None) is None:
             self._side = torch.cuda.Stream(self.device)
         side = self._side
         side.wait_stream(cur)
         with torch.cuda.stream(side):
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.pg)
+            self._all_reduce(t)
         return lambda: cur.wait_stream(side)
 
     def _steps(self, plan, f, n_steps, stream):

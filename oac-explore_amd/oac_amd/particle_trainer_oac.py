@@ -210,6 +210,7 @@ class ParticleTrainer(_ArenaTrainer):
         if self.use_automatic_entropy_tuning:
             self.log_alpha.copy_(torch.as_tensor(ss["log_alpha"]).reshape(1))
             self.alpha_optimizer.load_state_dict(ss["alpha_optim_state_dict"])
+            self.alpha_state[3] = torch.exp(self.log_alpha[0])
         self.eval_statistics = ss["eval_statistics"]
         self._n_train_steps_total = int(ss["_n_train_steps_total"])
         self._need_to_update_eval_statistics = ss["_need_to_update_eval_statistics"]

@@ -73,6 +73,31 @@ def ptrain_params(obs_dim, act_dim, hidden, seed, K, q_min, q_max, pi_init_w=1e-
                 target_qf1={k: v.copy() for k, v in d["qf1"].items()})
 
 
+def mid_state(params, groups, t, seed, g_scale=1e-2):
+    """A mid-training optimiser state (test infrastructure): torch-Adam moments
+    after ``t`` steps for every tensor of ``params[group]`` (group in
+    ``groups``), plus log-alpha and its moments.  exp_avg ~ N(0, g_scale),
+    exp_avg_sq = exp_avg^2 + Exp(g_scale^2) (so sqrt(v) >= |m|, as a real run
+    keeps it).  The mid-state goldens (make_golden.py gen_sac_mid /
+    gen_poac_mid) run ONE reference step from this state, so steps past the
+    first -- bias corrections at t > 1, non-zero moments, log-alpha away from
+    its init -- are pinned against the reference at 1e-5 without storing a
+    trajectory's state."""
+    rs = np.random.RandomState(seed)
+    out = {}
+    for g in groups:
+        out[g] = {}
+        for k, v in params[g].items():
+            m = rs.normal(0.0, g_scale, v.shape).astype(np.float32)
+            vv = (m.astype(np.float64) ** 2 + rs.exponential(g_scale ** 2, v.shape)).astype(np.float32)
+            out[g][k] = (m, vv)
+    out["log_alpha"] = np.float32(rs.uniform(-0.6, -0.2))
+    am = np.float32(rs.normal(0.0, g_scale))
+    out["alpha_adam"] = (am, np.float32(am * am + rs.exponential(g_scale ** 2)))
+    out["t"] = int(t)
+    return out
+
+
 def synthetic_transitions(n, obs_dim, act_dim, seed=0, term_p=0.01):
     """BASELINE.md section 3 synthetic replay content (float64, like the
     reference's numpy store, replay_buffer.py:32-45)."""

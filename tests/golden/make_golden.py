@@ -31,7 +31,7 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))  # tests/
-from fixtures_lib import (goac_params, ptrain_params, sac_params, synthetic_transitions,  # noqa
+from fixtures_lib import (goac_params, mid_state, ptrain_params, sac_params, synthetic_transitions,  # noqa
                           PARAM_ORDER_POLICY, PARAM_ORDER_Q)
 
 REF = "/root/reference"
@@ -254,10 +254,141 @@ def gen_sac(name, obs_dim, act_dim, hidden, B, steps, n_replay, full, seed=7,
     return meta, out
 
 
+# ------------------------------------------------- mid-training-state runs
+def _set_adam(opt, order, st, t):
+    """torch-Adam state (Adam14's layout) of every parameter of ``opt``."""
+    for pname, p in zip(order, opt.param_groups[0]["params"]):
+        m, v = st[pname]
+        opt.state[p] = dict(step=t, exp_avg=torch.from_numpy(m.copy()),
+                            exp_avg_sq=torch.from_numpy(v.copy()))
+
+
+def _set_alpha(tr, ms):
+    tr.log_alpha.data.fill_(float(ms["log_alpha"]))
+    am, av = ms["alpha_adam"]
+    tr.alpha_optimizer.state[tr.log_alpha] = dict(
+        step=ms["t"], exp_avg=torch.tensor([am]), exp_avg_sq=torch.tensor([av]))
+
+
+def gen_sac_mid(name, obs_dim, act_dim, hidden, B, n_replay, t=7, seed=7, state_seed=31,
+                lr=3e-4, tau=5e-3, idx_seed=3, eps_seed=4):
+    """ONE reference SAC step from a mid-training state (fixtures_lib.mid_state:
+    Adam moments after t steps, log-alpha off its init): gradients whole,
+    post-step parameters / targets / Adam moments sampled."""
+    pp, qp = _producers(obs_dim, act_dim, hidden)
+    torch.manual_seed(0)
+    tr = SACTrainer(pp, qp, action_space=Box(-1, 1, (act_dim,)), discount=0.99,
+                    reward_scale=1.0, policy_lr=lr, qf_lr=lr, optimizer_class=Adam14,
+                    soft_target_tau=tau, target_update_period=1,
+                    use_automatic_entropy_tuning=True)
+    params = sac_params(obs_dim, act_dim, hidden, seed)
+    for k in ("policy", "qf1", "qf2", "target_qf1", "target_qf2"):
+        load_sd(getattr(tr, k), params[k])
+    ms = mid_state(params, ("policy", "qf1", "qf2"), t, state_seed)
+    _set_adam(tr.policy_optimizer, PARAM_ORDER_POLICY, ms["policy"], t)
+    _set_adam(tr.qf1_optimizer, PARAM_ORDER_Q, ms["qf1"], t)
+    _set_adam(tr.qf2_optimizer, PARAM_ORDER_Q, ms["qf2"], t)
+    _set_alpha(tr, ms)
+    tr._n_train_steps_total = t
+    rb, _ = _fill_buffer(obs_dim, act_dim, n_replay)
+    np.random.seed(idx_seed)
+    torch.manual_seed(eps_seed)
+    EPS_LOG.clear()
+    batch, idx = _record_batch(rb, B)
+    tr.end_epoch(0)
+    tr.train(dict(batch))
+    assert len(EPS_LOG) == 2
+    out = {"s0/idx": idx.astype(np.int64), "s0/eps1": EPS_LOG[0], "s0/eps2": EPS_LOG[1]}
+    for k, v in tr.get_diagnostics().items():
+        out[f"s0/stat/{k}"] = np.array(v, np.float64)
+    for gname, opt, order in (("policy", tr.policy_optimizer, PARAM_ORDER_POLICY),
+                              ("qf1", tr.qf1_optimizer, PARAM_ORDER_Q),
+                              ("qf2", tr.qf2_optimizer, PARAM_ORDER_Q)):
+        for pname, g, p in zip(order, opt.recorded[-1], opt.param_groups[0]["params"]):
+            pack(out, f"s0/grad/{gname}/{pname}", g.numpy(), True)
+            st = opt.state[p]
+            pack(out, f"s0/adam/{gname}/{pname}/exp_avg", st["exp_avg"].numpy(), False)
+            pack(out, f"s0/adam/{gname}/{pname}/exp_avg_sq", st["exp_avg_sq"].numpy(), False)
+    out["s0/grad/log_alpha"] = tr.alpha_optimizer.recorded[-1][0].numpy()
+    out["s0/post/log_alpha"] = tr.log_alpha.detach().numpy().copy()
+    for gname in ("policy", "qf1", "qf2", "target_qf1", "target_qf2"):
+        for pname, tt in getattr(tr, gname).state_dict().items():
+            pack(out, f"s0/post/{gname}/{pname}", tt.numpy(), False)
+    meta = dict(kind="sac", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, B=B, steps=1,
+                n_replay=n_replay, seed=seed, pi_init_w=1e-3, q_init_w=3e-3, auto_alpha=True,
+                log_alpha0=float(ms["log_alpha"]), discount=0.99, reward_scale=1.0, tau=tau,
+                lr=lr, idx_seed=idx_seed, eps_seed=eps_seed, target_entropy=-float(act_dim),
+                target_update_period=1, mid_state=dict(t=t, seed=state_seed))
+    return meta, out
+
+
+def gen_poac_mid(name, obs_dim, act_dim, hidden, K, B, n_replay, t=7, seed=11, state_seed=37,
+                 q_min=0.0, q_max=500.0, lr=3e-4, tau=5e-3, idx_seed=3, eps_seed=4):
+    """ONE reference P-OAC step (particle_trainer_oac, share_layers) from a
+    mid-training state; gradients whole, the rest sampled."""
+    pp, qp = _producers(obs_dim, act_dim, hidden, q_out=K)
+    torch.manual_seed(0)
+    tr = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Box(-1, 1, (act_dim,)),
+                            discount=0.99, reward_scale=1.0, delta=0.95, policy_lr=lr,
+                            qf_lr=lr, optimizer_class=Adam14, soft_target_tau=tau,
+                            target_update_period=1, use_automatic_entropy_tuning=True,
+                            deterministic=False, q_min=q_min, q_max=q_max, share_layers=True)
+    params = sac_params(obs_dim, act_dim, hidden, seed, q_out=K,
+                        q_last_bias=np.linspace(q_min, q_max, K))
+    load_sd(tr.policy, params["policy"])
+    load_sd(tr.qfs[0], params["qf1"])
+    load_sd(tr.tfs[0], params["target_qf1"])
+    ms = mid_state(params, ("policy", "qf1"), t, state_seed)
+    _set_adam(tr.policy_optimizer, PARAM_ORDER_POLICY, ms["policy"], t)
+    _set_adam(tr.qf_optimizers[0], PARAM_ORDER_Q, ms["qf1"], t)
+    _set_alpha(tr, ms)
+    tr._n_train_steps_total = t
+    rb, _ = _fill_buffer(obs_dim, act_dim, n_replay)
+    np.random.seed(idx_seed)
+    torch.manual_seed(eps_seed)
+    EPS_LOG.clear()
+    batch, idx = _record_batch(rb, B)
+    tr.end_epoch(0)
+    tr.train(dict(batch))
+    assert len(EPS_LOG) == 2
+    out = {"s0/idx": idx.astype(np.int64), "s0/eps1": EPS_LOG[0], "s0/eps2": EPS_LOG[1]}
+    for k, v in tr.get_diagnostics().items():
+        out[f"s0/stat/{k}"] = np.array(v, np.float64)
+    for gname, opt, order in (("policy", tr.policy_optimizer, PARAM_ORDER_POLICY),
+                              ("qf", tr.qf_optimizers[0], PARAM_ORDER_Q)):
+        for pname, g, p in zip(order, opt.recorded[-1], opt.param_groups[0]["params"]):
+            pack(out, f"s0/grad/{gname}/{pname}", g.numpy(), True)
+            st = opt.state[p]
+            pack(out, f"s0/adam/{gname}/{pname}/exp_avg", st["exp_avg"].numpy(), False)
+            pack(out, f"s0/adam/{gname}/{pname}/exp_avg_sq", st["exp_avg_sq"].numpy(), False)
+    out["s0/grad/log_alpha"] = tr.alpha_optimizer.recorded[-1][0].numpy()
+    out["s0/post/log_alpha"] = tr.log_alpha.detach().numpy().copy()
+    for gname, mod in (("policy", tr.policy), ("qf", tr.qfs[0]), ("tf", tr.tfs[0])):
+        for pname, tt in mod.state_dict().items():
+            pack(out, f"s0/post/{gname}/{pname}", tt.numpy(), False)
+    meta = dict(kind="poac", obs_dim=obs_dim, act_dim=act_dim, hidden=hidden, K=K, B=B,
+                steps=1, n_replay=n_replay, seed=seed, delta=0.95, q_min=q_min, q_max=q_max,
+                discount=0.99, lr=lr, tau=tau, idx_seed=idx_seed, eps_seed=eps_seed,
+                delta_index=int(tr.delta_index), pi_init_w=1e-3,
+                target_entropy=-float(act_dim), counts=False, train_bias=True,
+                target_update_period=1, mid_state=dict(t=t, seed=state_seed))
+    return meta, out
+
+
+def gen_mid_all():
+    """The BASELINE configs' dims from a mid-training state (one step each)."""
+    save("sac_humanoid_mid", *gen_sac_mid("sac_humanoid_mid", 376, 17, [256, 256], 256, 20000))
+    save("sac_humanoid_b4096_mid", *gen_sac_mid("sac_humanoid_b4096_mid", 376, 17, [256, 256],
+                                                4096, 20000))
+    save("poac_ant_b4096_mid", *gen_poac_mid("poac_ant_b4096_mid", 111, 8, [256, 256], 10, 4096,
+                                             20000))
+
+
 # ------------------------------------------------------------- P-OAC runs
 def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=11,
              delta=0.95, q_min=0.0, q_max=500.0, discount=0.99, lr=3e-4, tau=5e-3,
-             idx_seed=1, eps_seed=2, pi_init_w=1e-3, counts=False, train_bias=True, period=1):
+             idx_seed=1, eps_seed=2, pi_init_w=1e-3, counts=False, train_bias=True, period=1,
+             full_s0=False):
     pp, qp = _producers(obs_dim, act_dim, hidden, q_out=K)
     torch.manual_seed(0)
     tr = ParticleTrainerOAC(pp, qp, n_estimators=K, action_space=Box(-1, 1, (act_dim,)),
@@ -306,12 +437,12 @@ def gen_poac(name, obs_dim, act_dim, hidden, K, B, steps, n_replay, full, seed=1
             for pname, g in zip(order, opt.recorded[-1]):
                 if g is None:   # frozen (train_bias=False)
                     g = torch.zeros_like(mod.state_dict()[pname])
-                pack(out, f"s{s}/grad/{gname}/{pname}", g.numpy(), full)
+                pack(out, f"s{s}/grad/{gname}/{pname}", g.numpy(), full or (full_s0 and s == 0))
         out[f"s{s}/grad/log_alpha"] = tr.alpha_optimizer.recorded[-1][0].numpy()
         out[f"s{s}/post/log_alpha"] = tr.log_alpha.detach().numpy().copy()
         for gname, mod in (("policy", tr.policy), ("qf", tr.qfs[0]), ("tf", tr.tfs[0])):
             for pname, t in mod.state_dict().items():
-                pack(out, f"s{s}/post/{gname}/{pname}", t.numpy(), full)
+                pack(out, f"s{s}/post/{gname}/{pname}", t.numpy(), full or (full_s0 and s == 0))
     return meta, out
 
 
@@ -776,6 +907,12 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] == "humanoid":
         gen_humanoid()
         return
+    if len(sys.argv) > 1 and sys.argv[1] == "mid":
+        gen_mid_all()
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "poac_b4096":
+        gen_poac_b4096()
+        return
     if len(sys.argv) > 1 and sys.argv[1] == "nobias":
         gen_nobias()
         return
@@ -834,8 +971,15 @@ def gen_humanoid():
     """The headline configs (BASELINE configs[1] / [2] dims): step 0 whole."""
     save("sac_humanoid", *gen_sac("sac_humanoid", 376, 17, [256, 256], 256, 3, 20000, False,
                                   full_s0=True))
-    save("sac_humanoid_b4096", *gen_sac("sac_humanoid_b4096", 376, 17, [256, 256], 4096, 1,
+    save("sac_humanoid_b4096", *gen_sac("sac_humanoid_b4096", 376, 17, [256, 256], 4096, 3,
                                         20000, False, full_s0=True))
+
+
+def gen_poac_b4096():
+    """BASELINE configs[4] at its own batch: K=10 shared-head critic, Ant-v2
+    dims, 2x256, B=4096, two steps, step 0 whole."""
+    save("poac_ant_b4096", *gen_poac("poac_ant_b4096", 111, 8, [256, 256], 10, 4096, 2, 20000,
+                                     False, full_s0=True))
 
 
 def gen_nobias():

@@ -72,7 +72,11 @@ def _trainer(dp, kind="sac"):
     from oac_amd.dp import DataParallelSACTrainer
     pp, qp = producers(sac_params(Do, Da, [H, H], 3, pi_init_w=0.2, q_init_w=0.1))
     cls = DataParallelSACTrainer if dp else SACTrainer
-    kw = dict(force_collectives=True) if dp == "rccl1" else {}
+    kw = {"rccl1": dict(force_collectives=True),
+          # the split schedule of the world > 1 RCCL step (phase "1a", the
+          # alpha exchange, phase "1b" = library phases 4 / 5)
+          "rccl1_overlap": dict(force_collectives=True, force_overlap=True),
+          "overlap": dict(force_overlap=True)}.get(dp, {})
     return cls(pp, qp, action_space=Space(Da), discount=0.99, reward_scale=1.0, policy_lr=1e-3,
                qf_lr=1e-3, soft_target_tau=5e-3, use_automatic_entropy_tuning=True, **kw)
 
@@ -94,7 +98,8 @@ def _worker(rank, world, port, q, kind="sac"):
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    tr = _trainer(True, kind)
+    tr = _trainer("overlap" if kind == "sac_overlap" else True, kind)
+    assert tr._overlap == (kind == "sac_overlap")
     for step, (batch, e1, e2) in enumerate(_inputs(world)):
         sl = slice(rank * BL, (rank + 1) * BL)
         if kind in ("goac", "ptrain"):
@@ -110,8 +115,11 @@ def _worker(rank, world, port, q, kind="sac"):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["sac", "goac", "poac", "ptrain"])
+@pytest.mark.parametrize("kind", ["sac", "sac_overlap", "goac", "poac", "ptrain"])
 def test_dp_trainer_two_ranks_equals_single_gpu_on_global_batch(kind):
+    """sac_overlap: the split schedule (phases 4 / 5 of sac_plan.hip with the
+    alpha all-reduce between them, synchronous over gloo) -- the library code
+    only the world > 1 RCCL step runs otherwise."""
     world = 2
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -126,7 +134,7 @@ def test_dp_trainer_two_ranks_equals_single_gpu_on_global_batch(kind):
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
-    tr = _trainer(False, kind)
+    tr = _trainer(False, "sac" if kind == "sac_overlap" else kind)
     for step, (batch, e1, e2) in enumerate(_inputs(world)):
         if kind in ("goac", "ptrain"):
             tr.train_from_torch(_with_counts(batch, step))
@@ -155,7 +163,7 @@ def _ring_run(tr, n_calls, n_steps):
     return torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy()
 
 
-def _nccl_worker(port, q, teardown="close"):
+def _nccl_worker(port, q, teardown="close", overlap=False):
     import faulthandler
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -168,8 +176,8 @@ def _nccl_worker(port, q, teardown="close"):
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    tr = _trainer("rccl1")   # the all-reduces issued through RCCL although world size is 1
-    assert tr.capture
+    tr = _trainer("rccl1_overlap" if overlap else "rccl1")   # RCCL all-reduces at world size 1
+    assert tr.capture and tr._overlap == overlap
     got = _ring_run(tr, 4, 4)          # call 1 eager, calls 2.. captured (RCCL inside the graph)
     n_graphs = len(tr._graphs)
     q.put((got, n_graphs))
@@ -182,19 +190,21 @@ def _nccl_worker(port, q, teardown="close"):
     # "atexit": neither -- the trainer's atexit hook releases the graphs
 
 
-@pytest.mark.parametrize("teardown", ["close", "atexit"])
-def test_dp_rccl_graph_capture_single_rank_equals_single_gpu(teardown):
+@pytest.mark.parametrize("teardown,overlap", [("close", False), ("atexit", False), ("close", True)])
+def test_dp_rccl_graph_capture_single_rank_equals_single_gpu(teardown, overlap):
     """The captured data-parallel step (phases + RCCL all-reduces in one
     hipGraph, 4 steps per replay) on one rank equals the single-GPU trainer on
     the same device index stream, and the process exits cleanly through the
-    trainer's teardown (explicit close(), or its atexit hook)."""
+    trainer's teardown (explicit close(), or its atexit hook).  overlap: the
+    world > 1 schedule -- phase "1a", the alpha all-reduce on a forked side
+    stream captured into the graph as a fork / join, phase "1b"."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    p = ctx.Process(target=_nccl_worker, args=(port, q, teardown))
+    p = ctx.Process(target=_nccl_worker, args=(port, q, teardown, overlap))
     p.start()
     p.join(timeout=150)
     assert p.exitcode == 0, p.exitcode
@@ -367,7 +377,7 @@ def _dropin_loop(tr, seed=1, steps=140):
     return torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy()
 
 
-def _nccl_dropin_worker(port, q):
+def _nccl_dropin_worker(port, q, overlap=False):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
@@ -376,7 +386,8 @@ def _nccl_dropin_worker(port, q):
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    tr = _trainer("rccl1")   # the all-reduces issued through RCCL although world size is 1
+    tr = _trainer("rccl1_overlap" if overlap else "rccl1")   # RCCL all-reduces at world size 1
+    assert tr._overlap == overlap
     got = _dropin_loop(tr)
     q.put((got, len(tr._attached)))
     tr.close()
@@ -384,7 +395,8 @@ def _nccl_dropin_worker(port, q):
     dist.destroy_process_group()
 
 
-def test_dp_rccl_dropin_step_graph_equals_single_gpu():
+@pytest.mark.parametrize("overlap", [False, True])
+def test_dp_rccl_dropin_step_graph_equals_single_gpu(overlap):
     """The drop-in loop on the data-parallel trainer over RCCL (one rank): from
     the third call on, the captured step (phases + RCCL all-reduces) is
     attached to the handle and each train() is one library call (staging +
@@ -396,7 +408,7 @@ def test_dp_rccl_dropin_step_graph_equals_single_gpu():
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    p = ctx.Process(target=_nccl_dropin_worker, args=(port, q))
+    p = ctx.Process(target=_nccl_dropin_worker, args=(port, q, overlap))
     p.start()
     p.join(timeout=150)
     assert p.exitcode == 0, p.exitcode

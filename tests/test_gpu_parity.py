@@ -16,9 +16,9 @@ SAC_FIXTURES = ["sac_small", "sac_stress", "sac_noalpha", "sac_riverswim", "sac_
 
 
 def _oracle_noise(meta, g):
-    """distance of each golden value from the float64 oracle (reference fp32 noise)."""
+    """per-key fp32 noise of the trajectory (test_oracle_golden.noise_of)."""
     import test_oracle_golden as tog
-    return tog.sac_errors(meta, g, tog.make_sac_oracle(meta, torch.float64))
+    return tog.sac_noise(meta, g)
 
 
 def _gpu_errors(meta, g, tr, use_device_batch=False):

@@ -29,8 +29,8 @@ def particle_trainer_for(meta, **kw):
                            share_layers=True, train_bias=meta.get("train_bias", True), **kw)
 
 
-@pytest.mark.parametrize("name", ["poac_small", "poac_ant", "poac_counts", "poac_nobias",
-                                  "poac_period2"])
+@pytest.mark.parametrize("name", ["poac_small", "poac_ant", "poac_ant_b4096", "poac_counts",
+                                  "poac_nobias", "poac_period2"])
 def test_particle_step_matches_reference_golden(name):
     meta, g = parity.load(name)
     tr = particle_trainer_for(meta, counts=bool(meta.get("counts")))
@@ -66,7 +66,7 @@ def test_particle_step_matches_reference_golden(name):
                 errs[gk] = parity.stat_err(st[k], g, gk)
     # every step under the noise-derived gate: max(1e-5, 3x the reference's
     # own fp32 distance from the float64 oracle, per key)
-    noise = tog.poac_errors(meta, g, tog.make_poac_oracle(meta, torch.float64))
+    noise = tog.poac_noise(meta, g)
     bad = tog.gated(errs, noise)
     print(name, "worst", sorted(errs.items(), key=lambda kv: -kv[1])[:3])
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]

@@ -1,0 +1,345 @@
+"""Teacher-forced per-step parity at the BASELINE dims.
+
+The trajectory tests (test_gpu_parity.py, test_gpu_particle.py) run the GPU
+trainer through a reference fixture's steps and gate every key at
+max(1e-5, 3 x the reference's own fp32 noise): past step 0 the fp32
+trajectories of two correct implementations drift apart (Adam's first step is
+lr * sign(g), ReLU masks flip), so that gate widens to ~1e-2 for some keys at
+Humanoid dims.  Here every step is checked at the north_star's 1e-5 instead:
+before step s the GPU trainer's OWN pre-step state -- parameters, target
+critics, Adam m / v and step count, log-alpha and its Adam state -- is loaded
+into the fp32 CPU oracle, both take step s on the fixture's batch and eps
+(reference-drawn), and gradients, post-step parameters, Adam moments, Polyak
+targets, log-alpha (gradient and value) and the losses are compared.
+
+Allowances, each reported by the test: elements of a post-step parameter
+whose gradient is within fp32 rounding of 0 (Adam moves them by ~lr * sign,
+bounded by 2.5 lr); and at most two rows of a critic hidden-layer gradient
+whose ReLU pre-activation sits within fp32 rounding of 0 for some sample
+(parity.relu_boundary_units), as in test_gpu_dp.py.
+
+Reference: trainer/trainer.py:126-280 (SAC), trainer/particle_trainer_oac.py:
+169-363 (P-OAC), torch-1.4 Adam (trainer/trainer.py:75-91).
+"""
+import numpy as np
+import pytest
+import torch
+
+import parity
+from fixtures_lib import PARAM_ORDER_POLICY, PARAM_ORDER_Q
+from gpu_helpers import batch_from, module_tensors, sac_trainer_for
+from oracle import sac_oracle as so
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def _np_sd(mod):
+    return {k: v.detach().cpu().numpy().copy() for k, v in mod.state_dict().items()}
+
+
+def _load_adam(opt, tr, mod):
+    m = module_tensors(tr, mod, tr.adam_m)
+    v = module_tensors(tr, mod, tr.adam_v)
+    for k in opt.m:
+        opt.m[k].copy_(m[k].detach().cpu())
+        opt.v[k].copy_(v[k].detach().cpu())
+    opt.t = tr._n_train_steps_total
+
+
+def _load_alpha(orc, tr):
+    a = tr.alpha_state.detach().cpu()
+    orc.log_alpha.copy_(a[0:1])
+    orc.opt_a.m["log_alpha"].copy_(a[1:2])
+    orc.opt_a.v["log_alpha"].copy_(a[2:3])
+    orc.opt_a.t = tr._n_train_steps_total
+    orc.n_steps = tr._n_train_steps_total
+
+
+def sac_oracle_from_gpu(tr, meta):
+    """The fp32 oracle holding the GPU SAC trainer's current state."""
+    params = {g: _np_sd(getattr(tr, g))
+              for g in ("policy", "qf1", "qf2", "target_qf1", "target_qf2")}
+    orc = so.SACOracle(params, meta["obs_dim"], meta["act_dim"], discount=meta["discount"],
+                       reward_scale=meta["reward_scale"], policy_lr=meta["lr"],
+                       qf_lr=meta["lr"], tau=meta["tau"], auto_alpha=meta["auto_alpha"],
+                       target_update_period=meta.get("target_update_period", 1))
+    for opt, mod in ((orc.opt_p, tr.policy), (orc.opt_q1, tr.qf1), (orc.opt_q2, tr.qf2)):
+        _load_adam(opt, tr, mod)
+    _load_alpha(orc, tr)
+    return orc
+
+
+def poac_oracle_from_gpu(tr, meta):
+    params = {"policy": _np_sd(tr.policy), "qf1": _np_sd(tr.qfs[0]),
+              "target_qf1": _np_sd(tr.tfs[0])}
+    orc = so.ParticleOACOracle(params, meta["obs_dim"], meta["act_dim"], meta["K"],
+                               discount=meta["discount"], policy_lr=meta["lr"],
+                               qf_lr=meta["lr"], tau=meta["tau"],
+                               target_update_period=meta.get("target_update_period", 1),
+                               train_bias=meta.get("train_bias", True))
+    _load_adam(orc.opt_p, tr, tr.policy)
+    _load_adam(orc.opt_q, tr, tr.qfs[0])
+    _load_alpha(orc, tr)
+    return orc
+
+
+def _post_err(got, ref, grad, lr, band=1e-3):
+    """Norm-relative error of a post-step parameter outside Adam's sign band;
+    band elements bounded by 2.5 lr.  Returns (err, band elements)."""
+    got, ref, grad = (np.asarray(x, np.float64).reshape(-1) for x in (got, ref, grad))
+    rms = np.sqrt(np.mean(grad * grad)) if grad.size else 0.0
+    ok = np.abs(grad) > band * rms
+    d = got - ref
+    assert np.all(np.abs(d[~ok]) <= 2.5 * lr + 1e-6)
+    n = np.linalg.norm(ref)
+    return (np.linalg.norm(d[ok]) / n if n else np.linalg.norm(d[ok])), int((~ok).sum())
+
+
+def _boundary_rows(x0, q):
+    """ReLU-boundary hidden units of a critic on input rows x0 (both layers)."""
+    u0, pre0 = parity.relu_boundary_units(x0, q["fc0.weight"], q["fc0.bias"])
+    u1, _ = parity.relu_boundary_units(np.maximum(pre0, 0), q["fc1.weight"], q["fc1.bias"])
+    return {"fc0.weight": u0, "fc0.bias": u0, "fc1.weight": u1, "fc1.bias": u1}
+
+
+def _check(errs, left_out, name, s):
+    bad = {k: v for k, v in errs.items() if v > TOL}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:4]
+    print(f"{name} step {s}: worst {worst}; ReLU-boundary rows left out {left_out}")
+    assert not bad, (name, s, sorted(bad.items(), key=lambda kv: -kv[1])[:10])
+
+
+@pytest.mark.parametrize("name", ["sac_humanoid", "sac_humanoid_b4096"])
+def test_sac_teacher_forced_every_step(name):
+    meta, g = parity.load(name)
+    tr = sac_trainer_for(meta)
+    lr = meta["lr"]
+    for s in range(meta["steps"]):
+        orc = sac_oracle_from_gpu(tr, meta)
+        pre = {grp: _np_sd(getattr(tr, grp)) for grp in ("qf1", "qf2")}
+        batch = batch_from(meta, g[f"s{s}/idx"])
+        e1, e2 = g[f"s{s}/eps1"], g[f"s{s}/eps2"]
+        tr.end_epoch(s)
+        tr.train_from_torch(batch, eps1=e1, eps2=e2)
+        torch.cuda.synchronize()
+        out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
+        x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
+        allowed = {grp: _boundary_rows(x0, pre[grp]) for grp in ("qf1", "qf2")}
+        errs, left_out = {}, {}
+        for grp, mod, order, opt, P in (("policy", tr.policy, PARAM_ORDER_POLICY, orc.opt_p, orc.P),
+                                        ("qf1", tr.qf1, PARAM_ORDER_Q, orc.opt_q1, orc.Q1),
+                                        ("qf2", tr.qf2, PARAM_ORDER_Q, orc.opt_q2, orc.Q2)):
+            gv = module_tensors(tr, mod, tr.grads)
+            mv = module_tensors(tr, mod, tr.adam_m)
+            vv = module_tensors(tr, mod, tr.adam_v)
+            sd = dict(mod.state_dict())
+            for pn in order:
+                gref = out["grads"][grp][pn].numpy()
+                rows = allowed.get(grp, {}).get(pn, [])
+                e, bad = parity.rel_err_rows(gv[pn].cpu().numpy(), gref, rows)
+                errs[f"grad/{grp}/{pn}"] = e
+                if bad:
+                    left_out[f"{grp}/{pn}"] = bad
+                keep = np.ones(gref.shape[0], bool)
+                keep[bad] = False
+                errs[f"m/{grp}/{pn}"] = parity.rel_err(mv[pn].cpu().numpy()[keep],
+                                                       opt.m[pn].numpy()[keep])
+                errs[f"v/{grp}/{pn}"] = parity.rel_err(vv[pn].cpu().numpy()[keep],
+                                                       opt.v[pn].numpy()[keep])
+                errs[f"post/{grp}/{pn}"], _ = _post_err(sd[pn].cpu().numpy()[keep],
+                                                        P[pn].numpy()[keep], gref[keep], lr)
+        for grp, mod, T in (("target_qf1", tr.target_qf1, orc.T1),
+                            ("target_qf2", tr.target_qf2, orc.T2)):
+            for pn, t in mod.state_dict().items():
+                errs[f"post/{grp}/{pn}"] = parity.rel_err(t.cpu().numpy(), T[pn].numpy())
+        if meta["auto_alpha"]:
+            a = tr.alpha_state.cpu().numpy()
+            errs["grad/log_alpha"] = parity.rel_err(a[5:6], out["grads"]["log_alpha"].numpy())
+            errs["post/log_alpha"] = parity.rel_err(a[0:1], orc.log_alpha.numpy())
+            errs["adam/log_alpha"] = parity.rel_err(a[1:3], np.concatenate(
+                [orc.opt_a.m["log_alpha"].numpy(), orc.opt_a.v["log_alpha"].numpy()]))
+        st = tr.get_diagnostics()
+        for k in ("QF1 Loss", "QF2 Loss", "Q Loss", "Policy Loss", "Alpha", "Alpha Loss",
+                  "Log Pis Mean", "Q Targets Mean", "Q1 Predictions Mean"):
+            if k in out["stats"]:
+                errs[f"stat/{k}"] = parity.rel_err(st[k], out["stats"][k])
+        _check(errs, left_out, name, s)
+
+
+@pytest.mark.parametrize("name", ["poac_ant", "poac_ant_b4096"])
+def test_particle_teacher_forced_every_step(name):
+    from test_gpu_particle import particle_trainer_for
+    meta, g = parity.load(name)
+    tr = particle_trainer_for(meta)
+    lr, K = meta["lr"], meta["K"]
+    for s in range(meta["steps"]):
+        orc = poac_oracle_from_gpu(tr, meta)
+        pre = _np_sd(tr.qfs[0])
+        batch = batch_from(meta, g[f"s{s}/idx"])
+        e1, e2 = g[f"s{s}/eps1"], g[f"s{s}/eps2"]
+        tr.end_epoch(s)
+        tr.train_from_torch(batch, eps1=e1, eps2=e2)
+        torch.cuda.synchronize()
+        out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
+        x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
+        allowed = {"qf": _boundary_rows(x0, pre)}
+        errs, left_out = {}, {}
+        for grp, mod, order, opt, P in (("policy", tr.policy, PARAM_ORDER_POLICY, orc.opt_p, orc.P),
+                                        ("qf", tr.qfs[0], PARAM_ORDER_Q, orc.opt_q, orc.Q)):
+            gv = module_tensors(tr, mod, tr.grads)
+            mv = module_tensors(tr, mod, tr.adam_m)
+            vv = module_tensors(tr, mod, tr.adam_v)
+            sd = dict(mod.state_dict())
+            for pn in order:
+                gref = out["grads"][grp][pn].numpy()
+                rows = allowed.get(grp, {}).get(pn, [])
+                e, bad = parity.rel_err_rows(gv[pn].cpu().numpy(), gref, rows)
+                errs[f"grad/{grp}/{pn}"] = e
+                if bad:
+                    left_out[f"{grp}/{pn}"] = bad
+                keep = np.ones(gref.shape[0], bool)
+                keep[bad] = False
+                errs[f"m/{grp}/{pn}"] = parity.rel_err(mv[pn].cpu().numpy()[keep],
+                                                       opt.m[pn].numpy()[keep])
+                errs[f"v/{grp}/{pn}"] = parity.rel_err(vv[pn].cpu().numpy()[keep],
+                                                       opt.v[pn].numpy()[keep])
+                errs[f"post/{grp}/{pn}"], _ = _post_err(sd[pn].cpu().numpy()[keep],
+                                                        P[pn].numpy()[keep], gref[keep], lr)
+        for pn, t in tr.tfs[0].state_dict().items():
+            errs[f"post/tf/{pn}"] = parity.rel_err(t.cpu().numpy(), orc.T[pn].numpy())
+        a = tr.alpha_state.cpu().numpy()
+        errs["grad/log_alpha"] = parity.rel_err(a[5:6], out["grads"]["log_alpha"].numpy())
+        errs["post/log_alpha"] = parity.rel_err(a[0:1], orc.log_alpha.numpy())
+        st = tr.get_diagnostics()
+        for i in range(K):
+            errs[f"stat/QF{i} Loss"] = parity.rel_err(st[f"QF{i} Loss"],
+                                                      float(out["qf_losses"][i]))
+        errs["stat/Policy Loss"] = parity.rel_err(st["Policy Loss"], float(out["policy_loss"]))
+        _check(errs, left_out, name, s)
+
+
+# ------------------------------------------------- mid-training-state goldens
+def _optim_sd(mod, st, t):
+    """torch-Adam state_dict of a module's parameters from mid_state moments."""
+    state = {i: dict(step=t, exp_avg=torch.from_numpy(st[n][0].copy()),
+                     exp_avg_sq=torch.from_numpy(st[n][1].copy()))
+             for i, (n, _) in enumerate(mod.named_parameters())}
+    return dict(state=state, param_groups=[dict(params=list(range(len(state))))])
+
+
+def _alpha_sd(ms):
+    am, av = ms["alpha_adam"]
+    return dict(state={0: dict(step=ms["t"], exp_avg=torch.tensor([am]),
+                               exp_avg_sq=torch.tensor([av]))},
+                param_groups=[dict(params=[0])])
+
+
+def _golden_errors(g, tr, groups, meta):
+    """One-step errors against a mid-state golden: gradients (whole),
+    post-step parameters, targets and Adam moments (sampled), log-alpha."""
+    errs = {}
+    for grp, mod, order in groups:
+        gv = module_tensors(tr, mod, tr.grads)
+        mv = module_tensors(tr, mod, tr.adam_m)
+        vv = module_tensors(tr, mod, tr.adam_v)
+        for pn in order:
+            errs[f"grad/{grp}/{pn}"] = parity.compare(g, f"s0/grad/{grp}/{pn}",
+                                                      gv[pn].cpu().numpy())
+            for nm, t in (("exp_avg", mv[pn]), ("exp_avg_sq", vv[pn])):
+                key = f"s0/adam/{grp}/{pn}/{nm}"
+                errs[key] = parity.compare(g, key, t.cpu().numpy())
+    a = tr.alpha_state.cpu().numpy()
+    errs["grad/log_alpha"] = parity.rel_err(a[5:6], g["s0/grad/log_alpha"])
+    errs["post/log_alpha"] = parity.rel_err(a[0:1], g["s0/post/log_alpha"])
+    return errs
+
+
+@pytest.mark.parametrize("name", ["sac_humanoid_mid", "sac_humanoid_b4096_mid"])
+def test_sac_mid_state_step_matches_reference_golden(name):
+    """One step from a mid-training state (fixtures_lib.mid_state: Adam moments
+    after t = 7 steps, log-alpha off its init), restored through the
+    reference-format snapshot (restore_from_snapshot), at 1e-5 against the
+    reference's own step and against the oracle on the same state."""
+    from fixtures_lib import mid_state, sac_params
+    meta, g = parity.load(name)
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                        pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"])
+    ms = mid_state(params, ("policy", "qf1", "qf2"), meta["mid_state"]["t"],
+                   meta["mid_state"]["seed"])
+    tr = sac_trainer_for(meta)
+    t = ms["t"]
+    sd = lambda grp: {k: torch.from_numpy(v.copy()) for k, v in params[grp].items()}
+    tr.restore_from_snapshot(dict(
+        policy_state_dict=sd("policy"), policy_optim_state_dict=_optim_sd(tr.policy, ms["policy"], t),
+        qf1_state_dict=sd("qf1"), qf1_optim_state_dict=_optim_sd(tr.qf1, ms["qf1"], t),
+        target_qf1_state_dict=sd("target_qf1"),
+        qf2_state_dict=sd("qf2"), qf2_optim_state_dict=_optim_sd(tr.qf2, ms["qf2"], t),
+        target_qf2_state_dict=sd("target_qf2"),
+        log_alpha=torch.tensor([float(ms["log_alpha"])]), alpha_optim_state_dict=_alpha_sd(ms),
+        eval_statistics={}, _n_train_steps_total=t, _need_to_update_eval_statistics=True))
+    orc = sac_oracle_from_gpu(tr, meta)
+    batch = batch_from(meta, g["s0/idx"])
+    tr.train_from_torch(batch, eps1=g["s0/eps1"], eps2=g["s0/eps2"])
+    torch.cuda.synchronize()
+    out = orc.step(so.NumpyReplay.to_torch(batch), g["s0/eps1"], g["s0/eps2"])
+    groups = (("policy", tr.policy, PARAM_ORDER_POLICY), ("qf1", tr.qf1, PARAM_ORDER_Q),
+              ("qf2", tr.qf2, PARAM_ORDER_Q))
+    errs = _golden_errors(g, tr, groups, meta)
+    for grp, mod in (("policy", tr.policy), ("qf1", tr.qf1), ("qf2", tr.qf2),
+                     ("target_qf1", tr.target_qf1), ("target_qf2", tr.target_qf2)):
+        for pn, tt in mod.state_dict().items():
+            errs[f"post/{grp}/{pn}"] = parity.compare(g, f"s0/post/{grp}/{pn}", tt.cpu().numpy())
+    st = tr.get_diagnostics()
+    for k in ("QF1 Loss", "QF2 Loss", "Policy Loss", "Alpha", "Alpha Loss", "Log Pis Mean"):
+        errs[f"stat/{k}"] = parity.stat_err(st[k], g, f"s0/stat/{k}")
+    # and the oracle on the same state (whole tensors)
+    for grp, mod, order in groups:
+        gv = module_tensors(tr, mod, tr.grads)
+        for pn in order:
+            errs[f"oracle/grad/{grp}/{pn}"] = parity.rel_err(gv[pn].cpu().numpy(),
+                                                             out["grads"][grp][pn].numpy())
+    _check(errs, {}, name, 0)
+
+
+def test_particle_mid_state_step_matches_reference_golden():
+    """BASELINE configs[4] (K=10 shared-head critic, Ant-v2 dims, B=4096): one
+    step from a mid-training state at 1e-5 against the reference's step."""
+    from fixtures_lib import mid_state, sac_params
+    from test_gpu_particle import particle_trainer_for
+    meta, g = parity.load("poac_ant_b4096_mid")
+    K = meta["K"]
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"], q_out=K,
+                        q_last_bias=np.linspace(meta["q_min"], meta["q_max"], K),
+                        pi_init_w=meta["pi_init_w"])
+    ms = mid_state(params, ("policy", "qf1"), meta["mid_state"]["t"], meta["mid_state"]["seed"])
+    tr = particle_trainer_for(meta)
+    t = ms["t"]
+    sd = lambda grp: {k: torch.from_numpy(v.copy()) for k, v in params[grp].items()}
+    tr.restore_from_snapshot(dict(
+        policy_state_dict=sd("policy"),
+        policy_optim_state_dict=_optim_sd(tr.policy, ms["policy"], t),
+        qfs_state_dicts=[sd("qf1")], qfs_optims_state_dicts=[_optim_sd(tr.qfs[0], ms["qf1"], t)],
+        target_qfs_state_dicts=[sd("target_qf1")],
+        log_alpha=torch.tensor([float(ms["log_alpha"])]), alpha_optim_state_dict=_alpha_sd(ms),
+        eval_statistics={}, _n_train_steps_total=t, _need_to_update_eval_statistics=True))
+    orc = poac_oracle_from_gpu(tr, meta)
+    batch = batch_from(meta, g["s0/idx"])
+    tr.train_from_torch(batch, eps1=g["s0/eps1"], eps2=g["s0/eps2"])
+    torch.cuda.synchronize()
+    out = orc.step(so.NumpyReplay.to_torch(batch), g["s0/eps1"], g["s0/eps2"])
+    groups = (("policy", tr.policy, PARAM_ORDER_POLICY), ("qf", tr.qfs[0], PARAM_ORDER_Q))
+    errs = _golden_errors(g, tr, groups, meta)
+    for grp, mod in (("policy", tr.policy), ("qf", tr.qfs[0]), ("tf", tr.tfs[0])):
+        for pn, tt in mod.state_dict().items():
+            errs[f"post/{grp}/{pn}"] = parity.compare(g, f"s0/post/{grp}/{pn}", tt.cpu().numpy())
+    st = tr.get_diagnostics()
+    for i in range(K):
+        errs[f"stat/QF{i} Loss"] = parity.stat_err(st[f"QF{i} Loss"], g, f"s0/stat/QF{i} Loss")
+    for grp, mod, order in groups:
+        gv = module_tensors(tr, mod, tr.grads)
+        for pn in order:
+            errs[f"oracle/grad/{grp}/{pn}"] = parity.rel_err(gv[pn].cpu().numpy(),
+                                                             out["grads"][grp][pn].numpy())
+    _check(errs, {}, "poac_ant_b4096_mid", 0)

@@ -1,8 +1,10 @@
-"""rollout / vec_rollout (oac_amd/rollout.py) against the contract of
+"""vec_rollout (oac_amd/rollout.py) against the contract of
 path_collector.rollout (/root/reference/path_collector.py:176-257): the path
-dict layout, terminal / max_path_length handling, and -- with a deterministic
-agent on the CPU, or fixed exploration noise on the GPU -- vec_rollout's paths
-equal to one rollout per environment."""
+dict layout (2-D observations / actions / rewards / next_observations /
+terminals, per-step info lists), terminal / max_path_length handling, and --
+with a deterministic agent on the CPU, or fixed exploration noise on the GPU
+-- every environment's path equal to stepping that environment alone with one
+single-observation action call per step (`walk` below)."""
 import numpy as np
 import pytest
 
@@ -40,6 +42,24 @@ class LinearAgent:
         return np.tanh(O @ self.W.T).astype(np.float32)
 
 
+def walk(env, act, max_path_length):
+    """One environment stepped alone: act(o) -> action per step; the
+    transitions it saw, as arrays."""
+    O, A, R, D, E = [], [], [], [], []
+    o = env.reset()
+    while len(O) < max_path_length:
+        a = act(o)
+        o2, r, d, info = env.step(a)
+        O.append(o); A.append(a); R.append(r); D.append(d); E.append(info)
+        o = o2
+        if d:
+            break
+    return dict(observations=np.array(O), actions=np.array(A),
+                rewards=np.array(R).reshape(-1, 1),
+                next_observations=np.vstack([np.array(O[1:]).reshape(-1, len(o)), o[None]]),
+                terminals=np.array(D).reshape(-1, 1), env_infos=E, agent_infos=[{}] * len(O))
+
+
 def _same(p, q):
     for k in ("observations", "actions", "rewards", "next_observations", "terminals"):
         assert p[k].shape == q[k].shape, k
@@ -48,28 +68,64 @@ def _same(p, q):
     assert len(p["agent_infos"]) == len(q["agent_infos"])
 
 
-def test_vec_rollout_equals_rollouts_cpu_agent():
-    from oac_amd.rollout import rollout, vec_rollout
+def test_vec_rollout_equals_single_env_walks_cpu_agent():
+    from oac_amd.rollout import vec_rollout
     Do, Da = 5, 3
     lengths = [1, 4, 9, 12]
     agent = LinearAgent(Do, Da)
     paths = vec_rollout([ToyEnv(Do, L, s) for s, L in enumerate(lengths)], agent,
                         max_path_length=10)
     for s, L in enumerate(lengths):
-        ref = rollout(ToyEnv(Do, L, s), agent, max_path_length=10)
+        ref = walk(ToyEnv(Do, L, s), lambda o: agent.get_action(o)[0], 10)
         _same(paths[s], ref)
-        assert len(ref["observations"]) == min(L, 10)
-        assert ref["terminals"][-1, 0] == (L <= 10)
-        np.testing.assert_array_equal(ref["next_observations"][:-1], ref["observations"][1:])
+        p = paths[s]
+        assert all(p[k].ndim == 2 for k in ("observations", "actions", "rewards",
+                                            "next_observations", "terminals"))
+        assert len(p["observations"]) == min(L, 10)
+        assert p["terminals"][-1, 0] == (L <= 10)
+        np.testing.assert_array_equal(p["next_observations"][:-1], p["observations"][1:])
+
+
+def test_vec_rollout_scalar_observations():
+    """1-D environments (riverswim: obs 1, act 1): observations, actions and
+    next_observations still come back as [T, 1]."""
+    from oac_amd.rollout import vec_rollout
+
+    class Scalar:
+        def __init__(self, L):
+            self.L = L
+
+        def reset(self):
+            self.t, self.o = 0, 0.5
+            return self.o
+
+        def step(self, a):
+            self.t += 1
+            self.o = float(np.tanh(self.o + float(np.asarray(a).reshape(-1)[0])))
+            return self.o, self.o, self.t >= self.L, {}
+
+    class Agent:
+        def reset(self):
+            pass
+
+        def get_actions(self, O, deterministic=False):
+            return (0.3 * np.asarray(O, np.float32)).reshape(-1, 1)
+
+    paths = vec_rollout([Scalar(3), Scalar(5)], Agent(), max_path_length=4)
+    for p, T in zip(paths, (3, 4)):
+        for k in ("observations", "actions", "rewards", "next_observations", "terminals"):
+            assert p[k].shape == (T, 1), (k, p[k].shape)
+        np.testing.assert_array_equal(p["next_observations"][:-1], p["observations"][1:])
 
 
 @pytest.mark.gpu
-def test_vec_rollout_oac_equals_rollouts():
+def test_vec_rollout_oac_equals_single_env_walks():
     """OAC exploration with fixed noise: the batched call per step reproduces
     every single-environment path bitwise (the action rows of a batched call
     are bitwise the single calls)."""
     import torch
-    from oac_amd.rollout import rollout, vec_rollout
+    from oac_amd import get_optimistic_exploration_action
+    from oac_amd.rollout import vec_rollout
     from gpu_helpers import Space
     import oac_amd
     Do, Da, H = 11, 3, [32, 32]
@@ -84,13 +140,13 @@ def test_vec_rollout_oac_equals_rollouts():
                         max_path_length=16, optimistic_exploration=True,
                         optimistic_exploration_kwargs=kw)
     for s, L in enumerate(lengths):
-        ref = rollout(ToyEnv(Do, L, 10 + s), tr.policy, max_path_length=16,
-                      optimistic_exploration=True, optimistic_exploration_kwargs=kw)
+        ref = walk(ToyEnv(Do, L, 10 + s),
+                   lambda o: get_optimistic_exploration_action(o, **kw)[0], 16)
         _same(paths[s], ref)
     # plain policy actions (no exploration): batched get_actions vs get_action
     paths = vec_rollout([ToyEnv(Do, L, s) for s, L in enumerate(lengths)], tr.policy,
                         max_path_length=5, deterministic_pol=True)
     for s, L in enumerate(lengths):
-        ref = rollout(ToyEnv(Do, L, s), tr.policy, max_path_length=5, deterministic_pol=True)
+        ref = walk(ToyEnv(Do, L, s), lambda o: tr.policy.get_action(o, deterministic=True)[0], 5)
         for k in ("observations", "actions", "rewards"):
             np.testing.assert_allclose(paths[s][k], ref[k], rtol=1e-6, atol=1e-6)
