@@ -189,9 +189,13 @@ int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* str
  * collectives -- into a graph on its own collective library and hands the
  * instantiated graph (hipGraphExec_t) to the handle; oac_sac_step_host_idx
  * then stages the indices and launches that graph on `stream`, exactly as the
- * single-process step launches its own.  NULL detaches it (the caller still
- * owns the graph and destroys it after the last step that launched it). */
-int oac_sac_set_step_graph(oac_sac* h, void* graph_exec);
+ * single-process step launches its own.  `flags` = the step flags the graph's
+ * phases were captured with (OAC_STEP_GATHER implied, OAC_STEP_USE_GRAPH
+ * ignored); while a graph is attached, oac_sac_step_host_idx must be called
+ * with the same flags or it fails without launching.  NULL detaches it (the
+ * caller still owns the graph and destroys it after the last step that
+ * launched it). */
+int oac_sac_set_step_graph(oac_sac* h, void* graph_exec, int flags);
 /* data-parallel split (config.world_size > 1): phase 0 = forward through the
  * policy sample and the local sum(logp + target_entropy) as per-16-row
  * partials into the workspace buffer OAC_WS_LOGP_PART (ceil(B / 16) floats):

@@ -394,6 +394,13 @@ void gemm_batch_finalize(GemmBatch& b, int cfg) {
 hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   if (b.total_tiles <= 0) return hipSuccess;
   if (b.side_adam > 0 && (cfg < 9 || cfg > 12)) return hipErrorInvalidValue;   // side Adam: gemm_bwdp only
+  // rows read through the direct gather's index slot (a_rows) and the side
+  // workgroups that copy the batch / draw eps (rg): only the small kernel and
+  // gemm_fwd implement them -- any other kernel would read replay rows 0..M-1
+  // and leave the batch copy and eps unwritten
+  bool gathers = b.rg.ring != nullptr;
+  for (int i = 0; i < b.ntasks; ++i) gathers = gathers || b.t[i].a_rows;
+  if (gathers && cfg != 0 && (cfg < 6 || cfg > 8)) return hipErrorInvalidValue;
   if (cfg == 0) return gemm_small_launch(b, s);
   if (b.fuse_adam) return hipErrorInvalidValue;   // fused optimizer: small-batch kernel only
   for (int i = 0; i < b.ntasks; ++i) {             // dual products / head backward: small kernel

@@ -31,6 +31,7 @@ struct PlanBase {
   hipStream_t cap_stream = nullptr;   // capture stream (graphs launch on the caller's stream)
   // the caller's captured data-parallel step (oac_sac_set_step_graph; not owned)
   hipGraphExec_t ext_exec = nullptr;
+  int ext_flags = 0;   // the step flags ext_exec was captured with
   int launches = 0;
   // drop-in host-index staging (oac_sac_set_host_ring): pinned [slots][B] int32,
   // one completion event per 16-slot chunk, recorded when staging leaves the

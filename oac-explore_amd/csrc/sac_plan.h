@@ -134,8 +134,10 @@ int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long
 // step either way -- its short-K layer 0 took the index round trips, +3.2 us;
 // not kept.)
 inline bool big_direct_ok(const SacPlan& p) {
+  // gemm_fwd's rank-Da continuation reads [obs | act] as one span of the row
   return p.c.kind == OAC_KIND_SAC && p.cfg == 2 && fwd2_on() && p.c.hidden >= 64 &&
-         p.c.row_stride % 4 == 0 && p.c.row_stride / 4 <= 256;
+         p.c.row_stride % 4 == 0 && p.c.row_stride / 4 <= 256 &&
+         p.c.off_act == p.c.off_obs + p.c.obs_dim;
 }
 
 // particle trainer (particle_plan.hip)

@@ -898,9 +898,10 @@ int oac_sac_stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* str
   return stage_host_idx(h, idx, bc, stream, h && h->plan.rows_direct);
 }
 
-int oac_sac_set_step_graph(oac_sac* h, void* graph_exec) {
+int oac_sac_set_step_graph(oac_sac* h, void* graph_exec, int flags) {
   if (!h) { set_error("null handle"); return 1; }
   h->plan.ext_exec = reinterpret_cast<hipGraphExec_t>(graph_exec);
+  h->plan.ext_flags = (flags | OAC_STEP_GATHER) & ~OAC_STEP_USE_GRAPH;
   return 0;
 }
 
@@ -908,6 +909,12 @@ int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags,
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
   if (p.ext_exec) {   // the caller's captured step (phases + collectives)
+    const int want = (flags | OAC_STEP_GATHER) & ~OAC_STEP_USE_GRAPH;
+    if (want != p.ext_flags) {
+      set_error("step flags %d differ from the flags %d the attached step graph was captured with",
+                want, p.ext_flags);
+      return 1;
+    }
     if (stage_host_idx(h, idx, bc, stream, p.rows_direct)) return 1;
     OAC_HIP_CHECK(hipGraphLaunch(p.ext_exec, reinterpret_cast<hipStream_t>(stream)));
     return 0;

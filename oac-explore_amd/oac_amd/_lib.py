@@ -89,7 +89,7 @@ _SIGS = {
                                              ctypes.c_int, ctypes.c_void_p]),
     "oac_sac_stage_host_idx": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                               ctypes.c_void_p]),
-    "oac_sac_set_step_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "oac_sac_set_step_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
     "oac_sac_workspace_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
                                               ctypes.POINTER(ctypes.c_int64),
                                               ctypes.POINTER(ctypes.c_int64),

@@ -157,7 +157,7 @@ class _DataParallel:
             return
         torch.cuda.synchronize(self.device)
         for h in self._attached.values():   # the handles launch the step graphs: detach first
-            check(_lib.lib().oac_sac_set_step_graph(h, None))
+            check(_lib.lib().oac_sac_set_step_graph(h, None, 0))
         self._attached.clear()
         self._graphs.clear()
         self._eager_seen.clear()
@@ -231,17 +231,19 @@ class _DataParallel:
         if idx.dtype != np.int64 or not idx.flags.c_contiguous:
             idx = np.ascontiguousarray(idx, dtype=np.int64)
         bc = self._bc_mirror
-        key = (id(plan), _lib.OAC_STEP_GATHER | _lib.OAC_STEP_DEVICE_EPS, 1)
+        step_flags = _lib.OAC_STEP_GATHER | _lib.OAC_STEP_DEVICE_EPS   # what _run captures
+        key = (id(plan), step_flags, 1)
         if self.capture and key in self._graphs and not self._closed:
             # the captured step attached to the handle: staging + one graph
             # launch on torch's current stream in one library call, as the
             # single-process drop-in step (no stream hop, no replay prologue)
             if plan.handle.value not in self._attached:
                 check(_lib.lib().oac_sac_set_step_graph(
-                    plan.handle, ctypes.c_void_p(self._graphs[key].raw_cuda_graph_exec())))
+                    plan.handle, ctypes.c_void_p(self._graphs[key].raw_cuda_graph_exec()),
+                    step_flags))
                 self._attached[plan.handle.value] = plan.handle
             check(_lib.lib().oac_sac_step_host_idx(
-                plan.handle, ctypes.c_void_p(idx.ctypes.data), bc, 0,
+                plan.handle, ctypes.c_void_p(idx.ctypes.data), bc, step_flags,
                 _lib.stream_ptr(torch.cuda.current_stream(self.device))))
             self._bc_mirror = bc + 1
             self._last_plan = plan

@@ -80,23 +80,26 @@ def get_optimistic_exploration_action(ob_np, policy=None, qfs=None, trainer=None
 
 
 # the per-environment-step call (path_collector.py:219-220) validates the same
-# (policy, qfs, trainer, share_layers) every step: the owner check is cached
-# (strong references, so an id is never reused while its entry lives)
-_OWNERS = {}
+# (policy, qfs, trainer, share_layers) every step: the validated combinations
+# are remembered on the policy object itself, so nothing outlives the trainer
+# (the policy already references its trainer).  A cached qfs key is ids of the
+# owning trainer's own critics, which that trainer keeps alive, so an id in it
+# cannot be reused by another object while the entry exists.
+_CACHE_ATTR = "_oac_expl_validated"
 
 
 def _action_now(ob_np, policy, qfs, trainer, hyper_params):
     """The single-observation Philox call on its shortest host path: cached
     owner validation, the raw current-stream handle, one C call."""
     share = bool(hyper_params.get("share_layers", False))
-    key = (id(policy), id(trainer), None if qfs is None else tuple(map(id, qfs)), share)
-    ent = _OWNERS.get(key)
-    if ent is None or ent[0] is not policy or ent[1] is not trainer:
+    key = (trainer is not None, None if qfs is None else tuple(map(id, qfs)), share)
+    t = getattr(policy, "oac_trainer", None)
+    seen = policy.__dict__.get(_CACHE_ATTR)
+    if seen is None or key not in seen or (trainer is not None and trainer is not t):
         t = _owner(policy, qfs, trainer, hyper_params)
-        if len(_OWNERS) > 16:
-            _OWNERS.clear()
-        ent = _OWNERS[key] = (policy, trainer, tuple(qfs) if qfs is not None else None, t)
-    t = ent[3]
+        if seen is None:
+            seen = policy.__dict__[_CACHE_ATTR] = set()
+        seen.add(key)
     e = t._expl_handle(1)
     L = _lib.lib()
     if t.layout.q2_base < 0:   # K heads: mean + beta std, or trainer.predict's sorted head

@@ -309,3 +309,39 @@ def test_oac_exploration_trainer_ub_matches_reference_golden(name):
     r = so.oac_exploration_action_shared(g["obs"][0], P, Q, meta["beta_UB"], meta["delta"],
                                          g["eps_discard"][0], g["eps"][0])
     assert parity.rel_err(a, r["action"].numpy()) <= parity.TOL
+
+
+def test_single_call_philox_path():
+    """The per-environment-step production path (path_collector.py:219-220):
+    an eps-free single call goes through _action_now (cached owner check, the
+    observation in the kernel arguments, tagged output granules, the Philox
+    draw and the expl_counter advance by the last arrival).  Two calls on one
+    observation differ, each advances step_state[2] by exactly 1, and the
+    first equals row 0 of an N=1 batched Philox call at the same counter."""
+    from oac_amd import get_optimistic_exploration_action, get_optimistic_exploration_actions
+    meta, g = parity.load("oac_expl_humanoid")
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                        pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"])
+    m = dict(obs_dim=meta["obs_dim"], act_dim=meta["act_dim"], hidden=meta["hidden"],
+             discount=0.99, reward_scale=1.0, lr=3e-4, tau=5e-3, auto_alpha=True, log_alpha0=0.0,
+             seed=meta["seed"], pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"])
+    tr = sac_trainer_for(m, params=params)
+    hp = dict(beta_UB=meta["beta_UB"], delta=meta["delta"], share_layers=False)
+    ob = g["obs"][0]
+    c0 = int(tr.step_state[2].item())
+    a1, info = get_optimistic_exploration_action(ob, policy=tr.policy, qfs=tr.qfs, hyper_params=hp)
+    assert info == {}
+    assert int(tr.step_state[2].item()) == c0 + 1
+    a2, _ = get_optimistic_exploration_action(ob, policy=tr.policy, qfs=tr.qfs, hyper_params=hp)
+    assert int(tr.step_state[2].item()) == c0 + 2
+    assert a1.shape == (meta["act_dim"],) and a1.dtype == np.float32
+    assert np.isfinite(a1).all() and not np.array_equal(a1, a2)
+    tr.step_state[2] = c0   # the same counter again, through the batched call
+    A, _ = get_optimistic_exploration_actions(ob[None, :], policy=tr.policy, qfs=tr.qfs,
+                                              hyper_params=hp)
+    np.testing.assert_array_equal(A[0], a1)
+    assert int(tr.step_state[2].item()) == c0 + 1
+    # the cached validation still rejects a foreign critic list
+    with pytest.raises(NotImplementedError):
+        get_optimistic_exploration_action(ob, policy=tr.policy, qfs=[tr.qf2, tr.qf1],
+                                          hyper_params=hp)
