@@ -18,8 +18,10 @@
 #include "adam_common.h"
 #include "policy_math.h"
 #include "gemm_operand.h"
+#include "gemm_pipe.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace oac {
 
@@ -33,12 +35,48 @@ __device__ long long g_gs_clock[4096 * 8];
 #define GS_STAGE(i)
 #endif
 
+// Staged k-contiguous operands (STG kernels): the workgroup's 32 operand rows
+// over [kst, k_hi) are copied into LDS by LDS-DMA (global_load_lds_dwordx4,
+// gemm_pipe.h glds16) before the k loop -- 8 lanes per 128-byte line, where a
+// fragment-shaped 16-byte load per lane touches one line per lane (64 per
+// wave instruction) -- and the k loop reads its fragments from the image.
+// Row stride S floats, S = 4 (mod 64): the 32 rows' 16-byte fragment reads
+// at one k start on 32 distinct 4-bank groups, half-waves 4 floats apart.
+__host__ __device__ inline int stage_stride(int span) {
+  const int s = (span + 7) & ~7;   // fragment reads reach the next multiple of 8
+  return s + ((4 - s) & 63);
+}
+
+// rows r = 0..31 of operand X(m0 + r, k) = base[row(r) * ld + k], k in
+// [kst, k_hi), into img[r * S + (k - kst)]; row(r) = rows[r] (the direct
+// gather's tile rows) or min(m0 + r, M - 1).  Issued by every wave; the
+// caller waits (vmcnt(0)) and meets at a barrier before reading the image.
+template <int NW>
+__device__ __forceinline__ void stage_kc(const float* base, long ld, const int* rows, int m0, int M,
+                                         int kst, int k_hi, float* img, int S) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nch = (k_hi - kst + 3) >> 2;   // 16-byte chunks per row
+  const int nq = (nch + 63) >> 6;          // wave instructions per row
+#pragma unroll 1
+  for (int it = wave; it < 32 * nq; it += NW) {
+    const int r = it / nq, q = it - r * nq;
+    const long row = rows ? (long)rows[r] : (long)min(m0 + r, M - 1);
+    const int c = 64 * q + lane;
+    if (c < nch) glds16(base + row * ld + kst + 4 * c, img + r * S + 256 * q);
+  }
+}
+
+struct Stage { const float* img; int S; int kst; };
+
 // acc += A[m0.., k_lo..k_hi) . B[k_lo..k_hi), n0..]  for this wave's k-groups
 // arow >= 0: this lane's A row is buffer row arow (the direct gather's index,
 // loaded by the caller ahead of everything else)
-template <int NW, int AK, int BK, int GPW = (NW >= 16 ? 4 : 5)>
+// SA / SB: the operand's fragments come from its LDS image (KC kinds only)
+template <int NW, int AK, int BK, int GPW = (NW >= 16 ? 4 : 5), bool SA = false, bool SB = false>
 __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
-                                       floatx16& acc, int arow = -1) {
+                                       floatx16& acc, int arow = -1, Stage sa = Stage{},
+                                       Stage sb = Stage{}) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   const int l32 = lane & 31;
@@ -54,6 +92,8 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
   const int g_lo = k_lo >> 3;                 // k_lo is a multiple of 8 (kchunk % 8 == 0)
   const int g_hi = (k_hi + 7) >> 3;
   const int kmax = k_hi - 1;
+  const float* fa = sa.img + l32 * sa.S - sa.kst;   // SA: this lane's image row (k-indexed)
+  const float* fb = sb.img + l32 * sb.S - sb.kst;
 #pragma unroll 1
   for (int g0 = g_lo + wave; g0 < g_hi; g0 += kGPW * NW) {
     float ax[kGPW][4], ay[kGPW][4], bx[kGPW][4], by[kGPW][4];
@@ -61,8 +101,22 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
     for (int j = 0; j < kGPW; ++j)
       if (g0 + j * NW < g_hi) {
         const int kb = 8 * (g0 + j * NW) + 4 * half;
-        load4<BK>(lb, kb, kmax, bx[j], by[j]);   // B first: it never waits on a row index
-        load4<AK>(la, kb, kmax, ax[j], ay[j]);
+        if (SB) {
+          const f4u v = *reinterpret_cast<const f4u*>(fb + kb);
+          bx[j][0] = v.x; bx[j][1] = v.y; bx[j][2] = v.z; bx[j][3] = v.w;
+        } else {
+          load4<BK>(lb, kb, kmax, bx[j], by[j]);   // B first: it never waits on a row index
+        }
+        if (SA) {
+          const f4u v = *reinterpret_cast<const f4u*>(fa + kb);
+          ax[j][0] = v.x; ax[j][1] = v.y; ax[j][2] = v.z; ax[j][3] = v.w;
+          if (AK == OP_KC_R1) {   // the rank-1 factor v[k]: one (broadcast) 16-byte load
+            const f4u w = *reinterpret_cast<const f4u*>(la.s + kb);
+            ay[j][0] = w.x; ay[j][1] = w.y; ay[j][2] = w.z; ay[j][3] = w.w;
+          }
+        } else {
+          load4<AK>(la, kb, kmax, ax[j], ay[j]);
+        }
       }
 #pragma unroll
     for (int j = 0; j < kGPW; ++j)
@@ -78,13 +132,13 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
   }
 }
 
-template <int NW, int GPW>
+template <int NW, int GPW, bool STG>
 __device__ __forceinline__ void k_dispatch(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
-                                           floatx16& acc, int arow) {
+                                           floatx16& acc, int arow, Stage sa, Stage sb) {
   const bool r1 = t.a_mode == A_RANK1_MASK;
-  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW>(t, m0, n0, k_lo, k_hi, acc, arow);   // forward
-  else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dX
-  else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dX, rank-1 seed
+  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW, STG, STG>(t, m0, n0, k_lo, k_hi, acc, arow, sa, sb);   // forward
+  else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN, GPW, STG>(t, m0, n0, k_lo, k_hi, acc, -1, sa);      // dX
+  else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN, GPW, STG>(t, m0, n0, k_lo, k_hi, acc, -1, sa);   // dX, rank-1 seed
   else if (!r1)                k_loop<NW, OP_MN, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dW
   else                         k_loop<NW, OP_MN_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dW, rank-1 seed
 }
@@ -199,7 +253,23 @@ struct SmallLds {
 
 constexpr int kGatherU = 4;   // float4s per lane of a side block's row copy (rows <= 1 KB)
 
-template <int NW, int GPW>
+// the direct gather's 32 tile rows (their own LDS object: the launch's
+// dynamic LDS holds the staged images and the reduction)
+__device__ __forceinline__ int* tile_rows_of(float*) {
+  __shared__ int tile_rows[32];
+  return tile_rows;
+}
+
+// LDS floats the STG kernel's images take for one task (0: nothing staged)
+__host__ __device__ inline int stage_floats(const GemmTask& t) {
+  if (!t.a_kc || t.ksplit > 1) return 0;
+  int n = 32 * stage_stride(t.K);                       // A (or A's ReLU mask)
+  if (t.b_kc) n += 32 * stage_stride(t.K);              // B of a forward product
+  if (t.K2 > 0) n += 32 * stage_stride(t.K2);           // the second product's A
+  return n;
+}
+
+template <int NW, int GPW, bool STG = false>
 __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int publish, int tb1,
                                                  int tb2, int tb3, int tb4, int tb5, int tb6,
                                                  int tb7, const GemmBatch& batch, float* red) {
@@ -224,17 +294,19 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     const int nwv = g.blocks * NW;
     const float4* src = reinterpret_cast<const float4*>(g.replay);
     float4* dst = reinterpret_cast<float4*>(g.out);
+    static_assert(kGatherU == 4, "the row copy below holds four float4s per lane");
     for (int r = sb * NW + wave; r < g.B; r += nwv) {
-      const long sr = rows[r];
-      float4 v[kGatherU];
-#pragma unroll
-      for (int u = 0; u < kGatherU; ++u) {
-        const long c = lane + 64 * u;
-        v[u] = src[sr * n4 + (c < n4 ? c : 0)];
-      }
-#pragma unroll
-      for (int u = 0; u < kGatherU; ++u)
-        if (lane + 64 * u < n4) dst[(long)r * n4 + lane + 64 * u] = v[u];
+      // four named registers, not an array: the array form went through
+      // scratch (a store and a dependent reload per float4)
+      const float4* s0 = src + rows[r] * n4;
+      float4* d0 = dst + (long)r * n4;
+      const long c0 = lane, c1 = lane + 64, c2 = lane + 128, c3 = lane + 192;
+      const float4 v0 = s0[c0 < n4 ? c0 : 0], v1 = s0[c1 < n4 ? c1 : 0];
+      const float4 v2 = s0[c2 < n4 ? c2 : 0], v3 = s0[c3 < n4 ? c3 : 0];
+      if (c0 < n4) d0[c0] = v0;
+      if (c1 < n4) d0[c1] = v1;
+      if (c2 < n4) d0[c2] = v2;
+      if (c3 < n4) d0[c3] = v3;
     }
     for (int e = sb * 64 * NW + threadIdx.x; g.eps1 && e < g.n_eps; e += g.blocks * 64 * NW) {
       g.eps1[e] = philox_normal(g.seed, (unsigned long long)bc, 1u, (unsigned)e);
@@ -284,12 +356,34 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   // through LDS -- one host request per workgroup, not one per wave
   int arow = -1;
   if (t.a_rows && rows) {
-    __shared__ int tile_rows[32];
+    int* tile_rows = tile_rows_of(red);
     if (wave == 0 && lane < 32) tile_rows[lane] = rows[min(m0 + lane, t.M - 1)];
     __syncthreads();
     arow = tile_rows[lane & 31];
   }
 
+  // STG: the k-contiguous operands' 32 rows into LDS images first (their
+  // DMA overlaps the epilogue prefetch below)
+  const bool stg = STG && t.a_kc && t.ksplit <= 1;
+  Stage sa{}, sb{}, sa2{};
+  if (stg) {
+    const bool ar1 = t.a_mode == A_RANK1_MASK;
+    const int S = stage_stride(t.K);
+    sa = Stage{red, S, k_lo};
+    stage_kc<NW>(ar1 ? t.a_mask : t.A, ar1 ? t.ld_mask : t.lda, arow >= 0 ? tile_rows_of(red) : nullptr,
+                 m0, t.M, k_lo, k_hi, red, S);
+    float* nxt = red + 32 * S;
+    if (t.b_kc) {
+      sb = Stage{nxt, S, k_lo};
+      stage_kc<NW>(t.B, t.ldb, nullptr, n0, t.N, k_lo, k_hi, nxt, S);
+      nxt += 32 * S;
+    }
+    if (t.K2 > 0) {
+      const int S2 = stage_stride(t.K2);
+      sa2 = Stage{nxt, S2, 0};
+      stage_kc<NW>(t.A2, t.lda, nullptr, m0, t.M, 0, t.K2, nxt, S2);
+    }
+  }
   EpiIn xin[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -297,15 +391,22 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     const int r = e >> 6, l = e & 63;
     xin[i] = epi_prefetch(batch, t, m0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), n0 + (l & 31));
   }
+  if (stg) {   // every wave's DMA landed, then the images are complete for all
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  k_dispatch<NW, GPW>(t, m0, n0, k_lo, k_hi, acc, arow);
+  if (stg) k_dispatch<NW, GPW, true>(t, m0, n0, k_lo, k_hi, acc, arow, sa, sb);
+  else k_dispatch<NW, GPW, false>(t, m0, n0, k_lo, k_hi, acc, arow, sa, sb);
   if (t.K2 > 0) {   // second product into the same accumulator (unsplit dX tasks only)
     GemmTask t2 = t;
     t2.A = t.A2; t2.B = t.B2; t2.K = t.K2;
-    k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc);
+    if (stg) k_loop<NW, OP_KC, OP_MN, GPW, true>(t2, m0, n0, 0, t.K2, acc, -1, sa2);
+    else k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc);
   }
+  if (stg) __syncthreads();   // the images are read by all waves before the reduction reuses the LDS
 
   GS_STAGE(2);
   // fixed-order split-K reduction through LDS
@@ -362,13 +463,13 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   GS_STAGE(4);
 }
 
-template <int NW, int GPW>
+template <int NW, int GPW, bool STG>
 __global__ void __launch_bounds__(64 * NW)
 gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6,
                   int tb7, const GemmBatch batch) {
-  __shared__ __attribute__((aligned(16))) float red[SmallLds<NW>::N];
-  gemm_small_block<NW, GPW>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6, tb7,
-                            batch, red);
+  extern __shared__ __attribute__((aligned(16))) float red[];   // SmallLds<NW>::N or the images
+  gemm_small_block<NW, GPW, STG>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6,
+                                 tb7, batch, red);
 }
 
 // tile geometry shared with the plan builder
@@ -399,6 +500,21 @@ void gemm_small_finalize(GemmBatch& b) {
   b.total_tiles = tiles;
 }
 
+static int SmallLdsFloats(int nw) {
+  switch (nw) {
+    case 1: return SmallLds<1>::N;
+    case 2: return SmallLds<2>::N;
+    case 4: return SmallLds<4>::N;
+    case 8: return SmallLds<8>::N;
+    default: return SmallLds<16>::N;
+  }
+}
+constexpr int kLdsBytesPerCu = 160 * 1024;
+static bool small_stage_on() {
+  static const bool on = [] { const char* e = getenv("OAC_SMALL_STAGE"); return e && atoi(e) == 1; }();
+  return on;
+}
+
 hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   if (b0.total_tiles <= 0) return hipSuccess;
   GemmBatch b = b0;
@@ -420,11 +536,35 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   }
   const int grid = b.total_tiles + b.adam_blocks + (b.rg.ring ? b.rg.blocks : 0);
   const GemmHead h = gemm_head(b);
+  // staged k-contiguous operands (OAC_SMALL_STAGE=1): when the images fit
+  // beside the workgroups per CU the grid needs (1 at >= 16 waves)
+  int lds = SmallLdsFloats(nw);
+  bool stg = false;
+  if (small_stage_on() && (nw == 16 || gpw == 5) && !(nw == 16 && gpw != 4)) {
+    int need = 0;
+    for (int i = 0; i < b.ntasks; ++i) need = std::max(need, stage_floats(b.t[i]));
+    const int per_cu = nw >= 16 ? 1 : std::max(1, (grid + 255) / 256);
+    if (need > 0 && 4 * std::max(need, lds) * per_cu <= kLdsBytesPerCu) {
+      stg = true;
+      lds = std::max(need, lds);
+    }
+  }
+  const size_t shm = 4 * (size_t)lds;
 #define OAC_GS(NW_, G_) \
-  if (nw == NW_ && gpw == G_) { \
-    OAC_LAUNCH((gemm_small_kernel<NW_, G_>), dim3(grid), dim3(64 * NW_), 0, s, h.total_tiles, h.publish, \
+  if (nw == NW_ && gpw == G_ && !stg) { \
+    OAC_LAUNCH((gemm_small_kernel<NW_, G_, false>), dim3(grid), dim3(64 * NW_), shm, s, h.total_tiles, h.publish, \
                h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b); \
     return hipGetLastError(); }
+#define OAC_GSS(NW_, G_) \
+  if (nw == NW_ && gpw == G_ && stg) { \
+    static const bool attr_set = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_small_kernel<NW_, G_, true>), \
+        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytesPerCu) == hipSuccess; \
+    (void)attr_set; \
+    OAC_LAUNCH((gemm_small_kernel<NW_, G_, true>), dim3(grid), dim3(64 * NW_), shm, s, h.total_tiles, h.publish, \
+               h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b); \
+    return hipGetLastError(); }
+  OAC_GSS(1, 5) OAC_GSS(2, 5) OAC_GSS(4, 5) OAC_GSS(8, 5) OAC_GSS(16, 4)
+#undef OAC_GSS
   OAC_GS(1, 5) OAC_GS(2, 5) OAC_GS(4, 5) OAC_GS(8, 5) OAC_GS(16, 4)
   OAC_GS(4, 3) OAC_GS(4, 4) OAC_GS(4, 6) OAC_GS(4, 8)
   OAC_GS(8, 3) OAC_GS(8, 4) OAC_GS(8, 6) OAC_GS(8, 8)
