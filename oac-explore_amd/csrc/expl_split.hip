@@ -656,15 +656,17 @@ __global__ void __launch_bounds__(1024) oac_expl_split_kernel(ExplFusedArgs a, i
 //    dh1_i = seed_i (sum_n W_last_i[n] [h2_i[n] > 0] W1_i[n, :]) (x) [h1_i > 0]
 //    and seed_i = 1/2 +- beta |.|' depends only on sign(Q1 - Q2); so the
 //    parts of critic layer 1's rows (16 per critic) publish their Q partial
-//    W_last . h2 and their seed-free u_p = sum_{n in part} ... W1_i[n, :]
-//    with the rows, and the workgroup whose arrival comes last reads the
-//    partials and finishes alone (seeds, dh1, da, shift, sample).
+//    W_last . h2 and their seed-free share of da, v_p = (u_p (x) [h1_i > 0])
+//    W0_i[:, Do:] with u_p = sum_{n in part} ... W1_i[n, :] (Da floats, not
+//    the H of u_p: round 4), and the workgroup whose arrival comes last reads
+//    the partials and finishes alone in one wave (seeds, da = seed-weighted
+//    sums of the parts, shift, sample).
 //   S1  policy layer 0 rows of the workgroup's parts, their z_p; the critic
 //       obs projections P_i of its parts      -> hand-off A (polled)
 //   S2  (every workgroup) h2 = relu(b1 + sum_p z_p), heads, a = tanh(mean),
 //       critic layer 0 h1_i = relu(P_i + W0_i[:, Do:] a); its parts of
-//       critic layer 1: Q partials and u_p   -> arrival B (the last one goes on)
-//   S3  (the last arrival) Q_i, seeds, dh1, da, grad, shift, sample.
+//       critic layer 1: Q partials and v_p   -> arrival B (the last one goes on)
+//   S3  (the last arrival, wave 0) Q_i, seeds, da, grad, shift, sample.
 // Every sum runs over fixed parts or fixed lanes in a fixed order, so a row of
 // a batched call is bitwise the same row of a single-observation call.
 constexpr int kTwinZW = 8;   // policy rows per part held in registers (H <= 8 * kTwinParts)
@@ -710,8 +712,8 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
   const float* pol = a.pol;
   float* Gv = scratch + (long)gi * expl_split_scratch(H);
   float* g_z = Gv;                         // [NP][H] policy layer-1 partials
-  float* g_u = g_z + (long)NP * H;         // [NP][H] seed-free dh1 partials (parts of 2H rows)
-  float* g_P = g_u + (long)NP * H;         // [2H]    critic obs projections (+ b0)
+  float* g_v = g_z + (long)NP * H;         // [NP][Da] seed-free da partials of the parts
+  float* g_P = g_v + (long)NP * H;         // [2H]    critic obs projections (+ b0) (g_v keeps [NP][H] room)
   float* g_q = g_P + 2 * H;                // [NP]    Q partials
   unsigned* ctr = reinterpret_cast<unsigned*>(g_q + 64);   // [2] hand-off A, arrival B
   float* x = sm;                           // [Dq] ob | a
@@ -721,9 +723,8 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
   float* head = h1q + 2 * H;               // [64] mean | raw log std
   float* misc = head + 64;                 // [128] Q, seeds, norm, row Q terms, da
   float* qrow = misc + 16;                 // [<= 48] per-row Q terms of a part
-  float* red = misc + 64;                  // [64] da, then g^2 sigma
   float* w0a = misc + 128;                 // [2H][Da] W0_i[:, Do:]
-  float* ctb = w0a + 2L * H * Da;          // [nw][H] per-row u terms; S3: dh1 [2H]
+  float* ctb = w0a + 2L * H * Da;          // [nw][H] per-row u terms, row 0 then u_p
   __shared__ long long cnt_s;
   if (t == 0) cnt_s = a.state->expl_counter;
   const int p0 = wg * NP / G, p1 = (wg + 1) * NP / G;   // this workgroup's parts
@@ -926,7 +927,8 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
     }
     __syncthreads();
     // (rows of a part <= 16: every LDS read before the first add; an empty
-    // part publishes zeros)
+    // part publishes zeros).  u_p[k] goes to row 0 of ctb: thread k is the
+    // only reader and writer of column k (H <= nt, expl_twin_ok)
     for (int k = t; k < H; k += nt) {
       float cc[16];
 #pragma unroll
@@ -935,7 +937,7 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
 #pragma unroll
       for (int w = 1; w < 16; ++w)
         if (w < nb - na) s += cc[w];
-      st_pub<WT>(g_u + (long)p * H + k, s);
+      ctb[k] = s;
     }
     if (t == nt - 64) {   // (a wave without u columns when H <= nt - 64)
       float cc[16];
@@ -946,6 +948,30 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
       for (int w = 1; w < 16; ++w)
         if (w < nb - na) s += cc[w];
       st_pub<WT>(g_q + p, s);
+    }
+    __syncthreads();
+    // the part's seed-free share of da: v_p[j] = sum_k [h1_i[k] > 0] u_p[k]
+    // W0_i[k, Do + j] (one half-wave per j, lanes along k in a fixed order),
+    // Da floats published instead of the H of u_p -- the last arrival then
+    // only weighs the parts by the seeds (S3)
+    {
+      const int hw = t >> 5, l32 = t & 31;
+      if (hw < Da) {
+        float cv[16], wv[16];   // (H <= 512: every LDS read before the first FMA)
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int k = l32 + 32 * u;
+          const bool in = k < H;
+          cv[u] = in && h1q[i * H + k] > 0.f ? ctb[k] : 0.f;
+          wv[u] = in ? w0a[(long)(i * H + k) * Da + hw] : 0.f;
+        }
+        float sj = 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) sj = fmaf(cv[u], wv[u], sj);
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) sj += __shfl_xor(sj, o, 32);
+        if (l32 == 0) st_pub<WT>(g_v + (long)p * Da + hw, sj);
+      }
     }
     __syncthreads();
   }
@@ -981,72 +1007,45 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
   if ((arrived & 0xffffu) != (unsigned)G - 1) return;
   const bool others_failed = (arrived >> 16) != 0;
   EXPL_CLK3(8);
-  // ---- S3 (the last arrival): Q_i, seeds, dh1, da
+  // ---- S3 (the last arrival): Q_i, seeds, da
   if (t == 0 && G > 1) {   // every member is past both hand-offs: re-arm
     __hip_atomic_store(ctr + 0, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // Q partials in wave 0 (lane p: part p; critic p / 16), the u sums on every
-  // thread below 2H (the critic's parts in order)
-  const float qv = wave == 0 ? ld_pub<WT>(g_q + (lane & (NP - 1))) : 0.f;
-  const float blast = wave == 0 ? Qp(lane >= NPQ ? 1 : 0)[a.q_last_b] : 0.f;
-  {
-    const int e = min(t, 2 * H - 1), i = e >= H ? 1 : 0, k = e - i * H;
-    float uu[NPQ];
-#pragma unroll
-    for (int p = 0; p < NPQ; ++p) uu[p] = ld_pub<WT>(g_u + (long)(i * NPQ + p) * H + k);
-    float su = uu[0];
-#pragma unroll
-    for (int p = 1; p < NPQ; ++p) su += uu[p];
-    if (t < 2 * H) ctb[t] = su;
-  }
-  if (wave == 0) {   // Q_i: a fixed butterfly over the critic's 16 parts, then the bias
-    float q = qv;
-#pragma unroll
-    for (int o = NPQ / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
-    q += blast;
-    const float q0 = __shfl(q, 0, 64), q1 = __shfl(q, NPQ, 64);
-    if (lane == 0) {
-      misc[0] = q0; misc[1] = q1;
-      // Q_UB = (Q1+Q2)/2 + beta |Q1-Q2|/2: d|x|/dx = sign(x) (0 at 0)
-      const float d = q0 - q1;
-      const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-      const float hb = a.beta_UB / 2.f;
-      misc[2] = 0.5f + hb * sg;
-      misc[3] = 0.5f - hb * sg;
-    }
-  }
-  __syncthreads();
-  for (int e = t; e < 2 * H; e += nt) ctb[e] = h1q[e] > 0.f ? misc[2 + e / H] * ctb[e] : 0.f;
-  __syncthreads();
-  EXPL_CLK3(9);
-  {   // da[j] = sum_e dh1[e] W0a[e, j]: one half-wave per j (Da <= 32), lanes along e
-    const int hw = t >> 5, l32 = t & 31;
-    if (hw < Da) {
-      const int j = hw;
-      float cv[16], wv[16];                 // (2H <= 512: every LDS read before the first FMA)
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int e = l32 + 32 * u;
-        cv[u] = e < 2 * H ? ctb[e] : 0.f;
-        wv[u] = e < 2 * H ? w0a[(long)e * Da + j] : 0.f;
-      }
-      float sj = 0.f;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) sj = fmaf(cv[u], wv[u], sj);
-#pragma unroll
-      for (int o = 16; o > 0; o >>= 1) sj += __shfl_xor(sj, o, 32);
-      if (l32 == 0) red[j] = sj;
-    }
-  }
-  __syncthreads();
-  EXPL_CLK3(10);
-  // grad, shift, sample: wave 0 (Da <= 32), the norm as a wave sum
+  // wave 0 alone: lane p < 32 reads part p's Q partial (critic p / 16), lane
+  // j < Da the 32 parts' da partials v_p[j]
   if (wave != 0) return;
+  const float qv = ld_pub<WT>(g_q + (lane & (NP - 1)));
+  const float blast = Qp(lane & NPQ ? 1 : 0)[a.q_last_b];
+  float vv[NP];
+  {
+    const int j = min(lane, Da - 1);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) vv[p] = ld_pub<WT>(g_v + (long)p * Da + j);
+  }
+  // Q_i: a fixed butterfly over the critic's 16 parts, then the bias
+  float q = qv;
+#pragma unroll
+  for (int o = NPQ / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  q += blast;
+  const float q0 = __shfl(q, 0, 64), q1 = __shfl(q, NPQ, 64);
+  // Q_UB = (Q1+Q2)/2 + beta |Q1-Q2|/2: d|x|/dx = sign(x) (0 at 0)
+  const float dq = q0 - q1;
+  const float sg = dq > 0.f ? 1.f : (dq < 0.f ? -1.f : 0.f);
+  const float hb = a.beta_UB / 2.f;
+  const float seed0 = 0.5f + hb * sg, seed1 = 0.5f - hb * sg;
+  EXPL_CLK3(9);
+  // da[j] = seed_1 sum_{p < 16} v_p[j] + seed_2 sum_{p >= 16} v_p[j], parts in order
+  float v0 = vv[0], v1 = vv[NPQ];
+#pragma unroll
+  for (int p = 1; p < NPQ; ++p) { v0 += vv[p]; v1 += vv[NPQ + p]; }
+  const float da = seed0 * v0 + seed1 * v1;
+  EXPL_CLK3(10);
+  // grad, shift, sample (Da <= 32), the norm as a wave sum
   float g = 0.f, sig = 0.f, sd = 0.f, mean = 0.f;
   if (lane < Da) {
     const float act = x[Do + lane];
-    g = red[lane] * (1.f - act * act);
+    g = da * (1.f - act * act);
     sd = expf(fminf(fmaxf(head[Da + lane], -20.f), 2.f));
     sig = sd * sd;
     mean = head[lane];
