@@ -16,6 +16,7 @@ steps of batch B processed by all ranks per second (weak scaling).
 """
 import argparse
 import ctypes
+import gc
 import json
 import os
 import sys
@@ -138,11 +139,20 @@ def timed(run, steps, warmup, world, device):
             torch.distributed.barrier()
             torch.cuda.synchronize()
     run(warmup)
-    barrier()
-    t0 = time.perf_counter()
-    run(steps)
-    barrier()
-    el = time.perf_counter() - t0
+    # host jitter: no Python garbage collection inside the timed region (the
+    # driver times 20 steps = ~2 ms; a collection pause is a visible share)
+    gc.collect()
+    gc_on = gc.isenabled()
+    gc.disable()
+    try:
+        barrier()
+        t0 = time.perf_counter()
+        run(steps)
+        barrier()
+        el = time.perf_counter() - t0
+    finally:
+        if gc_on:
+            gc.enable()
     if world > 1:
         t = torch.tensor([el], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -448,15 +458,19 @@ def cpu_threads_all():
     return (min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n), n
 
 
-def cpu_baseline(args, runs=5, steps=100, warmup=20, min_s=2.0):
-    """The oracle's PyTorch-CPU restatement of the reference step (incl. the
-    host numpy gather + fp32 conversion), timed on this host's cores with
-    BASELINE.md section 3's procedure, bounded: 20 warm-up steps, then the
-    median of `runs` runs of at least `steps` steps and at least `min_s`
-    seconds each, at 1 thread (the reference launcher's
-    torch.set_num_threads(1), launcher_util.py:90) and at all cores."""
+def cpu_baseline(args, runs=2, steps=1000, warmup=20, all_runs=1):
+    """The reference's PyTorch-CPU step restated on torch autograd
+    (oracle/sac_autograd.py: the reference's forward ops, backward() and the
+    torch-1.4 Adam, pinned against the reference-run goldens in
+    tests/test_oracle_golden.py), with the host numpy gather + fp32
+    conversion, timed on this host's cores with BASELINE.md section 3's
+    procedure, bounded: 20 warm-up steps, then runs of 1,000 steps each -- the
+    median of `runs` at 1 thread (the reference launcher's
+    torch.set_num_threads(1), launcher_util.py:90) and `all_runs` at all
+    cores."""
     sys.path.insert(0, ROOT)
     from oracle import sac_oracle as so
+    from oracle.sac_autograd import SACAutograd
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from fixtures_lib import sac_params
     Do, Da, H, B = args.obs_dim, args.act_dim, args.hidden, args.batch
@@ -467,7 +481,7 @@ def cpu_baseline(args, runs=5, steps=100, warmup=20, min_s=2.0):
                 terminals=(rs.uniform(0, 1, (n, 1)) < 0.01).astype(np.uint8),
                 next_observations=rs.standard_normal((n, Do)))
     rep = so.NumpyReplay(data)
-    orc = so.SACOracle(sac_params(Do, Da, [H, H], 0), Do, Da)
+    orc = SACAutograd(sac_params(Do, Da, [H, H], 0), Do, Da)
     g = torch.Generator().manual_seed(2)
     irs = np.random.RandomState(1)
 
@@ -477,30 +491,28 @@ def cpu_baseline(args, runs=5, steps=100, warmup=20, min_s=2.0):
         e2 = torch.randn(B, Da, generator=g)
         orc.step(so.NumpyReplay.to_torch(b), e1, e2)
 
-    def median_rate(threads):
+    def median_rate(threads, nruns):
         torch.set_num_threads(threads)
         for _ in range(warmup):
             step()
         rates = []
-        for _ in range(runs):
-            k = 0
+        for _ in range(nruns):
             t0 = time.perf_counter()
-            while k < steps or time.perf_counter() - t0 < min_s:
+            for _ in range(steps):
                 step()
-                k += 1
-            rates.append(k / (time.perf_counter() - t0))
+            rates.append(steps / (time.perf_counter() - t0))
         return float(np.median(rates)), [round(r, 2) for r in rates]
-    one, one_runs = median_rate(1)
+    one, one_runs = median_rate(1, runs)
     T, aff = cpu_threads_all()
-    allc, all_runs = median_rate(T)
+    allc, all_rates = median_rate(T, all_runs)
     torch.set_num_threads(1)
-    sample = (f"{warmup} warm-up steps, then median of {runs} runs of >= {steps} steps and "
-              f">= {min_s:g} s of oracle SAC steps (Humanoid dims, 2x256, B={B}, "
+    sample = (f"{warmup} warm-up steps, then runs of {steps} SAC steps of the reference's op "
+              f"sequence on torch autograd (oracle/sac_autograd.py; Humanoid dims, 2x256, B={B}, "
               f"numpy f64 replay of {n} rows, torch CPU fp32)")
     return dict(value=round(one, 2), unit="grad-steps/s", cores=1, kind="port",
-                sample=sample + ", 1 thread", runs=one_runs,
-                all_cores=dict(value=round(allc, 2), cores=T, affinity_cpus=aff, runs=all_runs,
-                               sample=sample + f", {T} threads"))
+                sample=sample + f", median of {runs} runs, 1 thread", runs=one_runs,
+                all_cores=dict(value=round(allc, 2), cores=T, affinity_cpus=aff, runs=all_rates,
+                               sample=sample + f", {all_runs} run(s), {T} threads"))
 
 
 def recipe_cpu_baseline(kind, args, steps=200):

@@ -506,3 +506,41 @@ def test_oac_exploration_trainer_ub_oracle_matches_reference_golden(name):
         assert parity.rel_err(r["std"].numpy(), g["std"][i]) <= 1e-6
         assert parity.rel_err(r["mu_E"].numpy(), g["mu_E"][i]) <= parity.TOL
         assert parity.rel_err(r["action"].numpy(), g["action"][i]) <= parity.TOL
+
+
+@pytest.mark.parametrize("name", ["sac_small", "sac_stress", "sac_noalpha", "sac_humanoid",
+                                  "sac_period2"])
+def test_sac_autograd_restatement_matches_reference_golden(name):
+    """oracle/sac_autograd.py (the reference's op sequence on torch autograd:
+    bench.py's CPU baseline) against the reference's own run: every gradient
+    and post-step parameter of every step under the trajectory gate."""
+    from oracle.sac_autograd import SACAutograd
+    meta, g = parity.load(name)
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
+                        pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"])
+    ag = SACAutograd(params, meta["obs_dim"], meta["act_dim"], discount=meta["discount"],
+                     reward_scale=meta["reward_scale"], policy_lr=meta["lr"], qf_lr=meta["lr"],
+                     tau=meta["tau"], auto_alpha=meta["auto_alpha"], log_alpha0=meta["log_alpha0"],
+                     target_update_period=meta.get("target_update_period", 1))
+    noise = sac_noise(meta, g)
+    errs = {}
+    for s in range(meta["steps"]):
+        out = ag.step(build_batch(meta, g[f"s{s}/idx"]), g[f"s{s}/eps1"], g[f"s{s}/eps2"])
+        for grp in ("policy", "qf1", "qf2"):
+            for pn, t in out["grads"][grp].items():
+                key = f"s{s}/grad/{grp}/{pn}"
+                errs[key] = parity.compare(g, key, t.numpy())
+        for grp, sd in ag.state().items():
+            for pn, t in sd.items():
+                key = f"s{s}/post/{grp}/{pn}"
+                gk = f"s{s}/grad/{grp}/{pn}" if s == 0 and grp in ("policy", "qf1", "qf2") else None
+                errs[key], _ = parity.compare_post(g, key, gk, t.numpy(), meta["lr"])
+        if meta["auto_alpha"]:
+            errs[f"s{s}/post/log_alpha"] = parity.rel_err(ag.log_alpha.detach().numpy(),
+                                                          g[f"s{s}/post/log_alpha"])
+        if f"s{s}/stat/QF1 Loss" in g:
+            errs[f"s{s}/stat/QF1 Loss"] = parity.stat_err(float(out["qf1_loss"]), g,
+                                                          f"s{s}/stat/QF1 Loss")
+    bad = {k: (v, noise.get(k, 0.0)) for k, v in errs.items()
+           if v > parity.gate(k, noise.get(k, 0.0))}
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
