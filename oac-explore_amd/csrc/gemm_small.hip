@@ -69,6 +69,8 @@ __device__ __forceinline__ void stage_kc(const float* base, long ld, const int* 
 
 struct Stage { const float* img; int S; int kst; };
 
+constexpr int kHeadParts = 16;   // A_HEAD_BWD: parts of dL/da summed per row (<= 16)
+
 // acc += A[m0.., k_lo..k_hi) . B[k_lo..k_hi), n0..]  for this wave's k-groups
 // arow >= 0: this lane's A row is buffer row arow (the direct gather's index,
 // loaded by the caller ahead of everything else)
@@ -174,7 +176,7 @@ __device__ __forceinline__ EpiIn epi_prefetch(const GemmBatch& batch, const Gemm
       x.xb = t.bias[nc]; break;
     case EPI_BIAS_RELU_DOT:
       x.xb = t.bias[nc]; x.xa = t.aux[nc]; break;
-    case EPI_ADD_RELU: case EPI_MASK:
+    case EPI_ADD_RELU: case EPI_MASK: case EPI_MASK_DA:
       x.xa = t.aux[(long)mc * t.ld_aux + nc]; break;
     default: break;
   }
@@ -215,7 +217,7 @@ __device__ __forceinline__ void epi_one(const GemmBatch& batch, const AdamConsts
       break;
     }
     case EPI_ADD_RELU: t.C[o] = fmaxf(acc + x.xa, 0.f); break;
-    case EPI_MASK: t.C[o] = x.xa > 0.f ? acc : 0.f; break;
+    case EPI_MASK: case EPI_MASK_DA: t.C[o] = x.xa > 0.f ? acc : 0.f; break;
     case EPI_HEAD_BWD: {
       float dmean, dls;
       tanh_gauss_backward(acc, x.xb, x.xa, x.am, x.av, x.at, x.s * (1.f / (float)t.M), dmean, dls);
@@ -262,7 +264,7 @@ __device__ __forceinline__ int* tile_rows_of(float*) {
 
 // LDS floats the STG kernel's images take for one task (0: nothing staged)
 __host__ __device__ inline int stage_floats(const GemmTask& t) {
-  if (!t.a_kc || t.ksplit > 1) return 0;
+  if (!t.a_kc || t.ksplit > 1 || t.a_mode == A_HEAD_BWD) return 0;
   int n = 32 * stage_stride(t.K);                       // A (or A's ReLU mask)
   if (t.b_kc) n += 32 * stage_stride(t.K);              // B of a forward product
   if (t.K2 > 0) n += 32 * stage_stride(t.K2);           // the second product's A
@@ -364,7 +366,8 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
 
   // STG: the k-contiguous operands' 32 rows into LDS images first (their
   // DMA overlaps the epilogue prefetch below)
-  const bool stg = STG && t.a_kc && t.ksplit <= 1;
+  const bool hbw = t.a_mode == A_HEAD_BWD;   // A computed below, not loaded
+  const bool stg = STG && t.a_kc && t.ksplit <= 1 && !hbw;
   Stage sa{}, sb{}, sa2{};
   if (stg) {
     const bool ar1 = t.a_mode == A_RANK1_MASK;
@@ -391,6 +394,18 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     const int r = e >> 6, l = e & 63;
     xin[i] = epi_prefetch(batch, t, m0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), n0 + (l & 31));
   }
+  // EPI_MASK_DA: the tile's rows of V (the next product's weights) requested
+  // now, used after the epilogue
+  constexpr int VPF = (1024 + 64 * NW - 1) / (64 * NW);   // 32 rows x R <= 32 per thread
+  float vpf[VPF];
+  if (t.epi == EPI_MASK_DA) {
+#pragma unroll
+    for (int q = 0; q < VPF; ++q) {
+      const int e = threadIdx.x + q * 64 * NW;
+      const int n = e / t.R, j = e - n * t.R;
+      vpf[q] = (e < 32 * t.R && n0 + n < t.N) ? t.V[(long)(n0 + n) * t.ldv + j] : 0.f;
+    }
+  }
   if (stg) {   // every wave's DMA landed, then the images are complete for all
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -398,15 +413,48 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  if (stg) k_dispatch<NW, GPW, true>(t, m0, n0, k_lo, k_hi, acc, arow, sa, sb);
-  else k_dispatch<NW, GPW, false>(t, m0, n0, k_lo, k_hi, acc, arow, sa, sb);
+  if (hbw) {
+    // A = [dmean | dls_raw] of the tile's 32 rows from the parts of dL/da
+    // (an EPI_MASK_DA launch wrote them), the head backward of EPI_HEAD_BWD:
+    // into an LDS image read by the k loop like a staged operand
+    const int Da = t.K >> 1, S = stage_stride(t.K);
+    const float G = (t.ex[5] ? t.ex[5][0] : 0.f) * (1.f / (float)t.M);
+    for (int e = threadIdx.x; e < 32 * Da; e += 64 * NW) {
+      const int r = e / Da, j = e - r * Da;
+      const int m = min(m0 + r, t.M - 1);
+      const long o = (long)m * Da + j;
+      float pv[kHeadParts];
+#pragma unroll
+      for (int q = 0; q < kHeadParts; ++q) pv[q] = q < t.R ? t.A[q * t.lda + o] : 0.f;
+      float da = pv[0];
+#pragma unroll
+      for (int q = 1; q < kHeadParts; ++q)
+        if (q < t.R) da += pv[q];
+      float dmean, dls;
+      tanh_gauss_backward(da, t.ex[0][o], t.ex[1][o], t.ex[2][o], t.ex[3][o],
+                          t.ex[4][(long)m * 2 * Da + Da + j], G, dmean, dls);
+      red[r * S + j] = dmean;
+      red[r * S + Da + j] = dls;
+      if (n0 == 0 && t.U && m0 + r < t.M) {   // dhead for the head's weight gradient (next launch)
+        float* u = const_cast<float*>(t.U) + (long)m * t.ldu;
+        u[j] = dmean;
+        u[Da + j] = dls;
+      }
+    }
+    __syncthreads();
+    k_loop<NW, OP_KC, OP_MN, GPW, true>(t, m0, n0, 0, t.K, acc, -1, Stage{red, S, 0});
+  } else if (stg) {
+    k_dispatch<NW, GPW, true>(t, m0, n0, k_lo, k_hi, acc, arow, sa, sb);
+  } else {
+    k_dispatch<NW, GPW, false>(t, m0, n0, k_lo, k_hi, acc, arow, sa, sb);
+  }
   if (t.K2 > 0) {   // second product into the same accumulator (unsplit dX tasks only)
     GemmTask t2 = t;
     t2.A = t.A2; t2.B = t.B2; t2.K = t.K2;
     if (stg) k_loop<NW, OP_KC, OP_MN, GPW, true>(t2, m0, n0, 0, t.K2, acc, -1, sa2);
     else k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc);
   }
-  if (stg) __syncthreads();   // the images are read by all waves before the reduction reuses the LDS
+  if (stg || hbw) __syncthreads();   // the images are read by all waves before the reduction reuses the LDS
 
   GS_STAGE(2);
   // fixed-order split-K reduction through LDS
@@ -458,13 +506,44 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
       if (nt == 0 && m < t.M) t.C2[(long)(n0 >> 5) * t.ldc2 + m] = x;   // tile-major
     }
   }
+  if (t.epi == EPI_MASK_DA) {
+    // the tile's part of C . V[:, :R]: the masked tile and V's 32 rows in LDS,
+    // one thread per (row, j), the 32 columns in order
+    __syncthreads();   // (the LDS held the reduction)
+    float* ct = red;             // [32][33]
+    float* vb = red + 32 * 33;   // [32][R]
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int e = threadIdx.x + i * 64 * NW;
+      const int r = e >> 6, l = e & 63;
+      const int mt = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), nt = l & 31;
+      const bool in = m0 + mt < t.M && n0 + nt < t.N;
+      ct[mt * 33 + nt] = (in && xin[i].xa > 0.f) ? vals[i] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < VPF; ++q) {
+      const int e = threadIdx.x + q * 64 * NW;
+      if (e < 32 * t.R) vb[e] = vpf[q];
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 32 * t.R; e += 64 * NW) {
+      const int r = e / t.R, j = e - r * t.R;
+      float sacc = 0.f;
+#pragma unroll 8
+      for (int n = 0; n < 32; ++n) sacc = fmaf(ct[r * 33 + n], vb[n * t.R + j], sacc);
+      if (m0 + r < t.M) t.C2[(long)(n0 >> 5) * t.ldc2 + (long)(m0 + r) * t.R + j] = sacc;
+    }
+  }
   if (batch.fuse_adam && bid == 0 && threadIdx.x == 0)
     step_bookkeeping(batch.adam.state, batch.adam.alpha, batch.adam.advance);
   GS_STAGE(4);
 }
 
+// 8- and 16-wave workgroups: 4 waves per SIMD (<= 128 VGPRs), so two 8-wave
+// workgroups share a CU past 256 tiles (fewer waves: no bound, their many
+// epilogue elements per thread would spill)
 template <int NW, int GPW, bool STG>
-__global__ void __launch_bounds__(64 * NW)
+__global__ void __launch_bounds__(64 * NW, NW >= 8 ? 4 : 1)
 gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6,
                   int tb7, const GemmBatch batch) {
   extern __shared__ __attribute__((aligned(16))) float red[];   // SmallLds<NW>::N or the images
@@ -518,12 +597,19 @@ static bool small_stage_on() {
 hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   if (b0.total_tiles <= 0) return hipSuccess;
   GemmBatch b = b0;
-  for (int i = 0; i < b.ntasks; ++i)   // second products: plain unsplit dX tasks
-    if (b.t[i].K2 > 0 && (b.t[i].ksplit > 1 || !b.t[i].a_kc || b.t[i].b_kc ||
-                          b.t[i].a_mode != A_PLAIN))
+  for (int i = 0; i < b.ntasks; ++i) {   // second products: plain unsplit dX tasks
+    const GemmTask& t = b.t[i];
+    if (t.K2 > 0 && (t.ksplit > 1 || !t.a_kc || t.b_kc || t.a_mode != A_PLAIN))
       return hipErrorInvalidValue;
+    // the computed head-backward operand: an unsplit dX with K = 2 Da, <= kHeadParts parts
+    if (t.a_mode == A_HEAD_BWD && (!t.a_kc || t.b_kc || t.ksplit > 1 || (t.K & 1) || t.K2 > 0 ||
+                                    t.R < 1 || t.R > kHeadParts || 32 * stage_stride(t.K) > 2 * 32 * 65))
+      return hipErrorInvalidValue;
+    if (t.epi == EPI_MASK_DA && (t.R < 1 || t.R > 32 || t.ksplit > 1 || !t.C2 || !t.V))
+      return hipErrorInvalidValue;
+  }
   const int nw = b.force_nw > 0 ? b.force_nw : gemm_small_waves(b);
-  const int gpw = b.force_gpw > 0 ? b.force_gpw : (nw >= 16 ? 4 : 5);
+  int gpw = b.force_gpw > 0 ? b.force_gpw : (nw >= 16 ? 4 : 5);
   b.adam_blocks = 0;
   if (b.fuse_adam) {
     long n4 = 0;
@@ -540,13 +626,14 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   // beside the workgroups per CU the grid needs (1 at >= 16 waves)
   int lds = SmallLdsFloats(nw);
   bool stg = false;
-  if (small_stage_on() && (nw == 16 || gpw == 5) && !(nw == 16 && gpw != 4)) {
+  if (small_stage_on() && b.force_gpw <= 0 && (nw == 8 || nw == 16)) {
     int need = 0;
     for (int i = 0; i < b.ntasks; ++i) need = std::max(need, stage_floats(b.t[i]));
     const int per_cu = nw >= 16 ? 1 : std::max(1, (grid + 255) / 256);
     if (need > 0 && 4 * std::max(need, lds) * per_cu <= kLdsBytesPerCu) {
       stg = true;
       lds = std::max(need, lds);
+      if (nw == 8) gpw = 4;
     }
   }
   const size_t shm = 4 * (size_t)lds;
@@ -563,7 +650,8 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
     OAC_LAUNCH((gemm_small_kernel<NW_, G_, true>), dim3(grid), dim3(64 * NW_), shm, s, h.total_tiles, h.publish, \
                h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b); \
     return hipGetLastError(); }
-  OAC_GSS(1, 5) OAC_GSS(2, 5) OAC_GSS(4, 5) OAC_GSS(8, 5) OAC_GSS(16, 4)
+  // staged operands: LDS fragment reads need fewer k-groups in flight (8 waves: 4)
+  OAC_GSS(8, 4) OAC_GSS(16, 4)
 #undef OAC_GSS
   OAC_GS(1, 5) OAC_GS(2, 5) OAC_GS(4, 5) OAC_GS(8, 5) OAC_GS(16, 4)
   OAC_GS(4, 3) OAC_GS(4, 4) OAC_GS(4, 6) OAC_GS(4, 8)

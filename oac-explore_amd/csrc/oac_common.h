@@ -17,6 +17,10 @@ namespace oac {
 enum AMode : int {
   A_PLAIN = 0,        // A[row*lda + col]
   A_RANK1_MASK = 1,   // s[row] * v[col] * (mask[row*ld_mask + col] > 0)
+  A_HEAD_BWD = 2,     // small kernel, K = 2 act_dim: A(m, .) = [dmean | dls_raw] of row m,
+                      // the tanh-Gaussian head backward (policy_math.h) of
+                      // dL/da[m][j] = sum_{p < R} A[p*lda + m*(K/2) + j] (parts in order),
+                      // ex[] as EPI_HEAD_BWD; the n0 == 0 tiles store the rows to U (ldu)
 };
 
 enum Epi : int {
@@ -35,6 +39,10 @@ enum Epi : int {
   EPI_BIAS_RELU_DOT = 7,  // C = relu(acc + bias[n]) and, per row, the partial
                           // dot of this 32-column tile with aux[n] (a width-1
                           // output layer): C2[(n0/32)*ldc2 + m]  (small kernel)
+  EPI_MASK_DA = 9,        // EPI_MASK, and the tile's part of the next product
+                          // C . V[:, :R] (V row-major, ldv; R <= 32):
+                          // C2[(n0/32)*ldc2 + m*R + j] = sum_{n in tile} C[m,n] V[n*ldv + j]
+                          // (small kernel; the parts feed an A_HEAD_BWD operand)
 };
 
 struct GemmTask {

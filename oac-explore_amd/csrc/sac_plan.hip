@@ -71,6 +71,7 @@ enum Ws {
   W_STD1, W_U1, W_STD2, W_U2, W_DQ1, W_DQ2, W_GQ1, W_GQ2,
   W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DA1, W_DA2, W_DHEAD, W_DH2P, W_DH1P,
   W_QPART,   // [6][B][tiles]: per-tile partial dots of the width-1 critic heads
+  W_DAP,     // [2 x tiles][B][Da]: the -min Q backward's per-tile parts of dL/da (pbwd_fuse)
   W_COUNT
 };
 
@@ -94,6 +95,7 @@ static void layout_workspace(SacPlan& p) {
   for (int id : {W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DH2P, W_DH1P}) set(id, B, H);
   set(W_DHEAD, B, 2 * Da);
   set(W_QPART, QV_COUNT * B, (H + 31) / 32);
+  set(W_DAP, 2 * ((H + 31) / 32) * B, Da);
   if (p.S_q > 1) set(WS_GSLAB_Q, p.S_q, p.L.n_critics * p.L.q_size);
   if (p.S_p > 1) set(WS_GSLAB_P, p.S_p, p.L.pol_size);
   int64_t off = 0;
@@ -477,6 +479,20 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
   return 0;
 }
 
+// The small-batch policy backward in four launches instead of five: the
+// -min Q backward's tiles also write their part of dL/da = dh1 . W0[:, Do:]
+// (EPI_MASK_DA: 32 x Da per tile, from the masked tile in LDS), and the dh2
+// launch computes its A operand -- [dmean | dls_raw], the tanh-Gaussian head
+// backward of the summed parts -- per row block itself (A_HEAD_BWD), with the
+// n0 == 0 tiles writing dhead for the head's weight gradient, which moves into
+// the policy layer-1 launch.  The dL/da + head-backward launch is gone.
+// OAC_PBWD_FUSE=1 turns it on (A/B against the five-launch form).
+static bool pbwd_fuse(const SacPlan& p) {
+  static const bool on = [] { const char* e = getenv("OAC_PBWD_FUSE"); return e && atoi(e) == 1; }();
+  const int parts = 2 * ((p.c.hidden + 31) / 32);
+  return on && p.cfg == 0 && p.c.q_out == 1 && parts <= 16 && p.c.act_dim <= 32;
+}
+
 // prefetch: batch of the next step (its critic-side forward rides on this
 // step's policy-backward launches, small-batch path only), or null
 static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch = nullptr,
@@ -489,6 +505,8 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
   const float* pol = p.b.params;
   const float* q1 = p.b.params + L.q1_base;
   const float* q2 = p.b.params + L.q2_base;
+  const bool pbf = pbwd_fuse(p);
+  const int ntn = (H + 31) / 32;   // column tiles of dh1: the parts of dL/da per critic
   {  // -min Q backward to layer 1 with post-step weights, pre-step masks
     GemmBatch gb{};
     const float* qs[2] = {q1, q2};
@@ -497,6 +515,11 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     for (int i = 0; i < 2; ++i) {
       GemmTask d = t_dx(nullptr, 0, B, H, qs[i] + L.q_fc1_w, H, H, p.W(out[i]), H, p.W(h1[i]), H);
       set_rank1(d, p.W(gq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
+      if (pbf) {   // + the tile's part of dL/da through the action columns of layer 0
+        d.epi = EPI_MASK_DA;
+        d.V = qs[i] + L.q_fc0_w + Do; d.ldv = Dq; d.R = Da;
+        d.C2 = p.W(W_DAP) + (long)i * ntn * B * Da; d.ldc2 = (long)B * Da;
+      }
       add(gb, d);
     }
     if (prefetch) add_critic_l0(p, gb, prefetch);
@@ -509,7 +532,31 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     }
     if (run_gemm(p, gb, s)) return 1;
   }
-  if (p.cfg == 0 || head_bwd_fused_big()) {  // dL/da through both critics' action columns + head backward, one launch (small kernel)
+  if (pbf) {
+    {  // dh2 = ([dmean | dls_raw] . W_head) * [h2 > 0], the A operand computed per row block
+      GemmBatch gb{};
+      GemmTask t = t_dx(p.W(W_DAP), (long)B * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(W_DH2P), H,
+                        p.W(W_H2P), H);
+      t.a_mode = A_HEAD_BWD; t.R = 2 * ntn;
+      t.ex[0] = p.W(OAC_WS_ACT1); t.ex[1] = p.W(W_STD1); t.ex[2] = p.W(W_U1);
+      t.ex[3] = p.E1(); t.ex[4] = p.W(OAC_WS_HEAD1);
+      t.ex[5] = c.auto_alpha ? &p.alpha()->alpha : nullptr;
+      t.U = p.W(W_DHEAD); t.ldu = 2 * Da;
+      add(gb, t);
+      if (prefetch) { add_target_l0(p, gb, prefetch); add_critic_l1(p, gb); }
+      if (run_gemm(p, gb, s)) return 1;
+    }
+    {  // policy layer 1 + the heads' weight gradient (dhead from the launch above)
+      GemmBatch gb{};
+      float* gp = grad_p(p);
+      add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
+                   L.pol_size, p.sp_p1));
+      add(gb, t_dx(p.W(W_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_DH1P), H, p.W(W_H1P), H));
+      add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, gp + L.pol_head_w,
+                   gp + L.pol_head_b, L.pol_size, p.sp_ph));
+      if (run_gemm(p, gb, s)) return 1;
+    }
+  } else if (p.cfg == 0 || head_bwd_fused_big()) {  // dL/da through both critics' action columns + head backward, one launch (small kernel)
     GemmBatch gb{};
     GemmTask t = t_dx(p.W(W_DH1N1), H, B, H, q1 + L.q_fc0_w + Do, Dq, Da, p.W(W_DHEAD), 2 * Da,
                       nullptr, 0);
@@ -538,7 +585,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
       p.launches++;
     }
   }
-  {  // policy heads: dW_head slab, dh2
+  if (!pbf) {  // policy heads: dW_head slab, dh2
     GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, gp + L.pol_head_w,
@@ -547,7 +594,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     if (prefetch) add_critic_l1(p, gb);
     if (run_gemm(p, gb, s)) return 1;
   }
-  {  // policy layer 1
+  if (!pbf) {  // policy layer 1
     GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
