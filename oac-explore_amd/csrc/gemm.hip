@@ -402,7 +402,8 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   for (int i = 0; i < b.ntasks; ++i) {
     gathers = gathers || b.t[i].a_rows;
     // the computed head-backward operand and the da-part epilogue: small kernel only
-    small_only = small_only || b.t[i].a_mode == A_HEAD_BWD || b.t[i].epi == EPI_MASK_DA;
+    small_only = small_only || b.t[i].a_mode == A_HEAD_BWD || b.t[i].a_mode == A_HEAD_FWD ||
+                 b.t[i].epi == EPI_MASK_DA;
   }
   if (gathers && cfg != 0 && (cfg < 6 || cfg > 8)) return hipErrorInvalidValue;
   if (small_only && cfg != 0) return hipErrorInvalidValue;

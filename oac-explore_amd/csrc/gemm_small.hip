@@ -145,6 +145,130 @@ __device__ __forceinline__ void k_dispatch(const GemmTask& t, int m0, int n0, in
   else                         k_loop<NW, OP_MN_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dW, rank-1 seed
 }
 
+// ---------------------------------------------------------------------------
+// A_HEAD_FWD: the fresh-action critic layer 1's A operand computed per 32-row
+// block inside the tile (what policy_head_kernel, head.hip, did as a launch of
+// its own): (1) the stacked heads [mean | ls_raw] = h2 . W_head^T for the 32
+// rows on v_mfma_f32_16x16x4_f32 (2 row x NTc column tiles of 16, K halved
+// over two waves, halves added in order), (2) the tanh-Gaussian sample and
+// log-prob (policy_math.h, one half-wave per row), (3) the critic's layer 0 on
+// the actions, h1 = relu(P + sum_j a_j W0[:, Do + j]) for all H columns, into
+// the LDS image the k loop reads.  Every tile of a row block computes the same
+// values in the same order; the writing task's n0 == 0 tiles store them.
+// LDS (floats): image [32][S] | head partials [2][8][256] | Y [32][65] |
+// act [32][33] | lp [32] | W0[:, Do:]^T [32][H]
+constexpr int kHfPart = 2 * 8 * 256, kHfY = 32 * 65, kHfAct = 32 * 33;
+__host__ __device__ inline int head_fwd_floats(int H) {
+  return 32 * stage_stride(H) + kHfPart + kHfY + kHfAct + 32 + 32 * H;
+}
+
+template <int NW>
+__device__ __forceinline__ void head_fwd_image(const GemmBatch& batch, const GemmTask& t, int m0,
+                                               int n0, float* lds) {
+  const HeadFwd& hf = batch.hf[t.a_aux & 1];
+  const bool wr = (t.a_aux & 2) && n0 == 0;
+  const int H = t.K, Da = hf.Da, D2 = 2 * Da, M = t.M;
+  const int S = stage_stride(H);
+  float* img = lds;
+  float* part = img + 32 * S;
+  float* Y = part + kHfPart;
+  float* act = Y + kHfY;
+  float* lp = act + kHfAct;
+  float* waT = lp + 32;                      // [Da][H]
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int ntc = (D2 + 15) >> 4;            // head column tiles of 16 (<= 4)
+  const int items = 2 * 2 * ntc;             // (row tile, column tile, k half)
+  // (1) heads: wave w < items takes one (row tile, column tile, k half)
+  typedef float floatx4 __attribute__((ext_vector_type(4)));
+  if (wave < items) {
+    const int kh = wave / (2 * ntc), tile = wave - kh * 2 * ntc;
+    const int rt = tile / ntc, ct = tile - rt * ntc;
+    const float* arow = hf.h2 + (long)min(m0 + 16 * rt + l16, M - 1) * H;
+    const int bc = 16 * ct + l16;
+    const float* brow = hf.wh + (long)min(bc, D2 - 1) * H;
+    const int k0 = kh * (H >> 1), nch = (H >> 1) >> 4;   // 16-k chunks of the half
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+    constexpr int U = 8;   // chunks in flight
+#pragma unroll 1
+    for (int c0 = 0; c0 < nch; c0 += U) {
+      f4u xa[U], xb[U];
+#pragma unroll
+      for (int c = 0; c < U; ++c) {
+        const int kb = k0 + 16 * min(c0 + c, nch - 1) + 4 * g4;
+        xa[c] = *reinterpret_cast<const f4u*>(arow + kb);
+        xb[c] = *reinterpret_cast<const f4u*>(brow + kb);
+      }
+#pragma unroll
+      for (int c = 0; c < U; ++c)
+        if (c0 + c < nch) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[c][j], bc < D2 ? xb[c][j] : 0.f, acc, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) part[(kh * 8 + tile) * 256 + r * 64 + lane] = acc[r];
+  }
+  // (3)'s W0[:, Do:] transposed into LDS (row n of W0 at a_v + n ld_mask)
+  constexpr int kNT = 64 * NW;
+  for (int e = threadIdx.x; e < H * Da; e += kNT) {
+    const int nn = e / Da, j = e - nn * Da;
+    waT[j * H + nn] = t.a_v[(long)nn * t.ld_mask + j];
+  }
+  const int n = threadIdx.x % H, r0 = threadIdx.x / H, rstep = kNT / H;   // (kNT % H == 0: launcher)
+  __syncthreads();
+  // Y = the two k halves in order + bias (D reg r: row 4 (l >> 4) + r, col l & 15)
+  for (int e = threadIdx.x; e < 2 * ntc * 256; e += kNT) {
+    const int tile = e >> 8, r = (e >> 6) & 3, l = e & 63;
+    const int rt = tile / ntc, ct = tile - rt * ntc;
+    const int row = 16 * rt + 4 * (l >> 4) + r, col = 16 * ct + (l & 15);
+    if (col < D2)
+      Y[row * 65 + col] = (part[tile * 256 + r * 64 + l] + part[(8 + tile) * 256 + r * 64 + l]) + hf.bh[col];
+  }
+  __syncthreads();
+  // (2) sample + log-prob: one half-wave per row, lane j = action dim
+  for (int e = threadIdx.x; e < 32 * 32; e += kNT) {
+    const int row = e >> 5, j = e & 31, m = m0 + row;
+    float l = 0.f, a = 0.f;
+    if (m < M && j < Da) {
+      float sd, u;
+      l = tanh_gauss_sample(Y[row * 65 + j], Y[row * 65 + Da + j], hf.eps[(long)m * Da + j], a, sd, u);
+      if (wr) {
+        const long o = (long)m * Da + j;
+        hf.act[o] = a; hf.stdv[o] = sd; hf.u[o] = u;
+        hf.head[(long)m * D2 + j] = Y[row * 65 + j];
+        hf.head[(long)m * D2 + Da + j] = Y[row * 65 + Da + j];
+      }
+    }
+    act[row * 33 + j] = a;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) l += __shfl_xor(l, o, 32);
+    if (j == 0) {
+      lp[row] = m < M ? l + hf.te : 0.f;
+      if (wr && m < M) hf.logp[m] = l;
+    }
+  }
+  __syncthreads();
+  if (wr && hf.logp_part && threadIdx.x < 2 && m0 + 16 * threadIdx.x < M) {   // data-parallel alpha
+    float sum = 0.f;
+    for (int r = 0; r < 16; ++r) sum += lp[16 * threadIdx.x + r];
+    hf.logp_part[(m0 >> 4) + threadIdx.x] = sum;
+  }
+  // (3) h1 = relu(P + sum_j a_j W0[n, Do + j]) for the 32 rows, column n
+  float* U = const_cast<float*>(t.U);
+  for (int r = r0; r < 32; r += rstep) {
+    const int m = min(m0 + r, M - 1);
+    float sacc = t.A[(long)m * t.lda + n];
+    for (int j = 0; j < Da; ++j) sacc = fmaf(act[r * 33 + j], waT[j * H + n], sacc);
+    const float h = fmaxf(sacc, 0.f);
+    img[r * S + n] = h;
+    if (U && n0 == 0 && m0 + r < M) U[(long)(m0 + r) * t.ldu + n] = h;
+  }
+  __syncthreads();
+}
+
 // Epilogue operands of one output element, loaded before the k loop so their
 // latency hides behind it: xb = bias[n] (or the fused-Adam p), xa = aux[m,n]
 // (EPI_ADD_RELU / EPI_MASK), aux[n] (EPI_BIAS_RELU_DOT).
@@ -263,7 +387,9 @@ __device__ __forceinline__ int* tile_rows_of(float*) {
 }
 
 // LDS floats the STG kernel's images take for one task (0: nothing staged)
+__host__ __device__ inline int head_fwd_floats(int H);
 __host__ __device__ inline int stage_floats(const GemmTask& t) {
+  if (t.a_mode == A_HEAD_FWD) return head_fwd_floats(t.K) + 32 * stage_stride(t.K);   // image + B
   if (!t.a_kc || t.ksplit > 1 || t.a_mode == A_HEAD_BWD) return 0;
   int n = 32 * stage_stride(t.K);                       // A (or A's ReLU mask)
   if (t.b_kc) n += 32 * stage_stride(t.K);              // B of a forward product
@@ -367,7 +493,8 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   // STG: the k-contiguous operands' 32 rows into LDS images first (their
   // DMA overlaps the epilogue prefetch below)
   const bool hbw = t.a_mode == A_HEAD_BWD;   // A computed below, not loaded
-  const bool stg = STG && t.a_kc && t.ksplit <= 1 && !hbw;
+  const bool hfw = t.a_mode == A_HEAD_FWD;   // A computed below, B staged by LDS-DMA
+  const bool stg = STG && t.a_kc && t.ksplit <= 1 && !hbw && !hfw;
   Stage sa{}, sb{}, sa2{};
   if (stg) {
     const bool ar1 = t.a_mode == A_RANK1_MASK;
@@ -413,7 +540,18 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  if (hbw) {
+  if (hfw) {
+    // B (the critic's layer-1 rows) into LDS behind the image, its DMA in
+    // flight while the heads, the sample and h1 are computed
+    const int S = stage_stride(t.K);
+    float* bimg = red + head_fwd_floats(t.K);
+    stage_kc<NW>(t.B, t.ldb, nullptr, n0, t.N, 0, t.K, bimg, S);
+    head_fwd_image<NW>(batch, t, m0, n0, red);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    k_loop<NW, OP_KC, OP_KC, GPW, true, true>(t, m0, n0, 0, t.K, acc, -1, Stage{red, S, 0},
+                                             Stage{bimg, S, 0});
+  } else if (hbw) {
     // A = [dmean | dls_raw] of the tile's 32 rows from the parts of dL/da
     // (an EPI_MASK_DA launch wrote them), the head backward of EPI_HEAD_BWD:
     // into an LDS image read by the k loop like a staged operand
@@ -454,7 +592,7 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     if (stg) k_loop<NW, OP_KC, OP_MN, GPW, true>(t2, m0, n0, 0, t.K2, acc, -1, sa2);
     else k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc);
   }
-  if (stg || hbw) __syncthreads();   // the images are read by all waves before the reduction reuses the LDS
+  if (stg || hbw || hfw) __syncthreads();   // the images are read by all waves before the reduction reuses the LDS
 
   GS_STAGE(2);
   // fixed-order split-K reduction through LDS
@@ -625,6 +763,16 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   // staged k-contiguous operands (OAC_SMALL_STAGE=1): when the images fit
   // beside the workgroups per CU the grid needs (1 at >= 16 waves)
   int lds = SmallLdsFloats(nw);
+  for (int i = 0; i < b.ntasks; ++i) {   // the computed fresh-action operand: 16 waves, its LDS
+    const GemmTask& t = b.t[i];
+    if (t.a_mode != A_HEAD_FWD) continue;
+    const HeadFwd& hf = b.hf[t.a_aux & 1];
+    if (nw != 16 || !t.b_kc || t.ksplit > 1 || t.K2 > 0 || t.K % 32 || (64 * nw) % t.K ||
+        hf.Da < 1 || hf.Da > 32 || !hf.h2 || !hf.wh || !hf.bh || !hf.eps || !t.a_v)
+      return hipErrorInvalidValue;
+    lds = std::max(lds, stage_floats(t));
+  }
+  if (4 * lds > kLdsBytesPerCu) return hipErrorInvalidValue;
   bool stg = false;
   if (small_stage_on() && b.force_gpw <= 0 && (nw == 8 || nw == 16)) {
     int need = 0;
@@ -639,6 +787,10 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   const size_t shm = 4 * (size_t)lds;
 #define OAC_GS(NW_, G_) \
   if (nw == NW_ && gpw == G_ && !stg) { \
+    if (shm > 64 * 1024) { \
+      static const bool attr_set = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_small_kernel<NW_, G_, false>), \
+          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytesPerCu) == hipSuccess; \
+      (void)attr_set; } \
     OAC_LAUNCH((gemm_small_kernel<NW_, G_, false>), dim3(grid), dim3(64 * NW_), shm, s, h.total_tiles, h.publish, \
                h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b); \
     return hipGetLastError(); }

@@ -17,6 +17,12 @@ namespace oac {
 enum AMode : int {
   A_PLAIN = 0,        // A[row*lda + col]
   A_RANK1_MASK = 1,   // s[row] * v[col] * (mask[row*ld_mask + col] > 0)
+  A_HEAD_FWD = 3,     // small kernel, forward with K = hidden: A = the critic's layer-0
+                      // output on the policy's fresh actions, h1 = relu(A[m*lda + n] +
+                      // sum_j act[m][j] a_v[n*ld_mask + j]) with act = the tanh-Gaussian
+                      // sample of GemmBatch::hf[a_aux & 1] (heads computed per row block);
+                      // a_aux & 2: the n0 == 0 tiles write hf's per-row outputs, and
+                      // U != null: the n0 == 0 tiles write h1 rows to U (ldu)
   A_HEAD_BWD = 2,     // small kernel, K = 2 act_dim: A(m, .) = [dmean | dls_raw] of row m,
                       // the tanh-Gaussian head backward (policy_math.h) of
                       // dL/da[m][j] = sum_{p < R} A[p*lda + m*(K/2) + j] (parts in order),
@@ -78,6 +84,7 @@ struct GemmTask {
   int K2;
   const float* ex[6];   // extra epilogue operands (EPI_HEAD_BWD)
   int a_rows;           // small kernel: A (and U) row m is row batch.rg rows[m] of the buffer
+  int a_aux;            // A_HEAD_FWD: segment (bit 0), write the segment's outputs (bit 1)
 };
 
 struct StepState;
@@ -114,10 +121,24 @@ struct RowGather {
   float* eps1; float* eps2; int n_eps; unsigned long long seed;
 };
 
+// A_HEAD_FWD's policy batch: TanhGaussianPolicy's heads on h2, the sample
+// with eps, and where the n0 == 0 tiles of the writing task store the per-row
+// results (policy_head_kernel's HeadSeg outputs, head.hip)
+struct HeadFwd {
+  const float* h2;       // [B, H] policy hidden layer 2
+  const float* wh; const float* bh;   // stacked heads [2 Da, H], [2 Da]
+  const float* eps;      // [B, Da]
+  float* head; float* act; float* stdv; float* u; float* logp;
+  float* logp_part;      // non-null: per-16-row sums of (logp + te), rows in order
+  float te;
+  int Da;
+};
+
 struct GemmBatch {
   GemmTask t[kMaxTasks];
   int ntasks;
   int total_tiles;
+  HeadFwd hf[2];             // A_HEAD_FWD tasks' policy batches
   // Fused optimizer (small-batch kernel, unsplit K): every EPI_GRAD element is
   // also Adam(+Polyak)-updated in the epilogue (its index in the group is its
   // gradient pointer minus adam.g), and blocks [total_tiles, +adam_blocks) run

@@ -233,6 +233,19 @@ static int head_col_chunks(int B, int H) {
   return B >= 1024 ? std::max(1, (H + 255) / 256) : std::max(1, (H + 63) / 64);
 }
 
+// The small-batch step without the policy-head launch (OAC_HEAD_FUSE=1, A/B):
+// the fresh-action critic layer-1 launch computes its A operand per row block
+// -- heads, tanh-Gaussian sample, the critic's action columns on the saved
+// obs projection -- inside each tile (A_HEAD_FWD, gemm_small.hip), and the
+// Q1 / TQ1 tasks' n0 == 0 tiles write the per-row outputs the later launches
+// read.  Single rank only: the data-parallel alpha exchange needs the head's
+// partials before that launch.
+static bool head_fuse(const SacPlan& p) {
+  static const bool on = [] { const char* e = getenv("OAC_HEAD_FUSE"); return e && atoi(e) == 1; }();
+  return on && p.cfg == 0 && p.c.kind == OAC_KIND_SAC && p.c.q_out == 1 && p.c.world_size <= 1 &&
+         p.c.hidden % 32 == 0 && 1024 % p.c.hidden == 0 && p.c.act_dim <= 32 && qdot(p);
+}
+
 static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool critic_done = false) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
@@ -305,7 +318,7 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
     add(gb, t_fwd(p.W(W_H2Q2), H, B, H, q2 + L.q_last_w, H, 1, p.W(OAC_WS_Q2), 1, EPI_BIAS, q2 + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
-  {  // policy heads, tanh-Gaussian sample + log-prob, critics' action columns
+  if (!head_fuse(p)) {  // policy heads, tanh-Gaussian sample + log-prob, critics' action columns
     HeadArgs a;
     std::memset(&a, 0, sizeof(a));
     a.wh = pol + L.pol_head_w; a.bh = pol + L.pol_head_b; a.ld_wa = Dq;
@@ -371,6 +384,28 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
     const int outs[4] = {W_H2N1, W_H2N2, W_H2T1, W_H2T2};
     const int qv[4] = {QV_QN1, QV_QN2, QV_TQ1, QV_TQ2};
     for (int i = 0; i < 4; ++i) add(gb, q_l1(p, p.W(ins[i]), nets[i], p.W(outs[i]), qv[i]));
+    if (head_fuse(p)) {   // the policy heads inside the tiles (A_HEAD_FWD)
+      const float* pol = p.b.params;
+      const int pre[4] = {W_P1, W_P2, W_PT1, W_PT2};
+      for (int i = 0; i < 4; ++i) {
+        GemmTask& t = gb.t[i];
+        t.a_mode = A_HEAD_FWD;
+        t.A = p.W(pre[i]); t.lda = H;
+        t.a_v = nets[i] + L.q_fc0_w + Do; t.ld_mask = Dq;
+        t.a_aux = (i >> 1) | ((i & 1) ? 0 : 2);      // Q1 / TQ1 tasks write their batch's outputs
+        t.U = i < 2 ? p.W(ins[i]) : nullptr; t.ldu = H;   // h1 of Q_i(obs, a~): the policy backward's masks
+      }
+      const int h2[2] = {W_H2P, W_H2P2}, head[2] = {OAC_WS_HEAD1, OAC_WS_HEAD2};
+      const int act[2] = {OAC_WS_ACT1, OAC_WS_ACT2}, sd[2] = {W_STD1, W_STD2}, uu[2] = {W_U1, W_U2};
+      const int lp[2] = {OAC_WS_LOGP1, OAC_WS_LOGP2};
+      for (int g = 0; g < 2; ++g) {
+        HeadFwd& hf = gb.hf[g];
+        hf.h2 = p.W(h2[g]); hf.wh = pol + L.pol_head_w; hf.bh = pol + L.pol_head_b;
+        hf.eps = g == 0 ? p.E1() : p.E2();
+        hf.head = p.W(head[g]); hf.act = p.W(act[g]); hf.stdv = p.W(sd[g]); hf.u = p.W(uu[g]);
+        hf.logp = p.W(lp[g]); hf.logp_part = nullptr; hf.te = c.target_entropy; hf.Da = Da;
+      }
+    }
     if (p.direct_big) {   // the direct-gather step's batch copy (its first reader is the
       RowGather& g = gb.rg;   // targets kernel next): side workgroups in the free slot per CU
       g.ring = p.direct_ring; g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
