@@ -646,18 +646,19 @@ def _launches(tr):
     return _lib.lib().oac_sac_launch_count(tr._last_plan.handle)
 
 
-def rocprof_gemm_avg(key, round_dir="r03"):
+def rocprof_gemm_avg(key, round_dir="r04"):
     """(average GEMM launch us, path) from the committed rocprofv3 summary of
     this workload (tools/prof_summary.py output), or None."""
-    path = os.path.join("profiles", round_dir, {256: "b256", 4096: "b4096"}.get(key, str(key))
-                        + "_gemm_avg.txt")
-    try:
-        with open(os.path.join(ROOT, path)) as f:
-            for line in f:
-                if line.startswith("GEMM kernel (all instances)"):
-                    return float(line.rsplit("avg", 1)[1].split()[0]), path
-    except OSError:
-        pass
+    for rd in (round_dir, "r03"):   # the newest round's summary, else the previous one
+        path = os.path.join("profiles", rd, {256: "b256", 4096: "b4096"}.get(key, str(key))
+                            + "_gemm_avg.txt")
+        try:
+            with open(os.path.join(ROOT, path)) as f:
+                for line in f:
+                    if line.startswith("GEMM kernel (all instances)"):
+                        return float(line.rsplit("avg", 1)[1].split()[0]), path
+        except OSError:
+            pass
     return None
 
 
