@@ -1,10 +1,9 @@
 #!/bin/bash
-# round 4 validation + A/B on one box:
+# round 4 validation + A/B on one box (~15 min):
 #  1. the new tests (teacher-forced, mid-state, forced-overlap DP) and the exploration tests
 #  2. the B=256 variants' parity subsets (OAC_SMALL_STAGE, OAC_PBWD_FUSE, OAC_HEAD_FUSE), each
 #     recorded pass / fail; a crash, abort or time-out ends the script
-#  3. the A/B bench of the variants that passed, per-launch times, micros, TA counters
-#  4. the full GPU suite (defaults)
+#  3. the A/B bench of the variants that passed, per-launch times
 mkdir -p gpurun_out
 crash() { case $1 in 124|134|137|139) echo "GPU step ended with $1: stopping"; exit $1;; esac; }
 T="--timeout 200 --timeout-method thread -p no:cacheprovider"
@@ -14,16 +13,17 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "expl or philo
 rc=$?; crash $rc; tail -3 gpurun_out/r4_expl_tests.log; echo "expl tests rc=$rc"
 timeout -k 10 60 tools/micro/expl_micro 400 1 0 > gpurun_out/r4_expl_micro.log 2>&1; crash $?
 head -20 gpurun_out/r4_expl_micro.log
-SUB="tests/test_gpu_parity.py tests/test_gpu_dropin.py tests/test_gpu_ring.py tests/test_gpu_teacher.py"
+SUB="tests/test_gpu_parity.py tests/test_gpu_teacher.py"
 ok=""
 for arm in "1 0 0" "0 1 0" "0 0 1" "1 1 1"; do
   set -- $arm
-  OAC_SMALL_STAGE=$1 OAC_PBWD_FUSE=$2 OAC_HEAD_FUSE=$3 timeout -k 10 400 python -u -m pytest $SUB -q -x $T > gpurun_out/r4_arm_$1$2$3.log 2>&1
+  X=""; [ "$arm" = "1 1 1" ] && X="tests/test_gpu_dropin.py tests/test_gpu_ring.py"
+  OAC_SMALL_STAGE=$1 OAC_PBWD_FUSE=$2 OAC_HEAD_FUSE=$3 timeout -k 10 400 python -u -m pytest $SUB $X -q -x -k "not b4096 and not poac and not particle" $T > gpurun_out/r4_arm_$1$2$3.log 2>&1
   rc=$?; crash $rc; echo "arm stage=$1 pbwd=$2 head=$3 rc=$rc: $(tail -1 gpurun_out/r4_arm_$1$2$3.log)"
   [ $rc -eq 0 ] && ok="$ok $1$2$3"
 done
 echo "arms passing:$ok"
-for i in 1 2 3; do
+for i in 1 2; do
   for a in 000 $ok; do
     OAC_SMALL_STAGE=${a:0:1} OAC_PBWD_FUSE=${a:1:1} OAC_HEAD_FUSE=${a:2:1} timeout -k 10 120 python bench.py --steps 3000 --warmup 300 --no-extras --no-cpu-baseline > gpurun_out/ab_$a.log 2>&1
     rc=$?; crash $rc
@@ -34,8 +34,3 @@ for a in 000 $ok; do
   OAC_SMALL_STAGE=${a:0:1} OAC_PBWD_FUSE=${a:1:1} OAC_HEAD_FUSE=${a:2:1} timeout -k 10 200 python tools/launch_times.py --batch 256 > gpurun_out/lt_$a.log 2>&1
   crash $?; echo "arm $a"; head -16 gpurun_out/lt_$a.log
 done
-timeout -k 10 120 tools/micro/gemm_micro > gpurun_out/r4_gemm_micro.log 2>&1; crash $?
-OAC_SMALL_STAGE=1 timeout -k 10 120 tools/micro/gemm_micro > gpurun_out/r4_gemm_micro_stage.log 2>&1; crash $?
-bash tools/pmc_ta.sh b256
-timeout -k 10 700 python -u -m pytest tests -m gpu -q $T > gpurun_out/r4_pytest_all.log 2>&1
-rc=$?; tail -5 gpurun_out/r4_pytest_all.log; exit $rc
