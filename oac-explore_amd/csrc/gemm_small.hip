@@ -561,9 +561,11 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
       const int r = e / Da, j = e - r * Da;
       const int m = min(m0 + r, t.M - 1);
       const long o = (long)m * Da + j;
+      // every part's load issued unconditionally (clamped part index): a
+      // load behind a runtime condition is waited for one at a time
       float pv[kHeadParts];
 #pragma unroll
-      for (int q = 0; q < kHeadParts; ++q) pv[q] = q < t.R ? t.A[q * t.lda + o] : 0.f;
+      for (int q = 0; q < kHeadParts; ++q) pv[q] = t.A[min(q, t.R - 1) * t.lda + o];
       float da = pv[0];
 #pragma unroll
       for (int q = 1; q < kHeadParts; ++q)
@@ -702,6 +704,8 @@ int gemm_small_waves(const GemmBatch& b) {
   // a 16-wave workgroup holds a whole CU (VGPRs); past 256 tiles the grid
   // would run in two rounds, so take 8 waves (two workgroups per CU)
   if (nw == 16 && b.total_tiles > 256) nw = 8;
+  for (int i = 0; i < b.ntasks; ++i)   // the computed fresh-action operand takes 16 waves
+    if (b.t[i].a_mode == A_HEAD_FWD) nw = 16;
   return nw;
 }
 
@@ -788,17 +792,18 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
 #define OAC_GS(NW_, G_) \
   if (nw == NW_ && gpw == G_ && !stg) { \
     if (shm > 64 * 1024) { \
-      static const bool attr_set = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_small_kernel<NW_, G_, false>), \
-          hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytesPerCu) == hipSuccess; \
-      (void)attr_set; } \
+      const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_small_kernel<NW_, G_, false>), \
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm); \
+      if (ea != hipSuccess) return ea; } \
     OAC_LAUNCH((gemm_small_kernel<NW_, G_, false>), dim3(grid), dim3(64 * NW_), shm, s, h.total_tiles, h.publish, \
                h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b); \
     return hipGetLastError(); }
 #define OAC_GSS(NW_, G_) \
   if (nw == NW_ && gpw == G_ && stg) { \
-    static const bool attr_set = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_small_kernel<NW_, G_, true>), \
-        hipFuncAttributeMaxDynamicSharedMemorySize, kLdsBytesPerCu) == hipSuccess; \
-    (void)attr_set; \
+    if (shm > 64 * 1024) { \
+      const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_small_kernel<NW_, G_, true>), \
+          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm); \
+      if (ea != hipSuccess) return ea; } \
     OAC_LAUNCH((gemm_small_kernel<NW_, G_, true>), dim3(grid), dim3(64 * NW_), shm, s, h.total_tiles, h.publish, \
                h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b); \
     return hipGetLastError(); }
