@@ -976,6 +976,17 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
     __syncthreads();
   }
   EXPL_CLK(7);
+  // S3's per-lane terms that need no other workgroup's parts -- the action,
+  // std, mean and the exploration draw -- ahead of the arrival in every
+  // workgroup's wave 0 (whichever arrives last goes on with them in registers)
+  float p_act = 0.f, p_sd = 0.f, p_mean = 0.f, p_ev = 0.f;
+  if (wave == 0 && lane < Da) {
+    p_act = x[Do + lane];
+    p_sd = expf(fminf(fmaxf(head[Da + lane], -20.f), 2.f));
+    p_mean = head[lane];
+    p_ev = a.eps ? a.eps[(long)r * Da + lane]
+                 : philox_normal(a.seed, (unsigned long long)cnt_s, 3u, (unsigned)(r * Da + lane));
+  }
   // ---- arrival B: the last workgroup of the group goes on to S3.  The add
   // carries this workgroup's hand-off failure in bit 16, so the last arrival
   // learns every member's from the value its add returns.
@@ -1042,14 +1053,8 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
   const float da = seed0 * v0 + seed1 * v1;
   EXPL_CLK3(10);
   // grad, shift, sample (Da <= 32), the norm as a wave sum
-  float g = 0.f, sig = 0.f, sd = 0.f, mean = 0.f;
-  if (lane < Da) {
-    const float act = x[Do + lane];
-    g = da * (1.f - act * act);
-    sd = expf(fminf(fmaxf(head[Da + lane], -20.f), 2.f));
-    sig = sd * sd;
-    mean = head[lane];
-  }
+  const float sd = p_sd, sig = p_sd * p_sd, mean = p_mean, ev = p_ev;
+  const float g = lane < Da ? da * (1.f - p_act * p_act) : 0.f;
   const float nrm = sqrtf(wsum64(lane < Da ? g * g * sig : 0.f)) + 10e-6f;
   // the call's only group with a host-polled completion word: the outputs
   // (host memory) as system-scope stores, drained, then the word -- no ticket
@@ -1059,8 +1064,6 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
     if (lane < Da) {
       const float mu_C = (a.sqrt_2delta * (sig * g)) / nrm;
       const float mu_E = mean + mu_C;
-      const float ev = a.eps ? a.eps[lane]
-                             : philox_normal(a.seed, (unsigned long long)cnt_s, 3u, (unsigned)lane);
       const float nan = __int_as_float(0x7fc00000);
       put_tagged(a.tags + lane, ok ? tanhf(__fadd_rn(__fmul_rn(ev, sd), mu_E)) : nan, tag);
       put_tagged(a.tags + Da + lane, ok ? mu_E : nan, tag);
@@ -1079,8 +1082,6 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
     const long e = (long)r * Da + lane;
     const float mu_C = (a.sqrt_2delta * (sig * g)) / nrm;
     const float mu_E = mean + mu_C;
-    const float ev = a.eps ? a.eps[e]
-                           : philox_normal(a.seed, (unsigned long long)cnt_s, 3u, (unsigned)(r * Da + lane));
     const long nd = (long)a.n * Da;
     const float nan = __int_as_float(0x7fc00000);
     const float o0 = ok ? tanhf(__fadd_rn(__fmul_rn(ev, sd), mu_E)) : nan, o1 = ok ? mu_E : nan;

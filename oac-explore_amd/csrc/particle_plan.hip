@@ -79,9 +79,18 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
   const int Dq = Do + Da;
   float* X = p.W(OAC_WS_BATCH);
-  const float* obs = X + c.off_obs;
-  const float* nobs = X + c.off_next_obs;
-  if (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS)) {
+  // direct gather at large batch (as the SAC step's, sac_plan.hip phase0): the
+  // layer-0 launch's LDS-DMA tiles read their rows straight from the replay
+  // through the step's index slot, side workgroups of that launch draw eps,
+  // and the batch copy (first read by the targets kernel) rides in the target
+  // critic's layer-1 launch -- no gather launch
+  const bool direct_big = big_direct_ok(p) && (flags & OAC_STEP_GATHER) && p.b.ring_slots > 0;
+  p.direct_big = direct_big;
+  p.direct_ring = gather_idx(p, flags);
+  const float* R0 = direct_big ? p.b.replay : X;
+  const float* obs = R0 + c.off_obs;
+  const float* nobs = R0 + c.off_next_obs;
+  if (!direct_big && (flags & (OAC_STEP_GATHER | OAC_STEP_DEVICE_EPS))) {
     GatherArgs g;
     std::memset(&g, 0, sizeof(g));
     g.replay = p.b.replay; g.row_stride = RS; g.idx = gather_idx(p, flags); g.ring_slots = p.b.ring_slots;
@@ -109,10 +118,19 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
     gb.publish = p.state(); gb.pub_beta1 = c.beta1; gb.pub_beta2 = c.beta2;   // step's Adam constants
     add(gb, t_fwd(nobs, RS, B, Do, pol + L.pol_fc0_w, Do, H, p.W(X_H1P2), H, EPI_BIAS_RELU, pol + L.pol_fc0_b));
     GemmTask t = t_fwd(obs, RS, B, Do, q + L.q_fc0_w, Dq, H, p.W(X_P), H, EPI_BIAS_RANK_RELU, q + L.q_fc0_b);
-    t.U = X + c.off_act; t.ldu = RS; t.V = q + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
+    t.U = R0 + c.off_act; t.ldu = RS; t.V = q + L.q_fc0_w + Do; t.ldv = Dq; t.R = Da;
     t.C2 = p.W(X_H1Q); t.ldc2 = H;
     add(gb, t);
     add(gb, t_fwd(nobs, RS, B, Do, tq + L.q_fc0_w, Dq, H, p.W(X_PT), H, EPI_BIAS, tq + L.q_fc0_b));
+    if (direct_big) {
+      for (int i = 0; i < gb.ntasks; ++i) gb.t[i].a_rows = 1;
+      RowGather& g = gb.rg;
+      g.ring = p.direct_ring; g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
+      if (flags & OAC_STEP_DEVICE_EPS) {   // 512 tiles of 128 x 64: a free slot per CU
+        g.eps1 = p.W(OAC_WS_EPS1); g.eps2 = p.W(OAC_WS_EPS2); g.n_eps = B * Da; g.seed = c.seed;
+        g.blocks = 256;
+      }
+    }
     if (run_gemm(p, gb, s)) return 1;
   }
   {
@@ -159,6 +177,12 @@ static int pphase1(SacPlan& p, int flags, hipStream_t s) {
   {  // target critic layer 1 (its layer 0 finished in the head launch)
     GemmBatch gb{};
     add(gb, t_fwd(p.W(X_H1T), H, B, H, tq + L.q_fc1_w, H, H, p.W(X_H2T), H, EPI_BIAS_RELU, tq + L.q_fc1_b));
+    if (p.direct_big) {   // the direct-gather step's batch copy: 256 tiles, a free slot per CU
+      RowGather& g = gb.rg;
+      g.ring = p.direct_ring; g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
+      g.replay = p.b.replay; g.row_stride = RS; g.out = X;
+      g.blocks = 256;
+    }
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // the target critic's K-output last layer runs inside the targets kernel (row_heads)

@@ -91,7 +91,11 @@ def test_dropin_rejects_out_of_range_indices():
 def _kind_trainer(kind, dropin):
     from fixtures_lib import goac_params
     from gpu_helpers import producers, Space
-    Hh = 32
+    # hidden 64 at B=1024: the direct large-batch gather (layer-0 tiles read the
+    # replay rows through the index slot, side workgroups draw eps and copy the
+    # batch -- sac_plan.h big_direct_ok); hidden 32 keeps the gather launch
+    Hh = 64 if kind.endswith("_direct") else 32
+    kind = kind.replace("_direct", "")
     if kind == "sac_large":
         from oac_amd import SACTrainer
         pp, qp = producers(sac_params(Do, Da, [Hh, Hh], 3, pi_init_w=0.2, q_init_w=0.1))
@@ -117,11 +121,12 @@ def _kind_trainer(kind, dropin):
     return tr
 
 
-@pytest.mark.parametrize("kind", ["sac_large", "poac", "goac"])
+@pytest.mark.parametrize("kind", ["sac_large", "sac_large_direct", "poac", "poac_direct", "goac"])
 def test_host_read_dropin_equals_device_index_path(kind):
     from oac_amd import ReplayBuffer
     from gpu_helpers import Space
-    Bk, Nk, steps = (1024, 3000, 136) if kind == "sac_large" else (B, N, 140)
+    Bk, Nk, steps = (1024, 3000, 136) if kind.startswith("sac_large") or kind.endswith("_direct") \
+        else (B, N, 140)
 
     def run(dropin):
         tr = _kind_trainer(kind, dropin)
