@@ -398,15 +398,9 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   // workgroups that copy the batch / draw eps (rg): only the small kernel and
   // gemm_fwd implement them -- any other kernel would read replay rows 0..M-1
   // and leave the batch copy and eps unwritten
-  bool gathers = b.rg.ring != nullptr, small_only = false;
-  for (int i = 0; i < b.ntasks; ++i) {
-    gathers = gathers || b.t[i].a_rows;
-    // the computed head-backward operand and the da-part epilogue: small kernel only
-    small_only = small_only || b.t[i].a_mode == A_HEAD_BWD || b.t[i].a_mode == A_HEAD_FWD ||
-                 b.t[i].epi == EPI_MASK_DA;
-  }
+  bool gathers = b.rg.ring != nullptr;
+  for (int i = 0; i < b.ntasks; ++i) gathers = gathers || b.t[i].a_rows;
   if (gathers && cfg != 0 && (cfg < 6 || cfg > 8)) return hipErrorInvalidValue;
-  if (small_only && cfg != 0) return hipErrorInvalidValue;
   if (cfg == 0) return gemm_small_launch(b, s);
   if (b.fuse_adam) return hipErrorInvalidValue;   // fused optimizer: small-batch kernel only
   for (int i = 0; i < b.ntasks; ++i) {             // dual products / head backward: small kernel

@@ -18,10 +18,8 @@
 #include "adam_common.h"
 #include "policy_math.h"
 #include "gemm_operand.h"
-#include "gemm_pipe.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace oac {
 
@@ -35,50 +33,12 @@ __device__ long long g_gs_clock[4096 * 8];
 #define GS_STAGE(i)
 #endif
 
-// Staged k-contiguous operands (STG kernels): the workgroup's 32 operand rows
-// over [kst, k_hi) are copied into LDS by LDS-DMA (global_load_lds_dwordx4,
-// gemm_pipe.h glds16) before the k loop -- 8 lanes per 128-byte line, where a
-// fragment-shaped 16-byte load per lane touches one line per lane (64 per
-// wave instruction) -- and the k loop reads its fragments from the image.
-// Row stride S floats, S = 4 (mod 64): the 32 rows' 16-byte fragment reads
-// at one k start on 32 distinct 4-bank groups, half-waves 4 floats apart.
-__host__ __device__ inline int stage_stride(int span) {
-  const int s = (span + 7) & ~7;   // fragment reads reach the next multiple of 8
-  return s + ((4 - s) & 63);
-}
-
-// rows r = 0..31 of operand X(m0 + r, k) = base[row(r) * ld + k], k in
-// [kst, k_hi), into img[r * S + (k - kst)]; row(r) = rows[r] (the direct
-// gather's tile rows) or min(m0 + r, M - 1).  Issued by every wave; the
-// caller waits (vmcnt(0)) and meets at a barrier before reading the image.
-template <int NW>
-__device__ __forceinline__ void stage_kc(const float* base, long ld, const int* rows, int m0, int M,
-                                         int kst, int k_hi, float* img, int S) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nch = (k_hi - kst + 3) >> 2;   // 16-byte chunks per row
-  const int nq = (nch + 63) >> 6;          // wave instructions per row
-#pragma unroll 1
-  for (int it = wave; it < 32 * nq; it += NW) {
-    const int r = it / nq, q = it - r * nq;
-    const long row = rows ? (long)rows[r] : (long)min(m0 + r, M - 1);
-    const int c = 64 * q + lane;
-    if (c < nch) glds16(base + row * ld + kst + 4 * c, img + r * S + 256 * q);
-  }
-}
-
-struct Stage { const float* img; int S; int kst; };
-
-constexpr int kHeadParts = 16;   // A_HEAD_BWD: parts of dL/da summed per row (<= 16)
-
 // acc += A[m0.., k_lo..k_hi) . B[k_lo..k_hi), n0..]  for this wave's k-groups
 // arow >= 0: this lane's A row is buffer row arow (the direct gather's index,
 // loaded by the caller ahead of everything else)
-// SA / SB: the operand's fragments come from its LDS image (KC kinds only)
-template <int NW, int AK, int BK, int GPW = (NW >= 16 ? 4 : 5), bool SA = false, bool SB = false>
+template <int NW, int AK, int BK, int GPW = (NW >= 16 ? 4 : 5)>
 __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
-                                       floatx16& acc, int arow = -1, Stage sa = Stage{},
-                                       Stage sb = Stage{}) {
+                                       floatx16& acc, int arow = -1) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   const int l32 = lane & 31;
@@ -94,8 +54,6 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
   const int g_lo = k_lo >> 3;                 // k_lo is a multiple of 8 (kchunk % 8 == 0)
   const int g_hi = (k_hi + 7) >> 3;
   const int kmax = k_hi - 1;
-  const float* fa = sa.img + l32 * sa.S - sa.kst;   // SA: this lane's image row (k-indexed)
-  const float* fb = sb.img + l32 * sb.S - sb.kst;
 #pragma unroll 1
   for (int g0 = g_lo + wave; g0 < g_hi; g0 += kGPW * NW) {
     float ax[kGPW][4], ay[kGPW][4], bx[kGPW][4], by[kGPW][4];
@@ -103,22 +61,8 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
     for (int j = 0; j < kGPW; ++j)
       if (g0 + j * NW < g_hi) {
         const int kb = 8 * (g0 + j * NW) + 4 * half;
-        if (SB) {
-          const f4u v = *reinterpret_cast<const f4u*>(fb + kb);
-          bx[j][0] = v.x; bx[j][1] = v.y; bx[j][2] = v.z; bx[j][3] = v.w;
-        } else {
-          load4<BK>(lb, kb, kmax, bx[j], by[j]);   // B first: it never waits on a row index
-        }
-        if (SA) {
-          const f4u v = *reinterpret_cast<const f4u*>(fa + kb);
-          ax[j][0] = v.x; ax[j][1] = v.y; ax[j][2] = v.z; ax[j][3] = v.w;
-          if (AK == OP_KC_R1) {   // the rank-1 factor v[k]: one (broadcast) 16-byte load
-            const f4u w = *reinterpret_cast<const f4u*>(la.s + kb);
-            ay[j][0] = w.x; ay[j][1] = w.y; ay[j][2] = w.z; ay[j][3] = w.w;
-          }
-        } else {
-          load4<AK>(la, kb, kmax, ax[j], ay[j]);
-        }
+        load4<BK>(lb, kb, kmax, bx[j], by[j]);   // B first: it never waits on a row index
+        load4<AK>(la, kb, kmax, ax[j], ay[j]);
       }
 #pragma unroll
     for (int j = 0; j < kGPW; ++j)
@@ -134,139 +78,15 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
   }
 }
 
-template <int NW, int GPW, bool STG>
+template <int NW, int GPW>
 __device__ __forceinline__ void k_dispatch(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
-                                           floatx16& acc, int arow, Stage sa, Stage sb) {
+                                           floatx16& acc, int arow) {
   const bool r1 = t.a_mode == A_RANK1_MASK;
-  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW, STG, STG>(t, m0, n0, k_lo, k_hi, acc, arow, sa, sb);   // forward
-  else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN, GPW, STG>(t, m0, n0, k_lo, k_hi, acc, -1, sa);      // dX
-  else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN, GPW, STG>(t, m0, n0, k_lo, k_hi, acc, -1, sa);   // dX, rank-1 seed
+  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW>(t, m0, n0, k_lo, k_hi, acc, arow);   // forward
+  else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dX
+  else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dX, rank-1 seed
   else if (!r1)                k_loop<NW, OP_MN, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dW
   else                         k_loop<NW, OP_MN_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dW, rank-1 seed
-}
-
-// ---------------------------------------------------------------------------
-// A_HEAD_FWD: the fresh-action critic layer 1's A operand computed per 32-row
-// block inside the tile (what policy_head_kernel, head.hip, did as a launch of
-// its own): (1) the stacked heads [mean | ls_raw] = h2 . W_head^T for the 32
-// rows on v_mfma_f32_16x16x4_f32 (2 row x NTc column tiles of 16, K halved
-// over two waves, halves added in order), (2) the tanh-Gaussian sample and
-// log-prob (policy_math.h, one half-wave per row), (3) the critic's layer 0 on
-// the actions, h1 = relu(P + sum_j a_j W0[:, Do + j]) for all H columns, into
-// the LDS image the k loop reads.  Every tile of a row block computes the same
-// values in the same order; the writing task's n0 == 0 tiles store them.
-// LDS (floats): image [32][S] | head partials [2][8][256] | Y [32][65] |
-// act [32][33] | lp [32] | W0[:, Do:]^T [32][H]
-constexpr int kHfPart = 2 * 8 * 256, kHfY = 32 * 65, kHfAct = 32 * 33;
-__host__ __device__ inline int head_fwd_floats(int H) {
-  return 32 * stage_stride(H) + kHfPart + kHfY + kHfAct + 32 + 32 * H;
-}
-
-template <int NW>
-__device__ __forceinline__ void head_fwd_image(const GemmBatch& batch, const GemmTask& t, int m0,
-                                               int n0, float* lds) {
-  const HeadFwd& hf = batch.hf[t.a_aux & 1];
-  const bool wr = (t.a_aux & 2) && n0 == 0;
-  const int H = t.K, Da = hf.Da, D2 = 2 * Da, M = t.M;
-  const int S = stage_stride(H);
-  float* img = lds;
-  float* part = img + 32 * S;
-  float* Y = part + kHfPart;
-  float* act = Y + kHfY;
-  float* lp = act + kHfAct;
-  float* waT = lp + 32;                      // [Da][H]
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int l16 = lane & 15, g4 = lane >> 4;
-  const int ntc = (D2 + 15) >> 4;            // head column tiles of 16 (<= 4)
-  const int items = 2 * 2 * ntc;             // (row tile, column tile, k half)
-  // (1) heads: wave w < items takes one (row tile, column tile, k half)
-  typedef float floatx4 __attribute__((ext_vector_type(4)));
-  if (wave < items) {
-    const int kh = wave / (2 * ntc), tile = wave - kh * 2 * ntc;
-    const int rt = tile / ntc, ct = tile - rt * ntc;
-    const float* arow = hf.h2 + (long)min(m0 + 16 * rt + l16, M - 1) * H;
-    const int bc = 16 * ct + l16;
-    const float* brow = hf.wh + (long)min(bc, D2 - 1) * H;
-    const int k0 = kh * (H >> 1), nch = (H >> 1) >> 4;   // 16-k chunks of the half
-    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
-    constexpr int U = 8;   // chunks in flight
-#pragma unroll 1
-    for (int c0 = 0; c0 < nch; c0 += U) {
-      f4u xa[U], xb[U];
-#pragma unroll
-      for (int c = 0; c < U; ++c) {
-        const int kb = k0 + 16 * min(c0 + c, nch - 1) + 4 * g4;
-        xa[c] = *reinterpret_cast<const f4u*>(arow + kb);
-        xb[c] = *reinterpret_cast<const f4u*>(brow + kb);
-      }
-#pragma unroll
-      for (int c = 0; c < U; ++c)
-        if (c0 + c < nch) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[c][j], bc < D2 ? xb[c][j] : 0.f, acc, 0, 0, 0);
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) part[(kh * 8 + tile) * 256 + r * 64 + lane] = acc[r];
-  }
-  // (3)'s W0[:, Do:] transposed into LDS (row n of W0 at a_v + n ld_mask)
-  constexpr int kNT = 64 * NW;
-  for (int e = threadIdx.x; e < H * Da; e += kNT) {
-    const int nn = e / Da, j = e - nn * Da;
-    waT[j * H + nn] = t.a_v[(long)nn * t.ld_mask + j];
-  }
-  const int n = threadIdx.x % H, r0 = threadIdx.x / H, rstep = kNT / H;   // (kNT % H == 0: launcher)
-  __syncthreads();
-  // Y = the two k halves in order + bias (D reg r: row 4 (l >> 4) + r, col l & 15)
-  for (int e = threadIdx.x; e < 2 * ntc * 256; e += kNT) {
-    const int tile = e >> 8, r = (e >> 6) & 3, l = e & 63;
-    const int rt = tile / ntc, ct = tile - rt * ntc;
-    const int row = 16 * rt + 4 * (l >> 4) + r, col = 16 * ct + (l & 15);
-    if (col < D2)
-      Y[row * 65 + col] = (part[tile * 256 + r * 64 + l] + part[(8 + tile) * 256 + r * 64 + l]) + hf.bh[col];
-  }
-  __syncthreads();
-  // (2) sample + log-prob: one half-wave per row, lane j = action dim
-  for (int e = threadIdx.x; e < 32 * 32; e += kNT) {
-    const int row = e >> 5, j = e & 31, m = m0 + row;
-    float l = 0.f, a = 0.f;
-    if (m < M && j < Da) {
-      float sd, u;
-      l = tanh_gauss_sample(Y[row * 65 + j], Y[row * 65 + Da + j], hf.eps[(long)m * Da + j], a, sd, u);
-      if (wr) {
-        const long o = (long)m * Da + j;
-        hf.act[o] = a; hf.stdv[o] = sd; hf.u[o] = u;
-        hf.head[(long)m * D2 + j] = Y[row * 65 + j];
-        hf.head[(long)m * D2 + Da + j] = Y[row * 65 + Da + j];
-      }
-    }
-    act[row * 33 + j] = a;
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) l += __shfl_xor(l, o, 32);
-    if (j == 0) {
-      lp[row] = m < M ? l + hf.te : 0.f;
-      if (wr && m < M) hf.logp[m] = l;
-    }
-  }
-  __syncthreads();
-  if (wr && hf.logp_part && threadIdx.x < 2 && m0 + 16 * threadIdx.x < M) {   // data-parallel alpha
-    float sum = 0.f;
-    for (int r = 0; r < 16; ++r) sum += lp[16 * threadIdx.x + r];
-    hf.logp_part[(m0 >> 4) + threadIdx.x] = sum;
-  }
-  // (3) h1 = relu(P + sum_j a_j W0[n, Do + j]) for the 32 rows, column n
-  float* U = const_cast<float*>(t.U);
-  for (int r = r0; r < 32; r += rstep) {
-    const int m = min(m0 + r, M - 1);
-    float sacc = t.A[(long)m * t.lda + n];
-    for (int j = 0; j < Da; ++j) sacc = fmaf(act[r * 33 + j], waT[j * H + n], sacc);
-    const float h = fmaxf(sacc, 0.f);
-    img[r * S + n] = h;
-    if (U && n0 == 0 && m0 + r < M) U[(long)(m0 + r) * t.ldu + n] = h;
-  }
-  __syncthreads();
 }
 
 // Epilogue operands of one output element, loaded before the k loop so their
@@ -300,7 +120,7 @@ __device__ __forceinline__ EpiIn epi_prefetch(const GemmBatch& batch, const Gemm
       x.xb = t.bias[nc]; break;
     case EPI_BIAS_RELU_DOT:
       x.xb = t.bias[nc]; x.xa = t.aux[nc]; break;
-    case EPI_ADD_RELU: case EPI_MASK: case EPI_MASK_DA:
+    case EPI_ADD_RELU: case EPI_MASK:
       x.xa = t.aux[(long)mc * t.ld_aux + nc]; break;
     default: break;
   }
@@ -341,7 +161,7 @@ __device__ __forceinline__ void epi_one(const GemmBatch& batch, const AdamConsts
       break;
     }
     case EPI_ADD_RELU: t.C[o] = fmaxf(acc + x.xa, 0.f); break;
-    case EPI_MASK: case EPI_MASK_DA: t.C[o] = x.xa > 0.f ? acc : 0.f; break;
+    case EPI_MASK: t.C[o] = x.xa > 0.f ? acc : 0.f; break;
     case EPI_HEAD_BWD: {
       float dmean, dls;
       tanh_gauss_backward(acc, x.xb, x.xa, x.am, x.av, x.at, x.s * (1.f / (float)t.M), dmean, dls);
@@ -379,25 +199,7 @@ struct SmallLds {
 
 constexpr int kGatherU = 4;   // float4s per lane of a side block's row copy (rows <= 1 KB)
 
-// the direct gather's 32 tile rows (their own LDS object: the launch's
-// dynamic LDS holds the staged images and the reduction)
-__device__ __forceinline__ int* tile_rows_of(float*) {
-  __shared__ int tile_rows[32];
-  return tile_rows;
-}
-
-// LDS floats the STG kernel's images take for one task (0: nothing staged)
-__host__ __device__ inline int head_fwd_floats(int H);
-__host__ __device__ inline int stage_floats(const GemmTask& t) {
-  if (t.a_mode == A_HEAD_FWD) return head_fwd_floats(t.K) + 32 * stage_stride(t.K);   // image + B
-  if (!t.a_kc || t.ksplit > 1 || t.a_mode == A_HEAD_BWD) return 0;
-  int n = 32 * stage_stride(t.K);                       // A (or A's ReLU mask)
-  if (t.b_kc) n += 32 * stage_stride(t.K);              // B of a forward product
-  if (t.K2 > 0) n += 32 * stage_stride(t.K2);           // the second product's A
-  return n;
-}
-
-template <int NW, int GPW, bool STG = false>
+template <int NW, int GPW>
 __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int publish, int tb1,
                                                  int tb2, int tb3, int tb4, int tb5, int tb6,
                                                  int tb7, const GemmBatch& batch, float* red) {
@@ -484,36 +286,12 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   // through LDS -- one host request per workgroup, not one per wave
   int arow = -1;
   if (t.a_rows && rows) {
-    int* tile_rows = tile_rows_of(red);
+    __shared__ int tile_rows[32];
     if (wave == 0 && lane < 32) tile_rows[lane] = rows[min(m0 + lane, t.M - 1)];
     __syncthreads();
     arow = tile_rows[lane & 31];
   }
 
-  // STG: the k-contiguous operands' 32 rows into LDS images first (their
-  // DMA overlaps the epilogue prefetch below)
-  const bool hbw = t.a_mode == A_HEAD_BWD;   // A computed below, not loaded
-  const bool hfw = t.a_mode == A_HEAD_FWD;   // A computed below, B staged by LDS-DMA
-  const bool stg = STG && t.a_kc && t.ksplit <= 1 && !hbw && !hfw;
-  Stage sa{}, sb{}, sa2{};
-  if (stg) {
-    const bool ar1 = t.a_mode == A_RANK1_MASK;
-    const int S = stage_stride(t.K);
-    sa = Stage{red, S, k_lo};
-    stage_kc<NW>(ar1 ? t.a_mask : t.A, ar1 ? t.ld_mask : t.lda, arow >= 0 ? tile_rows_of(red) : nullptr,
-                 m0, t.M, k_lo, k_hi, red, S);
-    float* nxt = red + 32 * S;
-    if (t.b_kc) {
-      sb = Stage{nxt, S, k_lo};
-      stage_kc<NW>(t.B, t.ldb, nullptr, n0, t.N, k_lo, k_hi, nxt, S);
-      nxt += 32 * S;
-    }
-    if (t.K2 > 0) {
-      const int S2 = stage_stride(t.K2);
-      sa2 = Stage{nxt, S2, 0};
-      stage_kc<NW>(t.A2, t.lda, nullptr, m0, t.M, 0, t.K2, nxt, S2);
-    }
-  }
   EpiIn xin[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -521,80 +299,15 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     const int r = e >> 6, l = e & 63;
     xin[i] = epi_prefetch(batch, t, m0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), n0 + (l & 31));
   }
-  // EPI_MASK_DA: the tile's rows of V (the next product's weights) requested
-  // now, used after the epilogue
-  constexpr int VPF = (1024 + 64 * NW - 1) / (64 * NW);   // 32 rows x R <= 32 per thread
-  float vpf[VPF];
-  if (t.epi == EPI_MASK_DA) {
-#pragma unroll
-    for (int q = 0; q < VPF; ++q) {
-      const int e = threadIdx.x + q * 64 * NW;
-      const int n = e / t.R, j = e - n * t.R;
-      vpf[q] = (e < 32 * t.R && n0 + n < t.N) ? t.V[(long)(n0 + n) * t.ldv + j] : 0.f;
-    }
-  }
-  if (stg) {   // every wave's DMA landed, then the images are complete for all
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  if (hfw) {
-    // B (the critic's layer-1 rows) into LDS behind the image, its DMA in
-    // flight while the heads, the sample and h1 are computed
-    const int S = stage_stride(t.K);
-    float* bimg = red + head_fwd_floats(t.K);
-    stage_kc<NW>(t.B, t.ldb, nullptr, n0, t.N, 0, t.K, bimg, S);
-    head_fwd_image<NW>(batch, t, m0, n0, red);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    k_loop<NW, OP_KC, OP_KC, GPW, true, true>(t, m0, n0, 0, t.K, acc, -1, Stage{red, S, 0},
-                                             Stage{bimg, S, 0});
-  } else if (hbw) {
-    // A = [dmean | dls_raw] of the tile's 32 rows from the parts of dL/da
-    // (an EPI_MASK_DA launch wrote them), the head backward of EPI_HEAD_BWD:
-    // into an LDS image read by the k loop like a staged operand
-    const int Da = t.K >> 1, S = stage_stride(t.K);
-    const float G = (t.ex[5] ? t.ex[5][0] : 0.f) * (1.f / (float)t.M);
-    for (int e = threadIdx.x; e < 32 * Da; e += 64 * NW) {
-      const int r = e / Da, j = e - r * Da;
-      const int m = min(m0 + r, t.M - 1);
-      const long o = (long)m * Da + j;
-      // every part's load issued unconditionally (clamped part index): a
-      // load behind a runtime condition is waited for one at a time
-      float pv[kHeadParts];
-#pragma unroll
-      for (int q = 0; q < kHeadParts; ++q) pv[q] = t.A[min(q, t.R - 1) * t.lda + o];
-      float da = pv[0];
-#pragma unroll
-      for (int q = 1; q < kHeadParts; ++q)
-        if (q < t.R) da += pv[q];
-      float dmean, dls;
-      tanh_gauss_backward(da, t.ex[0][o], t.ex[1][o], t.ex[2][o], t.ex[3][o],
-                          t.ex[4][(long)m * 2 * Da + Da + j], G, dmean, dls);
-      red[r * S + j] = dmean;
-      red[r * S + Da + j] = dls;
-      if (n0 == 0 && t.U && m0 + r < t.M) {   // dhead for the head's weight gradient (next launch)
-        float* u = const_cast<float*>(t.U) + (long)m * t.ldu;
-        u[j] = dmean;
-        u[Da + j] = dls;
-      }
-    }
-    __syncthreads();
-    k_loop<NW, OP_KC, OP_MN, GPW, true>(t, m0, n0, 0, t.K, acc, -1, Stage{red, S, 0});
-  } else if (stg) {
-    k_dispatch<NW, GPW, true>(t, m0, n0, k_lo, k_hi, acc, arow, sa, sb);
-  } else {
-    k_dispatch<NW, GPW, false>(t, m0, n0, k_lo, k_hi, acc, arow, sa, sb);
-  }
+  k_dispatch<NW, GPW>(t, m0, n0, k_lo, k_hi, acc, arow);
   if (t.K2 > 0) {   // second product into the same accumulator (unsplit dX tasks only)
     GemmTask t2 = t;
     t2.A = t.A2; t2.B = t.B2; t2.K = t.K2;
-    if (stg) k_loop<NW, OP_KC, OP_MN, GPW, true>(t2, m0, n0, 0, t.K2, acc, -1, sa2);
-    else k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc);
+    k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc);
   }
-  if (stg || hbw || hfw) __syncthreads();   // the images are read by all waves before the reduction reuses the LDS
 
   GS_STAGE(2);
   // fixed-order split-K reduction through LDS
@@ -646,49 +359,18 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
       if (nt == 0 && m < t.M) t.C2[(long)(n0 >> 5) * t.ldc2 + m] = x;   // tile-major
     }
   }
-  if (t.epi == EPI_MASK_DA) {
-    // the tile's part of C . V[:, :R]: the masked tile and V's 32 rows in LDS,
-    // one thread per (row, j), the 32 columns in order
-    __syncthreads();   // (the LDS held the reduction)
-    float* ct = red;             // [32][33]
-    float* vb = red + 32 * 33;   // [32][R]
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int e = threadIdx.x + i * 64 * NW;
-      const int r = e >> 6, l = e & 63;
-      const int mt = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), nt = l & 31;
-      const bool in = m0 + mt < t.M && n0 + nt < t.N;
-      ct[mt * 33 + nt] = (in && xin[i].xa > 0.f) ? vals[i] : 0.f;
-    }
-#pragma unroll
-    for (int q = 0; q < VPF; ++q) {
-      const int e = threadIdx.x + q * 64 * NW;
-      if (e < 32 * t.R) vb[e] = vpf[q];
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 32 * t.R; e += 64 * NW) {
-      const int r = e / t.R, j = e - r * t.R;
-      float sacc = 0.f;
-#pragma unroll 8
-      for (int n = 0; n < 32; ++n) sacc = fmaf(ct[r * 33 + n], vb[n * t.R + j], sacc);
-      if (m0 + r < t.M) t.C2[(long)(n0 >> 5) * t.ldc2 + (long)(m0 + r) * t.R + j] = sacc;
-    }
-  }
   if (batch.fuse_adam && bid == 0 && threadIdx.x == 0)
     step_bookkeeping(batch.adam.state, batch.adam.alpha, batch.adam.advance);
   GS_STAGE(4);
 }
 
-// 8- and 16-wave workgroups: 4 waves per SIMD (<= 128 VGPRs), so two 8-wave
-// workgroups share a CU past 256 tiles (fewer waves: no bound, their many
-// epilogue elements per thread would spill)
-template <int NW, int GPW, bool STG>
-__global__ void __launch_bounds__(64 * NW, NW >= 8 ? 4 : 1)
+template <int NW, int GPW>
+__global__ void __launch_bounds__(64 * NW)
 gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6,
                   int tb7, const GemmBatch batch) {
-  extern __shared__ __attribute__((aligned(16))) float red[];   // SmallLds<NW>::N or the images
-  gemm_small_block<NW, GPW, STG>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6,
-                                 tb7, batch, red);
+  __shared__ __attribute__((aligned(16))) float red[SmallLds<NW>::N];
+  gemm_small_block<NW, GPW>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6, tb7,
+                            batch, red);
 }
 
 // tile geometry shared with the plan builder
@@ -704,8 +386,6 @@ int gemm_small_waves(const GemmBatch& b) {
   // a 16-wave workgroup holds a whole CU (VGPRs); past 256 tiles the grid
   // would run in two rounds, so take 8 waves (two workgroups per CU)
   if (nw == 16 && b.total_tiles > 256) nw = 8;
-  for (int i = 0; i < b.ntasks; ++i)   // the computed fresh-action operand takes 16 waves
-    if (b.t[i].a_mode == A_HEAD_FWD) nw = 16;
   return nw;
 }
 
@@ -721,37 +401,15 @@ void gemm_small_finalize(GemmBatch& b) {
   b.total_tiles = tiles;
 }
 
-static int SmallLdsFloats(int nw) {
-  switch (nw) {
-    case 1: return SmallLds<1>::N;
-    case 2: return SmallLds<2>::N;
-    case 4: return SmallLds<4>::N;
-    case 8: return SmallLds<8>::N;
-    default: return SmallLds<16>::N;
-  }
-}
-constexpr int kLdsBytesPerCu = 160 * 1024;
-static bool small_stage_on() {
-  static const bool on = [] { const char* e = getenv("OAC_SMALL_STAGE"); return e && atoi(e) == 1; }();
-  return on;
-}
-
 hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   if (b0.total_tiles <= 0) return hipSuccess;
   GemmBatch b = b0;
-  for (int i = 0; i < b.ntasks; ++i) {   // second products: plain unsplit dX tasks
-    const GemmTask& t = b.t[i];
-    if (t.K2 > 0 && (t.ksplit > 1 || !t.a_kc || t.b_kc || t.a_mode != A_PLAIN))
+  for (int i = 0; i < b.ntasks; ++i)   // second products: plain unsplit dX tasks
+    if (b.t[i].K2 > 0 && (b.t[i].ksplit > 1 || !b.t[i].a_kc || b.t[i].b_kc ||
+                          b.t[i].a_mode != A_PLAIN))
       return hipErrorInvalidValue;
-    // the computed head-backward operand: an unsplit dX with K = 2 Da, <= kHeadParts parts
-    if (t.a_mode == A_HEAD_BWD && (!t.a_kc || t.b_kc || t.ksplit > 1 || (t.K & 1) || t.K2 > 0 ||
-                                    t.R < 1 || t.R > kHeadParts || 32 * stage_stride(t.K) > 2 * 32 * 65))
-      return hipErrorInvalidValue;
-    if (t.epi == EPI_MASK_DA && (t.R < 1 || t.R > 32 || t.ksplit > 1 || !t.C2 || !t.V))
-      return hipErrorInvalidValue;
-  }
   const int nw = b.force_nw > 0 ? b.force_nw : gemm_small_waves(b);
-  int gpw = b.force_gpw > 0 ? b.force_gpw : (nw >= 16 ? 4 : 5);
+  const int gpw = b.force_gpw > 0 ? b.force_gpw : (nw >= 16 ? 4 : 5);
   b.adam_blocks = 0;
   if (b.fuse_adam) {
     long n4 = 0;
@@ -764,52 +422,11 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   }
   const int grid = b.total_tiles + b.adam_blocks + (b.rg.ring ? b.rg.blocks : 0);
   const GemmHead h = gemm_head(b);
-  // staged k-contiguous operands (OAC_SMALL_STAGE=1): when the images fit
-  // beside the workgroups per CU the grid needs (1 at >= 16 waves)
-  int lds = SmallLdsFloats(nw);
-  for (int i = 0; i < b.ntasks; ++i) {   // the computed fresh-action operand: 16 waves, its LDS
-    const GemmTask& t = b.t[i];
-    if (t.a_mode != A_HEAD_FWD) continue;
-    const HeadFwd& hf = b.hf[t.a_aux & 1];
-    if (nw != 16 || !t.b_kc || t.ksplit > 1 || t.K2 > 0 || t.K % 32 || (64 * nw) % t.K ||
-        hf.Da < 1 || hf.Da > 32 || !hf.h2 || !hf.wh || !hf.bh || !hf.eps || !t.a_v)
-      return hipErrorInvalidValue;
-    lds = std::max(lds, stage_floats(t));
-  }
-  if (4 * lds > kLdsBytesPerCu) return hipErrorInvalidValue;
-  bool stg = false;
-  if (small_stage_on() && b.force_gpw <= 0 && (nw == 8 || nw == 16)) {
-    int need = 0;
-    for (int i = 0; i < b.ntasks; ++i) need = std::max(need, stage_floats(b.t[i]));
-    const int per_cu = nw >= 16 ? 1 : std::max(1, (grid + 255) / 256);
-    if (need > 0 && 4 * std::max(need, lds) * per_cu <= kLdsBytesPerCu) {
-      stg = true;
-      lds = std::max(need, lds);
-      if (nw == 8) gpw = 4;
-    }
-  }
-  const size_t shm = 4 * (size_t)lds;
 #define OAC_GS(NW_, G_) \
-  if (nw == NW_ && gpw == G_ && !stg) { \
-    if (shm > 64 * 1024) { \
-      const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_small_kernel<NW_, G_, false>), \
-          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm); \
-      if (ea != hipSuccess) return ea; } \
-    OAC_LAUNCH((gemm_small_kernel<NW_, G_, false>), dim3(grid), dim3(64 * NW_), shm, s, h.total_tiles, h.publish, \
+  if (nw == NW_ && gpw == G_) { \
+    OAC_LAUNCH((gemm_small_kernel<NW_, G_>), dim3(grid), dim3(64 * NW_), 0, s, h.total_tiles, h.publish, \
                h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b); \
     return hipGetLastError(); }
-#define OAC_GSS(NW_, G_) \
-  if (nw == NW_ && gpw == G_ && stg) { \
-    if (shm > 64 * 1024) { \
-      const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_small_kernel<NW_, G_, true>), \
-          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm); \
-      if (ea != hipSuccess) return ea; } \
-    OAC_LAUNCH((gemm_small_kernel<NW_, G_, true>), dim3(grid), dim3(64 * NW_), shm, s, h.total_tiles, h.publish, \
-               h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b); \
-    return hipGetLastError(); }
-  // staged operands: LDS fragment reads need fewer k-groups in flight (8 waves: 4)
-  OAC_GSS(8, 4) OAC_GSS(16, 4)
-#undef OAC_GSS
   OAC_GS(1, 5) OAC_GS(2, 5) OAC_GS(4, 5) OAC_GS(8, 5) OAC_GS(16, 4)
   OAC_GS(4, 3) OAC_GS(4, 4) OAC_GS(4, 6) OAC_GS(4, 8)
   OAC_GS(8, 3) OAC_GS(8, 4) OAC_GS(8, 6) OAC_GS(8, 8)

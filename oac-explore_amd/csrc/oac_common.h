@@ -17,16 +17,6 @@ namespace oac {
 enum AMode : int {
   A_PLAIN = 0,        // A[row*lda + col]
   A_RANK1_MASK = 1,   // s[row] * v[col] * (mask[row*ld_mask + col] > 0)
-  A_HEAD_FWD = 3,     // small kernel, forward with K = hidden: A = the critic's layer-0
-                      // output on the policy's fresh actions, h1 = relu(A[m*lda + n] +
-                      // sum_j act[m][j] a_v[n*ld_mask + j]) with act = the tanh-Gaussian
-                      // sample of GemmBatch::hf[a_aux & 1] (heads computed per row block);
-                      // a_aux & 2: the n0 == 0 tiles write hf's per-row outputs, and
-                      // U != null: the n0 == 0 tiles write h1 rows to U (ldu)
-  A_HEAD_BWD = 2,     // small kernel, K = 2 act_dim: A(m, .) = [dmean | dls_raw] of row m,
-                      // the tanh-Gaussian head backward (policy_math.h) of
-                      // dL/da[m][j] = sum_{p < R} A[p*lda + m*(K/2) + j] (parts in order),
-                      // ex[] as EPI_HEAD_BWD; the n0 == 0 tiles store the rows to U (ldu)
 };
 
 enum Epi : int {
@@ -45,10 +35,6 @@ enum Epi : int {
   EPI_BIAS_RELU_DOT = 7,  // C = relu(acc + bias[n]) and, per row, the partial
                           // dot of this 32-column tile with aux[n] (a width-1
                           // output layer): C2[(n0/32)*ldc2 + m]  (small kernel)
-  EPI_MASK_DA = 9,        // EPI_MASK, and the tile's part of the next product
-                          // C . V[:, :R] (V row-major, ldv; R <= 32):
-                          // C2[(n0/32)*ldc2 + m*R + j] = sum_{n in tile} C[m,n] V[n*ldv + j]
-                          // (small kernel; the parts feed an A_HEAD_BWD operand)
 };
 
 struct GemmTask {
@@ -84,7 +70,6 @@ struct GemmTask {
   int K2;
   const float* ex[6];   // extra epilogue operands (EPI_HEAD_BWD)
   int a_rows;           // small kernel: A (and U) row m is row batch.rg rows[m] of the buffer
-  int a_aux;            // A_HEAD_FWD: segment (bit 0), write the segment's outputs (bit 1)
 };
 
 struct StepState;
@@ -121,24 +106,10 @@ struct RowGather {
   float* eps1; float* eps2; int n_eps; unsigned long long seed;
 };
 
-// A_HEAD_FWD's policy batch: TanhGaussianPolicy's heads on h2, the sample
-// with eps, and where the n0 == 0 tiles of the writing task store the per-row
-// results (policy_head_kernel's HeadSeg outputs, head.hip)
-struct HeadFwd {
-  const float* h2;       // [B, H] policy hidden layer 2
-  const float* wh; const float* bh;   // stacked heads [2 Da, H], [2 Da]
-  const float* eps;      // [B, Da]
-  float* head; float* act; float* stdv; float* u; float* logp;
-  float* logp_part;      // non-null: per-16-row sums of (logp + te), rows in order
-  float te;
-  int Da;
-};
-
 struct GemmBatch {
   GemmTask t[kMaxTasks];
   int ntasks;
   int total_tiles;
-  HeadFwd hf[2];             // A_HEAD_FWD tasks' policy batches
   // Fused optimizer (small-batch kernel, unsplit K): every EPI_GRAD element is
   // also Adam(+Polyak)-updated in the epilogue (its index in the group is its
   // gradient pointer minus adam.g), and blocks [total_tiles, +adam_blocks) run

@@ -249,9 +249,7 @@ static inline int bwdp_cfg(const GemmBatch& gb) {
 static inline int launch_cfg(int cfg, const GemmBatch& gb) {
   if (cfg == 0) return 0;
   for (int i = 0; i < gb.ntasks; ++i)   // the fused head backward exists on the small kernel only
-    if (gb.t[i].epi == EPI_HEAD_BWD || gb.t[i].epi == EPI_MASK_DA || gb.t[i].a_mode == A_HEAD_BWD ||
-        gb.t[i].a_mode == A_HEAD_FWD)
-      return 0;
+    if (gb.t[i].epi == EPI_HEAD_BWD) return 0;
   // narrow products at large batch (width-1 critic heads, dL/da with N = act
   // dim): a 64-wide LDS tile computes 1-17 useful columns over 8 barriered K
   // blocks; the small-batch kernel's 32x32 tiles with K split over waves

@@ -71,7 +71,6 @@ enum Ws {
   W_STD1, W_U1, W_STD2, W_U2, W_DQ1, W_DQ2, W_GQ1, W_GQ2,
   W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DA1, W_DA2, W_DHEAD, W_DH2P, W_DH1P,
   W_QPART,   // [6][B][tiles]: per-tile partial dots of the width-1 critic heads
-  W_DAP,     // [2 x tiles][B][Da]: the -min Q backward's per-tile parts of dL/da (pbwd_fuse)
   W_COUNT
 };
 
@@ -95,7 +94,6 @@ static void layout_workspace(SacPlan& p) {
   for (int id : {W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DH2P, W_DH1P}) set(id, B, H);
   set(W_DHEAD, B, 2 * Da);
   set(W_QPART, QV_COUNT * B, (H + 31) / 32);
-  set(W_DAP, 2 * ((H + 31) / 32) * B, Da);
   if (p.S_q > 1) set(WS_GSLAB_Q, p.S_q, p.L.n_critics * p.L.q_size);
   if (p.S_p > 1) set(WS_GSLAB_P, p.S_p, p.L.pol_size);
   int64_t off = 0;
@@ -233,19 +231,6 @@ static int head_col_chunks(int B, int H) {
   return B >= 1024 ? std::max(1, (H + 255) / 256) : std::max(1, (H + 63) / 64);
 }
 
-// The small-batch step without the policy-head launch (OAC_HEAD_FUSE=1, A/B):
-// the fresh-action critic layer-1 launch computes its A operand per row block
-// -- heads, tanh-Gaussian sample, the critic's action columns on the saved
-// obs projection -- inside each tile (A_HEAD_FWD, gemm_small.hip), and the
-// Q1 / TQ1 tasks' n0 == 0 tiles write the per-row outputs the later launches
-// read.  Single rank only: the data-parallel alpha exchange needs the head's
-// partials before that launch.
-static bool head_fuse(const SacPlan& p) {
-  static const bool on = [] { const char* e = getenv("OAC_HEAD_FUSE"); return e && atoi(e) == 1; }();
-  return on && p.cfg == 0 && p.c.kind == OAC_KIND_SAC && p.c.q_out == 1 && p.c.world_size <= 1 &&
-         p.c.hidden % 32 == 0 && 1024 % p.c.hidden == 0 && p.c.act_dim <= 32 && qdot(p);
-}
-
 static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool critic_done = false) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
@@ -318,7 +303,7 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
     add(gb, t_fwd(p.W(W_H2Q2), H, B, H, q2 + L.q_last_w, H, 1, p.W(OAC_WS_Q2), 1, EPI_BIAS, q2 + L.q_last_b));
     if (run_gemm(p, gb, s)) return 1;
   }
-  if (!head_fuse(p)) {  // policy heads, tanh-Gaussian sample + log-prob, critics' action columns
+  {  // policy heads, tanh-Gaussian sample + log-prob, critics' action columns
     HeadArgs a;
     std::memset(&a, 0, sizeof(a));
     a.wh = pol + L.pol_head_w; a.bh = pol + L.pol_head_b; a.ld_wa = Dq;
@@ -384,28 +369,6 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
     const int outs[4] = {W_H2N1, W_H2N2, W_H2T1, W_H2T2};
     const int qv[4] = {QV_QN1, QV_QN2, QV_TQ1, QV_TQ2};
     for (int i = 0; i < 4; ++i) add(gb, q_l1(p, p.W(ins[i]), nets[i], p.W(outs[i]), qv[i]));
-    if (head_fuse(p)) {   // the policy heads inside the tiles (A_HEAD_FWD)
-      const float* pol = p.b.params;
-      const int pre[4] = {W_P1, W_P2, W_PT1, W_PT2};
-      for (int i = 0; i < 4; ++i) {
-        GemmTask& t = gb.t[i];
-        t.a_mode = A_HEAD_FWD;
-        t.A = p.W(pre[i]); t.lda = H;
-        t.a_v = nets[i] + L.q_fc0_w + Do; t.ld_mask = Dq;
-        t.a_aux = (i >> 1) | ((i & 1) ? 0 : 2);      // Q1 / TQ1 tasks write their batch's outputs
-        t.U = i < 2 ? p.W(ins[i]) : nullptr; t.ldu = H;   // h1 of Q_i(obs, a~): the policy backward's masks
-      }
-      const int h2[2] = {W_H2P, W_H2P2}, head[2] = {OAC_WS_HEAD1, OAC_WS_HEAD2};
-      const int act[2] = {OAC_WS_ACT1, OAC_WS_ACT2}, sd[2] = {W_STD1, W_STD2}, uu[2] = {W_U1, W_U2};
-      const int lp[2] = {OAC_WS_LOGP1, OAC_WS_LOGP2};
-      for (int g = 0; g < 2; ++g) {
-        HeadFwd& hf = gb.hf[g];
-        hf.h2 = p.W(h2[g]); hf.wh = pol + L.pol_head_w; hf.bh = pol + L.pol_head_b;
-        hf.eps = g == 0 ? p.E1() : p.E2();
-        hf.head = p.W(head[g]); hf.act = p.W(act[g]); hf.stdv = p.W(sd[g]); hf.u = p.W(uu[g]);
-        hf.logp = p.W(lp[g]); hf.logp_part = nullptr; hf.te = c.target_entropy; hf.Da = Da;
-      }
-    }
     if (p.direct_big) {   // the direct-gather step's batch copy (its first reader is the
       RowGather& g = gb.rg;   // targets kernel next): side workgroups in the free slot per CU
       g.ring = p.direct_ring; g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
@@ -514,20 +477,6 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
   return 0;
 }
 
-// The small-batch policy backward in four launches instead of five: the
-// -min Q backward's tiles also write their part of dL/da = dh1 . W0[:, Do:]
-// (EPI_MASK_DA: 32 x Da per tile, from the masked tile in LDS), and the dh2
-// launch computes its A operand -- [dmean | dls_raw], the tanh-Gaussian head
-// backward of the summed parts -- per row block itself (A_HEAD_BWD), with the
-// n0 == 0 tiles writing dhead for the head's weight gradient, which moves into
-// the policy layer-1 launch.  The dL/da + head-backward launch is gone.
-// OAC_PBWD_FUSE=1 turns it on (A/B against the five-launch form).
-static bool pbwd_fuse(const SacPlan& p) {
-  static const bool on = [] { const char* e = getenv("OAC_PBWD_FUSE"); return e && atoi(e) == 1; }();
-  const int parts = 2 * ((p.c.hidden + 31) / 32);
-  return on && p.cfg == 0 && p.c.q_out == 1 && parts <= 16 && p.c.act_dim <= 32;
-}
-
 // prefetch: batch of the next step (its critic-side forward rides on this
 // step's policy-backward launches, small-batch path only), or null
 static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch = nullptr,
@@ -540,8 +489,6 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
   const float* pol = p.b.params;
   const float* q1 = p.b.params + L.q1_base;
   const float* q2 = p.b.params + L.q2_base;
-  const bool pbf = pbwd_fuse(p);
-  const int ntn = (H + 31) / 32;   // column tiles of dh1: the parts of dL/da per critic
   {  // -min Q backward to layer 1 with post-step weights, pre-step masks
     GemmBatch gb{};
     const float* qs[2] = {q1, q2};
@@ -550,11 +497,6 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     for (int i = 0; i < 2; ++i) {
       GemmTask d = t_dx(nullptr, 0, B, H, qs[i] + L.q_fc1_w, H, H, p.W(out[i]), H, p.W(h1[i]), H);
       set_rank1(d, p.W(gq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
-      if (pbf) {   // + the tile's part of dL/da through the action columns of layer 0
-        d.epi = EPI_MASK_DA;
-        d.V = qs[i] + L.q_fc0_w + Do; d.ldv = Dq; d.R = Da;
-        d.C2 = p.W(W_DAP) + (long)i * ntn * B * Da; d.ldc2 = (long)B * Da;
-      }
       add(gb, d);
     }
     if (prefetch) add_critic_l0(p, gb, prefetch);
@@ -567,31 +509,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     }
     if (run_gemm(p, gb, s)) return 1;
   }
-  if (pbf) {
-    {  // dh2 = ([dmean | dls_raw] . W_head) * [h2 > 0], the A operand computed per row block
-      GemmBatch gb{};
-      GemmTask t = t_dx(p.W(W_DAP), (long)B * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(W_DH2P), H,
-                        p.W(W_H2P), H);
-      t.a_mode = A_HEAD_BWD; t.R = 2 * ntn;
-      t.ex[0] = p.W(OAC_WS_ACT1); t.ex[1] = p.W(W_STD1); t.ex[2] = p.W(W_U1);
-      t.ex[3] = p.E1(); t.ex[4] = p.W(OAC_WS_HEAD1);
-      t.ex[5] = c.auto_alpha ? &p.alpha()->alpha : nullptr;
-      t.U = p.W(W_DHEAD); t.ldu = 2 * Da;
-      add(gb, t);
-      if (prefetch) { add_target_l0(p, gb, prefetch); add_critic_l1(p, gb); }
-      if (run_gemm(p, gb, s)) return 1;
-    }
-    {  // policy layer 1 + the heads' weight gradient (dhead from the launch above)
-      GemmBatch gb{};
-      float* gp = grad_p(p);
-      add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
-                   L.pol_size, p.sp_p1));
-      add(gb, t_dx(p.W(W_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_DH1P), H, p.W(W_H1P), H));
-      add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, gp + L.pol_head_w,
-                   gp + L.pol_head_b, L.pol_size, p.sp_ph));
-      if (run_gemm(p, gb, s)) return 1;
-    }
-  } else if (p.cfg == 0 || head_bwd_fused_big()) {  // dL/da through both critics' action columns + head backward, one launch (small kernel)
+  if (p.cfg == 0 || head_bwd_fused_big()) {  // dL/da through both critics' action columns + head backward, one launch (small kernel)
     GemmBatch gb{};
     GemmTask t = t_dx(p.W(W_DH1N1), H, B, H, q1 + L.q_fc0_w + Do, Dq, Da, p.W(W_DHEAD), 2 * Da,
                       nullptr, 0);
@@ -620,7 +538,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
       p.launches++;
     }
   }
-  if (!pbf) {  // policy heads: dW_head slab, dh2
+  {  // policy heads: dW_head slab, dh2
     GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, gp + L.pol_head_w,
@@ -629,7 +547,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     if (prefetch) add_critic_l1(p, gb);
     if (run_gemm(p, gb, s)) return 1;
   }
-  if (!pbf) {  // policy layer 1
+  {  // policy layer 1
     GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,

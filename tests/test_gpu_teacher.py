@@ -19,7 +19,8 @@ whose ReLU pre-activation sits within fp32 rounding of 0 for some sample
 (parity.relu_boundary_units), as in test_gpu_dp.py; and, for a SAC critic's
 first layer, the layer-1 mask flips of such (sample, unit) entries, which
 reach every fc0 row (_flip_adjusted: the oracle's fc0 reference is corrected
-by the flips that explain the GPU's gradient, then gated at 1e-5).
+by the flips, picked greedily, that explain the GPU's gradient; then gated at
+1e-5).
 
 Reference: trainer/trainer.py:126-280 (SAC), trainer/particle_trainer_oac.py:
 169-363 (P-OAC), torch-1.4 Adam (trainer/trainer.py:75-91).
@@ -107,30 +108,32 @@ def _boundary_rows(x0, q):
     return {"fc0.weight": u0, "fc0.bias": u0, "fc1.weight": u1, "fc1.bias": u1}
 
 
-def _flip_adjusted(got, gref, cache, dq, q, opt, lr, tol=1e-5, max_pairs=8):
+def _flip_adjusted(got, gref, cache, dq, q, opt, lr, tol=3e-5, max_pairs=64, max_flips=8):
     """fc0 references under the layer-1 ReLU mask flips that best explain the
     GPU's fc0 gradient.
 
     A layer-1 pre-activation within fp32 rounding of 0 for sample s, unit u
-    (parity.relu_boundary_units) may take the other sign on the GPU; the
-    backward then passes (or stops) that sample's dL/dpre1[s, u] =
-    dq[s] . W_last[:, u], which reaches EVERY fc0 row through W1[u, :] (a
-    rank-one change dd0 x[s]^T).  The fc1 rows u are already allowed; here the
-    fc0 reference is corrected by the subset of such flips (at most 2^8
-    tried) closest to the GPU's gradient, and m, v and the post-step fc0
-    follow through torch-1.4 Adam in float64.  Returns ({pn: (g, m, v, P)},
-    flips used)."""
+    may take the other sign on the GPU; the backward then passes (or stops)
+    that sample's dL/dpre1[s, u] = dq[s] . W_last[:, u], which reaches EVERY
+    fc0 row through W1[u, :] (a rank-one change dd0 x[s]^T).  The fc1 rows u
+    are already allowed; here the fc0 reference is corrected by the flips --
+    picked greedily, each only if it lowers the fc0 error, at most
+    ``max_flips`` of the ``max_pairs`` entries closest to 0 -- and m, v and
+    the post-step fc0 follow through torch-1.4 Adam in float64.  Returns
+    ({pn: (g, m, v, P)}, flips used)."""
     x = cache["hs"][0].double().numpy()
     h1 = cache["hs"][1].double().numpy()
     h2 = cache["hs"][2].numpy()
     W1 = np.asarray(q["fc1.weight"], np.float64)
     pre1 = h1 @ W1.T + np.asarray(q["fc1.bias"], np.float64)
-    rms = np.sqrt(np.mean(pre1 * pre1))
-    rows, units = np.nonzero(np.abs(pre1) < tol * rms)
+    rel = np.abs(pre1) / np.sqrt(np.mean(pre1 * pre1))
+    near = np.argsort(rel, axis=None)[:max_pairs]
+    near = [int(i) for i in near if rel.flat[i] < tol]
     dqn = dq.double().numpy().reshape(dq.shape[0], -1)
     wl = np.asarray(q["last_fc.weight"], np.float64)
     deltas = []
-    for s_, u in list(zip(rows.tolist(), units.tolist()))[:max_pairs]:
+    for i in near:
+        s_, u = divmod(i, pre1.shape[1])
         val = float(dqn[s_] @ wl[:, u])
         sign = -1.0 if h2[s_, u] > 0 else 1.0
         dd0 = sign * val * W1[u] * (h1[s_] > 0)
@@ -139,14 +142,22 @@ def _flip_adjusted(got, gref, cache, dq, q, opt, lr, tol=1e-5, max_pairs=8):
     gb = np.asarray(got["fc0.bias"], np.float64)
     rw = gref["fc0.weight"].double().numpy()
     rb = gref["fc0.bias"].double().numpy()
-    best = (parity.rel_err(gw, rw) + parity.rel_err(gb, rb), 0)
-    for mask in range(1, 1 << len(deltas)):
-        sel = [d for i, d in enumerate(deltas) if mask >> i & 1]
-        e = (parity.rel_err(gw, rw + sum(d[1] for d in sel))
-             + parity.rel_err(gb, rb + sum(d[2] for d in sel)))
-        if e < best[0]:
-            best = (e, mask)
-    sel = [d for i, d in enumerate(deltas) if best[1] >> i & 1]
+    err = lambda aw, ab: parity.rel_err(gw, aw) + parity.rel_err(gb, ab)
+    sel, cur = [], err(rw, rb)
+    while len(sel) < max_flips:
+        best = None
+        for i, d in enumerate(deltas):
+            if i in sel:
+                continue
+            e = err(rw + d[1], rb + d[2])
+            if e < cur and (best is None or e < best[0]):
+                best = (e, i)
+        if best is None:
+            break
+        cur = best[0]
+        sel.append(best[1])
+        rw, rb = rw + deltas[best[1]][1], rb + deltas[best[1]][2]
+    sel = [deltas[i] for i in sel]
     out = {}
     t = opt.t
     bc1, bc2 = 1 - opt.b1 ** t, 1 - opt.b2 ** t
