@@ -15,7 +15,9 @@ python3 tools/prof_summary.py gpurun_out/prof_b256 > $D/b256_gemm_avg.txt
 python3 tools/prof_summary.py gpurun_out/prof_b4096 > $D/b4096_gemm_avg.txt
 python3 tools/prof_summary.py gpurun_out/prof_poac4096 > $D/poac4096_gemm_avg.txt
 python3 tools/prof_summary.py gpurun_out/prof_expl > $D/expl_kernel_avg.txt
-python3 tools/trace.py gpurun_out/prof_b256 ${NLAUNCH:-12} > $D/b256_step_trace.txt
+python3 tools/trace.py gpurun_out/prof_b256 12 > $D/b256_step_trace.txt
+python3 tools/trace.py gpurun_out/prof_b4096 13 > $D/b4096_step_trace.txt
+python3 tools/trace.py gpurun_out/prof_poac4096 17 > $D/poac4096_step_trace.txt || true
 rm -f profiles/pmc_gemm_traffic.json
 python3 tools/pmc_summary.py b256 $D/pmc_b256.json --traffic 256 profiles/pmc_gemm_traffic.json > $D/pmc_b256.txt
 python3 tools/pmc_summary.py b4096 $D/pmc_b4096.json --traffic 4096 profiles/pmc_gemm_traffic.json > $D/pmc_b4096.txt
