@@ -319,7 +319,6 @@ hipError_t launch_policy_sample(const PolicySampleArgs& a, int nseg, hipStream_t
 hipError_t launch_critic_targets(const CriticTargetArgs& a, hipStream_t s);
 hipError_t launch_policy_head_backward(const PolicyHeadBwdArgs& a, hipStream_t s);
 hipError_t launch_gather(const GatherArgs& a, hipStream_t s);
-hipError_t launch_idx_copy(const int* src, int* dst, int n, hipStream_t s);
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s);
 hipError_t launch_mt_randint(unsigned* mt_state, unsigned long long size, int count, int* out,
                              hipStream_t s);

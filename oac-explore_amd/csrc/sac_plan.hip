@@ -831,10 +831,7 @@ int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring) {
     // (a direct large-batch step's 768 layer-0 tiles would each read their
     // rows' indices across the host link: its slot is copied to the device
     // ring instead, one H2D copy ahead of the step)
-    // (OAC_BIG_HOST_IDX=1, A/B: the large-batch direct step's tiles read the
-    // slot from the host ring too)
-    static const bool big_host = [] { const char* e = getenv("OAC_BIG_HOST_IDX"); return e && atoi(e) == 1; }();
-    p.idx_host = !p.rows_direct && (big_host || !big_direct_ok(p));
+    p.idx_host = !p.rows_direct && !big_direct_ok(p);
     // not direct (large batch): the copy path still stages through this ring
     if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }
     if (p.graph) { (void)hipGraphDestroy(p.graph); p.graph = nullptr; }
@@ -892,11 +889,6 @@ static int stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stre
     dst[i] = (int32_t)v;
   }
   if (host_read) return 0;   // the step's first launch reads the slot from host memory
-  static const bool copy_kernel = [] { const char* e = getenv("OAC_IDX_COPY"); return e && atoi(e) == 1; }();
-  if (copy_kernel && (B & 3) == 0) {
-    OAC_HIP_CHECK(launch_idx_copy(dst, const_cast<int32_t*>(p.b.idx_ring) + (long)slot * B, B, s));
-    return 0;
-  }
   OAC_HIP_CHECK(hipMemcpyAsync(const_cast<int32_t*>(p.b.idx_ring) + (long)slot * B, dst,
                                sizeof(int32_t) * B, hipMemcpyHostToDevice, s));
   return 0;
