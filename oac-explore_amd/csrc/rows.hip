@@ -501,16 +501,59 @@ __device__ __forceinline__ void particle_targets_rows(const ParticleTargetArgs& 
   }
 }
 
+// threads of the prefetching dh2 pass: rows_per_pass(n4) rows of n4 float4s
+// per 256 threads (n4 <= 64), four passes over a 16-row block
+__device__ __forceinline__ int rows_per_pass(int n4) { return 256 / n4; }
+
 // the targets kernel's row logic, then (p.dh2) the 16 rows' backward into
 // the last hidden layer by the whole block
 __global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArgs p) {
   __shared__ RowHeadLds hs, qs;
   __shared__ float sdq[kRowBlock][kMaxHeads];
   const int r0 = blockIdx.x * kRowBlock;
+  const int K = p.K, H = p.qh.H, n4 = H >> 2;
+  // the backward's operands need nothing the row logic computes: with H <= 256
+  // a thread's 4 elements share one float4 column c of the K weight rows, so
+  // those and the 4 hidden-row float4s are requested before the heads (the
+  // dh2 pass then starts on registers, not on a round trip after the rows)
+  const bool pre = p.dh2 && n4 <= 64 && n4 * kRowBlock <= 1024 && K <= kMaxHeads;
+  float4 hpf[4], wpf[kMaxHeads];
+  if (pre) {
+    const int c = 4 * (threadIdx.x % n4), rr0 = threadIdx.x / n4, rstep = 256 / n4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = min(r0 + rr0 + j * rstep, p.B - 1);
+      hpf[j] = *reinterpret_cast<const float4*>(p.qh.h + (long)m * H + c);
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxHeads; ++k)
+      wpf[k] = *reinterpret_cast<const float4*>(p.qh.w + (long)min(k, K - 1) * H + c);
+  }
   particle_targets_rows(p, hs, qs, sdq);
   if (!p.dh2) return;
   __syncthreads();
-  const int K = p.K, H = p.qh.H, n4 = H >> 2;
+  if (pre && threadIdx.x < rows_per_pass(n4) * n4) {
+    const int c = 4 * (threadIdx.x % n4), rr0 = threadIdx.x / n4, rstep = 256 / n4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int rr = min(rr0 + j * rstep, kRowBlock - 1), m = r0 + rr;
+      if (rr0 + j * rstep >= kRowBlock || m >= p.B) continue;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < kMaxHeads; ++k) {   // k order, as the GEMM's accumulation
+        const float g = k < K ? sdq[rr][k] : 0.f;   // (+0 past K: the sum is unchanged)
+        a.x = fmaf(g, wpf[k].x, a.x); a.y = fmaf(g, wpf[k].y, a.y);
+        a.z = fmaf(g, wpf[k].z, a.z); a.w = fmaf(g, wpf[k].w, a.w);
+      }
+      const float4 h = hpf[j];
+      float4 o;
+      o.x = h.x > 0.f ? a.x : 0.f; o.y = h.y > 0.f ? a.y : 0.f;
+      o.z = h.z > 0.f ? a.z : 0.f; o.w = h.w > 0.f ? a.w : 0.f;
+      *reinterpret_cast<float4*>(p.dh2 + (long)m * H + c) = o;
+    }
+    return;
+  }
+  if (pre) return;
   for (int e = threadIdx.x; e < kRowBlock * n4; e += 256) {
     const int rr = e / n4, c = 4 * (e - rr * n4), m = r0 + rr;
     if (m >= p.B) continue;
@@ -535,7 +578,9 @@ __global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArg
 // the policy Adam, which reads no alpha field).
 __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
   __shared__ float red[256];
-  if (p.alpha && blockIdx.x == 0) {
+  const int nrb = (p.B + kRowBlock - 1) / kRowBlock;
+  if ((int)blockIdx.x == nrb) {   // the alpha update: its own block, beside the row blocks
+    if (!p.alpha) return;
     const float S = (p.world_size > 1) ? (p.logp_part ? block_part_sum(p.logp_part, p.n_logp_part, red)
                                                       : p.alpha->sum)
                                        : block_logp_sum(p.logp, p.B, p.target_entropy, red);
@@ -554,10 +599,28 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
       as->next_log_alpha = la; as->next_m = m; as->next_v = v;
       as->alpha = expf(la); as->grad = g; as->alpha_loss = -(la_old * S) / n;
     }
+    return;
   }
   __shared__ RowHeadLds hs;
   const int r0 = blockIdx.x * kRowBlock, r = r0 + threadIdx.x;
   const int K = p.K;
+  const int H = p.hn.H, n4 = H >> 2;
+  // the backward's operands (the 4 hidden-row float4s of this thread and the
+  // K weight rows' float4 of its column) requested before the heads, as in
+  // particle_targets_kernel
+  const bool pre = p.dh2 && n4 <= 64;
+  float4 hpf[4], wpf[kMaxHeads];
+  if (pre) {
+    const int c = 4 * (threadIdx.x % n4), rr0 = threadIdx.x / n4, rstep = 256 / n4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = min(r0 + rr0 + j * rstep, p.B - 1);
+      hpf[j] = *reinterpret_cast<const float4*>(p.hn.h + (long)m * H + c);
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxHeads; ++k)
+      wpf[k] = *reinterpret_cast<const float4*>(p.hn.w + (long)min(k, K - 1) * H + c);
+  }
   if (p.hn.h) {
     row_heads(p.hn, K, p.B, r0, hs);
     __syncthreads();
@@ -580,7 +643,31 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
   // -min Q backward into the last hidden layer (the dX launch it replaces
   // summed gq[r, k] W[k, n] over k: one nonzero product, the rest +0)
   __syncthreads();
-  const int H = p.hn.H, n4 = H >> 2;
+  if (pre) {
+    if (threadIdx.x >= rows_per_pass(n4) * n4) return;
+    const int c = 4 * (threadIdx.x % n4), rr0 = threadIdx.x / n4, rstep = 256 / n4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int rr = min(rr0 + j * rstep, kRowBlock - 1), m = r0 + rr;
+      if (rr0 + j * rstep >= kRowBlock || m >= p.B) continue;
+      const int b = sbest[rr];
+      // the argmin head's row as a masked sum (exact: one term is w, the rest
+      // +-0), so the prefetched rows stay in registers
+      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < kMaxHeads; ++k) {
+        const float sel = b == k ? 1.f : 0.f;
+        w.x = fmaf(sel, wpf[k].x, w.x); w.y = fmaf(sel, wpf[k].y, w.y);
+        w.z = fmaf(sel, wpf[k].z, w.z); w.w = fmaf(sel, wpf[k].w, w.w);
+      }
+      const float4 h = hpf[j];
+      float4 o;
+      o.x = h.x > 0.f ? -invB * w.x : 0.f; o.y = h.y > 0.f ? -invB * w.y : 0.f;
+      o.z = h.z > 0.f ? -invB * w.z : 0.f; o.w = h.w > 0.f ? -invB * w.w : 0.f;
+      *reinterpret_cast<float4*>(p.dh2 + (long)m * H + c) = o;
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < kRowBlock * n4; e += 256) {
     const int rr = e / n4, c = 4 * (e - rr * n4), m = r0 + rr;
     if (m >= p.B) continue;
@@ -602,7 +689,8 @@ hipError_t launch_particle_targets(const ParticleTargetArgs& a, hipStream_t s) {
 hipError_t launch_particle_min(const ParticleMinArgs& a, hipStream_t s) {
   if (a.dh2 && (!a.hn.h || (a.hn.H & 3))) return hipErrorInvalidValue;
   if (a.K > kMaxHeads || !head_ok(a.hn)) return hipErrorInvalidValue;
-  OAC_LAUNCH(particle_min_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock), dim3(256), 0, s, a);
+  // the row blocks, then one block for the alpha update
+  OAC_LAUNCH(particle_min_kernel, dim3((a.B + kRowBlock - 1) / kRowBlock + 1), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
