@@ -12,3 +12,6 @@ for i in 1 2; do
     echo "armed=$v $(tail -1 gpurun_out/r4_t8_expl_$v.log)"
   done
 done
+# the row-block dataflow form of the B=256 critic branch against its three launches
+timeout -k 10 120 tools/micro/dataflow_micro > gpurun_out/r4_dataflow_micro.log 2>&1; crash $?
+cat gpurun_out/r4_dataflow_micro.log
