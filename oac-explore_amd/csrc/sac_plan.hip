@@ -921,7 +921,11 @@ int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags,
   }
   const bool hr = h->plan.idx_host;
   if (stage_host_idx(h, idx, bc, stream, hr || h->plan.rows_direct)) return 1;
-  return oac_sac_step_n(h, flags | OAC_STEP_GATHER | OAC_STEP_USE_GRAPH | (hr ? kStepHostIdx : 0), 1,
+  // (OAC_DROPIN_DIRECT=1, A/B: the step's launches issued directly instead
+  // of as one graph launch)
+  static const bool direct_launch = [] { const char* e = getenv("OAC_DROPIN_DIRECT"); return e && atoi(e) == 1; }();
+  return oac_sac_step_n(h, flags | OAC_STEP_GATHER | (direct_launch ? 0 : OAC_STEP_USE_GRAPH) |
+                               (hr ? kStepHostIdx : 0), 1,
                         stream);
 }
 
