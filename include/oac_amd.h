@@ -314,16 +314,6 @@ int oac_expl_set_host_io(oac_expl* h, const float* host_obs, float* host_out);
  * work already queued there) and returns once the results are in *out. */
 int oac_expl_host_staging(oac_expl* h, float** obs, float** out);
 int oac_expl_action_now(oac_expl* h, const float* eps, float beta_UB, float delta, void* stream);
-/* The single-observation Philox call (eps == NULL, twin critics) runs through
- * an ARMED kernel by default (OAC_EXPL_ARMED=0: off): each call also launches
- * the next call's kernel on a stream of the handle, where it waits -- polling
- * host memory -- for its observation, so a call's latency no longer includes
- * the launch.  Before publishing, the call completes every update queued on
- * `stream` (the kernel reads the weights after its observation arrives).  A
- * waiting kernel leaves by itself 20 ms after it started; oac_expl_disarm
- * cancels it now (a trainer step, or anything that wants all CUs, calls it
- * first).  The plain call, the graph call and destroy disarm first. */
-int oac_expl_disarm(oac_expl* h);
 /* --trainer_UB with particle_trainer_oac.ParticleTrainer (optimistic_exploration.py:38-39
  * -> trainer.predict(upper_bound=True), particle_trainer_oac.py:147-167): with a K-head
  * handle, index in [0, K) makes Q_UB = sort_k(Q_k)[index] (the trainer's delta_index;

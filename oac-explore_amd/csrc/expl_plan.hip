@@ -23,7 +23,6 @@
 #include <cstring>
 #include <algorithm>
 #include <cstdlib>
-#include <ctime>
 
 #include "../../include/oac_amd.h"
 #include "kernels.h"
@@ -54,16 +53,6 @@ struct ExplPlan {
   // single-observation calls: the outputs as tagged granules (ExplFusedArgs::tags)
   unsigned long long* hc_tag = nullptr;
   unsigned seq = 0;
-  // the armed single-observation call (expl_armed_call): the next call's
-  // kernel is launched ahead on arm_stream and waits for its observation in
-  // hc_obs_tag (tagged granules) or the cancel word hc_cancel
-  hipStream_t arm_stream = nullptr;
-  unsigned long long* hc_obs_tag = nullptr;
-  unsigned* hc_cancel = nullptr;
-  unsigned arm_seq = 0;                 // seq of the waiting kernel (0: none)
-  double arm_t = 0.0;                   // host time of its launch, us
-  float arm_beta = 0.f, arm_delta = 0.f;
-  int arm_ub = -1;
   hipStream_t cap_stream = nullptr;   // graph capture (the graphs launch on the caller's stream)
   // captured call graphs by (eps slot, beta_UB, delta, ub_index): alternating
   // bounds on one handle (e.g. --trainer_UB and plain calls) replay their own
@@ -151,13 +140,6 @@ static int expl_host_alloc(ExplPlan& p) {
   std::memset(p.hc_obs, 0, sizeof(float) * (size_t)p.N * (p.Do + p.Da));
   std::memset(p.hc_out, 0, sizeof(float) * 3 * (size_t)p.N * p.Da);
   *p.hc_done = p.seq;
-  if (p.N == 1) {   // the armed call's observation granules and cancel word
-    OAC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p.hc_obs_tag),
-                                sizeof(unsigned long long) * (size_t)p.Do, fl));
-    OAC_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p.hc_cancel), 64, fl));
-    std::memset(p.hc_obs_tag, 0, sizeof(unsigned long long) * (size_t)p.Do);
-    *p.hc_cancel = 0;
-  }
   return 0;
 }
 
@@ -233,86 +215,6 @@ static int expl_wait_tags(ExplPlan& p, unsigned seq, hipStream_t s) {
     return 1;
   }
   return 0;
-}
-
-static double host_us() {
-  timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  return 1e6 * (double)ts.tv_sec + 1e-3 * (double)ts.tv_nsec;
-}
-
-// a kernel armed longer ago than this (host clock, from its launch call) is
-// not published to: its workgroups leave on their own after kExplArmTicks
-// (20 ms of the GPU wall clock, from their start), twice this
-constexpr double kArmHostLimitUs = 10000.0;
-
-static bool armed_enabled() {
-  static const bool on = [] { const char* e = getenv("OAC_EXPL_ARMED"); return !e || atoi(e) != 0; }();
-  return on;
-}
-
-static unsigned next_seq(ExplPlan& p) {
-  p.seq = (p.seq + 1) & 0x7fffffffu;   // bit 31 of the completion word is the failure flag
-  if (p.seq == 0) p.seq = 1;           // 0 is the words' initial value
-  return p.seq;
-}
-
-// cancel the waiting kernel (its workgroups leave without touching state)
-static void expl_cancel(ExplPlan& p) {
-  if (!p.arm_seq) return;
-  __atomic_store_n(p.hc_cancel, p.arm_seq, __ATOMIC_RELEASE);
-  p.arm_seq = 0;
-}
-
-// launch the next call's kernel on the arming stream; 1 = launched, 0 = this
-// plan cannot take the armed call (the caller uses the plain one), -1 = error
-static int expl_arm(ExplPlan& p, float beta, float delta) {
-  if (!p.arm_stream) OAC_HIP_CHECK(hipStreamCreateWithFlags(&p.arm_stream, hipStreamNonBlocking));
-  ExplFusedArgs a = expl_args(p, nullptr, beta, delta);
-  a.obs = nullptr;
-  a.out = p.hc_out;
-  a.done = p.hc_done;
-  a.done_seq = next_seq(p);
-  a.tags = p.hc_tag;
-  a.obs_tags = p.hc_obs_tag;
-  a.cancel = p.hc_cancel;
-  const hipError_t e = launch_expl_armed(a, p.ws + p.o_split, p.arm_stream);
-  if (e == hipErrorNotSupported) return 0;
-  if (e != hipSuccess) { set_error("exploration (armed): %s", hipGetErrorString(e)); return -1; }
-  p.arm_seq = a.done_seq;
-  p.arm_t = host_us();
-  p.arm_beta = beta; p.arm_delta = delta; p.arm_ub = p.ub_index;
-  return 1;
-}
-
-// One single-observation Philox call through an armed kernel: every update on
-// the caller's stream is complete first (the kernel reads the weights once its
-// observation is there), then the observation goes out as tagged granules to
-// the kernel armed by the previous call (or one armed now), the next call's
-// kernel is armed behind it, and the call waits for this one's tagged outputs.
-// Returns 0 / 1 (error) / 2 (this plan cannot arm: use the plain call).
-static int expl_armed_call(ExplPlan& p, float beta, float delta, hipStream_t s) {
-  const hipError_t q = hipStreamQuery(s);
-  if (q == hipErrorNotReady) OAC_HIP_CHECK(hipStreamSynchronize(s));
-  else if (q != hipSuccess) { set_error("exploration: %s", hipGetErrorString(q)); return 1; }
-  const bool live = p.arm_seq && p.arm_beta == beta && p.arm_delta == delta &&
-                    p.arm_ub == p.ub_index && host_us() - p.arm_t < kArmHostLimitUs;
-  if (!live) {
-    expl_cancel(p);
-    const int r = expl_arm(p, beta, delta);
-    if (r <= 0) return r < 0 ? 1 : 2;
-  }
-  const unsigned seq = p.arm_seq;
-  p.arm_seq = 0;
-  for (int k = 0; k < p.Do; ++k) {   // {value bits, seq}: whole 8-byte granules
-    unsigned bits;
-    std::memcpy(&bits, p.hc_obs + k, sizeof(bits));
-    __atomic_store_n(p.hc_obs_tag + k, ((unsigned long long)seq << 32) | bits, __ATOMIC_RELAXED);
-  }
-  __atomic_thread_fence(__ATOMIC_RELEASE);
-  const int r = expl_arm(p, beta, delta);   // the next call's kernel, behind this one
-  if (r < 0) return 1;
-  return expl_wait_tags(p, seq, p.arm_stream);
 }
 
 }  // namespace oac
@@ -395,21 +297,8 @@ int oac_expl_create(int obs_dim, int act_dim, int hidden, const float* policy, c
                                seed, out);
 }
 
-int oac_expl_disarm(oac_expl* h) {
-  if (!h) return 0;
-  ExplPlan& p = h->p;
-  if (!p.arm_stream) return 0;
-  expl_cancel(p);
-  OAC_HIP_CHECK(hipStreamSynchronize(p.arm_stream));   // its workgroups have left
-  return 0;
-}
-
 int oac_expl_destroy(oac_expl* h) {
   if (!h) return 0;
-  if (oac_expl_disarm(h)) return 1;
-  if (h->p.arm_stream) (void)hipStreamDestroy(h->p.arm_stream);
-  if (h->p.hc_obs_tag) (void)hipHostFree(h->p.hc_obs_tag);
-  if (h->p.hc_cancel) (void)hipHostFree(h->p.hc_cancel);
   h->p.drop_graphs();
   if (h->p.cap_stream) (void)hipStreamDestroy(h->p.cap_stream);
   if (h->p.hc_obs) (void)hipHostFree(h->p.hc_obs);
@@ -427,7 +316,6 @@ int oac_expl_action(oac_expl* h, const float* eps, float beta_UB, float delta, f
   if (!h) { set_error("null handle"); return 1; }
   ExplPlan& p = h->p;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (p.arm_stream && oac_expl_disarm(h)) return 1;   // (the workspace is shared)
   int gi = -1;
   for (int i = 0; i < p.n_graphs && gi < 0; ++i) {
     const ExplPlan::Graph& g = p.graphs[i];
@@ -481,18 +369,13 @@ int oac_expl_action_now(oac_expl* h, const float* eps, float beta_UB, float delt
   ExplPlan& p = h->p;
   if (expl_host_alloc(p)) return 1;
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (p.N == 1 && !eps && p.q2 && p.Do <= kExplObsArg && armed_enabled()) {
-    const int r = expl_armed_call(p, beta_UB, delta, s);
-    if (r != 2) return r;
-  }
-  // the plain call on the caller's stream: no kernel of this plan may still
-  // wait on the arming stream (they share the workspace and the counter)
-  if (p.arm_stream && oac_expl_disarm(h)) return 1;
   ExplFusedArgs a = expl_args(p, eps, beta_UB, delta);
   a.obs = p.hc_obs;
   a.out = p.hc_out;
+  p.seq = (p.seq + 1) & 0x7fffffffu;   // bit 31 of the word is the failure flag
+  if (p.seq == 0) p.seq = 1;           // 0 is the word's initial value
   a.done = p.hc_done;
-  a.done_seq = next_seq(p);
+  a.done_seq = p.seq;
   if (p.N == 1 && p.Do <= kExplObsArg) {   // one observation: it travels in the arguments,
     ExplObsArg o;                            // the outputs come back as tagged granules
     std::memcpy(o.v, p.hc_obs, sizeof(float) * p.Do);

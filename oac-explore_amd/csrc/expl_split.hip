@@ -690,45 +690,7 @@ static bool expl_twin_ok(const ExplFusedArgs& a, int threads, bool wt) {
 #define EXPL_CLK3(i) do {} while (0)
 #endif
 
-// The armed single-observation call (OBSM = 2, oac_expl_action_now with an
-// armed kernel): the launch is issued ahead of the call, and every workgroup
-// waits here for its observation -- Do tagged granules {value bits, call seq}
-// the host writes into host-coherent memory when the call comes -- so the
-// call's latency no longer holds the launch.  Each thread polls its own
-// granule (system scope); the workgroup goes on when all have this call's
-// seq, and leaves (no output, no state touched) on the host's cancel word or
-// after kExplArmTicks of the 100 MHz wall clock.  The host never publishes to
-// a kernel armed longer than half of that ago (expl_plan.hip), so every
-// workgroup of a kernel takes the same branch.
-constexpr unsigned long long kExplArmTicks = 2000000;   // 20 ms
-__device__ __forceinline__ bool expl_wait_armed(const ExplFusedArgs& a, float* x, int Do,
-                                                long long* cnt) {
-  const int t = threadIdx.x;
-  const unsigned long long t0 = wall_clock64();
-  bool have = t >= Do;
-  float v = 0.f;
-  for (;;) {
-    if (!have) {
-      const unsigned long long g =
-          __hip_atomic_load(a.obs_tags + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      if ((unsigned)(g >> 32) == a.done_seq) { v = __uint_as_float((unsigned)g); have = true; }
-    }
-    bool quit = false;
-    if (t == 0)
-      quit = __hip_atomic_load(a.cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == a.done_seq ||
-             wall_clock64() - t0 > kExplArmTicks;
-    if (__syncthreads_and(have)) break;
-    if (__syncthreads_or(quit)) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  if (t < Do) x[t] = v;
-  // the Philox counter: read once the call is here (the kernel before it on
-  // the arming stream has advanced it)
-  if (t == 0) *cnt = a.state->expl_counter;
-  return true;
-}
-
-template <bool WT, int OBSM>
+template <bool WT, bool OBS>
 __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, int row0, int G,
                                                              float* scratch, ExplObsArg oa) {
   float* sm;
@@ -764,11 +726,7 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
   float* w0a = misc + 128;                 // [2H][Da] W0_i[:, Do:]
   float* ctb = w0a + 2L * H * Da;          // [nw][H] per-row u terms, row 0 then u_p
   __shared__ long long cnt_s;
-  if constexpr (OBSM == 2) {   // (the weights are read after the call is here: the host
-    if (!expl_wait_armed(a, x, Do, &cnt_s)) return;   // published it behind every update)
-  } else {
-    if (t == 0) cnt_s = a.state->expl_counter;
-  }
+  if (t == 0) cnt_s = a.state->expl_counter;
   const int p0 = wg * NP / G, p1 = (wg + 1) * NP / G;   // this workgroup's parts
   // ---- ahead of everything: the weights of S1's first rows and of z.  The
   // S1 rows of this workgroup form one list -- its policy layer-0 rows
@@ -813,9 +771,9 @@ __global__ void __launch_bounds__(1024) oac_expl_twin_kernel(ExplFusedArgs a, in
     }
   }
   EXPL_CLK(0);
-  if constexpr (OBSM == 1) {
+  if constexpr (OBS) {
     for (int k = t; k < Do; k += nt) x[k] = oa.v[k];
-  } else if constexpr (OBSM == 0) {
+  } else {
     for (int k = t; k < Do; k += nt) x[k] = a.obs[(long)r * a.ld_obs + k];
   }
   __syncthreads();
@@ -1231,10 +1189,10 @@ hipError_t launch_expl_split(const ExplFusedArgs& a, int row0, int n_rows, float
   const bool own_cu = G > 1 && (long)n_rows * G <= expl_device_cus();
   if (!g_expl_twin_off && expl_twin_ok(a, nt, own_cu)) {
     if (own_cu) {
-      OAC_LAUNCH((oac_expl_twin_kernel<true, 0>), dim3(n_rows * G), dim3(nt), 0, s, a, row0, G,
+      OAC_LAUNCH((oac_expl_twin_kernel<true, false>), dim3(n_rows * G), dim3(nt), 0, s, a, row0, G,
                  scratch, none);
     } else {
-      OAC_LAUNCH((oac_expl_twin_kernel<false, 0>), dim3(n_rows * G), dim3(nt),
+      OAC_LAUNCH((oac_expl_twin_kernel<false, false>), dim3(n_rows * G), dim3(nt),
                  expl_twin_lds(a.Do, a.Da, a.H, nt) * sizeof(float), s, a, row0, G, scratch, none);
     }
     return hipGetLastError();
@@ -1260,27 +1218,12 @@ hipError_t launch_expl_split_obs(const ExplFusedArgs& a, const ExplObsArg& obs, 
   const int G = expl_split_group(1);
   const bool own_cu = G > 1 && G <= expl_device_cus();
   if (own_cu && !g_expl_twin_off && expl_twin_ok(a, nt, true)) {
-    OAC_LAUNCH((oac_expl_twin_kernel<true, 1>), dim3(G), dim3(nt), 0, s, a, 0, G, scratch, obs);
+    OAC_LAUNCH((oac_expl_twin_kernel<true, true>), dim3(G), dim3(nt), 0, s, a, 0, G, scratch, obs);
     return hipGetLastError();
   }
   const long lds = expl_split_lds(a.Do, a.Da, a.H, nt);
   if (!(own_cu && lds <= kWtLdsFloats)) return launch_expl_split(a, 0, 1, scratch, s);
   OAC_LAUNCH((oac_expl_split_kernel<true, true>), dim3(G), dim3(nt), 0, s, a, 0, G, scratch, obs);
-  return hipGetLastError();
-}
-
-// the armed call's kernel (expl_wait_armed): the twin kernel on workgroups of
-// their own CUs, or hipErrorNotSupported (the caller launches the plain call)
-hipError_t launch_expl_armed(const ExplFusedArgs& a, float* scratch, hipStream_t s) {
-  if (a.n != 1 || a.Do > kExplObsArg || !a.obs_tags || !a.cancel || !a.tags || a.eps)
-    return hipErrorInvalidValue;
-  const int nt = expl_split_threads();
-  const int G = expl_split_group(1);
-  if (!(G > 1 && G <= expl_device_cus() && !g_expl_twin_off && expl_twin_ok(a, nt, true) &&
-        a.Do <= nt))
-    return hipErrorNotSupported;
-  static const ExplObsArg none{};   // (unread)
-  OAC_LAUNCH((oac_expl_twin_kernel<true, 2>), dim3(G), dim3(nt), 0, s, a, 0, G, scratch, none);
   return hipGetLastError();
 }
 

@@ -137,11 +137,6 @@ struct ExplFusedArgs {                  // expl_split.hip: the exploration actio
   // 8-byte granules {value bits, done_seq | failed << 31} in host memory, in
   // place of the drained outputs + completion word (no wait for the stores)
   unsigned long long* tags;
-  // the armed call (launch_expl_armed): the observation as [Do] tagged host
-  // granules {value bits, done_seq}, and the host's cancel word (== done_seq:
-  // leave without a result)
-  const unsigned long long* obs_tags;
-  const unsigned* cancel;
 };
 // expl_split.hip: one observation per group of expl_split_group(rows) <=
 // kExplGroup workgroups; a launch carries at most kExplRows observations
@@ -160,7 +155,6 @@ constexpr int kExplObsArg = 512;
 struct ExplObsArg { float v[kExplObsArg]; };
 hipError_t launch_expl_split_obs(const ExplFusedArgs& a, const ExplObsArg& obs, float* scratch,
                                  hipStream_t s);
-hipError_t launch_expl_armed(const ExplFusedArgs& a, float* scratch, hipStream_t s);
 
 // row-wise network evaluation off the gradient step (mlp_eval.hip)
 struct MlpEvalArgs {

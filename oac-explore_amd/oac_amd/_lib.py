@@ -157,7 +157,6 @@ _SIGS = {
                                              ctypes.POINTER(ctypes.c_void_p)]),
     "oac_expl_action_now": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float,
                                            ctypes.c_float, ctypes.c_void_p]),
-    "oac_expl_disarm": (ctypes.c_int, [ctypes.c_void_p]),
 }
 
 # every symbol include/oac_amd.h declares (checked by tests/test_abi.py)

@@ -262,8 +262,6 @@ class _DataParallel:
     def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None, n_steps=1,
              counts=None, pre=None):
         self._closed = False
-        if self._expl_armed:
-            self._disarm_expl()
 
         def go(sp):
             if pre is not None:

@@ -109,7 +109,6 @@ def _action_now(ob_np, policy, qfs, trainer, hyper_params):
                                            torch.cuda.current_device())
     check(L.oac_expl_action_now(e.handle, None, float(hyper_params["beta_UB"]),
                                 float(hyper_params["delta"]), ctypes.c_void_p(s)))
-    t._expl_armed = _ARMED   # the next call's kernel waits (oac_expl_action_now)
     return e.out_np[0, 0].copy()
 
 
@@ -127,9 +126,6 @@ def get_optimistic_exploration_actions(obs_np, policy=None, qfs=None, trainer=No
 
 
 _USE_GRAPH = os.environ.get("OAC_EXPL_GRAPH", "0") == "1"
-# the single-observation Philox call arms the next call's kernel (liboac_amd's
-# OAC_EXPL_ARMED, default on); the trainer's next step cancels it first
-_ARMED = os.environ.get("OAC_EXPL_ARMED", "1") != "0"
 
 
 def _actions(t, obs, hyper_params, eps, return_info, trainer_ub=False):
@@ -139,8 +135,6 @@ def _actions(t, obs, hyper_params, eps, return_info, trainer_ub=False):
     OAC_EXPL_GRAPH=1: the captured-graph path instead (oac_expl_action: upload,
     kernel and download replayed, then a stream synchronisation)."""
     n = obs.shape[0]
-    if t._expl_armed:   # a waiting single-call kernel holds 32 CUs: the batched
-        t._disarm_expl()   # call's workgroups must all be resident at once
     e = t._expl_handle(n)
     if t.layout.q2_base < 0:   # K heads: mean + beta std, or trainer.predict's sorted head
         check(_lib.lib().oac_expl_set_ub_index(e.handle, int(t.delta_index) if trainer_ub else -1))

@@ -158,7 +158,6 @@ class _ArenaTrainer(object):
         self._bc_mirror = None   # host copy of step_state.batch_counter (drop-in path)
         self._idx = None
         self._expl = None
-        self._expl_armed = False   # a single-observation exploration kernel may be armed
         self._last_plan = None
         # all library work runs on a dedicated stream: hipGraph capture needs a
         # non-default stream, and it keeps the step off torch's null stream.
@@ -260,18 +259,8 @@ class _ArenaTrainer(object):
         put(r["off_term"], 1, batch["terminals"])
         put(r["off_next_obs"], Do, batch["next_observations"])
 
-    def _disarm_expl(self):
-        """Cancel the armed exploration kernel of the single-observation
-        handle (oac_expl_disarm): the training step gets every CU."""
-        self._expl_armed = False
-        L = _lib.lib()
-        for e in (self._expl or {}).values():
-            check(L.oac_expl_disarm(e.handle))
-
     def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None, n_steps=1,
              counts=None):
-        if self._expl_armed:
-            self._disarm_expl()
         def go(sp):
             f = flags
             if batch is not None:
@@ -306,8 +295,6 @@ class _ArenaTrainer(object):
         """trainer.py:99-103.  Accepts the reference's numpy batch dict, or the
         device batch returned by oac_amd.ReplayBuffer.random_batch (gathered
         on the GPU inside the step -- no host copy)."""
-        if self._expl_armed:
-            self._disarm_expl()
         np_batch = dict(np_batch) if not hasattr(np_batch, "device_gather") else np_batch
         if hasattr(np_batch, "device_gather"):
             self.train_device_batch(np_batch)

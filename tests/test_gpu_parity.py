@@ -345,45 +345,3 @@ def test_single_call_philox_path():
     with pytest.raises(NotImplementedError):
         get_optimistic_exploration_action(ob, policy=tr.policy, qfs=[tr.qf2, tr.qf1],
                                           hyper_params=hp)
-
-
-def test_armed_single_calls_equal_plain_calls():
-    """The armed single-observation call (oac_expl_action_now launches the next
-    call's kernel ahead; it waits for its observation in host memory): every
-    call is bitwise the plain launch on the same Philox counter (row 0 of a
-    2-row call, another handle), across a re-arm after the host limit (a call
-    more than 10 ms after arming), a bound change (the waiting kernel is
-    cancelled), and a training step in between (the trainer disarms first;
-    the next call reads the updated weights)."""
-    import time
-    from oac_amd import get_optimistic_exploration_action, get_optimistic_exploration_actions
-    meta, g = parity.load("oac_expl_humanoid")
-    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"],
-                        pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"])
-    m = dict(obs_dim=meta["obs_dim"], act_dim=meta["act_dim"], hidden=meta["hidden"],
-             discount=0.99, reward_scale=1.0, lr=3e-4, tau=5e-3, auto_alpha=True, log_alpha0=0.0,
-             seed=meta["seed"], pi_init_w=meta["pi_init_w"], q_init_w=meta["q_init_w"])
-    tr = sac_trainer_for(m, params=params)
-    hp = dict(beta_UB=meta["beta_UB"], delta=meta["delta"], share_layers=False)
-    rs = np.random.RandomState(11)
-    Do, Da, B = meta["obs_dim"], meta["act_dim"], 256
-    batch = dict(observations=rs.standard_normal((B, Do)).astype(np.float32),
-                 actions=rs.uniform(-0.9, 0.9, (B, Da)).astype(np.float32),
-                 rewards=rs.standard_normal((B, 1)).astype(np.float32),
-                 terminals=(rs.uniform(size=(B, 1)) < 0.1).astype(np.float32),
-                 next_observations=rs.standard_normal((B, Do)).astype(np.float32))
-    obs = list(g["obs"]) + list(rs.standard_normal((4, Do)))
-    for i, ob in enumerate(obs):
-        h = dict(hp, beta_UB=hp["beta_UB"] * 0.5) if i == 4 else hp
-        if i == 2:
-            time.sleep(0.015)   # past the host limit: the waiting kernel is not published to
-        if i == 5:
-            tr.train(batch)     # disarms; the weights change
-        c = int(tr.step_state[2].item())
-        a, _ = get_optimistic_exploration_action(ob, policy=tr.policy, qfs=tr.qfs, hyper_params=h)
-        assert int(tr.step_state[2].item()) == c + 1
-        tr.step_state[2] = c
-        A, _ = get_optimistic_exploration_actions(np.stack([ob, ob]), policy=tr.policy, qfs=tr.qfs,
-                                                  hyper_params=h)
-        assert int(tr.step_state[2].item()) == c + 1
-        np.testing.assert_array_equal(a, A[0])
