@@ -13,3 +13,6 @@ for i in 1 2; do
     echo "direct=$v poac $(grep -v amdgpu gpurun_out/r4_t9_lt.log | head -1)"
   done
 done
+# the dataflow critic branch with its batches in the kernel arguments (global loads)
+timeout -k 10 120 tools/micro/dataflow_micro > gpurun_out/r4_dataflow_micro2.log 2>&1; crash $?
+cat gpurun_out/r4_dataflow_micro2.log

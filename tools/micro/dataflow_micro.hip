@@ -89,10 +89,19 @@ __device__ __forceinline__ void signal_dep(unsigned* ctr, const TileDep& d) {
   }
 }
 
+// the three stages' batches travel in the kernel arguments (as a launch's
+// batch does): pointers loaded from the argument segment are known to be
+// global, so the tiles' operand accesses are global loads -- from a batch in
+// global memory they were flat loads (generic pointers), which also count
+// against lgkmcnt and serialise with the LDS reduction
+struct Stages { GemmBatch st[3]; GemmHead hh[3]; };
+
 template <int NW, int GPW, bool FENCE>
 __global__ void __launch_bounds__(64 * NW)
-dataflow_kernel(const GemmBatch* bs, const GemmHead* hs, const TileDep* deps, int nst,
+dataflow_kernel(const Stages sg, const TileDep* __restrict__ deps, int nst,
                 unsigned* ctr, unsigned long long* clk) {
+  const GemmBatch* bs = sg.st;
+  const GemmHead* hs = sg.hh;
   __shared__ __attribute__((aligned(16))) float red[SmallLds<NW>::N];
   unsigned long long* my = clk + (long)blockIdx.x * kEdges;
   if (threadIdx.x == 0) my[0] = wall_clock64();
@@ -253,11 +262,14 @@ int main() {
         CK(gemm_small_launch(b, s));
       }
     };
+    Stages sg;
+    for (int i = 0; i < 3; ++i) { sg.st[i] = br.st[i]; sg.hh[i] = hh[i]; }
     auto dataflow = [&]() {
       if (uncached)
-        hipLaunchKernelGGL((dataflow_kernel<16, 4, false>), dim3(256), dim3(1024), 0, s, d_st, d_hh, d_dep, 3, ctr, clk);
+        hipLaunchKernelGGL((dataflow_kernel<16, 4, false>), dim3(256), dim3(1024), 0, s, sg, d_dep, 3, ctr, clk);
       else
-        hipLaunchKernelGGL((dataflow_kernel<16, 4, true>), dim3(256), dim3(1024), 0, s, d_st, d_hh, d_dep, 3, ctr, clk);
+        hipLaunchKernelGGL((dataflow_kernel<16, 4, true>), dim3(256), dim3(1024), 0, s, sg, d_dep, 3, ctr, clk);
+      CK(hipGetLastError());
     };
     launches(16); CK(hipStreamSynchronize(s));
     const std::vector<float> ref = snapshot();
