@@ -169,15 +169,16 @@ int oac_sac_step_n(oac_sac* h, int flags, int n_steps, void* stream);
  * (ring_slots = the handle's idx_ring slots, a multiple of 16).  step_host_idx
  * copies the step's B int64 indices (host memory, each in [0, replay_rows))
  * into staging slot bc % ring_slots, enqueues the H2D copy into the idx_ring
- * slot the step's gather reads, and enqueues the captured one-step graph --
+ * slot the step's gather reads, and enqueues the step's launches (issued
+ * directly: a one-step graph launch cost more than the launches it holds;
+ * OAC_DROPIN_GRAPH=1 enqueues the captured one-step graph instead) --
  * all on `stream`, with no host synchronisation (a staging slot is rewritten
  * only after the copy that last read it has completed).  bc = the device
  * step_state batch counter at this step (the caller mirrors it).
  * pinned_ring = NULL: the handle allocates its own host-coherent ring
  * (oac_sac_host_ring returns it) and, at small batch (the batch-256 kernel
  * set), reads the step's indices straight from it inside the step's first
- * launch -- no H2D copy and no gather launch (OAC_DROPIN_DIRECT=0: the copy
- * path on the same ring). */
+ * launch -- no H2D copy and no gather launch. */
 int oac_sac_set_host_ring(oac_sac* h, int32_t* pinned_ring);
 int32_t* oac_sac_host_ring(oac_sac* h);
 int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags, void* stream);

@@ -921,9 +921,12 @@ int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags,
   }
   const bool hr = h->plan.idx_host;
   if (stage_host_idx(h, idx, bc, stream, hr || h->plan.rows_direct)) return 1;
-  // (OAC_DROPIN_DIRECT=1, A/B: the step's launches issued directly instead
-  // of as one graph launch)
-  static const bool direct_launch = [] { const char* e = getenv("OAC_DROPIN_DIRECT"); return e && atoi(e) == 1; }();
+  // the one-step drop-in call issues its launches directly: the same kernels
+  // as the step graph, but one hipGraphLaunch per step cost more than the
+  // host's 12 launch calls (same-box A/B, the bench line: B=256 10,443-10,491
+  // -> 11,015-11,049 steps/s, B=4096 3,688-3,696 -> 3,740-3,749, configs[4]
+  // 4,878-4,897 -> 5,028-5,035).  OAC_DROPIN_GRAPH=1: the graph launch.
+  static const bool direct_launch = [] { const char* e = getenv("OAC_DROPIN_GRAPH"); return !e || atoi(e) == 0; }();
   return oac_sac_step_n(h, flags | OAC_STEP_GATHER | (direct_launch ? 0 : OAC_STEP_USE_GRAPH) |
                                (hr ? kStepHostIdx : 0), 1,
                         stream);

@@ -343,7 +343,7 @@ class _ArenaTrainer(object):
     def _train_host_indices(self, dbatch):
         """rl_algorithm.py:160-167 as the reference calls it: random_batch drew
         the indices on numpy's global stream; this call stages them through a
-        pinned ring and enqueues copy + one-step graph on torch's current
+        pinned ring and enqueues the step's launches on torch's current
         stream (ordered after replay inserts and before any later use of the
         parameters, with no host synchronisation)."""
         plan = self._dropin_plan(dbatch)
