@@ -105,19 +105,23 @@ dataflow_kernel(const Stages sg, const TileDep* __restrict__ deps, int nst,
   __shared__ __attribute__((aligned(16))) float red[SmallLds<NW>::N];
   unsigned long long* my = clk + (long)blockIdx.x * kEdges;
   if (threadIdx.x == 0) my[0] = wall_clock64();
-  int off = 0;
+  int off = 0, extra = 0;   // extra: workgroups [0, extra) took a second tile last stage
   for (int st = 0; st < nst; ++st) {
     const GemmHead h = hs[st];
-    for (int vb = blockIdx.x; vb < h.total_tiles; vb += gridDim.x) {
+    // this stage's tiles start past the workgroups still busy with a second
+    // tile of the last stage (tile (w - extra) mod grid for workgroup w)
+    const int w0 = ((int)blockIdx.x - extra + (int)gridDim.x) % (int)gridDim.x;
+    for (int vb = w0; vb < h.total_tiles; vb += gridDim.x) {
       const TileDep d = deps[off + vb];
       wait_dep<FENCE>(ctr, d);
-      if (threadIdx.x == 0 && vb == (int)blockIdx.x && st > 0) my[2 * st] = wall_clock64();
+      if (threadIdx.x == 0 && vb == w0 && st > 0) my[2 * st] = wall_clock64();
       gemm_small_block<NW, GPW>(vb, h.total_tiles, h.publish, h.tb1, h.tb2, h.tb3, h.tb4, h.tb5,
                                 h.tb6, h.tb7, bs[st], red);
       signal_dep<FENCE>(ctr, d);
     }
     if (threadIdx.x == 0) my[2 * st + 1] = wall_clock64();
     off += h.total_tiles;
+    extra = h.total_tiles > (int)gridDim.x ? h.total_tiles - (int)gridDim.x : 0;
   }
   // exit: the last workgroup out resets every counter for the next replay
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
