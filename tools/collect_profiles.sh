@@ -27,4 +27,5 @@ cp gpurun_out/lt_b256.log $D/launch_times_b256.txt
 cp gpurun_out/lt_b4096.log $D/launch_times_b4096.txt
 cp gpurun_out/lt_poac.log $D/launch_times_poac.txt
 cp gpurun_out/expl_micro.log $D/expl_micro.txt
+cp gpurun_out/dataflow_micro.log $D/dataflow_micro_b256.txt
 echo "profiles -> $D"

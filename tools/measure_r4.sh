@@ -23,4 +23,5 @@ timeout -k 10 200 python tools/launch_times.py --batch 256 > gpurun_out/lt_b256.
 timeout -k 10 200 python tools/launch_times.py --batch 4096 > gpurun_out/lt_b4096.log 2>&1; crash $?
 timeout -k 10 200 python tools/launch_times.py --batch 4096 --poac > gpurun_out/lt_poac.log 2>&1; crash $?
 timeout -k 10 60 tools/micro/expl_micro 400 1 0 > gpurun_out/expl_micro.log 2>&1; crash $?
+timeout -k 10 120 tools/micro/dataflow_micro > gpurun_out/dataflow_micro.log 2>&1; crash $?
 tail -1 gpurun_out/bench256.log | cut -c1-300
