@@ -1,9 +1,9 @@
 """Per-edge clocks of one step from a rocprofv3 kernel trace.
 
-The drop-in step is one graph launch per train() call, so in the trace a
+The drop-in step is one train() call's queued launches, so in the trace a
 step is a burst of back-to-back kernels separated from the next by the host's
 per-call work.  Bursts of exactly N kernels (the step's launch count) are the
-graph steps; this prints the median-span one: each kernel's duration and the
+steps; this prints the median-span one: each kernel's duration and the
 gap from the previous kernel's end (the launch edge inside the graph), then
 the burst's span and kernel sum, and the edge statistics over all bursts.
 
@@ -43,7 +43,7 @@ for j, i in enumerate(b):
     nm = r[i]['Kernel_Name'].split('(')[0].replace('void ', '')[:48]
     print(nm.ljust(50), 'dur %6.2f us  edge %5.2f us  wg %s grid %s'
           % (dur, gap, r[i]['Workgroup_Size_X'], r[i]['Grid_Size_X']))
-print('median step of %d graph steps: span %.1f us, kernel sum %.1f us, %d edges %.2f us'
+print('median step of %d steps: span %.1f us, kernel sum %.1f us, %d edges %.2f us'
       % (len(steps), span(b), tot, n - 1, span(b) - tot))
 edges = [(t0[i] - t1[i - 1]) / 1e3 for s in steps for i in s[1:]]
 print('edges over all steps: median %.2f us, p10 %.2f, p90 %.2f'
