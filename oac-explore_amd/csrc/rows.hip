@@ -431,14 +431,39 @@ __device__ __forceinline__ void particle_targets_rows(const ParticleTargetArgs& 
       __syncthreads();
     }
   }
+  // both sorts by the whole block: 16 lanes per row, lane k ranks its value
+  // against the row's 16 (ties by head index, the +inf padding last) -- the
+  // order sort16's comparator defines, so the same permutation -- and scatters
+  // it into LDS; a row thread's bitonic network was ~1,000 dependent VALU ops
+  __shared__ float s_qv[kRowBlock][kMaxHeads], s_tv[kRowBlock][kMaxHeads];
+  __shared__ int s_qi[kRowBlock][kMaxHeads], s_ti[kRowBlock][kMaxHeads];
+  {
+    static_assert(kRowBlock * kMaxHeads == 256, "one thread per (row, head slot)");
+    const int row = threadIdx.x >> 4, k = threadIdx.x & 15, m = min(r0 + row, p.B - 1);
+    const int base = (threadIdx.x & 63) & ~15;
+    const float inf = __builtin_huge_valf();
+    const float qv = k < K ? (p.qh.h ? qs.out[row][k] : p.q[(long)m * K + k]) : inf;
+    const float tv = k < K ? (p.th.h ? hs.out[row][k] : p.tq[(long)m * K + k]) : inf;
+    int rq = 0, rt = 0;
+#pragma unroll
+    for (int j = 0; j < kMaxHeads; ++j) {
+      const float qj = __shfl(qv, base | j, 64), tj = __shfl(tv, base | j, 64);
+      rq += (qj < qv || (qj == qv && j < k)) ? 1 : 0;
+      rt += (tj < tv || (tj == tv && j < k)) ? 1 : 0;
+    }
+    s_qv[row][rq] = qv; s_qi[row][rq] = k;
+    s_tv[row][rt] = tv; s_ti[row][rt] = k;
+  }
+  __syncthreads();
   if (threadIdx.x >= kRowBlock || r >= p.B) return;
   const float fK = (float)K;
   float q[kMaxHeads], t[kMaxHeads];
   int qi[kMaxHeads], tix[kMaxHeads];
-  load_row16(p.qh.h ? &qs.out[threadIdx.x][0] : p.q + (long)r * K, K, q, qi);
-  load_row16(p.th.h ? &hs.out[threadIdx.x][0] : p.tq + (long)r * K, K, t, tix);
-  sort16(q, qi);
-  sort16(t, tix);
+#pragma unroll
+  for (int i = 0; i < kMaxHeads; ++i) {
+    q[i] = s_qv[threadIdx.x][i]; qi[i] = s_qi[threadIdx.x][i];
+    t[i] = s_tv[threadIdx.x][i]; tix[i] = s_ti[threadIdx.x][i];
+  }
   const float rew = p.batch[(long)r * p.ld_batch + p.off_rew];
   const float term = p.batch[(long)r * p.ld_batch + p.off_term];
   const float invB = 1.f / (float)p.B;
