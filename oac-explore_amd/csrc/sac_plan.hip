@@ -757,9 +757,7 @@ int oac_sac_step_n(oac_sac* h, int flags, int n_steps, void* stream) {
     }
     return 0;
   };
-  // (OAC_STEP_GRAPH=0, A/B: every graph-flagged call issued as direct launches)
-  static const bool graphs_on = [] { const char* e = getenv("OAC_STEP_GRAPH"); return !e || atoi(e) != 0; }();
-  if (!(flags & OAC_STEP_USE_GRAPH) || p.timing || !graphs_on) return steps(flags & ~OAC_STEP_USE_GRAPH);
+  if (!(flags & OAC_STEP_USE_GRAPH) || p.timing) return steps(flags & ~OAC_STEP_USE_GRAPH);
   const int gflags = flags & ~OAC_STEP_USE_GRAPH;
   if (!p.exec || p.graph_flags != gflags || p.graph_n != n_steps) {
     if (p.exec) { (void)hipGraphExecDestroy(p.exec); p.exec = nullptr; }

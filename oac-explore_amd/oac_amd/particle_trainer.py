@@ -34,7 +34,7 @@ class ParticleTrainer(_TargetPolicyTrainer):
                  mean_update=False, global_opt=False, std_soft_update=False,
                  std_soft_update_prob=0., train_bias=True, use_target_policy=False,
                  rescale_targets_around_mean=False,
-                 device=None, seed=0, use_graph=True, gemm_cfg=-1):
+                 device=None, seed=0, use_graph=False, gemm_cfg=-1):
         unsupported = dict(share_layers=not share_layers, deterministic=not deterministic,
                            ensemble=ensemble, global_opt=global_opt)
         bad = [k for k, v in unsupported.items() if v]

@@ -33,7 +33,7 @@ class ParticleTrainer(_ArenaTrainer):
                  r_mellow_max=1., b_mellow_max=None, mellow_max=False, counts=False,
                  mean_update=False, global_opt=False, std_soft_update=False,
                  std_soft_update_prob=0., train_bias=True, lb=0.1,
-                 device=None, seed=0, use_graph=True, gemm_cfg=-1):
+                 device=None, seed=0, use_graph=False, gemm_cfg=-1):
         unsupported = dict(share_layers=not share_layers, deterministic=deterministic,
                            ensemble=ensemble, mellow_max=mellow_max,
                            global_opt=global_opt, std_soft_update=std_soft_update)

@@ -364,7 +364,7 @@ class _ArenaTrainer(object):
         self._n_train_steps_total += 1
 
     def train_device_batch(self, dbatch, eps1=None, eps2=None):
-        if (dbatch.host_indices is not None and eps1 is None and self.use_graph
+        if (dbatch.host_indices is not None and eps1 is None
                 and self._batch_counts(dbatch) is None and not getattr(self, "_no_dropin", False)):
             return self._train_host_indices(dbatch)
         B = dbatch.batch_size
@@ -445,7 +445,7 @@ class SACTrainer(_ArenaTrainer):
                  reward_scale=1.0, policy_lr=1e-3, qf_lr=1e-3, optimizer_class=None,
                  soft_target_tau=1e-2, target_update_period=1,
                  use_automatic_entropy_tuning=True, target_entropy=None, deterministic=False,
-                 device=None, seed=0, use_graph=True, gemm_cfg=-1):
+                 device=None, seed=0, use_graph=False, gemm_cfg=-1):
         self.device = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
         self.use_automatic_entropy_tuning = use_automatic_entropy_tuning
@@ -462,6 +462,11 @@ class SACTrainer(_ArenaTrainer):
         self.discount = discount
         self.reward_scale = reward_scale
         self.policy_lr, self.qf_lr = policy_lr, qf_lr
+        # use_graph: each step call replayed as a captured hipGraph (n steps per
+        # graph on the ring path).  Off by default: on MI355X / ROCm 7 the
+        # direct launches of the same kernels measured faster (same box: ring
+        # path 9,838 -> 10,456 steps/s, the counts recipes 6,444-6,565 ->
+        # 7,209-7,260; the drop-in call issues its launches directly anyway)
         self.use_graph = use_graph
         self.seed = int(seed)
         self._gemm_cfg = gemm_cfg
