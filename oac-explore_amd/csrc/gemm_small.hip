@@ -343,30 +343,12 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     ac = adam_consts(batch.adam.state, batch.adam.advance, batch.adam.lr, batch.adam.beta1,
                      batch.adam.beta2, batch.adam.eps, batch.adam.target, batch.adam.tau,
                      batch.adam.period);
-  // EPI_HEAD_BWD with t.C2 (the head's dX fused in): the tile's rows of
-  // dhead = [dmean | dls] also go to LDS for the dh2 pass below
-  const bool head_dx = t.epi == EPI_HEAD_BWD && t.C2 != nullptr;
-  float* hd = red;   // [32][2 N]
-  if (head_dx) __syncthreads();   // (every wave's reduction reads of red are done)
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int e = threadIdx.x + i * 64 * NW;
     const int r = e >> 6, l = e & 63;
     const int mt = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5);
     const int nt = l & 31;
-    if (head_dx) {
-      const int m = m0 + mt, n = n0 + nt;
-      float dmean = 0.f, dls = 0.f;
-      if (m < t.M && n < t.N) {
-        tanh_gauss_backward(vals[i], xin[i].xb, xin[i].xa, xin[i].am, xin[i].av, xin[i].at,
-                            xin[i].s * (1.f / (float)t.M), dmean, dls);
-        const long o = (long)m * t.ldc + n;
-        t.C[o] = dmean;
-        t.C[o + t.N] = dls;
-      }
-      if (nt < t.N) { hd[mt * 2 * t.N + nt] = dmean; hd[mt * 2 * t.N + t.N + nt] = dls; }
-      continue;
-    }
     epi_one(batch, ac, t, m0 + mt, n0 + nt, vals[i], xin[i], lds_u, lds_v, mt, nt);
     if (t.epi == EPI_BIAS_RELU_DOT) {
       // the 32 lanes of a half-wave hold one row's 32 columns: fixed butterfly
@@ -375,37 +357,6 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
 #pragma unroll
       for (int off = 16; off > 0; off >>= 1) x += __shfl_xor(x, off, 32);
       if (nt == 0 && m < t.M) t.C2[(long)(n0 >> 5) * t.ldc2 + m] = x;   // tile-major
-    }
-  }
-  if (head_dx) {
-    // dh2 = (dhead . W_head) masked by h2 > 0 for the tile's 32 rows and all
-    // t.R hidden columns: one 32-column block per wave and pass, K = 2 N in
-    // v_mfma_f32_32x32x2_f32 steps (lane l: A = dhead[l & 31][k], B =
-    // W_head[k][col], k = 2 step + (l >> 5)); the h2 mask loads go first
-    __syncthreads();
-    const int D2 = 2 * t.N, nsteps = (D2 + 1) >> 1, ncb = t.R >> 5;
-    for (int cb = wave; cb < ncb; cb += NW) {
-      const int col = 32 * cb + (lane & 31);
-      float h2v[16];
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        const int m = min(m0 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5), t.M - 1);
-        h2v[rr] = t.aux[(long)m * t.ld_aux + col];
-      }
-      floatx16 c;
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr) c[rr] = 0.f;
-      for (int st = 0; st < nsteps; ++st) {
-        const int k = 2 * st + (lane >> 5);
-        const float a = k < D2 ? hd[(lane & 31) * D2 + k] : 0.f;
-        const float b = k < D2 ? t.V[(long)k * t.ldv + col] : 0.f;
-        c = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
-      }
-#pragma unroll
-      for (int rr = 0; rr < 16; ++rr) {
-        const int m = m0 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
-        if (m < t.M) t.C2[(long)m * t.ldc2 + col] = h2v[rr] > 0.f ? c[rr] : 0.f;
-      }
     }
   }
   if (batch.fuse_adam && bid == 0 && threadIdx.x == 0)
@@ -457,13 +408,6 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
     if (b.t[i].K2 > 0 && (b.t[i].ksplit > 1 || !b.t[i].a_kc || b.t[i].b_kc ||
                           b.t[i].a_mode != A_PLAIN))
       return hipErrorInvalidValue;
-  for (int i = 0; i < b.ntasks; ++i) {   // the fused head dX (EPI_HEAD_BWD with C2)
-    const GemmTask& t = b.t[i];
-    if (t.epi == EPI_HEAD_BWD && t.C2 &&
-        (t.N > 32 || t.ksplit > 1 || t.R < 32 || (t.R & 31) || !t.V || !t.aux ||
-         2 * t.N * 32 > SmallLds<1>::N))
-      return hipErrorInvalidValue;
-  }
   const int nw = b.force_nw > 0 ? b.force_nw : gemm_small_waves(b);
   const int gpw = b.force_gpw > 0 ? b.force_gpw : (nw >= 16 ? 4 : 5);
   b.adam_blocks = 0;

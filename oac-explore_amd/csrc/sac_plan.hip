@@ -477,17 +477,6 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
   return 0;
 }
 
-// Small batch: the heads' dX (dh2 = dhead . W_head through the h2 mask) in
-// the dL/da + head-backward launch -- each tile has all 2 Da dhead values of
-// its 32 rows, so it runs the K = 2 Da product for them (EPI_HEAD_BWD with
-// C2, gemm_small.hip) -- and the heads' dW in the policy layer-1 launch: one
-// launch fewer.  (At large batch the heads' dW in the layer-1 launch measured
-// slower, round 3.)  OAC_HEAD_DX=0 keeps the separate launch.
-static bool head_dx_fused(const SacPlan& p) {
-  static const bool on = [] { const char* e = getenv("OAC_HEAD_DX"); return !e || atoi(e) != 0; }();
-  return on && p.cfg == 0 && p.c.act_dim <= 32 && p.c.hidden % 32 == 0;
-}
-
 // prefetch: batch of the next step (its critic-side forward rides on this
 // step's policy-backward launches, small-batch path only), or null
 static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch = nullptr,
@@ -500,7 +489,6 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
   const float* pol = p.b.params;
   const float* q1 = p.b.params + L.q1_base;
   const float* q2 = p.b.params + L.q2_base;
-  const bool head_dx = head_dx_fused(p);
   {  // -min Q backward to layer 1 with post-step weights, pre-step masks
     GemmBatch gb{};
     const float* qs[2] = {q1, q2};
@@ -530,10 +518,6 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     t.ex[0] = p.W(OAC_WS_ACT1); t.ex[1] = p.W(W_STD1); t.ex[2] = p.W(W_U1);
     t.ex[3] = p.E1(); t.ex[4] = p.W(OAC_WS_HEAD1);
     t.ex[5] = c.auto_alpha ? &p.alpha()->alpha : nullptr;
-    if (head_dx) {   // dh2 = (dhead . W_head) [h2 > 0] of the tile's rows in the same launch
-      t.C2 = p.W(W_DH2P); t.ldc2 = H; t.aux = p.W(W_H2P); t.ld_aux = H;
-      t.V = pol + L.pol_head_w; t.ldv = H; t.R = H;
-    }
     add(gb, t);
     if (prefetch) add_target_l0(p, gb, prefetch);
     if (run_gemm(p, gb, s)) return 1;
@@ -554,7 +538,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
       p.launches++;
     }
   }
-  if (!head_dx) {  // policy heads: dW_head slab, dh2
+  {  // policy heads: dW_head slab, dh2
     GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, gp + L.pol_head_w,
@@ -563,18 +547,12 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     if (prefetch) add_critic_l1(p, gb);
     if (run_gemm(p, gb, s)) return 1;
   }
-  {  // policy layer 1 (with head_dx also the heads' dW, and the ring path's
-     // next-step critic layer 1)
+  {  // policy layer 1
     GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
                  L.pol_size, p.sp_p1));
     add(gb, t_dx(p.W(W_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_DH1P), H, p.W(W_H1P), H));
-    if (head_dx) {
-      add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, gp + L.pol_head_w,
-                   gp + L.pol_head_b, L.pol_size, p.sp_ph));
-      if (prefetch) add_critic_l1(p, gb);
-    }
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 0
