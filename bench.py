@@ -190,10 +190,12 @@ def roofline_of(kt, flop_per_sample, B, n, traffic_key=None, exec_flop_per_sampl
         a2 = fpl / (us * 1e-6) / 1e12
         out["rocprof"] = {"avg_launch_us": us, "achieved": round(a2, 3),
                           "frac": round(a2 / PEAK_FP32_TFLOPS, 4), "source": path,
-                          "note": "rocprofv3 stamps a queued kernel's start at the previous "
-                                  "kernel's end, so its durations include the launch edge "
-                                  "(step traces in the same directory: edges 0.00 us); the "
-                                  "dispatch events above exclude it"}
+                          "note": "a profiled run of the same command: under rocprofv3 the "
+                                  "direct-launch step is host-bound (kernels start after host "
+                                  "gaps), and back to back it stamps a kernel's start at the "
+                                  "previous kernel's end (the launch edge inside the duration); "
+                                  "the dispatch events above are the timed process's own "
+                                  "(DESIGN.md section 4)"}
     if exec_flop_per_sample:
         out["executed_flops_per_launch"] = round(exec_flop_per_sample * B * n / max(gk["launches"], 1))
         out["note"] = ("numerator = SURVEY 8d algorithmic GEMM FLOPs; the MFMAs execute %.1f %% fewer "
