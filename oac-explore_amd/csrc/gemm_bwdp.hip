@@ -47,7 +47,7 @@ struct BwdG {
 };
 
 // one operand's LDS-DMA sources.  KC: ROWS x 32 k, 8 rows per instruction,
-// lane j -> row 8p + j / 8, chunk (j % 8) ^ (row & 7).  MN: 32 k x ROWS,
+// lane j -> row 8p + j / 8, chunk (j % 8) ^ kc_swz(row).  MN: 32 k x ROWS,
 // 256 / ROWS k-rows per instruction, lane j -> k-row p RP + j / (ROWS / 4),
 // columns 4 (j % (ROWS / 4)) .. + 3.
 template <bool KC, int ROWS>
@@ -65,7 +65,7 @@ struct PSrc {
       const int p = wave * P + q;
       if (KC) {
         const int r = 8 * p + (lane >> 3);
-        off[q] = 4 * ((lane & 7) ^ (r & 7));
+        off[q] = 4 * ((lane & 7) ^ kc_swz(r));
         row[q] = base + (long)min(r0 + r, rmax - 1) * ld_;
       } else {
         constexpr int LPR = ROWS / 4;             // lanes per k-row
@@ -97,7 +97,7 @@ struct PSrc {
 template <bool KC, int ROWS>
 __device__ __forceinline__ float4 pfrag(const float* img, int rr, int g, int half) {
   if (KC) {
-    const int slot = 4 * ((2 * g + half) ^ (rr & 7));
+    const int slot = 4 * ((2 * g + half) ^ kc_swz(rr));
     return *reinterpret_cast<const float4*>(img + rr * kFK + slot);
   } else {
     const float* p = img + (8 * g + 4 * half) * ROWS + rr;

@@ -15,7 +15,7 @@
 // third is read, the waits are counted (vmcnt = one stage's loads), and one
 // raw barrier per stage orders both the DMA's landing and the ring's reuse.
 // The LDS image is lane-linear, so the bank swizzle (16-byte chunk c of row r
-// at slot c ^ (r & 7)) is applied to the per-lane SOURCE address and undone
+// at slot c ^ kc_swz(r), gemm_pipe.h) is applied to the per-lane SOURCE address and undone
 // on the ds_read_b128 fragment reads.
 //
 // The MFMA sequence per accumulator is the register-direct kernel's (8-deep
@@ -106,21 +106,21 @@ __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // LDS-DMA sources: piece p (8 rows) of an operand is wave p / P's
   // instruction p % P; lane j fills row 8p + j / 8, slot j % 8 = chunk
-  // (j % 8) ^ (row & 7)
+  // (j % 8) ^ kc_swz(row)
   const float* sa[PA];
   const float* sb[PB];
   int ca[PA], cb[PB];
 #pragma unroll
   for (int q = 0; q < PA; ++q) {
     const int r = 8 * (wave * PA + q) + (lane >> 3);
-    ca[q] = 4 * ((lane & 7) ^ (r & 7));
+    ca[q] = 4 * ((lane & 7) ^ kc_swz(r));
     const int m = min(m0 + r, M - 1);
     sa[q] = A + (long)(rows ? rows[m] : m) * lda;
   }
 #pragma unroll
   for (int q = 0; q < PB; ++q) {
     const int r = 8 * (wave * PB + q) + (lane >> 3);
-    cb[q] = 4 * ((lane & 7) ^ (r & 7));
+    cb[q] = 4 * ((lane & 7) ^ kc_swz(r));
     sb[q] = B + (long)min(n0 + r, N - 1) * ldb;
   }
   auto issue = [&](int st) {
@@ -137,9 +137,10 @@ __device__ __forceinline__ void fwd_pipe(const float* A, long lda, int M, const 
       glds16(sb[q] + (k < k_hi ? k : kst), base + BM * kFK + (wave * PB + q) * 256);
     }
   };
-  // fragment reads: row r = (wave block) + 32 i + l32, chunk (2g + half) ^ (r & 7)
+  // fragment reads: row r = (wave block) + 32 i + l32, chunk (2g + half) ^ kc_swz(r)
+  // (the block bases are multiples of 32, so kc_swz(r) = kc_swz(l32))
   const int l32 = lane & 31, half = lane >> 5;
-  const int xh = l32 & 6, hl = half ^ (l32 & 1);
+  const int xh = kc_swz(l32) & 6, hl = half ^ (kc_swz(l32) & 1);
   int aoff[WM], boff[WN];
 #pragma unroll
   for (int i = 0; i < WM; ++i) aoff[i] = ((wave >> 1) * (BM / 2) + 32 * i + l32) * kFK;

@@ -27,6 +27,15 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Bank swizzle of a k-contiguous operand image (128-byte rows, 16-byte chunk
+// c of row r at slot c ^ kc_swz(r)).  ds_read_b128 is serviced in 16-lane
+// groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, the same + 32) over 64 banks
+// = two 128-byte rows, so a group's 8 even and 8 odd rows each need 8
+// distinct slots: r >> 1 gives that for the fragment reads (row = block base
+// + lane), r itself repeated every group's slots twice (2-way: SQ
+// LDS_BANK_CONFLICT was ~half of the forward's LDS cycles)
+__device__ __forceinline__ int kc_swz(int r) { return (r >> 1) & 7; }
+
 // LDS-DMA of 16 bytes per lane into dst + 16 lane (dst wave-uniform).  Inline
 // asm, so the compiler neither tracks it nor inserts its conservative
 // vmcnt(0) before every later ds_read of the same LDS array (the builtin

@@ -109,7 +109,7 @@ __device__ __forceinline__ EpiIn epi_prefetch(const GemmBatch& batch, const Gemm
       break;
     }
     case EPI_GRAD:
-      if (batch.fuse_adam) {
+      if (batch.fuse_adam && !t.no_adam) {
         const float* g = (t.b_ones && nc == t.N - 1) ? t.bias_grad + mc : t.C + (long)mc * t.ldc + nc;
         const long i = g - batch.adam.g;
         x.xb = batch.adam.p[i]; x.am = batch.adam.m[i]; x.av = batch.adam.v[i];
@@ -137,11 +137,12 @@ __device__ __forceinline__ void epi_one(const GemmBatch& batch, const AdamConsts
     case EPI_GRAD: {
       float* g = (t.b_ones && n == t.N - 1) ? t.bias_grad + m : t.C + o;
       *g = acc;
-      if (batch.fuse_adam) {   // adam_elem on the prefetched p, m, v, target
+      if (batch.fuse_adam && !t.no_adam) {   // adam_elem on the prefetched p, m, v, target
         const long i = g - batch.adam.g;
         float p = x.xb, m = x.am, v = x.av;
         adam1(ac, p, acc, m, v);
-        batch.adam.p[i] = p; batch.adam.m[i] = m; batch.adam.v[i] = v;
+        (batch.adam.p_out ? batch.adam.p_out : batch.adam.p)[i] = p;
+        batch.adam.m[i] = m; batch.adam.v[i] = v;
         if (ac.polyak) batch.adam.target[i] = polyak1(ac, x.at, p);
       }
       break;
@@ -246,6 +247,17 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   }
   if (bid >= total_tiles) {   // fused optimizer: flat Adam over the other ranges
     const AdamArgs& a = batch.adam;
+    if (a.copy_src) {   // (or the copy of updates an earlier launch computed into a.copy_src)
+      const long stride = (long)batch.adam_blocks * 64 * NW;
+      for (int sgi = 0; sgi < batch.nseg; ++sgi) {
+        const float4* src = reinterpret_cast<const float4*>(a.copy_src + batch.seg_off[sgi]);
+        float4* dst = reinterpret_cast<float4*>(a.p + batch.seg_off[sgi]);
+        const long n4 = batch.seg_n[sgi] >> 2;
+        for (long i = (long)(bid - total_tiles) * 64 * NW + threadIdx.x; i < n4; i += stride)
+          dst[i] = src[i];
+      }
+      return;
+    }
     const AdamConsts c = adam_consts(a.state, a.advance, a.lr, a.beta1, a.beta2, a.eps,
                                      a.target, a.tau, a.period);
     const long stride = (long)batch.adam_blocks * 64 * NW;
@@ -359,7 +371,7 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
       if (nt == 0 && m < t.M) t.C2[(long)(n0 >> 5) * t.ldc2 + m] = x;   // tile-major
     }
   }
-  if (batch.fuse_adam && bid == 0 && threadIdx.x == 0)
+  if (batch.fuse_adam && !batch.adam.no_book && bid == 0 && threadIdx.x == 0)
     step_bookkeeping(batch.adam.state, batch.adam.alpha, batch.adam.advance);
   GS_STAGE(4);
 }
@@ -418,7 +430,7 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
       n4 = std::max(n4, b.seg_n[i] >> 2);
     }
     b.adam_blocks = (int)std::min<long>((n4 + 64 * nw - 1) / (64 * nw), 1024);
-    if (b.adam_blocks < 1) b.adam_blocks = 1;
+    if (b.adam_blocks < 1 && b.nseg > 0) b.adam_blocks = 1;
   }
   const int grid = b.total_tiles + b.adam_blocks + (b.rg.ring ? b.rg.blocks : 0);
   const GemmHead h = gemm_head(b);

@@ -70,6 +70,7 @@ struct GemmTask {
   int K2;
   const float* ex[6];   // extra epilogue operands (EPI_HEAD_BWD)
   int a_rows;           // small kernel: A (and U) row m is row batch.rg rows[m] of the buffer
+  int no_adam;          // EPI_GRAD in a fused-Adam batch: store the gradient only (another group's)
 };
 
 struct StepState;
@@ -89,6 +90,8 @@ struct AdamArgs {
   float gscale;      // gradient scale (1/world_size after an all-reduce SUM)
   int reduce_only;   // data-parallel: only reduce the slabs into g (all-reduce next)
   int no_book;       // skip the state / alpha bookkeeping (a partial range of the group)
+  float* p_out;      // small-kernel epilogue Adam: the updated p goes here (same index), not to p
+  const float* copy_src;   // small-kernel side blocks: copy this (same index) into p, no Adam
 };
 
 constexpr int kMaxTasks = 8;

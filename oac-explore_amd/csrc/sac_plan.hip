@@ -71,6 +71,7 @@ enum Ws {
   W_STD1, W_U1, W_STD2, W_U2, W_DQ1, W_DQ2, W_GQ1, W_GQ2,
   W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DA1, W_DA2, W_DHEAD, W_DH2P, W_DH1P,
   W_QPART,   // [6][B][tiles]: per-tile partial dots of the width-1 critic heads
+  W_QSHADOW, // fused small-batch step: both critics' post-step layer 1 + last layer (minq_merged)
   W_COUNT
 };
 
@@ -94,6 +95,7 @@ static void layout_workspace(SacPlan& p) {
   for (int id : {W_DH1Q1, W_DH1Q2, W_DH1N1, W_DH1N2, W_DH2P, W_DH1P}) set(id, B, H);
   set(W_DHEAD, B, 2 * Da);
   set(W_QPART, QV_COUNT * B, (H + 31) / 32);
+  if (can_fuse_adam(p)) set(W_QSHADOW, 1, p.L.n_critics * p.L.q_size);   // (same indexing as the group)
   if (p.S_q > 1) set(WS_GSLAB_Q, p.S_q, p.L.n_critics * p.L.q_size);
   if (p.S_p > 1) set(WS_GSLAB_P, p.S_p, p.L.pol_size);
   int64_t off = 0;
@@ -184,6 +186,72 @@ static void add_critic_l1(SacPlan& p, GemmBatch& gb) {
   const float* q2 = p.b.params + p.L.q2_base;
   add(gb, q_l1(p, p.W(W_H1Q1), q1, p.W(W_H2Q1), QV_Q1));
   add(gb, q_l1(p, p.W(W_H1Q2), q2, p.W(W_H2Q2), QV_Q2));
+}
+
+// Fused small-batch step (can_fuse_adam): the critic layer-1 backward launch
+// applies Adam to its layer-1 / last-layer dW tiles in their epilogue, with
+// the updated weights written to W_QSHADOW instead of in place (that
+// launch's dh1 tiles still read the pre-step weights).  The -min Q backward to
+// layer 1 -- which needs exactly those post-step weights -- then reads them
+// from the shadow and runs inside the critic layer-0 dW launch (whose side
+// blocks copy the shadow into the parameters) instead of a launch of its own:
+// one launch fewer on the step's chain.  OAC_MINQ_MERGE=0 keeps the separate
+// launch (A/B runs).
+static bool defer_dw0_on() {   // OAC_DW0_DEFER=0: keep the obs columns' dW in the layer-0 launch
+  static const bool on = [] { const char* e = getenv("OAC_DW0_DEFER"); return !e || atoi(e) != 0; }();
+  return on;
+}
+static bool minq_merged(const SacPlan& p) {
+  static const bool on = [] { const char* e = getenv("OAC_MINQ_MERGE"); return !e || atoi(e) != 0; }();
+  return on && can_fuse_adam(p) && p.ws[W_QSHADOW].rows > 0;
+}
+
+// -min Q backward to layer 1 with post-step weights (critic i's layer 1 and
+// last layer at qw[i]: the parameters, or the shadow), pre-step masks
+static void add_minq_bwd(SacPlan& p, GemmBatch& gb, const float* const (&qw)[2]) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  const int B = c.batch, H = c.hidden;
+  const int gq[2] = {W_GQ1, W_GQ2}, h2[2] = {W_H2N1, W_H2N2}, h1[2] = {W_H1N1, W_H1N2};
+  const int out[2] = {W_DH1N1, W_DH1N2};
+  for (int i = 0; i < 2; ++i) {
+    GemmTask d = t_dx(nullptr, 0, B, H, qw[i] + L.q_fc1_w, H, H, p.W(out[i]), H, p.W(h1[i]), H);
+    set_rank1(d, p.W(gq[i]), qw[i] + L.q_last_w, p.W(h2[i]), H);
+    add(gb, d);
+  }
+}
+
+// Critic i's layer-0 dW over input columns [c0, c0 + n) of the [obs | act]
+// row (+ the bias column when `bias`); (0, Dq, true) is the whole product.
+// Each element's sum over the batch does not depend on the column range, so
+// the parts are bitwise the whole.
+static GemmTask critic_dw0(SacPlan& p, int i, int c0, int n, bool bias) {
+  const oac_sac_config& c = p.c;
+  const oac_sac_layout& L = p.L;
+  float* g = grad_q(p) + i * L.q_size;
+  const int dh1 = i ? W_DH1Q2 : W_DH1Q1;
+  GemmTask t = t_dw(p.W(dh1), c.hidden, c.hidden, c.batch, p.X() + c.off_obs + c0, c.row_stride, n,
+                    g + L.q_fc0_w + c0, g + L.q_fc0_b, q_group(p), p.sp_q0);
+  t.ldc = c.obs_dim + c.act_dim;
+  if (!bias) { t.N = n; t.b_ones = 0; t.bias_grad = nullptr; }
+  return t;
+}
+
+// With the -min Q backward merged (minq_merged), the dL/da launch after it
+// reads only the action columns of the post-step critic layer 0, so the obs
+// columns' dW + Adam (+ Polyak) -- 192 of that launch's 208 tiles at B=256,
+// which had pushed it past one workgroup per CU -- move to the two launches
+// after the dL/da one (policy heads, policy layer 1: nothing in them or
+// later in the step reads the critic's layer 0), one critic each, their
+// epilogues applying the critic Adam to these tiles only.  Not with a
+// next-step prefetch (its critic forward reads the post-step layer 0 in the
+// launch after the dL/da one).
+static void add_deferred_dw0(SacPlan& p, GemmBatch& gb, int i) {
+  for (int k = 0; k < gb.ntasks; ++k) gb.t[k].no_adam = 1;   // (the policy's gradients)
+  add(gb, critic_dw0(p, i, 0, p.c.obs_dim, false));
+  AdamArgs a = critic_adam(p, 0, nullptr);
+  a.no_book = 1;
+  fuse_adam(gb, a, 0, nullptr, nullptr);
 }
 
 int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long* off,
@@ -352,7 +420,8 @@ static bool wl_in_targets(const SacPlan& p) {
 // part 0: the whole phase; 1: the fresh-action critic forward only (layer 1 +
 // last layer: no alpha needed, so the data-parallel alpha all-reduce overlaps
 // it); 2: the rest (targets through the critic gradients)
-static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool split = false) {
+static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool split = false,
+                  bool defer = false) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -442,19 +511,30 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
       set_rank1(d, p.W(dq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
       add(gb, d);
     }
+    if (fused && minq_merged(p)) {   // layer 1 + last layer: Adam in the dW epilogues, into the shadow
+      AdamArgs a = critic_adam(p, 0, nullptr);
+      a.no_book = 1;   // (the layer-0 launch does the step's bookkeeping)
+      a.p_out = p.W(W_QSHADOW);
+      fuse_adam(gb, a, 0, nullptr, nullptr);
+    }
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // critic backward, layer 0 (input = [obs | act] contiguous in the row)
     GemmBatch gb{};
-    float* gq = grad_q(p);
-    const long gs = q_group(p);
-    add(gb, t_dw(p.W(W_DH1Q1), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_fc0_w, gq + L.q_fc0_b, gs, p.sp_q0));
-    add(gb, t_dw(p.W(W_DH1Q2), H, H, B, X + c.off_obs, RS, Dq, gq + L.q_size + L.q_fc0_w,
-                 gq + L.q_size + L.q_fc0_b, gs, p.sp_q0));
+    const bool dfr = defer && fused && minq_merged(p);   // obs columns later (add_deferred_dw0)
+    for (int i = 0; i < 2; ++i)
+      add(gb, dfr ? critic_dw0(p, i, Do, Da, true) : critic_dw0(p, i, 0, Dq, true));
     if (fused) {  // SAC commits the alpha update in the critic Adam
       const long off[2] = {(long)L.q_fc1_w, (long)(L.q_size + L.q_fc1_w)};
       const long n[2] = {(long)(L.q_size - L.q_fc1_w), (long)(L.q_size - L.q_fc1_w)};
-      fuse_adam(gb, critic_adam(p, 0, c.auto_alpha ? p.alpha() : nullptr), 2, off, n);
+      AdamArgs a = critic_adam(p, 0, c.auto_alpha ? p.alpha() : nullptr);
+      if (minq_merged(p)) {   // side blocks: the shadow's layer 1 + last layer into the parameters;
+        a.copy_src = p.W(W_QSHADOW);   // the -min Q backward reads them from the shadow
+        const float* sh = p.W(W_QSHADOW);
+        const float* const qw[2] = {sh, sh + L.q_size};
+        add_minq_bwd(p, gb, qw);
+      }
+      fuse_adam(gb, a, 2, off, n);
     } else if (split) {   // layer 1 + last layer of both critics (their gradients are final)
       const long off[2] = {(long)L.q_fc1_w, (long)(L.q_size + L.q_fc1_w)};
       const long n[2] = {(long)(L.q_size - L.q_fc1_w), (long)(L.q_size - L.q_fc1_w)};
@@ -480,7 +560,7 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
 // prefetch: batch of the next step (its critic-side forward rides on this
 // step's policy-backward launches, small-batch path only), or null
 static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch = nullptr,
-                  bool split = false) {
+                  bool split = false, bool defer = false) {
   const oac_sac_config& c = p.c;
   const oac_sac_layout& L = p.L;
   const int B = c.batch, H = c.hidden, Do = c.obs_dim, Da = c.act_dim, RS = c.row_stride;
@@ -489,16 +569,12 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
   const float* pol = p.b.params;
   const float* q1 = p.b.params + L.q1_base;
   const float* q2 = p.b.params + L.q2_base;
-  {  // -min Q backward to layer 1 with post-step weights, pre-step masks
+  const bool merged = fused && minq_merged(p);   // (then the critic layer-0 dW launch ran it)
+  const bool dfr = defer && merged && !prefetch;
+  if (!merged) {  // -min Q backward to layer 1 with post-step weights, pre-step masks
     GemmBatch gb{};
-    const float* qs[2] = {q1, q2};
-    const int gq[2] = {W_GQ1, W_GQ2}, h2[2] = {W_H2N1, W_H2N2}, h1[2] = {W_H1N1, W_H1N2};
-    const int out[2] = {W_DH1N1, W_DH1N2};
-    for (int i = 0; i < 2; ++i) {
-      GemmTask d = t_dx(nullptr, 0, B, H, qs[i] + L.q_fc1_w, H, H, p.W(out[i]), H, p.W(h1[i]), H);
-      set_rank1(d, p.W(gq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
-      add(gb, d);
-    }
+    const float* const qs[2] = {q1, q2};
+    add_minq_bwd(p, gb, qs);
     if (prefetch) add_critic_l0(p, gb, prefetch);
     if (split) {   // the critics' layer 0 (not read here; the dL/da launch reads it next)
       const long off[2] = {0, (long)L.q_size};
@@ -519,6 +595,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     t.ex[3] = p.E1(); t.ex[4] = p.W(OAC_WS_HEAD1);
     t.ex[5] = c.auto_alpha ? &p.alpha()->alpha : nullptr;
     add(gb, t);
+    if (prefetch && merged) add_critic_l0(p, gb, prefetch);
     if (prefetch) add_target_l0(p, gb, prefetch);
     if (run_gemm(p, gb, s)) return 1;
   } else {
@@ -545,6 +622,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
                  gp + L.pol_head_b, L.pol_size, p.sp_ph));
     add(gb, t_dx(p.W(W_DHEAD), 2 * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(W_DH2P), H, p.W(W_H2P), H));
     if (prefetch) add_critic_l1(p, gb);
+    if (dfr) add_deferred_dw0(p, gb, 0);
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 1
@@ -553,6 +631,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
                  L.pol_size, p.sp_p1));
     add(gb, t_dx(p.W(W_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_DH1P), H, p.W(W_H1P), H));
+    if (dfr) add_deferred_dw0(p, gb, 1);
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 0
@@ -590,11 +669,12 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
   const bool ahead = p.cfg == 0 && (flags & OAC_STEP_GATHER);
   if (phase0(p, flags, s, gather_n, ahead && p.slot > 0)) return 1;
   const bool split = !fused && split_adam_on(p);
-  if (phase1(p, s, fused, 0, split)) return 1;
-  if (!fused && !split && phase2_adam(p, s, 0)) return 1;
   const bool pf = ahead && i + 1 < n && p.slot + 1 < kXSlots;
+  const bool defer = !pf && defer_dw0_on();
+  if (phase1(p, s, fused, 0, split, defer)) return 1;
+  if (!fused && !split && phase2_adam(p, s, 0)) return 1;
   if (phase2(p, s, fused, pf ? p.W(OAC_WS_BATCH) + (long)(p.slot + 1) * c_batch_rows(p) : nullptr,
-             split))
+             split, defer))
     return 1;
   if (!fused) {
     AdamArgs a = policy_adam(p, 0, nullptr);
@@ -726,6 +806,16 @@ int oac_sac_create(const oac_sac_config* cfg, const oac_sac_buffers* bufs, oac_s
   else if (has_target_policy(p.c.kind)) det_layout_workspace(p);
   else layout_workspace(p);
   p.b = *bufs;
+  if (p.ws[W_QSHADOW].rows > 0 && p.b.workspace && p.b.params) {
+    // the shadow's float4 copies also carry the segments' al4 padding back
+    // into the parameters: start it as the parameters' own
+    const size_t bytes = sizeof(float) * (size_t)p.L.n_critics * p.L.q_size;
+    if (hipMemcpy(p.W(W_QSHADOW), p.b.params + p.L.q1_base, bytes, hipMemcpyDeviceToDevice) != hipSuccess) {
+      set_error("shadow init: %s", hipGetErrorString(hipGetLastError()));
+      delete h;
+      return 1;
+    }
+  }
   *out = h;
   return 0;
 }
