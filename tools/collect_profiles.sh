@@ -15,7 +15,7 @@ python3 tools/prof_summary.py gpurun_out/prof_b256 > $D/b256_gemm_avg.txt
 python3 tools/prof_summary.py gpurun_out/prof_b4096 > $D/b4096_gemm_avg.txt
 python3 tools/prof_summary.py gpurun_out/prof_poac4096 > $D/poac4096_gemm_avg.txt
 python3 tools/prof_summary.py gpurun_out/prof_expl > $D/expl_kernel_avg.txt
-python3 tools/trace.py gpurun_out/prof_b256 12 > $D/b256_step_trace.txt
+python3 tools/trace.py gpurun_out/prof_b256 11 > $D/b256_step_trace.txt
 python3 tools/trace.py gpurun_out/prof_b4096 13 > $D/b4096_step_trace.txt
 python3 tools/trace.py gpurun_out/prof_poac4096 17 > $D/poac4096_step_trace.txt || true
 rm -f profiles/pmc_gemm_traffic.json
