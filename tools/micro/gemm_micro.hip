@@ -86,7 +86,14 @@ int main(int argc, char** argv) {
   const Case cases[] = {
     {"fwd 256x256 K=256 x1", 0, 1}, {"fwd 256x256 K=256 x4", 0, 4}, {"fwd 256x256 K=376 x6", 1, 6},
     {"dW 256x257 K=B=256 x2", 2, 2}, {"dX 256x256 K=256 x2 (mask)", 3, 2}, {"fwd 32x32 K=256 x1 (1 tile)", 4, 1},
+    {"dW 256x257 x2 + fused Adam", 5, 2},
   };
+  // fused-Adam operands for case 5 (the critic group layout: the dW tiles' gradient
+  // addresses index p / m / v / target)
+  const long ng = (long)4 * H * (H + 1);
+  float* ap = dev_rand(ng); float* am = dev_rand(ng); float* at = dev_rand(ng);
+  float* av = dev_rand(ng);
+  StepState* st; CK(hipMalloc(&st, sizeof(StepState))); CK(hipMemset(st, 0, sizeof(StepState)));
   for (const Case& c : cases) {
     for (int nw : {0, 4, 8, 16}) for (int gpw : {0, 3, 5, 6}) {
       if (nw == 0 && gpw) continue;
@@ -102,9 +109,18 @@ int main(int argc, char** argv) {
           case 2: t = t_dw(h[i], H, H, B, h[2 + i], H, H, gw + (long)i * H * (H + 1), gw + (long)i * H * (H + 1) + H * H,
                            0, Split{1, B}); break;
           case 3: t = t_dx(h[i], H, B, H, W1, H, H, h[4 + i], H, h[2 + i], H); break;
+          case 5: t = t_dw(h[i], H, H, B, h[2 + i], H, H, gw + (long)i * H * (H + 1), gw + (long)i * H * (H + 1) + H * H,
+                           0, Split{1, B}); break;
           default: t = t_fwd(h[i], H, 32, H, W1, H, 32, h[4], H, EPI_BIAS_RELU, bias); break;
         }
         add(gb, t);
+      }
+      if (c.kind == 5) {   // v >= 0 (sqrt), the step's constants unpublished (computed per block)
+        CK(hipMemset(av, 0, ng * 4));
+        AdamArgs a{}; a.p = ap; a.g = gw; a.m = am; a.v = av; a.n = ng; a.gslab = gw; a.S = 1;
+        a.slab_stride = ng; a.target = at; a.tau = 0.005f; a.period = 1;
+        a.lr = 3e-4; a.beta1 = 0.9; a.beta2 = 0.999; a.eps = 1e-8; a.state = st; a.no_book = 1;
+        gb.fuse_adam = 1; gb.adam = a; gb.nseg = 0;
       }
       gemm_small_finalize(gb);
       gb.force_nw = nw; gb.force_gpw = gpw;
