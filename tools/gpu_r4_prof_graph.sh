@@ -4,4 +4,4 @@
 # kernels start after host gaps and the trace shows no back-to-back steps)
 mkdir -p gpurun_out
 OAC_DROPIN_GRAPH=1 bash tools/prof.sh b256g; rc=$?; [ $rc -eq 0 ] || exit $rc
-python3 tools/trace.py gpurun_out/prof_b256g 12 | tail -3
+python3 tools/trace.py gpurun_out/prof_b256g 11 | tail -3
