@@ -48,16 +48,24 @@ __device__ __forceinline__ AdamConsts adam_consts(const StepState* st, int advan
 }
 
 // m = b1 m + (1-b1) g ; v = b2 v + (1-b2) g g ; p += -(lr/bc1) m / (sqrt(v)/sqrt(bc2) + eps)
+// Every operation rounded on its own, as torch's Adam does, in every caller:
+// __fmul_rn / __fadd_rn are plain * / + inside the HIP headers, whose own
+// contraction setting let the compiler fuse them into (packed) FMAs in the
+// flat float4 pass but not in the GEMM epilogue, so the same update differed
+// in the last bit between launch layouts -- hence plain operators under the
+// pragma here (the pragma does not reach into a called header function)
 __device__ __forceinline__ void adam1(const AdamConsts& c, float& p, float g, float& m, float& v) {
-  m = __fadd_rn(__fmul_rn(m, c.b1), __fmul_rn(c.omb1, g));
-  v = __fadd_rn(__fmul_rn(v, c.b2), __fmul_rn(__fmul_rn(c.omb2, g), g));
-  const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), c.sbc2), c.eps);
-  p = __fadd_rn(p, __fdiv_rn(__fmul_rn(-c.step_size, m), denom));
+#pragma clang fp contract(off)
+  m = m * c.b1 + c.omb1 * g;
+  v = v * c.b2 + (c.omb2 * g) * g;
+  const float denom = __fsqrt_rn(v) / c.sbc2 + c.eps;
+  p = p + (-c.step_size * m) / denom;
 }
 
 // target = target*(1-tau) + p*tau
 __device__ __forceinline__ float polyak1(const AdamConsts& c, float t, float p) {
-  return __fadd_rn(__fmul_rn(t, c.omtau), __fmul_rn(p, c.tau));
+#pragma clang fp contract(off)
+  return t * c.omtau + p * c.tau;
 }
 
 // Block 0, thread 0 only.  advance == 0 (critic Adam): snapshot t for the

@@ -142,8 +142,10 @@ __device__ __forceinline__ void epi_one(const GemmBatch& batch, const AdamConsts
         float p = x.xb, m = x.am, v = x.av;
         adam1(ac, p, acc, m, v);
         (batch.adam.p_out ? batch.adam.p_out : batch.adam.p)[i] = p;
-        batch.adam.m[i] = m; batch.adam.v[i] = v;
-        if (ac.polyak) batch.adam.target[i] = polyak1(ac, x.at, p);
+        if (!batch.adam.preview) {
+          batch.adam.m[i] = m; batch.adam.v[i] = v;
+          if (ac.polyak) batch.adam.target[i] = polyak1(ac, x.at, p);
+        }
       }
       break;
     }

@@ -92,6 +92,7 @@ struct AdamArgs {
   int no_book;       // skip the state / alpha bookkeeping (a partial range of the group)
   float* p_out;      // small-kernel epilogue Adam: the updated p goes here (same index), not to p
   const float* copy_src;   // small-kernel side blocks: copy this (same index) into p, no Adam
+  int preview;       // small-kernel epilogue Adam: write only p (to p_out), leave m, v, target
 };
 
 constexpr int kMaxTasks = 8;

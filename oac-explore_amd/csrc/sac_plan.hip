@@ -197,10 +197,6 @@ static void add_critic_l1(SacPlan& p, GemmBatch& gb) {
 // blocks copy the shadow into the parameters) instead of a launch of its own:
 // one launch fewer on the step's chain.  OAC_MINQ_MERGE=0 keeps the separate
 // launch (A/B runs).
-static bool defer_dw0_on() {   // OAC_DW0_DEFER=0: keep the obs columns' dW in the layer-0 launch
-  static const bool on = [] { const char* e = getenv("OAC_DW0_DEFER"); return !e || atoi(e) != 0; }();
-  return on;
-}
 static bool minq_merged(const SacPlan& p) {
   static const bool on = [] { const char* e = getenv("OAC_MINQ_MERGE"); return !e || atoi(e) != 0; }();
   return on && can_fuse_adam(p) && p.ws[W_QSHADOW].rows > 0;
@@ -238,20 +234,28 @@ static GemmTask critic_dw0(SacPlan& p, int i, int c0, int n, bool bias) {
 }
 
 // With the -min Q backward merged (minq_merged), the dL/da launch after it
-// reads only the action columns of the post-step critic layer 0, so the obs
-// columns' dW + Adam (+ Polyak) -- 192 of that launch's 208 tiles at B=256,
-// which had pushed it past one workgroup per CU -- move to the two launches
-// after the dL/da one (policy heads, policy layer 1: nothing in them or
-// later in the step reads the critic's layer 0), one critic each, their
-// epilogues applying the critic Adam to these tiles only.  Not with a
-// next-step prefetch (its critic forward reads the post-step layer 0 in the
-// launch after the dL/da one).
-static void add_deferred_dw0(SacPlan& p, GemmBatch& gb, int i) {
+// reads only the action columns of the post-step critic layer 0 -- so the
+// layer-0 launch computes the action columns' Adam as a preview of p into the
+// shadow (the dL/da launch reads them there; m, v, target untouched) and
+// only one critic's obs-column dW (the other's rides in the dL/da launch),
+// 240 tiles on 16-wave workgroups instead of 336 on 8; the whole layer-0
+// Adam + Polyak of both critics then runs as side blocks of the policy-head
+// launch (nothing in it or later in the step reads the critic's layer 0).
+// Not with a next-step prefetch: its critic forward reads the post-step
+// layer 0 in the dL/da launch.  OAC_DW0_DEFER=0 keeps the layer-0 dW + Adam
+// in the layer-0 launch.
+static bool defer_dw0_on() {
+  static const bool on = [] { const char* e = getenv("OAC_DW0_DEFER"); return !e || atoi(e) != 0; }();
+  return on;
+}
+static void add_dw0_side_adam(SacPlan& p, GemmBatch& gb) {
   for (int k = 0; k < gb.ntasks; ++k) gb.t[k].no_adam = 1;   // (the policy's gradients)
-  add(gb, critic_dw0(p, i, 0, p.c.obs_dim, false));
+  const oac_sac_layout& L = p.L;
+  const long off[2] = {0, (long)L.q_size};
+  const long n[2] = {(long)L.q_fc1_w, (long)L.q_fc1_w};
   AdamArgs a = critic_adam(p, 0, nullptr);
   a.no_book = 1;
-  fuse_adam(gb, a, 0, nullptr, nullptr);
+  fuse_adam(gb, a, 2, off, n);
 }
 
 int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long* off,
@@ -521,13 +525,19 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
   }
   {  // critic backward, layer 0 (input = [obs | act] contiguous in the row)
     GemmBatch gb{};
-    const bool dfr = defer && fused && minq_merged(p);   // obs columns later (add_deferred_dw0)
+    const bool dfr = defer && fused && minq_merged(p);   // (defer_dw0_on)
     for (int i = 0; i < 2; ++i)
       add(gb, dfr ? critic_dw0(p, i, Do, Da, true) : critic_dw0(p, i, 0, Dq, true));
+    if (dfr) {   // critic 1's obs columns: gradient only (their Adam: the policy-head launch)
+      GemmTask t = critic_dw0(p, 0, 0, Do, false);
+      t.no_adam = 1;
+      add(gb, t);
+    }
     if (fused) {  // SAC commits the alpha update in the critic Adam
       const long off[2] = {(long)L.q_fc1_w, (long)(L.q_size + L.q_fc1_w)};
       const long n[2] = {(long)(L.q_size - L.q_fc1_w), (long)(L.q_size - L.q_fc1_w)};
       AdamArgs a = critic_adam(p, 0, c.auto_alpha ? p.alpha() : nullptr);
+      if (dfr) { a.p_out = p.W(W_QSHADOW); a.preview = 1; }   // action columns: p preview only
       if (minq_merged(p)) {   // side blocks: the shadow's layer 1 + last layer into the parameters;
         a.copy_src = p.W(W_QSHADOW);   // the -min Q backward reads them from the shadow
         const float* sh = p.W(W_QSHADOW);
@@ -571,6 +581,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
   const float* q2 = p.b.params + L.q2_base;
   const bool merged = fused && minq_merged(p);   // (then the critic layer-0 dW launch ran it)
   const bool dfr = defer && merged && !prefetch;
+  const float* qa = dfr ? p.W(W_QSHADOW) : q1;   // critic 1's post-step layer 0 (critic 2: + q_size)
   if (!merged) {  // -min Q backward to layer 1 with post-step weights, pre-step masks
     GemmBatch gb{};
     const float* const qs[2] = {q1, q2};
@@ -587,9 +598,9 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
   }
   if (p.cfg == 0 || head_bwd_fused_big()) {  // dL/da through both critics' action columns + head backward, one launch (small kernel)
     GemmBatch gb{};
-    GemmTask t = t_dx(p.W(W_DH1N1), H, B, H, q1 + L.q_fc0_w + Do, Dq, Da, p.W(W_DHEAD), 2 * Da,
+    GemmTask t = t_dx(p.W(W_DH1N1), H, B, H, qa + L.q_fc0_w + Do, Dq, Da, p.W(W_DHEAD), 2 * Da,
                       nullptr, 0);
-    t.A2 = p.W(W_DH1N2); t.B2 = q2 + L.q_fc0_w + Do; t.K2 = H;   // same leading dims
+    t.A2 = p.W(W_DH1N2); t.B2 = qa + L.q_size + L.q_fc0_w + Do; t.K2 = H;   // same leading dims
     t.epi = EPI_HEAD_BWD;
     t.ex[0] = p.W(OAC_WS_ACT1); t.ex[1] = p.W(W_STD1); t.ex[2] = p.W(W_U1);
     t.ex[3] = p.E1(); t.ex[4] = p.W(OAC_WS_HEAD1);
@@ -597,6 +608,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     add(gb, t);
     if (prefetch && merged) add_critic_l0(p, gb, prefetch);
     if (prefetch) add_target_l0(p, gb, prefetch);
+    if (dfr) add(gb, critic_dw0(p, 1, 0, Do, false));   // critic 2's obs columns: gradient only
     if (run_gemm(p, gb, s)) return 1;
   } else {
     {  // to the action columns of layer 0
@@ -622,7 +634,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
                  gp + L.pol_head_b, L.pol_size, p.sp_ph));
     add(gb, t_dx(p.W(W_DHEAD), 2 * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(W_DH2P), H, p.W(W_H2P), H));
     if (prefetch) add_critic_l1(p, gb);
-    if (dfr) add_deferred_dw0(p, gb, 0);
+    if (dfr) add_dw0_side_adam(p, gb);   // both critics' layer 0 (+ bias): Adam + Polyak
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 1
@@ -631,7 +643,6 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
                  L.pol_size, p.sp_p1));
     add(gb, t_dx(p.W(W_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_DH1P), H, p.W(W_H1P), H));
-    if (dfr) add_deferred_dw0(p, gb, 1);
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 0
