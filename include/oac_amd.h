@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define OAC_ABI_VERSION 2
+#define OAC_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- config */
 enum oac_kind {

@@ -432,9 +432,12 @@ __device__ __forceinline__ void particle_targets_rows(const ParticleTargetArgs& 
     }
   }
   // both sorts by the whole block: 16 lanes per row, lane k ranks its value
-  // against the row's 16 (ties by head index, the +inf padding last) -- the
-  // order sort16's comparator defines, so the same permutation -- and scatters
-  // it into LDS; a row thread's bitonic network was ~1,000 dependent VALU ops
+  // against the row's 16 (ties by head index, the padding slots past K last)
+  // -- the order sort16's comparator defines, so the same permutation -- and
+  // scatters it into LDS; a row thread's bitonic network was ~1,000 dependent
+  // VALU ops.  The order is total: NaN ranks after every number, as in
+  // torch.sort (a diverged critic then gives NaN losses, and every rank is
+  // still taken exactly once, so the scatters below stay inside [0, K)).
   __shared__ float s_qv[kRowBlock][kMaxHeads], s_tv[kRowBlock][kMaxHeads];
   __shared__ int s_qi[kRowBlock][kMaxHeads], s_ti[kRowBlock][kMaxHeads];
   {
@@ -444,12 +447,19 @@ __device__ __forceinline__ void particle_targets_rows(const ParticleTargetArgs& 
     const float inf = __builtin_huge_valf();
     const float qv = k < K ? (p.qh.h ? qs.out[row][k] : p.q[(long)m * K + k]) : inf;
     const float tv = k < K ? (p.th.h ? hs.out[row][k] : p.tq[(long)m * K + k]) : inf;
+    // slot j precedes slot k: real before padding, then value (NaN last), then index
+    auto before = [&](float vj, float vk, int j) {
+      if ((j < K) != (k < K)) return j < K;
+      const bool nj = vj != vj, nk = vk != vk;
+      if (nj != nk) return nk;
+      return (vj < vk) || ((vj == vk || nj) && j < k);
+    };
     int rq = 0, rt = 0;
 #pragma unroll
     for (int j = 0; j < kMaxHeads; ++j) {
       const float qj = __shfl(qv, base | j, 64), tj = __shfl(tv, base | j, 64);
-      rq += (qj < qv || (qj == qv && j < k)) ? 1 : 0;
-      rt += (tj < tv || (tj == tv && j < k)) ? 1 : 0;
+      rq += before(qj, qv, j) ? 1 : 0;
+      rt += before(tj, tv, j) ? 1 : 0;
     }
     s_qv[row][rq] = qv; s_qi[row][rq] = k;
     s_tv[row][rt] = tv; s_ti[row][rt] = k;
@@ -598,9 +608,9 @@ __global__ void __launch_bounds__(256) particle_targets_kernel(ParticleTargetArg
 }
 
 // sorted_qs[0] of Q(obs, a~) with the post-step critic (particle_trainer_oac.py:286-295)
-// -> gradient seed -1/B on the argmin head; plus the alpha update (274-281),
-// computed identically by every block, published by block 0 (committed by
-// the policy Adam, which reads no alpha field).
+// -> gradient seed -1/B on the argmin head; plus the alpha update (274-281)
+// on a block of its own after the row blocks (committed by the policy Adam,
+// which reads no alpha field).
 __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
   __shared__ float red[256];
   const int nrb = (p.B + kRowBlock - 1) / kRowBlock;
@@ -658,7 +668,7 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
     float bv = qn[0];
     for (int i = 1; i < K; ++i) {
       const float x = qn[i];
-      if (x < bv) { bv = x; best = i; }
+      if (x < bv || (bv != bv && x == x)) { bv = x; best = i; }   // (NaN last, as torch.sort)
     }
     for (int i = 0; i < K; ++i) p.gq[(long)r * K + i] = (i == best) ? -invB : 0.f;
     p.qmin[r] = bv;
@@ -676,15 +686,11 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
       const int rr = min(rr0 + j * rstep, kRowBlock - 1), m = r0 + rr;
       if (rr0 + j * rstep >= kRowBlock || m >= p.B) continue;
       const int b = sbest[rr];
-      // the argmin head's row as a masked sum (exact: one term is w, the rest
-      // +-0), so the prefetched rows stay in registers
-      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
+      // the argmin head's row by a select chain (exact, whatever the other
+      // heads' rows hold), so the prefetched rows stay in registers
+      float4 w = wpf[0];
 #pragma unroll
-      for (int k = 0; k < kMaxHeads; ++k) {
-        const float sel = b == k ? 1.f : 0.f;
-        w.x = fmaf(sel, wpf[k].x, w.x); w.y = fmaf(sel, wpf[k].y, w.y);
-        w.z = fmaf(sel, wpf[k].z, w.z); w.w = fmaf(sel, wpf[k].w, w.w);
-      }
+      for (int k = 1; k < kMaxHeads; ++k) w = (b == k) ? wpf[k] : w;
       const float4 h = hpf[j];
       float4 o;
       o.x = h.x > 0.f ? -invB * w.x : 0.f; o.y = h.y > 0.f ? -invB * w.y : 0.f;

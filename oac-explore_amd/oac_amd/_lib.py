@@ -179,7 +179,7 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.oac_abi_version() != 2:
+    if L.oac_abi_version() != 3:
         raise RuntimeError("liboac_amd ABI version mismatch")
     _LIB = L
     return L

@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_error_channel():
     from oac_amd import _lib
     L = _lib.lib()
-    assert L.oac_abi_version() == 2
+    assert L.oac_abi_version() == 3
     cfg = _lib.SacConfig()
     cfg.kind = 7
     lay = _lib.SacLayout()

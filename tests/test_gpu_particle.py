@@ -72,6 +72,34 @@ def test_particle_step_matches_reference_golden(name):
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
 
 
+def test_particle_step_with_a_nan_head_sorts_it_last():
+    """A diverged head (NaN Q values in every row): the targets kernel's rank
+    sort puts NaN after every number, as torch.sort does
+    (particle_trainer_oac.py:192, 202), so each slot is taken once and the
+    dq / LDS scatters stay inside the K heads.  The finite slots' losses equal
+    the oracle's (torch.sort on the same NaN head); the NaN slot's loss is NaN."""
+    meta, g = parity.load("poac_small")
+    K = meta["K"]
+    tr = particle_trainer_for(meta)
+    with torch.no_grad():
+        tr.qfs[0].state_dict()["last_fc.weight"][K // 2].fill_(float("nan"))
+    orc = tog.make_poac_oracle(meta)
+    orc.Q["last_fc.weight"][K // 2] = float("nan")
+    b = batch_from(meta, g["s0/idx"])
+    tr.end_epoch(0)
+    tr.train_from_torch(b, eps1=g["s0/eps1"], eps2=g["s0/eps2"])
+    torch.cuda.synchronize()
+    out = orc.step(b, g["s0/eps1"], g["s0/eps2"])
+    st = tr.get_diagnostics()
+    for i in range(K - 1):
+        ref = float(out["qf_losses"][i])
+        assert np.isfinite(ref) and parity.rel_err(st[f"QF{i} Loss"], ref) < 1e-5, (i, st[f"QF{i} Loss"], ref)
+    assert np.isnan(st[f"QF{K - 1} Loss"]) and np.isnan(float(out["qf_losses"][K - 1]))
+    # the trainer keeps stepping (no fault, no stale LDS slot)
+    tr.train_from_torch(b, eps1=g["s0/eps1"], eps2=g["s0/eps2"])
+    torch.cuda.synchronize()
+
+
 def test_particle_stats_keys_match_reference_order():
     meta, g = parity.load("poac_small")
     tr = particle_trainer_for(meta)
