@@ -14,6 +14,8 @@
  *                         ReplayBuffer.random_batch gather (replay_buffer.py:106-115)
  *                         and np_to_pytorch_batch (utils/core.py:56-61)
  *   oac_sac_step_phase    the same step split at the data-parallel exchange points
+ *   oac_sac_set_allreduce the data-parallel step with its exchanges (no reference
+ *   oac_rccl_*            counterpart: main.py:575-578 runs replicas)
  *   oac_particle_*        ParticleTrainer.train_from_torch, share_layers=True
  *                         (trainer/particle_trainer_oac.py:169-363)
  *   OAC_KIND_GAUSS        GaussianTrainer.train_from_torch (g-oac), share_layers=True
@@ -138,6 +140,9 @@ enum oac_ws_buffer {
   OAC_WS_LOGP_PART,                    /* [ceil(B/16)] sum of (logp1 + target_entropy) per 16-row
                                           block: the data-parallel alpha exchange (world_size > 1)
                                           all-reduces this vector, the targets kernel sums it */
+  OAC_WS_H2Q1, OAC_WS_H2Q2,            /* SAC: the critics' second hidden layer on (obs, a) [B, H]
+                                          after the ReLU -- the masks their backward used (parity
+                                          checks; 0 rows for the other kinds) */
   OAC_WS_COUNT_PUBLIC
 };
 
@@ -212,6 +217,52 @@ int oac_sac_set_step_graph(oac_sac* h, void* graph_exec, int flags);
  * phase 5 = the rest of phase 1, so 0, [alpha all-reduce || 4], 5, 2, 3 is
  * the same step with the first exchange overlapped. */
 int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream);
+
+/* ------------------------------------------------ data-parallel exchanges */
+/* The data-parallel step with its exchanges issued by the library itself
+ * (SURVEY 8b "oac_allreduce_hook(...) (or an RCCL comm passed in)", 8e: the
+ * alpha partials OAC_WS_LOGP_PART, the critic gradients [q1_base, q1_base +
+ * n_critics * q_size) and the policy gradients [0, q1_base) of the grads arena
+ * -- three in-place SUM all-reduces per step, at the points of the torch-1.4
+ * order of trainer/trainer.py:139-210 where a whole-batch quantity is needed).
+ * fn(ctx, buf, n, stream) must enqueue an in-place fp32 SUM of buf[0:n] over
+ * the ranks on `stream` (stream-ordered) and return 0.  With a hook attached
+ * and config.world_size > 1 (or OAC_DP_FORCE), every step entry
+ * (oac_sac_step, _step_n, _step_host_idx) runs phase 0, [alpha], 1, [critic
+ * grads], 2, [policy grads], 3 with the exchanges in between, as direct
+ * launches on `stream` (no graph); at world size 1 without OAC_DP_FORCE a sum
+ * over one rank is the identity and the single-process step runs.  fn = NULL
+ * detaches the hook.  Replaces the caller-side exchange loop over
+ * oac_sac_step_phase (and a captured graph of it, oac_sac_set_step_graph). */
+typedef int (*oac_allreduce_fn)(void* ctx, float* buf, int64_t n, void* stream);
+#define OAC_DP_FORCE    1   /* issue the exchanges at world size 1 too (measurement, tests) */
+#define OAC_DP_OVERLAP  2   /* SAC: the alpha exchange on the handle's side stream beside
+                               phase 4 (the critics on the fresh actions), joined before phase 5 */
+int oac_sac_set_allreduce(oac_sac* h, oac_allreduce_fn fn, void* ctx, int flags);
+/* RCCL implementation of the hook.  librccl is loaded at run time from
+ * librccl_path (the librccl.so the process already uses, e.g. torch's);
+ * unique_id: rank 0 fills 128 bytes that every rank passes to create
+ * (collective: all ranks call create together).  oac_rccl_allreduce is an
+ * oac_allreduce_fn with ctx = the oac_rccl handle. */
+typedef struct oac_rccl oac_rccl;
+int oac_rccl_unique_id(const char* librccl_path, void* id128);
+int oac_rccl_create(const char* librccl_path, const void* id128, int rank, int world,
+                    oac_rccl** out);
+int oac_rccl_destroy(oac_rccl* c);
+int oac_rccl_allreduce(void* rccl, float* buf, int64_t n, void* stream);
+
+/* which branches of the launch plan the steps issued since the last reset
+ * took (bitmask of OAC_TRACE_*; reset != 0 clears it after reading) */
+#define OAC_TRACE_DIRECT        1    /* small batch: layer 0 reads rows through the index slot */
+#define OAC_TRACE_DIRECT_BIG    2    /* large batch: the LDS-DMA layer 0 reads rows through the slot */
+#define OAC_TRACE_BATCH_COPY    4    /* large batch: the batch copy in the fresh-action critic launch */
+#define OAC_TRACE_QDOT          8    /* width-1 critic heads as layer-1 epilogue partials */
+#define OAC_TRACE_WL_TARGETS    16   /* the critics' last-layer dW slabs in the targets kernel */
+#define OAC_TRACE_SPLIT_PHASE1  32   /* phase 1 issued as 4 + 5 (the overlapped alpha exchange) */
+#define OAC_TRACE_FUSED         64   /* the single-process fused-Adam step */
+#define OAC_TRACE_EXCHANGE      128  /* data-parallel exchanges issued through the hook */
+int oac_sac_trace(oac_sac* h, int reset);
+
 int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows, int64_t* cols);
 /* number of kernel launches of one step (for the launch/graph accounting) */
 int oac_sac_launch_count(oac_sac* h);

@@ -28,6 +28,15 @@ struct SacPlan : PlanBase {
   // phase1's fresh-action critic launch then carries the batch copy)
   bool direct_big = false;
   const int* direct_ring = nullptr;   // its index ring (device or host-coherent)
+  // data-parallel exchanges issued by the library (oac_sac_set_allreduce):
+  // the hook, its flags, and the side stream + fork / join events of the
+  // overlapped alpha exchange (created on first use, owned by the plan)
+  oac_allreduce_fn ar_fn = nullptr;
+  void* ar_ctx = nullptr;
+  int ar_flags = 0;
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int trace = 0;   // OAC_TRACE_* bits of the branches issued since the last read
 
   float* W(int id) const { return b.workspace + ws[id].off; }
   float* X() const { return W(OAC_WS_BATCH) + (long)slot * c.batch * c.row_stride; }

@@ -338,6 +338,8 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
     }
     p.direct_big = direct_big;
     p.direct_ring = gather_idx(p, flags);
+    if (direct) p.trace |= OAC_TRACE_DIRECT;
+    if (direct_big) p.trace |= OAC_TRACE_DIRECT_BIG;
     if (direct_big) {   // every layer-0 product reads its rows through the index slot
       for (int i = 0; i < gb.ntasks; ++i) gb.t[i].a_rows = 1;
       RowGather& g = gb.rg;
@@ -447,6 +449,7 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
       g.ring = p.direct_ring; g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
       g.replay = p.b.replay; g.row_stride = RS; g.out = X;
       g.blocks = 256;
+      p.trace |= OAC_TRACE_BATCH_COPY;
     }
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -474,6 +477,7 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
       }
     }
     a.n_part = qdot(p) ? (int)p.ws[W_QPART].cols : 0;
+    if (qdot(p)) p.trace |= OAC_TRACE_QDOT;
     a.logp2 = p.W(OAC_WS_LOGP2);
     a.batch = X; a.ld_batch = RS; a.off_rew = c.off_rew; a.off_term = c.off_term;
     a.alpha = c.auto_alpha ? p.alpha() : nullptr;
@@ -493,6 +497,7 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
         a.wl_gb[i] = gq + i * L.q_size + L.q_last_b;
       }
       a.wl_slab_stride = q_group(p); a.wl_H = H;
+      p.trace |= OAC_TRACE_WL_TARGETS;
     }
     TIMED(p, K_ROW, s, OAC_HIP_CHECK(launch_critic_targets(a, s)));
     p.launches++;
@@ -673,6 +678,7 @@ static long c_batch_rows(const SacPlan& p) { return (long)p.c.batch * p.c.row_st
 static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) {
   p.launches = 0;
   const bool fused = can_fuse_adam(p);
+  if (fused) p.trace |= OAC_TRACE_FUSED;
   p.slot = i % kXSlots;
   const int gather_n = p.slot == 0 ? std::min(kXSlots, n - i) : 0;
   // steps after the first of a gather batch had their critic-side forward
@@ -695,6 +701,91 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
   }
   p.slot = 0;
   return 0;
+}
+
+static int step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
+  if (p.c.kind == OAC_KIND_PARTICLE) return particle_step_phase(p, phase, flags, s);
+  if (has_target_policy(p.c.kind)) return det_step_phase(p, phase, flags, s);
+  switch (phase) {
+    case 0: return phase0(p, flags, s);
+    case 1:
+    case 5:   // phase 1 without its first part (after phase 4)
+      if (phase1(p, s, false, phase == 5 ? 2 : 0)) return 1;
+      if (p.S_q > 1) {
+        AdamArgs a = critic_adam(p, 1, nullptr);
+        OAC_HIP_CHECK(launch_adam(a, s));
+      }
+      return 0;
+    case 4:   // phase 1's fresh-action critic forward (needs no alpha)
+      p.trace |= OAC_TRACE_SPLIT_PHASE1;
+      return phase1(p, s, false, 1);
+    case 2:
+      if (phase2_adam(p, s, 1)) return 1;
+      if (phase2(p, s, false)) return 1;
+      if (p.S_p > 1) {
+        AdamArgs a = policy_adam(p, 1, nullptr);
+        OAC_HIP_CHECK(launch_adam(a, s));
+      }
+      return 0;
+    case 3: {
+      AdamArgs a = policy_adam(p, -1, nullptr);
+      OAC_HIP_CHECK(launch_adam(a, s));
+      return 0;
+    }
+    default:
+      set_error("bad phase %d", phase);
+      return 1;
+  }
+}
+
+
+// The data-parallel step with the library's own exchanges (oac_sac_set_allreduce):
+// phase 0, the alpha partials' all-reduce (beside phase 4 on the side stream
+// with OAC_DP_OVERLAP, SAC), the rest of phase 1, the critic gradients'
+// all-reduce, phase 2 (critic Adam with the averaged gradients, the policy
+// gradient through the post-step critics), the policy gradients' all-reduce,
+// phase 3 -- trainer/trainer.py:139-210's order with a whole-batch quantity
+// exchanged at each point the single-GPU step needs one.  Direct
+// launches on `s`: the exchanges are stream-ordered calls of the hook.
+static bool dp_exchanges(const SacPlan& p) {
+  return p.ar_fn && (p.c.world_size > 1 || (p.ar_flags & OAC_DP_FORCE));
+}
+static int exchange(SacPlan& p, float* buf, int64_t n, hipStream_t s) {
+  g_err[0] = 0;
+  if (p.ar_fn(p.ar_ctx, buf, n, s)) {
+    if (!g_err[0]) set_error("data-parallel all-reduce hook failed (%lld floats)", (long long)n);
+    return 1;
+  }
+  p.trace |= OAC_TRACE_EXCHANGE;
+  return 0;
+}
+static int run_step_dp(SacPlan& p, int flags, hipStream_t s) {
+  const oac_sac_config& c = p.c;
+  p.launches = 0;
+  p.slot = 0;
+  if (step_phase(p, 0, flags, s)) return 1;
+  if (c.auto_alpha) {
+    float* part = p.W(OAC_WS_LOGP_PART);
+    const int64_t np = (c.batch + 15) / 16;
+    if ((p.ar_flags & OAC_DP_OVERLAP) && c.kind == OAC_KIND_SAC && p.side) {
+      OAC_HIP_CHECK(hipEventRecord(p.ev_fork, s));
+      OAC_HIP_CHECK(hipStreamWaitEvent(p.side, p.ev_fork, 0));
+      if (exchange(p, part, np, p.side)) return 1;
+      OAC_HIP_CHECK(hipEventRecord(p.ev_join, p.side));
+      if (step_phase(p, 4, flags, s)) return 1;
+      OAC_HIP_CHECK(hipStreamWaitEvent(s, p.ev_join, 0));
+      if (step_phase(p, 5, flags, s)) return 1;
+    } else {
+      if (exchange(p, part, np, s)) return 1;
+      if (step_phase(p, 1, flags, s)) return 1;
+    }
+  } else if (step_phase(p, 1, flags, s)) {
+    return 1;
+  }
+  if (exchange(p, p.b.grads + p.L.q1_base, q_group(p), s)) return 1;
+  if (step_phase(p, 2, flags, s)) return 1;
+  if (exchange(p, p.b.grads, p_group(p), s)) return 1;
+  return step_phase(p, 3, flags, s);
 }
 
 }  // namespace oac
@@ -838,6 +929,9 @@ int oac_sac_destroy(oac_sac* h) {
   if (h->plan.exec) (void)hipGraphExecDestroy(h->plan.exec);
   if (h->plan.graph) (void)hipGraphDestroy(h->plan.graph);
   if (h->plan.cap_stream) (void)hipStreamDestroy(h->plan.cap_stream);
+  if (h->plan.side) (void)hipStreamDestroy(h->plan.side);
+  if (h->plan.ev_fork) (void)hipEventDestroy(h->plan.ev_fork);
+  if (h->plan.ev_join) (void)hipEventDestroy(h->plan.ev_join);
   if (h->plan.owns_host_ring && h->plan.host_ring) (void)hipHostFree(h->plan.host_ring);
   delete h;
   return 0;
@@ -846,9 +940,18 @@ int oac_sac_destroy(oac_sac* h) {
 int oac_sac_step_n(oac_sac* h, int flags, int n_steps, void* stream) {
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
-  if (p.c.world_size > 1) { set_error("world_size > 1: drive the step with oac_sac_step_phase"); return 1; }
   if (n_steps < 1 || n_steps > 1024) { set_error("n_steps %d out of range", n_steps); return 1; }
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (dp_exchanges(p)) {   // the data-parallel step, exchanges through the hook (direct launches)
+    for (int i = 0; i < n_steps; ++i)
+      if (run_step_dp(p, flags & ~OAC_STEP_USE_GRAPH, s)) return 1;
+    return 0;
+  }
+  if (p.c.world_size > 1) {
+    set_error("world_size > 1: attach an all-reduce hook (oac_sac_set_allreduce) or drive the "
+              "step with oac_sac_step_phase");
+    return 1;
+  }
   auto steps = [&](int f) {
     for (int i = 0; i < n_steps; ++i) {
       const int rc = p.c.kind == OAC_KIND_PARTICLE ? particle_run_step(p, f, s)
@@ -1035,44 +1138,36 @@ int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags,
 
 int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {
   if (!h) { set_error("null handle"); return 1; }
+  return step_phase(h->plan, phase, flags, reinterpret_cast<hipStream_t>(stream));
+}
+
+int oac_sac_set_allreduce(oac_sac* h, oac_allreduce_fn fn, void* ctx, int flags) {
+  if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (p.c.kind == OAC_KIND_PARTICLE) return particle_step_phase(p, phase, flags, s);
-  if (has_target_policy(p.c.kind)) return det_step_phase(p, phase, flags, s);
-  switch (phase) {
-    case 0: return phase0(p, flags, s);
-    case 1:
-    case 5:   // phase 1 without its first part (after phase 4)
-      if (phase1(p, s, false, phase == 5 ? 2 : 0)) return 1;
-      if (p.S_q > 1) {
-        AdamArgs a = critic_adam(p, 1, nullptr);
-        OAC_HIP_CHECK(launch_adam(a, s));
-      }
-      return 0;
-    case 4:   // phase 1's fresh-action critic forward (needs no alpha)
-      return phase1(p, s, false, 1);
-    case 2:
-      if (phase2_adam(p, s, 1)) return 1;
-      if (phase2(p, s, false)) return 1;
-      if (p.S_p > 1) {
-        AdamArgs a = policy_adam(p, 1, nullptr);
-        OAC_HIP_CHECK(launch_adam(a, s));
-      }
-      return 0;
-    case 3: {
-      AdamArgs a = policy_adam(p, -1, nullptr);
-      OAC_HIP_CHECK(launch_adam(a, s));
-      return 0;
-    }
-    default:
-      set_error("bad phase %d", phase);
-      return 1;
+  if (fn && (flags & OAC_DP_OVERLAP) && !p.side) {
+    OAC_HIP_CHECK(hipStreamCreateWithFlags(&p.side, hipStreamNonBlocking));
+    OAC_HIP_CHECK(hipEventCreateWithFlags(&p.ev_fork, hipEventDisableTiming));
+    OAC_HIP_CHECK(hipEventCreateWithFlags(&p.ev_join, hipEventDisableTiming));
   }
+  p.ar_fn = fn;
+  p.ar_ctx = fn ? ctx : nullptr;
+  p.ar_flags = fn ? flags : 0;
+  return 0;
+}
+
+int oac_sac_trace(oac_sac* h, int reset) {
+  if (!h) { set_error("null handle"); return -1; }
+  const int t = h->plan.trace;
+  if (reset) h->plan.trace = 0;
+  return t;
 }
 
 int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows, int64_t* cols) {
   if (!h || which < 0 || which >= OAC_WS_COUNT_PUBLIC) { set_error("bad workspace id"); return 1; }
-  const WsBuf& w = h->plan.ws[which];
+  int id = which;
+  if (which == OAC_WS_H2Q1 || which == OAC_WS_H2Q2)   // aliases of the SAC layout's buffers
+    id = h->plan.c.kind == OAC_KIND_SAC ? (which == OAC_WS_H2Q1 ? W_H2Q1 : W_H2Q2) : which;
+  const WsBuf& w = h->plan.ws[id];
   *offset = w.off; *rows = w.rows; *cols = w.cols;
   if (which == OAC_WS_BATCH || which == OAC_WS_EPS1 || which == OAC_WS_EPS2)
     *rows = h->plan.c.batch;   // slot 0: the batch / eps of a single-step call

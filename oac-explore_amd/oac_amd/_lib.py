@@ -22,11 +22,22 @@ OAC_STEP_DEVICE_EPS = 2
 OAC_STEP_USE_GRAPH = 4
 OAC_STEP_COUNTS = 8
 
+OAC_DP_FORCE = 1
+OAC_DP_OVERLAP = 2
+
+# oac_sac_trace bits
+TRACE = dict(direct=1, direct_big=2, batch_copy=4, qdot=8, wl_targets=16, split_phase1=32,
+             fused=64, exchange=128)
+
+# oac_allreduce_fn: int (*)(void* ctx, float* buf, int64_t n, void* stream)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                ctypes.c_void_p)
+
 # public workspace ids (enum oac_ws_buffer)
 WS = {name: i for i, name in enumerate([
     "batch", "eps1", "eps2", "head1", "head2", "act1", "act2", "logp1", "logp2",
     "q1", "q2", "qn1", "qn2", "tq1", "tq2", "y", "sqe1", "sqe2", "qnew", "counts",
-    "head3", "act3", "logp_part"])}
+    "head3", "act3", "logp_part", "h2q1", "h2q2"])}
 
 
 class SacConfig(ctypes.Structure):
@@ -90,6 +101,15 @@ _SIGS = {
     "oac_sac_stage_host_idx": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                               ctypes.c_void_p]),
     "oac_sac_set_step_graph": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    "oac_sac_set_allreduce": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_int]),
+    "oac_sac_trace": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "oac_rccl_unique_id": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p]),
+    "oac_rccl_create": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_void_p)]),
+    "oac_rccl_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "oac_rccl_allreduce": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_void_p]),
     "oac_sac_workspace_view": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int,
                                               ctypes.POINTER(ctypes.c_int64),
                                               ctypes.POINTER(ctypes.c_int64),

@@ -19,9 +19,18 @@ are the gradients of the concatenated global batch, so a DP step equals the
 single-process step on the union of the ranks' batches (tests/test_dp.py
 checks this with the CPU oracle over gloo).
 
-``dp_step`` is the transport-agnostic driver: it runs with the GPU executor
-below (liboac_amd phases + torch.distributed over RCCL) and, in the CPU
-tests, with an oracle-backed executor over gloo.
+The exchanges are issued by liboac_amd itself, between its own launches
+(``oac_sac_set_allreduce``, sac_plan.hip ``run_step_dp``): over RCCL through
+the library's own communicator (``oac_rccl_*``, bootstrapped from the process
+group; the nccl backend) or, over gloo, through a host callback into
+torch.distributed (tests).  A step is then one library call of direct
+launches and stream-ordered all-reduces, like the single-process step.
+
+``dp_step`` is the transport-agnostic Python driver of the same sequence: the
+CPU tests run it with an oracle-backed executor over gloo, and
+``OAC_DP_TRANSPORT=torch`` (or ``transport="torch"``) keeps the round-1..4
+GPU path -- the library's phases driven from Python with torch's
+all-reduces, RCCL steps captured into a torch graph -- for A/B runs.
 """
 import atexit
 import ctypes
@@ -92,6 +101,13 @@ class _GpuExecutor:
         return self._pol
 
 
+def _librccl_path():
+    """The librccl.so torch's process group uses (so the library's
+    communicator and torch's share one RCCL instance), else ROCm's."""
+    p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    return p if os.path.exists(p) else "/opt/rocm/lib/librccl.so"
+
+
 def _close_at_exit(ref):
     tr = ref()
     if tr is not None and dist.is_initialized():
@@ -113,10 +129,20 @@ class _DataParallel:
     (``capture=False`` keeps every step eager)."""
 
     def __init__(self, *args, process_group=None, capture=None, force_collectives=False,
-                 force_overlap=False, **kwargs):
+                 force_overlap=False, transport=None, **kwargs):
         if not dist.is_initialized():
             raise RuntimeError("DataParallelSACTrainer needs torch.distributed initialised")
         self.pg = process_group
+        # "library": liboac_amd issues the exchanges itself (RCCL communicator
+        # of its own, or a host callback over gloo); "torch": Python drives the
+        # phases with torch's all-reduces (the round-1..4 path, A/B runs)
+        self.transport = transport or os.environ.get("OAC_DP_TRANSPORT", "library")
+        if self.transport not in ("library", "torch"):
+            raise ValueError(f"transport {self.transport!r}: 'library' or 'torch'")
+        self._force = force_collectives
+        self._rccl = None          # the library's communicator (oac_rccl*), created on first use
+        self._ar = None            # (fn, ctx) of the attached hook
+        self._ar_err = None
         self.world = dist.get_world_size(process_group)
         # a sum over one rank is the identity: at world size 1 the exchanges
         # are skipped (force_collectives=True issues them anyway: what the
@@ -164,15 +190,100 @@ class _DataParallel:
         torch.cuda.synchronize(self.device)
 
     def close(self):
-        """The data-parallel trainer's teardown: finish the queued steps and
-        release the captured graphs, so the caller may then destroy the
-        process group (``dist.destroy_process_group()``).  Idempotent; a step
-        after close() re-captures."""
+        """The data-parallel trainer's teardown: finish the queued steps,
+        release the captured graphs and the library's communicator, so the
+        caller may then destroy the process group
+        (``dist.destroy_process_group()``).  Idempotent; a step after close()
+        re-captures / re-creates the communicator (collectively)."""
         if self._closed:
             return
         self._closed = True
         self.release_graphs()
         self._side = None
+        if self._ar is not None:
+            torch.cuda.synchronize(self.device)
+            for p in self._plans.values():
+                if getattr(p, "hooked", False):
+                    check(_lib.lib().oac_sac_set_allreduce(p.handle, None, None, 0))
+                    p.hooked = False
+            if self._rccl is not None:
+                check(_lib.lib().oac_rccl_destroy(self._rccl))
+                self._rccl = None
+            self._ar = None
+
+    # ---------------------------------------------------- library transport
+    def _hook(self):
+        """(fn, ctx) of the all-reduce hook the plans carry: the library's RCCL
+        communicator (nccl backend; created collectively on first use, its
+        unique id broadcast from the group's rank 0) or a host callback into
+        torch.distributed (gloo)."""
+        if self._ar is not None:
+            return self._ar
+        L = _lib.lib()
+        if self._nccl:
+            path = _librccl_path().encode()
+            uid = (ctypes.c_char * 128)()
+            if dist.get_rank(self.pg) == 0:
+                check(L.oac_rccl_unique_id(path, uid))
+            obj = [bytes(uid)]
+            src = 0 if self.pg is None else dist.get_global_rank(self.pg, 0)
+            dist.broadcast_object_list(obj, src=src, group=self.pg, device=self.device)
+            ctypes.memmove(uid, obj[0], 128)
+            h = ctypes.c_void_p()
+            check(L.oac_rccl_create(path, uid, dist.get_rank(self.pg), self.world, ctypes.byref(h)))
+            self._rccl = h
+            self._ar = (ctypes.cast(L.oac_rccl_allreduce, ctypes.c_void_p), h)
+        else:
+            self._ar_cb = _lib.ALLREDUCE_FN(self._host_allreduce)
+            self._ar = (ctypes.cast(self._ar_cb, ctypes.c_void_p), None)
+        self._closed = False
+        return self._ar
+
+    def _host_allreduce(self, ctx, buf, n, stream):
+        """The hook over a host transport (gloo): the stream's work so far,
+        a host all-reduce, the sum copied back before the library continues."""
+        try:
+            t = self._view_of(buf, n)
+            s = (torch.cuda.ExternalStream(stream, device=self.device) if stream
+                 else torch.cuda.default_stream(self.device))
+            s.synchronize()
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.pg)
+            with torch.cuda.stream(s):
+                t.copy_(h)
+            s.synchronize()
+            return 0
+        except BaseException as e:   # (a ctypes callback cannot raise through C)
+            self._ar_err = e
+            return 1
+
+    def _view_of(self, addr, n):
+        """The tensor view of the hook's buffer: the grads arena or a plan's workspace."""
+        for t in [self.grads] + [p.ws for p in self._plans.values()]:
+            b = t.data_ptr()
+            if b <= addr and addr + 4 * n <= b + 4 * t.numel():
+                o = (addr - b) // 4
+                return t[o:o + n]
+        raise RuntimeError("all-reduce hook: buffer outside the trainer's arenas")
+
+    def _plan(self, B, *args, **kwargs):
+        p = super()._plan(B, *args, **kwargs)
+        if self.transport == "library" and not getattr(p, "hooked", False):
+            fn, ctx = self._hook()
+            flags = ((_lib.OAC_DP_FORCE if self._force else 0)
+                     | (_lib.OAC_DP_OVERLAP if self._overlap else 0))
+            check(_lib.lib().oac_sac_set_allreduce(p.handle, fn, ctx, flags))
+            p.hooked = True
+        return p
+
+    def _lib_call(self, fn, *args, **kwargs):
+        self._ar_err = None
+        try:
+            return fn(*args, **kwargs)
+        except RuntimeError:
+            if self._ar_err is not None:
+                raise self._ar_err
+            raise
 
     def __enter__(self):
         return self
@@ -214,6 +325,11 @@ class _DataParallel:
             dp_step(ex, self._all_reduce, overlap)
 
     def _train_host_indices(self, dbatch):
+        if self.transport == "library":   # one library call: staging + the DP step
+            return self._lib_call(super()._train_host_indices, dbatch)
+        return self._train_host_indices_torch(dbatch)
+
+    def _train_host_indices_torch(self, dbatch):
         """The drop-in call (random_batch + train per step) at world > 1: this
         rank's host-drawn indices are staged into the plan's ring, then the
         one-step data-parallel graph (phases + the three all-reduces) runs.
@@ -261,6 +377,9 @@ class _DataParallel:
 
     def _run(self, plan, flags, eps1=None, eps2=None, batch=None, idx=None, n_steps=1,
              counts=None, pre=None):
+        if self.transport == "library" and pre is None:
+            return self._lib_call(super()._run, plan, flags, eps1=eps1, eps2=eps2, batch=batch,
+                                  idx=idx, n_steps=n_steps, counts=counts)
         self._closed = False
 
         def go(sp):

@@ -32,7 +32,7 @@ def _inputs(world):
     return out
 
 
-def _trainer(dp, kind="sac"):
+def _trainer(dp, kind="sac", transport=None):
     from gpu_helpers import producers, Space
     if kind == "goac":
         from fixtures_lib import goac_params
@@ -77,6 +77,8 @@ def _trainer(dp, kind="sac"):
           # alpha exchange, phase "1b" = library phases 4 / 5)
           "rccl1_overlap": dict(force_collectives=True, force_overlap=True),
           "overlap": dict(force_overlap=True)}.get(dp, {})
+    if dp and transport:
+        kw["transport"] = transport
     return cls(pp, qp, action_space=Space(Da), discount=0.99, reward_scale=1.0, policy_lr=1e-3,
                qf_lr=1e-3, soft_target_tau=5e-3, use_automatic_entropy_tuning=True, **kw)
 
@@ -163,7 +165,7 @@ def _ring_run(tr, n_calls, n_steps):
     return torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy()
 
 
-def _nccl_worker(port, q, teardown="close", overlap=False):
+def _nccl_worker(port, q, teardown="close", overlap=False, transport="torch"):
     import faulthandler
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -176,40 +178,54 @@ def _nccl_worker(port, q, teardown="close", overlap=False):
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    tr = _trainer("rccl1_overlap" if overlap else "rccl1")   # RCCL all-reduces at world size 1
-    assert tr.capture and tr._overlap == overlap
-    got = _ring_run(tr, 4, 4)          # call 1 eager, calls 2.. captured (RCCL inside the graph)
-    n_graphs = len(tr._graphs)
-    q.put((got, n_graphs))
+    tr = _trainer("rccl1_overlap" if overlap else "rccl1", transport=transport)
+    assert tr._overlap == overlap and tr.transport == transport
+    got = _ring_run(tr, 4, 4)          # torch: call 1 eager, calls 2.. captured (RCCL inside the graph)
+    if transport == "torch":
+        n = len(tr._graphs)
+    else:   # the library's own communicator, exchanges issued between its launches
+        from oac_amd import _lib
+        n = _lib.lib().oac_sac_trace(tr._last_plan.handle, 1)
+    q.put((got, n))
     if teardown == "close":
         # the trainer's own teardown, then the process group: destroying the
         # group under live graphs (they hold RCCL kernels) aborted the process
         tr.close()
-        assert not tr._graphs
+        assert not tr._graphs and tr._rccl is None
         dist.destroy_process_group()
     # "atexit": neither -- the trainer's atexit hook releases the graphs
 
 
-@pytest.mark.parametrize("teardown,overlap", [("close", False), ("atexit", False), ("close", True)])
-def test_dp_rccl_graph_capture_single_rank_equals_single_gpu(teardown, overlap):
+@pytest.mark.parametrize("teardown,overlap,transport",
+                         [("close", False, "torch"), ("atexit", False, "torch"), ("close", True, "torch"),
+                          ("close", False, "library"), ("atexit", True, "library")])
+def test_dp_rccl_graph_capture_single_rank_equals_single_gpu(teardown, overlap, transport):
     """The captured data-parallel step (phases + RCCL all-reduces in one
     hipGraph, 4 steps per replay) on one rank equals the single-GPU trainer on
     the same device index stream, and the process exits cleanly through the
     trainer's teardown (explicit close(), or its atexit hook).  overlap: the
     world > 1 schedule -- phase "1a", the alpha all-reduce on a forked side
-    stream captured into the graph as a fork / join, phase "1b"."""
+    stream captured into the graph as a fork / join, phase "1b".
+    transport="library": no graph -- the library issues the three RCCL
+    all-reduces itself on its own communicator between its launches (the
+    split schedule on its side stream), checked through the plan's trace."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    p = ctx.Process(target=_nccl_worker, args=(port, q, teardown, overlap))
+    p = ctx.Process(target=_nccl_worker, args=(port, q, teardown, overlap, transport))
     p.start()
     p.join(timeout=150)
     assert p.exitcode == 0, p.exitcode
-    got, n_graphs = q.get()
-    assert n_graphs == 1
+    got, n = q.get()
+    if transport == "torch":
+        assert n == 1   # one captured graph
+    else:
+        from oac_amd._lib import TRACE
+        assert n & TRACE["exchange"] and not n & TRACE["fused"], n
+        assert bool(n & TRACE["split_phase1"]) == overlap, n
     want = _ring_run(_trainer(False), 4, 4)
     assert parity.rel_err(got, want) < 1e-6, parity.rel_err(got, want)
 
@@ -234,14 +250,14 @@ def _h_inputs(world, steps=2):
     return out
 
 
-def _h_trainer(dp):
+def _h_trainer(dp, **kw):
     from gpu_helpers import producers, Space
     from oac_amd import SACTrainer
     from oac_amd.dp import DataParallelSACTrainer
     pp, qp = producers(sac_params(HD, HA, [HH, HH], 4, pi_init_w=1e-3, q_init_w=3e-3))
     cls = DataParallelSACTrainer if dp else SACTrainer
     return cls(pp, qp, action_space=Space(HA), discount=0.99, reward_scale=1.0, policy_lr=3e-4,
-               qf_lr=3e-4, soft_target_tau=5e-3, use_automatic_entropy_tuning=True)
+               qf_lr=3e-4, soft_target_tau=5e-3, use_automatic_entropy_tuning=True, **kw)
 
 
 def _flat_state(tr):
@@ -377,7 +393,7 @@ def _dropin_loop(tr, seed=1, steps=140):
     return torch.cat([tr.params, tr.targets, tr.alpha_state[:3]]).cpu().numpy()
 
 
-def _nccl_dropin_worker(port, q, overlap=False):
+def _nccl_dropin_worker(port, q, overlap=False, transport="torch"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
@@ -386,17 +402,18 @@ def _nccl_dropin_worker(port, q, overlap=False):
     os.environ["MASTER_PORT"] = str(port)
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-    tr = _trainer("rccl1_overlap" if overlap else "rccl1")   # RCCL all-reduces at world size 1
+    tr = _trainer("rccl1_overlap" if overlap else "rccl1", transport=transport)
     assert tr._overlap == overlap
     got = _dropin_loop(tr)
-    q.put((got, len(tr._attached)))
+    q.put((got, len(tr._attached) if transport == "torch" else 1))
     tr.close()
     assert not tr._attached
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", [False, True])
-def test_dp_rccl_dropin_step_graph_equals_single_gpu(overlap):
+@pytest.mark.parametrize("overlap,transport", [(False, "torch"), (True, "torch"), (False, "library"),
+                                               (True, "library")])
+def test_dp_rccl_dropin_step_graph_equals_single_gpu(overlap, transport):
     """The drop-in loop on the data-parallel trainer over RCCL (one rank): from
     the third call on, the captured step (phases + RCCL all-reduces) is
     attached to the handle and each train() is one library call (staging +
@@ -408,7 +425,7 @@ def test_dp_rccl_dropin_step_graph_equals_single_gpu(overlap):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    p = ctx.Process(target=_nccl_dropin_worker, args=(port, q, overlap))
+    p = ctx.Process(target=_nccl_dropin_worker, args=(port, q, overlap, transport))
     p.start()
     p.join(timeout=150)
     assert p.exitcode == 0, p.exitcode
@@ -439,3 +456,190 @@ def test_dp_dropin_loop_equals_device_index_path():
             p.join(timeout=300)
             assert p.exitcode == 0
     assert np.array_equal(got[True], got[False])
+
+
+# ------------------------------------------- the 8-GPU step's code at BASELINE dims
+# bench.py --gpus 8 runs the drop-in loop on DataParallelSACTrainer over RCCL
+# with the split schedule on (dp.py: _overlap at world > 1): at B=4096 per rank
+# phase 0 gathers directly (direct_big), phase 4 carries the batch copy, the
+# targets kernel the width-1 heads' partials (qdot) and the last layers' dW
+# slabs (wl_in_targets).  These tests run exactly that code at Humanoid dims.
+NR = 20000
+BIG_BRANCHES = ("direct_big", "batch_copy", "qdot", "wl_targets", "split_phase1", "exchange")
+
+
+def _h_replay(seed):
+    from oac_amd import ReplayBuffer
+    from gpu_helpers import Space
+    rb = ReplayBuffer(NR, Space(HD), Space(HA), device="cuda:0")
+    d = synthetic_transitions(NR, HD, HA, seed=seed)
+    rb.add_paths([dict(observations=d["observations"], actions=d["actions"],
+                       rewards=d["rewards"], next_observations=d["next_observations"],
+                       terminals=d["terminals"])])
+    return rb, d
+
+
+def _h_dropin_worker(rank, world, port, q, steps):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oac_amd import _lib
+    tr = _h_trainer(True, force_overlap=True, seed=rank)   # the world > 1 RCCL schedule
+    assert tr.transport == "library" and tr._overlap
+    rb, _ = _h_replay(10 + rank)                              # this rank's shard
+    np.random.seed(1 + rank)                                  # this rank's index stream
+    recs, grads0 = [], None
+    for step in range(steps):
+        b = rb.random_batch(HB)
+        b["buffer"] = rb
+        tr.train(b)                                           # rl_algorithm.py:160-167
+        torch.cuda.synchronize()
+        v = tr._last_plan.views
+        recs.append((np.array(b.host_indices), v["eps1"].cpu().numpy(), v["eps2"].cpu().numpy()))
+        if step == 0:
+            grads0 = (tr.grads / world).cpu().numpy()
+    trace = _lib.lib().oac_sac_trace(tr._last_plan.handle, 1)
+    q.put((rank, recs, grads0 if rank == 0 else None, _flat_state(tr) if rank == 0 else None, trace))
+    dist.barrier()
+    tr.close()
+    dist.destroy_process_group()
+
+
+def test_dp_humanoid_b4096_two_ranks_split_schedule_dropin_equals_single_gpu_and_oracle():
+    """configs[3] per rank (Humanoid, B=4096, own replay shard and index
+    stream per rank, Philox eps), two ranks over gloo with the split schedule
+    forced on, through the drop-in call -- the exact code path of the 8-GPU
+    run: phases 0, [alpha exchange || 4], 5, 2, 3 issued by the library, with
+    the large-batch branches (trace).  Against the single-GPU step on the
+    concatenated 8,192 rows with the ranks' own eps, and the oracle (step 0)."""
+    from gpu_helpers import module_tensors
+    from oac_amd._lib import TRACE
+    from oracle import sac_oracle as so
+    world, steps = 2, 2
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    procs = [ctx.Process(target=_h_dropin_worker, args=(r, world, port, q, steps))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((m[0], m[1:]) for m in (q.get(), q.get()))
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    dp_grads0, dp_state = got[0][1], got[0][2]
+    for r in range(world):
+        tr_bits = got[r][3]
+        missing = [b for b in BIG_BRANCHES if not tr_bits & TRACE[b]]
+        assert not missing, (r, missing, tr_bits)
+    shards = [synthetic_transitions(NR, HD, HA, seed=10 + r) for r in range(world)]
+    inputs = []
+    for step in range(steps):
+        parts = [({k: v[got[r][0][step][0]] for k, v in shards[r].items()}, got[r][0][step][1],
+                  got[r][0][step][2]) for r in range(world)]
+        batch = {k: np.concatenate([p[0][k] for p in parts]) for k in parts[0][0]}
+        inputs.append((batch, np.concatenate([p[1] for p in parts]),
+                       np.concatenate([p[2] for p in parts])))
+    tr = _h_trainer(False)
+    single0 = None
+    for step, (batch, e1, e2) in enumerate(inputs):
+        tr.train_from_torch(batch, eps1=e1, eps2=e2)
+        if step == 0:
+            single0 = tr.grads.clone()
+    torch.cuda.synchronize()
+    e_g, e_s = parity.rel_err(dp_grads0, single0.cpu().numpy()), parity.rel_err(dp_state, _flat_state(tr))
+    print("dp vs single: grads0 %.2e, state after %d steps %.2e" % (e_g, steps, e_s))
+    assert e_g < 1e-5 and e_s < 1e-5
+    # step 0 against the oracle on the global batch, per tensor (ReLU-boundary
+    # rows of the critics' hidden layers aside, as in the test above)
+    prm = sac_params(HD, HA, [HH, HH], 4, pi_init_w=1e-3, q_init_w=3e-3)
+    orc = so.SACOracle(prm, HD, HA, policy_lr=3e-4, qf_lr=3e-4, tau=5e-3)
+    batch, e1, e2 = inputs[0]
+    out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
+    x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
+    allowed = {}
+    for grp in ("qf1", "qf2"):
+        qq = prm[grp]
+        u0, pre0 = parity.relu_boundary_units(x0, qq["fc0.weight"], qq["fc0.bias"])
+        u1, _ = parity.relu_boundary_units(np.maximum(pre0, 0), qq["fc1.weight"], qq["fc1.bias"])
+        allowed[grp] = {"fc0.weight": u0, "fc0.bias": u0, "fc1.weight": u1, "fc1.bias": u1}
+    dp_view = torch.from_numpy(dp_grads0).to(tr.grads.device)
+    for grp, mod in (("policy", tr.policy), ("qf1", tr.qf1), ("qf2", tr.qf2)):
+        got_dp = module_tensors(tr, mod, dp_view)
+        for name, ref in out["grads"][grp].items():
+            e, _ = parity.rel_err_rows(got_dp[name].cpu().numpy(), ref.numpy(),
+                                       allowed.get(grp, {}).get(name, []))
+            assert e < 1e-5, (grp, name, e)
+
+
+def _nccl_h_worker(port, q, B, steps):
+    import faulthandler
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    os.makedirs(os.path.join(os.path.dirname(here), "gpurun_out"), exist_ok=True)
+    trace = open(os.path.join(os.path.dirname(here), "gpurun_out", "dp_nccl_h_worker_stack.txt"), "w")
+    faulthandler.dump_traceback_later(100, exit=True, file=trace)
+    for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    from oac_amd import _lib
+    tr = _h_trainer(True, force_collectives=True, force_overlap=True)
+    rb, _ = _h_replay(7)
+    np.random.seed(3)
+    for _ in range(steps):
+        b = rb.random_batch(B)
+        b["buffer"] = rb
+        tr.train(b)
+    torch.cuda.synchronize()
+    bits = _lib.lib().oac_sac_trace(tr._last_plan.handle, 1)
+    q.put((_flat_state(tr), bits))
+    tr.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("B", [256, 4096])
+def test_dp_rccl_humanoid_split_schedule_dropin_equals_single_gpu(B):
+    """The 8-GPU step's code over RCCL at one rank, Humanoid dims at the
+    headline batch (256) and configs[3]'s (4096): the library's own
+    communicator, the three all-reduces issued between its launches, the
+    alpha exchange on the side stream beside phase 4 -- through the drop-in
+    call, against the single-process drop-in step on the same replay, index
+    stream and Philox eps."""
+    from oac_amd._lib import TRACE
+    steps = 24
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    p = ctx.Process(target=_nccl_h_worker, args=(port, q, B, steps))
+    p.start()
+    p.join(timeout=200)
+    assert p.exitcode == 0, p.exitcode
+    got, bits = q.get()
+    want_bits = ("direct",) if B == 256 else BIG_BRANCHES
+    missing = [b for b in want_bits + ("exchange", "split_phase1") if not bits & TRACE[b]]
+    assert not missing and not bits & TRACE["fused"], (missing, bits)
+    tr = _h_trainer(False)
+    rb, _ = _h_replay(7)
+    np.random.seed(3)
+    for _ in range(steps):
+        b = rb.random_batch(B)
+        b["buffer"] = rb
+        tr.train(b)
+    torch.cuda.synchronize()
+    e = parity.rel_err(got, _flat_state(tr))
+    print("B=%d DP (RCCL, split schedule) vs single-process: %.2e" % (B, e))
+    assert e < 1e-5
