@@ -464,22 +464,25 @@ def cpu_threads_all():
     return (min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n), n
 
 
-def cpu_baseline(args, runs=2, steps=1000, warmup=20, all_runs=1):
+def cpu_baseline(args, runs=5, steps=300, warmup=20, all_runs=1, kind="sac", B=None,
+                 dims=None):
     """The reference's PyTorch-CPU step restated on torch autograd
     (oracle/sac_autograd.py: the reference's forward ops, backward() and the
     torch-1.4 Adam, pinned against the reference-run goldens in
     tests/test_oracle_golden.py), with the host numpy gather + fp32
     conversion, timed on this host's cores with BASELINE.md section 3's
-    procedure, bounded: 20 warm-up steps, then runs of 1,000 steps each -- the
+    procedure, bounded: `warmup` steps, then runs of `steps` steps each -- the
     median of `runs` at 1 thread (the reference launcher's
     torch.set_num_threads(1), launcher_util.py:90) and `all_runs` at all
-    cores."""
+    cores (none when 0).  kind "sac": SACTrainer (trainer/trainer.py); kind
+    "poac": particle_trainer_oac.ParticleTrainer, K=10 shared heads."""
     sys.path.insert(0, ROOT)
     from oracle import sac_oracle as so
-    from oracle.sac_autograd import SACAutograd
+    from oracle.sac_autograd import ParticleOACAutograd, SACAutograd
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from fixtures_lib import sac_params
-    Do, Da, H, B = args.obs_dim, args.act_dim, args.hidden, args.batch
+    Do, Da, H = dims or (args.obs_dim, args.act_dim, args.hidden)
+    B = B or args.batch
     n = 100_000
     rs = np.random.RandomState(0)
     data = dict(observations=rs.standard_normal((n, Do)), actions=rs.uniform(-1, 1, (n, Da)),
@@ -487,7 +490,14 @@ def cpu_baseline(args, runs=2, steps=1000, warmup=20, all_runs=1):
                 terminals=(rs.uniform(0, 1, (n, 1)) < 0.01).astype(np.uint8),
                 next_observations=rs.standard_normal((n, Do)))
     rep = so.NumpyReplay(data)
-    orc = SACAutograd(sac_params(Do, Da, [H, H], 0), Do, Da)
+    if kind == "poac":
+        K = 10
+        orc = ParticleOACAutograd(sac_params(Do, Da, [H, H], 0, q_out=K,
+                                             q_last_bias=np.linspace(0.0, 500.0, K)), Do, Da, K)
+        what = "P-OAC (particle_trainer_oac K=10) steps"
+    else:
+        orc = SACAutograd(sac_params(Do, Da, [H, H], 0), Do, Da)
+        what = "SAC steps"
     g = torch.Generator().manual_seed(2)
     irs = np.random.RandomState(1)
 
@@ -509,16 +519,18 @@ def cpu_baseline(args, runs=2, steps=1000, warmup=20, all_runs=1):
             rates.append(steps / (time.perf_counter() - t0))
         return float(np.median(rates)), [round(r, 2) for r in rates]
     one, one_runs = median_rate(1, runs)
-    T, aff = cpu_threads_all()
-    allc, all_rates = median_rate(T, all_runs)
+    sample = (f"{warmup} warm-up steps, then runs of {steps} {what} of the reference's op "
+              f"sequence on torch autograd (oracle/sac_autograd.py; obs {Do}, act {Da}, 2x{H}, "
+              f"B={B}, numpy f64 replay of {n} rows, torch CPU fp32)")
+    out = dict(value=round(one, 2), unit="grad-steps/s", cores=1, kind="port",
+               sample=sample + f", median of {runs} runs, 1 thread", runs=one_runs)
+    if all_runs:
+        T, aff = cpu_threads_all()
+        allc, all_rates = median_rate(T, all_runs)
+        out["all_cores"] = dict(value=round(allc, 2), cores=T, affinity_cpus=aff, runs=all_rates,
+                                sample=sample + f", {all_runs} run(s), {T} threads")
     torch.set_num_threads(1)
-    sample = (f"{warmup} warm-up steps, then runs of {steps} SAC steps of the reference's op "
-              f"sequence on torch autograd (oracle/sac_autograd.py; Humanoid dims, 2x256, B={B}, "
-              f"numpy f64 replay of {n} rows, torch CPU fp32)")
-    return dict(value=round(one, 2), unit="grad-steps/s", cores=1, kind="port",
-                sample=sample + f", median of {runs} runs, 1 thread", runs=one_runs,
-                all_cores=dict(value=round(allc, 2), cores=T, affinity_cpus=aff, runs=all_rates,
-                               sample=sample + f", {all_runs} run(s), {T} threads"))
+    return out
 
 
 def recipe_cpu_baseline(kind, args, steps=200):
@@ -835,11 +847,18 @@ def main():
             torch.cuda.synchronize()
 
     run(args.warmup)
-    barrier()
-    t0 = time.perf_counter()
-    run(args.steps)
-    barrier()
-    elapsed = time.perf_counter() - t0
+    # no Python garbage collection inside the timed region (as in timed():
+    # a 20-step window is ~2 ms, and a collection pause is a visible share)
+    gc.collect()
+    gc.disable()
+    try:
+        barrier()
+        t0 = time.perf_counter()
+        run(args.steps)
+        barrier()
+        elapsed = time.perf_counter() - t0
+    finally:
+        gc.enable()
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -912,6 +931,12 @@ def main():
                     out[kind]["cpu_baseline"] = recipe_cpu_baseline(kind, args)
         if not args.no_cpu_baseline and world == 1:   # the CPU baseline is an N=1 figure
             out["cpu_baseline"] = cpu_baseline(args)
+            if big is not None:      # configs[2]: the same step at batch 4096
+                out["b4096"]["cpu_baseline"] = cpu_baseline(args, steps=4, warmup=2, all_runs=0,
+                                                            B=4096)
+            if "poac_ant_b4096" in out:   # configs[4]: P-OAC K=10, Ant dims, batch 4096
+                out["poac_ant_b4096"]["cpu_baseline"] = cpu_baseline(
+                    args, steps=8, warmup=2, all_runs=0, kind="poac", B=4096, dims=(111, 8, 256))
         print(json.dumps(out), flush=True)
     if dp:
         # the trainer's teardown (its captured step graphs hold RCCL kernels),

@@ -194,3 +194,92 @@ class SACAutograd:
         """{group: {reference key: tensor}} of the post-step parameters."""
         return {g: {k: p.detach() for k, p in getattr(self, g).named().items()}
                 for g in ("policy", "qf1", "qf2", "target_qf1", "target_qf2")}
+
+
+class ParticleOACAutograd:
+    """ParticleTrainer of trainer/particle_trainer_oac.py (share_layers=True:
+    one critic with K outputs, the P-OAC trainer of BASELINE configs[4]) on
+    torch autograd, CPU -- the reference's op sequence of train_from_torch
+    (lines 169-324) for the configs[4] CPU baseline:
+
+    * critic on (obs, a), permute to [K, B, 1], torch.sort over K     :185-192
+    * policy(next_obs) (eps1), target critic, sort, quantile target   :193-208
+    * counts=True re-centring of drawn rows                          :220-224
+    * the K MSEs summed (not averaged), one backward, Adam             :247-256
+    * policy(obs) (eps2) after the critic step, alpha loss and step   :271-284
+    * the post-step critic on (obs, a~), sort, policy loss on slot 0  :286-300
+    * Polyak                                                           :320-324
+
+    As in the reference, the policy backward also runs through (and
+    accumulates into) the critic's parameters, whose grads the next step's
+    zero_grad drops."""
+
+    def __init__(self, params, obs_dim, act_dim, K, discount=0.99, reward_scale=1.0,
+                 policy_lr=3e-4, qf_lr=3e-4, tau=5e-3, target_update_period=1,
+                 target_entropy=None, dtype=torch.float32):
+        self.dtype, self.K = dtype, K
+        self.policy = _Mlp(params["policy"], dtype, policy=True)
+        self.qf = _Mlp(params["qf1"], dtype)
+        self.tf = _Mlp(params["target_qf1"], dtype)
+        self.discount, self.reward_scale, self.tau = discount, reward_scale, tau
+        self.period = target_update_period
+        self.target_entropy = -float(act_dim) if target_entropy is None else target_entropy
+        self.log_alpha = torch.zeros(1, dtype=dtype, requires_grad=True)
+        self.qf_optimizer = Adam14(self.qf.parameters(), qf_lr)
+        self.policy_optimizer = Adam14(self.policy.parameters(), policy_lr)
+        self.alpha_optimizer = Adam14([self.log_alpha], policy_lr)
+        self.n_steps = 0
+
+    def step(self, batch, eps1, eps2):
+        dt = self.dtype
+        t = lambda k: torch.as_tensor(batch[k]).to(dt)
+        obs, actions, next_obs = t("observations"), t("actions"), t("next_observations")
+        rewards, terminals = t("rewards"), t("terminals")
+        eps1, eps2 = torch.as_tensor(eps1).to(dt), torch.as_tensor(eps2).to(dt)
+        qs = torch.stack([self.qf.q(obs, actions)], dim=0).permute(2, 1, 0)      # [K, B, 1]
+        sorted_qs, _ = torch.sort(qs, dim=0)
+        next_actions, _, _, _ = self.policy.policy(next_obs, eps1)
+        target_qs = torch.stack([self.tf.q(next_obs, next_actions)], dim=0).permute(2, 1, 0)
+        target_sorted, _ = torch.sort(target_qs, dim=0)
+        q_target = self.reward_scale * rewards + (1.0 - terminals) * self.discount * target_sorted
+        if batch.get("counts") is not None:
+            counts = t("counts")
+            factor = torch.zeros_like(counts)
+            factor[counts == 0] = 1
+            q_target = (q_target * factor) + (1 - factor) * (
+                sorted_qs - torch.mean(sorted_qs, dim=0) + torch.mean(q_target, dim=0))
+        qf_losses, qf_loss = [], 0
+        for i in range(self.K):
+            q_loss = ((sorted_qs[i] - q_target[i].detach()) ** 2).mean()
+            qf_losses.append(q_loss)
+            qf_loss = qf_loss + q_loss
+        self.qf_optimizer.zero_grad()
+        qf_loss.backward(retain_graph=True)
+        gq = {k: p.grad.clone() for k, p in self.qf.named().items()}
+        self.qf_optimizer.step()
+        new_actions, mean, log_std, log_pi = self.policy.policy(obs, eps2)
+        alpha_loss = -(self.log_alpha * (log_pi + self.target_entropy).detach()).mean()
+        self.alpha_optimizer.zero_grad()
+        alpha_loss.backward()
+        g_la = self.log_alpha.grad.clone()   # (the policy backward adds to it later)
+        self.alpha_optimizer.step()
+        alpha = self.log_alpha.exp()
+        pi_qs = torch.stack([self.qf.q(obs, new_actions)], dim=0).permute(2, 1, 0)
+        q_new = torch.sort(pi_qs, dim=0)[0][0]
+        policy_loss = (alpha * log_pi - q_new).mean()
+        self.policy_optimizer.zero_grad()
+        policy_loss.backward()
+        gp = {k: p.grad.clone() for k, p in self.policy.named().items()}
+        self.policy_optimizer.step()
+        if self.n_steps % self.period == 0:
+            with torch.no_grad():
+                for ps, pt in zip(self.qf.parameters(), self.tf.parameters()):
+                    pt.data.copy_(pt.data * (1.0 - self.tau) + ps.data * self.tau)
+        self.n_steps += 1
+        return dict(grads=dict(policy=gp, qf=gq, log_alpha=g_la),
+                    qf_losses=torch.stack([q.detach() for q in qf_losses]),
+                    policy_loss=policy_loss.detach(), alpha_loss=alpha_loss.detach())
+
+    def state(self):
+        return {g: {k: p.detach() for k, p in m.named().items()}
+                for g, m in (("policy", self.policy), ("qf", self.qf), ("tf", self.tf))}

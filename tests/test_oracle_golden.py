@@ -547,3 +547,44 @@ def test_sac_autograd_restatement_matches_reference_golden(name):
     bad = {k: (v, noise.get(k, 0.0)) for k, v in errs.items()
            if v > parity.gate(k, noise.get(k, 0.0))}
     assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
+
+
+@pytest.mark.parametrize("name", ["poac_small", "poac_ant_b4096", "poac_counts", "poac_period2"])
+def test_poac_autograd_restatement_matches_reference_golden(name):
+    """oracle/sac_autograd.py ParticleOACAutograd (particle_trainer_oac.py's op
+    sequence on torch autograd: bench.py's configs[4] CPU baseline) against
+    the reference's own run, every step under the trajectory gate (step 0 at
+    the reference's own float64 distance)."""
+    from oracle.sac_autograd import ParticleOACAutograd
+    meta, g = parity.load(name)
+    K = meta["K"]
+    params = sac_params(meta["obs_dim"], meta["act_dim"], meta["hidden"], meta["seed"], q_out=K,
+                        q_last_bias=np.linspace(meta["q_min"], meta["q_max"], K),
+                        pi_init_w=meta["pi_init_w"])
+    ag = ParticleOACAutograd(params, meta["obs_dim"], meta["act_dim"], K,
+                             discount=meta["discount"], policy_lr=meta["lr"], qf_lr=meta["lr"],
+                             tau=meta["tau"], target_update_period=meta.get("target_update_period", 1))
+    noise = poac_noise(meta, g)
+    errs = {}
+    for s in range(meta["steps"]):
+        b = build_batch(meta, g[f"s{s}/idx"])
+        if meta.get("counts"):
+            b["counts"] = g[f"s{s}/counts"][:, None]
+        out = ag.step(b, g[f"s{s}/eps1"], g[f"s{s}/eps2"])
+        for grp in ("policy", "qf"):
+            for pn, t in out["grads"][grp].items():
+                key = f"s{s}/grad/{grp}/{pn}"
+                errs[key] = parity.compare(g, key, t.numpy())
+        errs[f"s{s}/grad/log_alpha"] = parity.rel_err(out["grads"]["log_alpha"].numpy(),
+                                                      g[f"s{s}/grad/log_alpha"])
+        for grp, sd in ag.state().items():
+            for pn, t in sd.items():
+                key = f"s{s}/post/{grp}/{pn}"
+                gk = f"s{s}/grad/{grp}/{pn}" if s == 0 and grp != "tf" else None
+                errs[key], _ = parity.compare_post(g, key, gk, t.numpy(), meta["lr"])
+        for i in range(K):
+            if f"s{s}/stat/QF{i} Loss" in g:
+                errs[f"s{s}/stat/QF{i} Loss"] = parity.stat_err(float(out["qf_losses"][i]), g,
+                                                                f"s{s}/stat/QF{i} Loss")
+    bad = gated(errs, noise)
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:10]
