@@ -20,6 +20,7 @@
 #include "gemm_operand.h"
 
 #include <algorithm>
+#include <cstring>
 
 namespace oac {
 
@@ -205,14 +206,18 @@ constexpr int kGatherU = 4;   // float4s per lane of a side block's row copy (ro
 template <int NW, int GPW>
 __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int publish, int tb1,
                                                  int tb2, int tb3, int tb4, int tb5, int tb6,
-                                                 int tb7, const GemmBatch& batch, float* red) {
+                                                 int tb7, const GemmBatch& batch, float* red,
+                                                 const int* inl = nullptr) {
   constexpr int PER = 1024 / (64 * NW);   // epilogue elements per thread
   GS_STAGE(0);
   if (publish && bid == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
   const int* rows = nullptr;   // direct drop-in gather: this step's index slot (host memory)
   long long bc = 0;
-  if (batch.rg.ring) {
+  if (inl) {   // the indices in the kernel arguments (gemm_small_kernel_inl)
+    bc = batch.rg.state->batch_counter;
+    rows = inl;
+  } else if (batch.rg.ring) {
     bc = batch.rg.state->batch_counter;
     rows = batch.rg.ring + (long)(bc % batch.rg.slots) * batch.rg.B;
   }
@@ -387,6 +392,19 @@ gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int t
                             batch, red);
 }
 
+// The direct drop-in layer-0 launch with the step's B <= 256 indices in the
+// kernel arguments: no dependent read of the host-coherent slot before the
+// tiles can request their rows.
+struct InlineRows { int r[kInlineRows]; };
+template <int NW, int GPW>
+__global__ void __launch_bounds__(64 * NW)
+gemm_small_kernel_inl(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5,
+                      int tb6, int tb7, const GemmBatch batch, const InlineRows ir) {
+  __shared__ __attribute__((aligned(16))) float red[SmallLds<NW>::N];
+  gemm_small_block<NW, GPW>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6, tb7,
+                            batch, red, ir.r);
+}
+
 // tile geometry shared with the plan builder
 int gemm_small_waves(const GemmBatch& b) {
   int kmax = 1;
@@ -436,6 +454,17 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   }
   const int grid = b.total_tiles + b.adam_blocks + (b.rg.ring ? b.rg.blocks : 0);
   const GemmHead h = gemm_head(b);
+  if (b.rg.inl && b.rg.ring && b.rg.B <= kInlineRows && ((nw == 16 && gpw == 4) || (nw == 8 && gpw == 5))) {
+    InlineRows ir;
+    std::memcpy(ir.r, b.rg.inl, sizeof(int) * b.rg.B);
+    if (nw == 16)
+      OAC_LAUNCH((gemm_small_kernel_inl<16, 4>), dim3(grid), dim3(64 * 16), 0, s, h.total_tiles, h.publish,
+                 h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b, ir);
+    else
+      OAC_LAUNCH((gemm_small_kernel_inl<8, 5>), dim3(grid), dim3(64 * 8), 0, s, h.total_tiles, h.publish,
+                 h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b, ir);
+    return hipGetLastError();
+  }
 #define OAC_GS(NW_, G_) \
   if (nw == NW_ && gpw == G_) { \
     OAC_LAUNCH((gemm_small_kernel<NW_, G_>), dim3(grid), dim3(64 * NW_), 0, s, h.total_tiles, h.publish, \

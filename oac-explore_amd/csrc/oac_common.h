@@ -102,8 +102,13 @@ constexpr int kMaxTasks = 8;
 // index slot rows = ring + (batch_counter % slots) * B, and `blocks` extra
 // workgroups copy those rows to `out` (the step's batch for the later launches)
 // and draw the step's Philox eps -- the gather launch's work, off the chain.
+// inl (host pointer, B <= kInlineRows): the step's indices themselves, which
+// the launcher copies into the kernel arguments (no host-memory read in the
+// kernel; never under stream capture, whose kernel arguments are frozen).
+constexpr int kInlineRows = 256;
 struct RowGather {
   const int* ring; int slots, B;
+  const int* inl;
   const StepState* state;
   int blocks;
   const float* replay; long row_stride; float* out;

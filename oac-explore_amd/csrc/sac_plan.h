@@ -37,6 +37,10 @@ struct SacPlan : PlanBase {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int trace = 0;   // OAC_TRACE_* bits of the branches issued since the last read
+  // the drop-in step's staged indices (B <= kInlineRows), passed to the
+  // direct layer-0 launch in its kernel arguments; valid after a staging call
+  int inline_rows[kInlineRows];
+  bool inline_ok = false;
 
   float* W(int id) const { return b.workspace + ws[id].off; }
   float* X() const { return W(OAC_WS_BATCH) + (long)slot * c.batch * c.row_stride; }

@@ -244,6 +244,10 @@ static GemmTask critic_dw0(SacPlan& p, int i, int c0, int n, bool bias) {
 // Not with a next-step prefetch: its critic forward reads the post-step
 // layer 0 in the dL/da launch.  OAC_DW0_DEFER=0 keeps the layer-0 dW + Adam
 // in the layer-0 launch.
+static bool inline_rows_on() {
+  static const bool on = [] { const char* e = getenv("OAC_INLINE_ROWS"); return !e || atoi(e) != 0; }();
+  return on;
+}
 static bool defer_dw0_on() {
   static const bool on = [] { const char* e = getenv("OAC_DW0_DEFER"); return !e || atoi(e) != 0; }();
   return on;
@@ -350,6 +354,12 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
       RowGather& g = gb.rg;
       g.ring = p.host_ring; g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
       g.replay = p.b.replay; g.row_stride = RS; g.out = X;
+      // the staged indices in the kernel arguments (not under capture: a
+      // captured launch would replay this step's indices)
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (p.inline_ok && B <= kInlineRows && hipStreamIsCapturing(s, &cs) == hipSuccess &&
+          cs == hipStreamCaptureStatusNone && inline_rows_on())
+        g.inl = p.inline_rows;
       if (flags & OAC_STEP_DEVICE_EPS) {
         g.eps1 = p.E1(); g.eps2 = p.E2(); g.n_eps = B * Da;
       }
@@ -358,6 +368,7 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
       g.blocks = std::max(1, (B + 7) / 8);
     }
     if (run_gemm(p, gb, s)) return 1;
+    p.inline_ok = false;   // (one staging call, one step)
   }
   {  // layer 1
     GemmBatch gb{};
@@ -1091,6 +1102,11 @@ static int stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stre
       return 1;
     }
     dst[i] = (int32_t)v;
+  }
+  p.inline_ok = false;
+  if (p.rows_direct && B <= kInlineRows) {   // the direct step passes them as kernel arguments
+    std::memcpy(p.inline_rows, dst, sizeof(int32_t) * B);
+    p.inline_ok = true;
   }
   if (host_read) return 0;   // the step's first launch reads the slot from host memory
   OAC_HIP_CHECK(hipMemcpyAsync(const_cast<int32_t*>(p.b.idx_ring) + (long)slot * B, dst,

@@ -21,6 +21,12 @@
 //   UNCACHED the handed-off activations (h2, dh1) in uncached device memory
 //           (hipDeviceMallocUncached): stores and loads go past the L2s, so
 //           the hand-off needs only the drain and the counter.
+// PREFETCH (round 5): before a tile waits, each wave
+// issues the loads of its first k-groups of the operand that is not handed
+// off (B: W1 for dh1, h1 for dW1, the batch rows X for dW0) and keeps the
+// values live, so the tile's own loads of those lines after the wait hit the
+// CU's L1 instead of L2 / MALL -- the one overlap a launch boundary cannot
+// have.
 // Per-workgroup wall clocks (s_memrealtime, 100 MHz) at every stage edge give
 // the edge waits; outputs are compared bitwise with the launches (the same
 // 16-wave geometry, so the same summation order).  The last workgroup out
@@ -89,6 +95,43 @@ __device__ __forceinline__ void signal_dep(unsigned* ctr, const TileDep& d) {
   }
 }
 
+// the loads k_loop will issue first for this tile's B operand (its first GPW
+// k-groups per wave), summed into a register the caller keeps live
+template <int NW, int GPW>
+__device__ __forceinline__ float warm_b(int bid, const GemmHead& h, const GemmBatch& batch) {
+  int ti = 0;
+  ti = bid >= h.tb1 ? 1 : ti; ti = bid >= h.tb2 ? 2 : ti; ti = bid >= h.tb3 ? 3 : ti;
+  ti = bid >= h.tb4 ? 4 : ti; ti = bid >= h.tb5 ? 5 : ti; ti = bid >= h.tb6 ? 6 : ti;
+  ti = bid >= h.tb7 ? 7 : ti;
+  ti = __builtin_amdgcn_readfirstlane(ti);
+  const GemmTask& t = batch.t[ti];
+  const int local = bid - t.tile_begin;   // (ksplit == 1 in this branch)
+  const int n0 = (local % t.tiles_n) * 32;
+  const int lane = threadIdx.x & 63, l32 = lane & 31, half = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g_hi = (t.K + 7) >> 3, kmax = t.K - 1;
+  float s = 0.f, x[4], y[4];
+  if (t.b_kc) {
+    const Lane lb = lane_init<OP_KC>(n0 + l32, t.N, false, t.B, t.ldb, nullptr, nullptr);
+#pragma unroll
+    for (int j = 0; j < GPW; ++j)
+      if (wave + j * NW < g_hi) {
+        load4<OP_KC>(lb, 8 * (wave + j * NW) + 4 * half, kmax, x, y);
+        s += (x[0] + x[1]) + (x[2] + x[3]);
+      }
+  } else {
+    const Lane lb = lane_init<OP_MN>(n0 + l32, t.b_ones ? t.N - 1 : t.N, t.b_ones != 0, t.B, t.ldb,
+                                     nullptr, nullptr);
+#pragma unroll
+    for (int j = 0; j < GPW; ++j)
+      if (wave + j * NW < g_hi) {
+        load4<OP_MN>(lb, 8 * (wave + j * NW) + 4 * half, kmax, x, y);
+        s += (x[0] + x[1]) + (x[2] + x[3]);
+      }
+  }
+  return s;
+}
+
 // the three stages' batches travel in the kernel arguments (as a launch's
 // batch does): pointers loaded from the argument segment are known to be
 // global, so the tiles' operand accesses are global loads -- from a batch in
@@ -96,7 +139,7 @@ __device__ __forceinline__ void signal_dep(unsigned* ctr, const TileDep& d) {
 // against lgkmcnt and serialise with the LDS reduction
 struct Stages { GemmBatch st[3]; GemmHead hh[3]; };
 
-template <int NW, int GPW, bool FENCE>
+template <int NW, int GPW, bool FENCE, bool PF = false>
 __global__ void __launch_bounds__(64 * NW)
 dataflow_kernel(const Stages sg, const TileDep* __restrict__ deps, int nst,
                 unsigned* ctr, unsigned long long* clk) {
@@ -113,7 +156,10 @@ dataflow_kernel(const Stages sg, const TileDep* __restrict__ deps, int nst,
     const int w0 = ((int)blockIdx.x - extra + (int)gridDim.x) % (int)gridDim.x;
     for (int vb = w0; vb < h.total_tiles; vb += gridDim.x) {
       const TileDep d = deps[off + vb];
+      float warm = 0.f;
+      if (PF && d.wait >= 0) warm = warm_b<NW, GPW>(vb, h, bs[st]);
       wait_dep<FENCE>(ctr, d);
+      asm volatile("" ::"v"(warm));
       if (threadIdx.x == 0 && vb == w0 && st > 0) my[2 * st] = wall_clock64();
       gemm_small_block<NW, GPW>(vb, h.total_tiles, h.publish, h.tb1, h.tb2, h.tb3, h.tb4, h.tb5,
                                 h.tb6, h.tb7, bs[st], red);
@@ -273,15 +319,23 @@ int main() {
     };
     Stages sg;
     for (int i = 0; i < 3; ++i) { sg.st[i] = br.st[i]; sg.hh[i] = hh[i]; }
+    bool pf = false;
     auto dataflow = [&]() {
-      if (uncached)
+      if (uncached && pf)
+        hipLaunchKernelGGL((dataflow_kernel<16, 4, false, true>), dim3(256), dim3(1024), 0, s, sg, d_dep, 3, ctr, clk);
+      else if (uncached)
         hipLaunchKernelGGL((dataflow_kernel<16, 4, false>), dim3(256), dim3(1024), 0, s, sg, d_dep, 3, ctr, clk);
+      else if (pf)
+        hipLaunchKernelGGL((dataflow_kernel<16, 4, true, true>), dim3(256), dim3(1024), 0, s, sg, d_dep, 3, ctr, clk);
       else
         hipLaunchKernelGGL((dataflow_kernel<16, 4, true>), dim3(256), dim3(1024), 0, s, sg, d_dep, 3, ctr, clk);
       CK(hipGetLastError());
     };
     launches(16); CK(hipStreamSynchronize(s));
     const std::vector<float> ref = snapshot();
+    for (int pass = 0; pass < 2; ++pass) {
+    pf = pass == 1;
+    printf("-- %s\n", pf ? "PREFETCH: non-handed-off operand loaded before the wait" : "no prefetch");
     dataflow(); CK(hipStreamSynchronize(s));
     const std::vector<float> got = snapshot();
     size_t bad = 0;
@@ -311,6 +365,7 @@ int main() {
     printf("3 launches per step (default waves) : %7.2f us/step\n", per_step_us(s, [&] { launches(0); }));
     printf("3 launches per step (16 waves)      : %7.2f us/step\n", per_step_us(s, [&] { launches(16); }));
     printf("1 dataflow launch                   : %7.2f us/step\n", per_step_us(s, [&] { dataflow(); }));
+    }
   }
   return 0;
 }
