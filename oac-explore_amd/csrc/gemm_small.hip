@@ -396,13 +396,23 @@ gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int t
 // kernel arguments: no dependent read of the host-coherent slot before the
 // tiles can request their rows.
 struct InlineRows { int r[kInlineRows]; };
+// (read in place in the kernel-argument segment: taking the address of the
+// by-value argument made the compiler copy its 1 KB into every thread's
+// scratch -- 1,028 bytes of private segment, that launch 11.7 -> 45.8 us)
+constexpr size_t kInlineRowsOff =
+    (9 * sizeof(int) + alignof(GemmBatch) - 1) / alignof(GemmBatch) * alignof(GemmBatch) +
+    sizeof(GemmBatch);
 template <int NW, int GPW>
 __global__ void __launch_bounds__(64 * NW)
 gemm_small_kernel_inl(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5,
                       int tb6, int tb7, const GemmBatch batch, const InlineRows ir) {
   __shared__ __attribute__((aligned(16))) float red[SmallLds<NW>::N];
+  (void)ir;
+  const __attribute__((address_space(4))) char* ka =
+      (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+  const int* rows = (const int*)(ka + kInlineRowsOff);
   gemm_small_block<NW, GPW>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6, tb7,
-                            batch, red, ir.r);
+                            batch, red, rows);
 }
 
 // tile geometry shared with the plan builder

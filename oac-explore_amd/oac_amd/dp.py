@@ -159,8 +159,17 @@ class _DataParallel:
         # all-reduce captured into the step graph) and over gloo (a
         # synchronous all-reduce between the two halves)
         self._nccl = dist.get_backend(process_group) == "nccl"
-        self._overlap = force_overlap or (self._nccl and self.world > 1
-                                          and os.environ.get("OAC_DP_OVERLAP", "1") != "0")
+        if self.transport == "library":
+            # the library's fork / join of the overlapped alpha exchange (an
+            # event record + a cross-stream wait each way, direct launches)
+            # measured ~24 us per step at one rank over RCCL (7,459 -> 6,321
+            # steps/s with the exchanges forced): more than a 16-float
+            # all-reduce's link latency, so the exchange stays in line unless
+            # asked for (OAC_DP_OVERLAP=1)
+            self._overlap = force_overlap or os.environ.get("OAC_DP_OVERLAP") == "1"
+        else:
+            self._overlap = force_overlap or (self._nccl and self.world > 1
+                                              and os.environ.get("OAC_DP_OVERLAP", "1") != "0")
         self._graphs, self._eager_seen = {}, set()
         self._attached = {}   # plan handles a captured step graph is attached to
         self._closed = False

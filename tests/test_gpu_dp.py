@@ -479,7 +479,7 @@ def _h_replay(seed):
     return rb, d
 
 
-def _h_dropin_worker(rank, world, port, q, steps):
+def _h_dropin_worker(rank, world, port, q, steps, overlap):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (here, os.path.join(os.path.dirname(here), "oac-explore_amd")):
@@ -489,8 +489,8 @@ def _h_dropin_worker(rank, world, port, q, steps):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oac_amd import _lib
-    tr = _h_trainer(True, force_overlap=True, seed=rank)   # the world > 1 RCCL schedule
-    assert tr.transport == "library" and tr._overlap
+    tr = _h_trainer(True, force_overlap=overlap, seed=rank)
+    assert tr.transport == "library" and tr._overlap == overlap
     rb, _ = _h_replay(10 + rank)                              # this rank's shard
     np.random.seed(1 + rank)                                  # this rank's index stream
     recs, grads0 = [], None
@@ -510,12 +510,14 @@ def _h_dropin_worker(rank, world, port, q, steps):
     dist.destroy_process_group()
 
 
-def test_dp_humanoid_b4096_two_ranks_split_schedule_dropin_equals_single_gpu_and_oracle():
+@pytest.mark.parametrize("overlap", [False, True])
+def test_dp_humanoid_b4096_two_ranks_split_schedule_dropin_equals_single_gpu_and_oracle(overlap):
     """configs[3] per rank (Humanoid, B=4096, own replay shard and index
-    stream per rank, Philox eps), two ranks over gloo with the split schedule
-    forced on, through the drop-in call -- the exact code path of the 8-GPU
-    run: phases 0, [alpha exchange || 4], 5, 2, 3 issued by the library, with
-    the large-batch branches (trace).  Against the single-GPU step on the
+    stream per rank, Philox eps), two ranks over gloo, through the drop-in
+    call -- the exact code path of the 8-GPU run: phases 0, [alpha exchange],
+    1, [critic grads], 2, [policy grads], 3 issued by the library, with the
+    large-batch branches (trace); overlap: the split schedule (phases 4 / 5
+    with the alpha exchange on the plan's side stream, OAC_DP_OVERLAP).  Against the single-GPU step on the
     concatenated 8,192 rows with the ranks' own eps, and the oracle (step 0)."""
     from gpu_helpers import module_tensors
     from oac_amd._lib import TRACE
@@ -527,7 +529,7 @@ def test_dp_humanoid_b4096_two_ranks_split_schedule_dropin_equals_single_gpu_and
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_h_dropin_worker, args=(r, world, port, q, steps))
+    procs = [ctx.Process(target=_h_dropin_worker, args=(r, world, port, q, steps, overlap))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -538,8 +540,9 @@ def test_dp_humanoid_b4096_two_ranks_split_schedule_dropin_equals_single_gpu_and
     dp_grads0, dp_state = got[0][1], got[0][2]
     for r in range(world):
         tr_bits = got[r][3]
-        missing = [b for b in BIG_BRANCHES if not tr_bits & TRACE[b]]
+        missing = [b for b in BIG_BRANCHES if b != "split_phase1" and not tr_bits & TRACE[b]]
         assert not missing, (r, missing, tr_bits)
+        assert bool(tr_bits & TRACE["split_phase1"]) == overlap, tr_bits
     shards = [synthetic_transitions(NR, HD, HA, seed=10 + r) for r in range(world)]
     inputs = []
     for step in range(steps):
@@ -554,16 +557,31 @@ def test_dp_humanoid_b4096_two_ranks_split_schedule_dropin_equals_single_gpu_and
         tr.train_from_torch(batch, eps1=e1, eps2=e2)
         if step == 0:
             single0 = tr.grads.clone()
+            # the layer-1 masks the step's critic backward used (8,192 rows)
+            h2g = {g: tr._last_plan.views["h2q" + g[-1]].cpu().numpy() for g in ("qf1", "qf2")}
     torch.cuda.synchronize()
     e_g, e_s = parity.rel_err(dp_grads0, single0.cpu().numpy()), parity.rel_err(dp_state, _flat_state(tr))
     print("dp vs single: grads0 %.2e, state after %d steps %.2e" % (e_g, steps, e_s))
     assert e_g < 1e-5 and e_s < 1e-5
     # step 0 against the oracle on the global batch, per tensor (ReLU-boundary
-    # rows of the critics' hidden layers aside, as in the test above)
+    # rows of the critics' hidden layers aside, as in the test above; a
+    # critic's fc0 against the oracle corrected by exactly the layer-1 mask
+    # flips the GPU's saved activations show, each within 3e-5 rms of 0:
+    # test_gpu_teacher._flip_adjusted)
+    from test_gpu_teacher import _flip_adjusted
     prm = sac_params(HD, HA, [HH, HH], 4, pi_init_w=1e-3, q_init_w=3e-3)
     orc = so.SACOracle(prm, HD, HA, policy_lr=3e-4, qf_lr=3e-4, tau=5e-3)
     batch, e1, e2 = inputs[0]
     out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
+    Bg = len(batch["rewards"])
+    flipped = {}
+    for grp, c, opt in (("qf1", "c1", orc.opt_q1), ("qf2", "c2", orc.opt_q2)):
+        dq = 2.0 * (orc.S[c]["q"] - orc.S["y"]) / Bg
+        adj, fl = _flip_adjusted(out["grads"][grp], orc.S[c], dq, prm[grp], opt, 3e-4, h2g[grp])
+        flipped[grp] = fl
+        for pn in ("fc0.weight", "fc0.bias"):
+            out["grads"][grp][pn] = torch.from_numpy(adj[pn][0])
+    print("layer-1 mask flips (sample, unit):", flipped)
     x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
     allowed = {}
     for grp in ("qf1", "qf2"):
@@ -626,9 +644,9 @@ def test_dp_rccl_humanoid_split_schedule_dropin_equals_single_gpu(B):
     q = ctx.SimpleQueue()
     p = ctx.Process(target=_nccl_h_worker, args=(port, q, B, steps))
     p.start()
+    got, bits = q.get()   # (before the join: the state does not fit the pipe's buffer)
     p.join(timeout=200)
     assert p.exitcode == 0, p.exitcode
-    got, bits = q.get()
     want_bits = ("direct",) if B == 256 else BIG_BRANCHES
     missing = [b for b in want_bits + ("exchange", "split_phase1") if not bits & TRACE[b]]
     assert not missing and not bits & TRACE["fused"], (missing, bits)

@@ -45,6 +45,8 @@ def main():
         for _ in range(a.warmup):
             step()
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
+        for e in evs:   # torch creates the HIP event on its first record: not inside the window
+            e.record()
         host = []
         gc.collect()
         gc.disable()
