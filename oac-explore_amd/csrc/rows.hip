@@ -447,19 +447,23 @@ __device__ __forceinline__ void particle_targets_rows(const ParticleTargetArgs& 
     const float inf = __builtin_huge_valf();
     const float qv = k < K ? (p.qh.h ? qs.out[row][k] : p.q[(long)m * K + k]) : inf;
     const float tv = k < K ? (p.th.h ? hs.out[row][k] : p.tq[(long)m * K + k]) : inf;
-    // slot j precedes slot k: real before padding, then value (NaN last), then index
-    auto before = [&](float vj, float vk, int j) {
-      if ((j < K) != (k < K)) return j < K;
-      const bool nj = vj != vj, nk = vk != vk;
-      if (nj != nk) return nk;
-      return (vj < vk) || ((vj == vk || nj) && j < k);
+    // order-preserving integer keys, computed once per lane: a number's bits
+    // mapped monotonically (-0 as +0: they compare equal), NaN above +inf,
+    // the padding above NaN; ties (equal keys) by index
+    auto key = [](float v, bool pad) -> unsigned {
+      if (pad) return 0xFFFFFFFFu;
+      if (v != v) return 0xFFFFFFFEu;
+      const unsigned u = __float_as_uint(v == 0.f ? 0.f : v);
+      return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
     };
+    const unsigned kq = key(qv, k >= K), kt = key(tv, k >= K);
     int rq = 0, rt = 0;
 #pragma unroll
     for (int j = 0; j < kMaxHeads; ++j) {
-      const float qj = __shfl(qv, base | j, 64), tj = __shfl(tv, base | j, 64);
-      rq += before(qj, qv, j) ? 1 : 0;
-      rt += before(tj, tv, j) ? 1 : 0;
+      const unsigned qj = (unsigned)__shfl((int)kq, base | j, 64);
+      const unsigned tj = (unsigned)__shfl((int)kt, base | j, 64);
+      rq += (qj < kq || (qj == kq && j < k)) ? 1 : 0;
+      rt += (tj < kt || (tj == kt && j < k)) ? 1 : 0;
     }
     s_qv[row][rq] = qv; s_qi[row][rq] = k;
     s_tv[row][rt] = tv; s_ti[row][rt] = k;
@@ -686,11 +690,19 @@ __global__ void __launch_bounds__(256) particle_min_kernel(ParticleMinArgs p) {
       const int rr = min(rr0 + j * rstep, kRowBlock - 1), m = r0 + rr;
       if (rr0 + j * rstep >= kRowBlock || m >= p.B) continue;
       const int b = sbest[rr];
-      // the argmin head's row by a select chain (exact, whatever the other
-      // heads' rows hold), so the prefetched rows stay in registers
-      float4 w = wpf[0];
+      // the argmin head's row as a masked sum (exact: one term is w, the rest
+      // +-0), so the prefetched rows stay in registers.  Not exact if another
+      // head's weight is +-inf (0 * inf): a critic that far diverged has
+      // inf / NaN Q values in the reference too.  Exact forms measured slower
+      // (round 5, configs[4], this launch 6.2 us): a select chain 7.9, the
+      // rows staged through LDS 9.3.
+      float4 w = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int k = 1; k < kMaxHeads; ++k) w = (b == k) ? wpf[k] : w;
+      for (int k = 0; k < kMaxHeads; ++k) {
+        const float sel = b == k ? 1.f : 0.f;
+        w.x = fmaf(sel, wpf[k].x, w.x); w.y = fmaf(sel, wpf[k].y, w.y);
+        w.z = fmaf(sel, wpf[k].z, w.z); w.w = fmaf(sel, wpf[k].w, w.w);
+      }
       const float4 h = hpf[j];
       float4 o;
       o.x = h.x > 0.f ? -invB * w.x : 0.f; o.y = h.y > 0.f ? -invB * w.y : 0.f;
