@@ -138,13 +138,14 @@ def timed(run, steps, warmup, world, device):
         if world > 1:
             torch.distributed.barrier()
             torch.cuda.synchronize()
-    run(warmup)
     # host jitter: no Python garbage collection inside the timed region (the
-    # driver times 20 steps = ~2 ms; a collection pause is a visible share)
+    # driver times 20 steps = ~2 ms; a collection pause is a visible share),
+    # collected before the warm-up (which re-warms the host caches)
     gc.collect()
     gc_on = gc.isenabled()
     gc.disable()
     try:
+        run(warmup)
         barrier()
         t0 = time.perf_counter()
         run(steps)
@@ -846,12 +847,15 @@ def main():
             torch.distributed.barrier()
             torch.cuda.synchronize()
 
-    run(args.warmup)
-    # no Python garbage collection inside the timed region (as in timed():
-    # a 20-step window is ~2 ms, and a collection pause is a visible share)
+    # no Python garbage collection inside the timed region: a 20-step window
+    # is ~2 ms, and a collection pause is a visible share of it.  The collection
+    # runs before the warm-up, which then re-warms the host caches it walked
+    # (collected right before the window, the first step's host work took
+    # 200-350 us instead of ~50: tools/fill_drain.py, round 5)
     gc.collect()
     gc.disable()
     try:
+        run(args.warmup)
         barrier()
         t0 = time.perf_counter()
         run(args.steps)

@@ -66,7 +66,8 @@ typedef struct oac_sac_config {
   int row_stride;        /* floats per replay row (multiple of 4) */
   int off_obs, off_act, off_rew, off_term, off_next_obs; /* row layout; off_act == off_obs+obs_dim */
   uint64_t seed;         /* Philox key for the policy noise */
-  int gemm_cfg;          /* -1 auto, 0 small tiles + split-K, 1 large tiles */
+  int gemm_cfg;          /* -1 auto (2 at batch >= 1024, else 0), 0 small tiles + split-K,
+                            1 LDS-tiled large tiles, 2 large-batch per-launch choice */
   int world_size;        /* data-parallel ranks (alpha / gradient averaging) */
   /* OAC_KIND_GAUSS (gaussian_trainer.py:65-72, main.py:219-233, 549-554) */
   float std_bound;       /* standard_bound = norm.ppf(delta) */

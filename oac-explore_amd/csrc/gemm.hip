@@ -344,12 +344,6 @@ __global__ void __launch_bounds__(256) gemm_grouped_kernel(const GemmBatch batch
 // 64x64x16 variants measured 0.6-1.02x and were retired.)
 using CfgLarge = GemmCfg<64, 64, 32, 2, 2, 1>;
 
-// cfg 2: the register-direct kernel of gemm_big.hip (128 x 128 workgroup tiles)
-// cfg 3: the same kernel with the backward tile (dX / dW batches)
-int gemm_big_tile_m(bool bwd);
-int gemm_big_tile_n(bool bwd);
-hipError_t gemm_big_launch(const GemmBatch& b, hipStream_t s, bool bwd);
-
 hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s);
 int gemm_fwd_tile_m(int cfg);
 int gemm_fwd_tile_n(int cfg);
@@ -361,12 +355,12 @@ int gemm_bwdp_tile_n(int cfg);
 int gemm_tile_m(int cfg) {
   if (cfg >= 9) return gemm_bwdp_tile_m(cfg);
   if (cfg >= 6) return gemm_fwd_tile_m(cfg);
-  return cfg == 0 ? 32 : cfg >= 2 ? gemm_big_tile_m(cfg == 3) : 64;
+  return cfg == 0 ? 32 : 64;
 }
 int gemm_tile_n(int cfg) {
   if (cfg >= 9) return gemm_bwdp_tile_n(cfg);
   if (cfg >= 6) return gemm_fwd_tile_n(cfg);
-  return cfg == 0 ? 32 : cfg >= 2 ? gemm_big_tile_n(cfg == 3) : 64;
+  return cfg == 0 ? 32 : 64;
 }
 
 void gemm_small_finalize(GemmBatch& b);
@@ -405,12 +399,12 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   if (b.fuse_adam) return hipErrorInvalidValue;   // fused optimizer: small-batch kernel only
   for (int i = 0; i < b.ntasks; ++i) {             // dual products / head backward: small kernel
     if (b.t[i].K2 > 0 || b.t[i].epi == EPI_HEAD_BWD) return hipErrorInvalidValue;
-    // the width-1 head dot: small kernel, the register-direct one (cfg 2 / 3) or gemm_fwd (6-8)
-    if (b.t[i].epi == EPI_BIAS_RELU_DOT && cfg != 2 && cfg != 3 && (cfg < 6 || cfg > 8)) return hipErrorInvalidValue;
+    // the width-1 head dot: small kernel or gemm_fwd (6-8)
+    if (b.t[i].epi == EPI_BIAS_RELU_DOT && (cfg < 6 || cfg > 8)) return hipErrorInvalidValue;
   }
   if (cfg >= 9) return gemm_bwdp_launch(b, cfg, s);
   if (cfg >= 6) return gemm_fwd_launch(b, cfg, s);
-  if (cfg >= 2) return gemm_big_launch(b, s, cfg == 3);
+  if (cfg != 1) return hipErrorInvalidValue;
   OAC_LAUNCH(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b);
   return hipGetLastError();
 }

@@ -84,8 +84,7 @@ static int pphase0(SacPlan& p, int flags, hipStream_t s) {
   // through the step's index slot, side workgroups of that launch draw eps,
   // and the batch copy (first read by the targets kernel) rides in the target
   // critic's layer-1 launch -- no gather launch
-  static const bool direct_on = [] { const char* e = getenv("OAC_POAC_DIRECT"); return !e || atoi(e) != 0; }();
-  const bool direct_big = direct_on && big_direct_ok(p) && (flags & OAC_STEP_GATHER) && p.b.ring_slots > 0;
+  const bool direct_big = big_direct_ok(p) && (flags & OAC_STEP_GATHER) && p.b.ring_slots > 0;
   p.direct_big = direct_big;
   p.direct_ring = gather_idx(p, flags);
   const float* R0 = direct_big ? p.b.replay : X;

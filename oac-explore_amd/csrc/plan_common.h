@@ -181,33 +181,27 @@ static inline int tock(PlanBase& p, int kind, int i, hipStream_t s) {
   } while (0)
 
 
-// The register-direct kernel (gemm_big.hip) runs the large-batch products
-// the pipelined kernels below do not take, with N >= 64: forward batches as
-// cfg 2 (64x32 wave blocks) and backward batches -- dX / dW, batch-major
-// operands, one dword load per lane and k -- as cfg 3 (32x32 wave blocks).
-// Narrow outputs go to the small-batch kernel, the rest to the LDS kernel
-// (cfg 1).  (The register-staged LDS kernels of round 2, gemm_lds.hip / cfg 4,
-// and gemm_bwd.hip / cfg 5, were slower in every geometry and are retired to
-// tools/micro/retired.)
-static inline int large_batch_cfg() { return 2; }
+// Plan-level tile configuration (PlanBase::cfg): 0 = the small-batch kernel
+// for every product, 1 = the LDS-tiled kernel (gemm.hip) for every product the
+// small kernel does not take, 2 = the large-batch per-launch choice below
+// (the default at batch >= 1024).  The round-1 register-direct kernel
+// (gemm_big.hip, launch cfg 2 / 3) that cfg 2 once fell back on took no
+// launch of any measured workload after round 3 and was removed in round 5.
+constexpr int kCfgLargeBatch = 2;
+// split-K sizing tile of the products sized before the per-launch choice
+// (the head dW's sp_ph at large batch: 128 x 64, as the kernel the sizing was
+// tuned on)
+static inline int split_tile_m(int cfg) { return cfg == 0 ? 32 : cfg == kCfgLargeBatch ? 128 : 64; }
+static inline int split_tile_n(int cfg) { return cfg == 0 ? 32 : 64; }
 
-// a forward batch with fewer 128x64 tiles than this runs on the register-
-// direct kernel's 64x64 tiles (cfg 3) when the pipelined kernel does not take
-// it: twice the workgroups (configs[4]: single N = 256 products at B=4096)
-constexpr int kSmallFwdTiles = 512;
 bool gemm_fwd_supports(const GemmBatch& b);
 
 // Forward batches at large batch go to gemm_fwd.hip (LDS-DMA pipelined
-// 128x128 / 128x64 / 64x64 tiles, cfg 6 / 7 / 8); OAC_FWD2=0 keeps them on the
-// register-direct kernel (cfg 2) for A/B runs.  Measured per launch at B=4096
-// (tools/micro/fwd_micro, bitwise equal to cfg 2): SAC layer 0 (6 tasks)
-// 77.5 -> 66.4 us on 128x64 (74.6 on 128x128: 384 tiles = 1.5 rounds), critic
+// 128x128 / 128x64 / 64x64 tiles, cfg 6 / 7 / 8).  Measured per launch at B=4096
+// against the register-direct kernel of rounds 1-3 (tools/micro/fwd_micro,
+// bitwise equal to it): SAC layer 0 (6 tasks) 77.5 -> 66.4 us on 128x64 (74.6 on 128x128: 384 tiles = 1.5 rounds), critic
 // layer 1 + head partials (4 tasks) 35.6 -> 27.7 us on 128x128, policy layer 1
 // (2 tasks) 21.9 -> 15.4 us on 128x64.
-static inline bool fwd2_on() {
-  static const bool v = [] { const char* e = getenv("OAC_FWD2"); return !e || atoi(e) != 0; }();
-  return v;
-}
 // 128x64 tiles (three workgroups per CU on the 2-stage ring) when they give
 // every CU at least one, 64x64 otherwise (a single 4096 x 256 product: 128
 // tiles of 128x64 would leave half the chip idle).  128x128 measured equal to
@@ -227,14 +221,8 @@ static inline int fwd2_cfg(const GemmBatch& gb) {
 }
 
 // Backward batches at large batch go to gemm_bwdp.hip (LDS-DMA pipelined,
-// cfg 9 = 128x64 tiles, 10 = 64x64 when 128x64 leaves CUs idle);
-// OAC_BWDP=0 keeps them on the register-direct kernel (A/B parity runs,
-// tests/test_gpu_altkernels.py).
+// cfg 9 = 128x64 tiles, 10 = 64x64, 11 = 128x128, 12 = 64x64 on a 2-stage ring).
 bool gemm_bwdp_supports(const GemmBatch& b);
-static inline bool bwdp_on() {
-  static const bool v = [] { const char* e = getenv("OAC_BWDP"); return !e || atoi(e) != 0; }();
-  return v;
-}
 static inline int bwdp_cfg(const GemmBatch& gb) {
   // 64x64 tiles beat 128x64 on every backward launch of the B=4096 SAC step
   // (tools/micro/bwd_micro: critic layer 1 48.8 -> 38.6 us, layer 0 dW 37.9
@@ -258,49 +246,24 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
   for (int i = 0; i < gb.ntasks && narrow; ++i)
     narrow = gb.t[i].N <= 32 && gb.t[i].ksplit <= 1 && gb.t[i].K2 == 0;
   if (narrow) return 0;
-  if (cfg != 2) return cfg;
-  // (narrow-row dW batches on the small kernel measured -1 % at B=4096 and were dropped)
-  if (fwd2_on()) {
-    bool all_fwd = true;
-    for (int i = 0; i < gb.ntasks; ++i)
-      all_fwd = all_fwd && gb.t[i].a_kc && gb.t[i].b_kc && gb.t[i].N >= 64;
-    if (all_fwd && gemm_fwd_supports(gb)) return fwd2_cfg(gb);
-  }
-  if (bwdp_on()) {
-    // a dX with a short K (the head's 2 Da, a K-output critic's K) rides
-    // along with its batch's dW (same-box A/B, B=4096: SAC 3,276 -> 3,310,
-    // configs[4] 4,106 -> 4,200 steps/s against keeping those batches on the
-    // register-direct kernel)
-    bool all_bwd = true;
-    for (int i = 0; i < gb.ntasks; ++i) all_bwd = all_bwd && !gb.t[i].b_kc;
-    if (all_bwd && gemm_bwdp_supports(gb)) return bwdp_cfg(gb);
-  }
-  // a width-1 head riding on a layer-1 epilogue (EPI_BIAS_RELU_DOT) exists on
-  // the small and register-direct kernels only: a batch the register-direct
-  // kernel does not take (hidden < 64, ragged dims) runs on the small kernel
-  bool any_bwd = false, dot = false;
-  for (int i = 0; i < gb.ntasks; ++i) dot = dot || gb.t[i].epi == EPI_BIAS_RELU_DOT;
+  if (cfg != kCfgLargeBatch) return cfg;
+  bool all_fwd = true, all_bwd = true, dot = false;
   for (int i = 0; i < gb.ntasks; ++i) {
-    const GemmTask& t = gb.t[i];
-    const bool fwd = t.a_kc && t.b_kc && t.a_mode == A_PLAIN;
-    const bool bwd = !t.b_kc;   // dX / dW products (register-direct, gemm_big.hip)
-    if (!(fwd || bwd) || t.N < 64 || t.K2 > 0 || t.epi == EPI_HEAD_BWD || gb.fuse_adam)
-      return dot ? 0 : 1;
-    any_bwd |= bwd;
-    // the big kernel runs the rank-R columns on the same accumulators: as a
-    // continuation of the row (the action stored right after the observation)
-    // or from a separate action buffer (the policy's a~)
-    if (t.epi == EPI_BIAS_RANK_RELU && (!t.C2 || t.ksplit > 1)) return dot ? 0 : 1;
+    all_fwd = all_fwd && gb.t[i].a_kc && gb.t[i].b_kc && gb.t[i].N >= 64;
+    all_bwd = all_bwd && !gb.t[i].b_kc;
+    dot = dot || gb.t[i].epi == EPI_BIAS_RELU_DOT;
   }
-  if (!any_bwd) {
-    // a forward batch with fewer 128x64 tiles than CUs (one GEMM of N = 256 at
-    // B=4096: 128 tiles) runs on 64x64 tiles instead: twice the workgroups
-    int tiles = 0;
-    for (int i = 0; i < gb.ntasks; ++i)
-      tiles += ((gb.t[i].M + 127) / 128) * ((gb.t[i].N + 63) / 64) * std::max(1, gb.t[i].ksplit);
-    if (tiles < kSmallFwdTiles) return 3;
-  }
-  return any_bwd ? 3 : 2;
+  // (narrow-row dW batches on the small kernel measured -1 % at B=4096 and were dropped)
+  if (all_fwd && gemm_fwd_supports(gb)) return fwd2_cfg(gb);
+  // a dX with a short K (the head's 2 Da, a K-output critic's K) rides
+  // along with its batch's dW (same-box A/B, B=4096: SAC 3,276 -> 3,310,
+  // configs[4] 4,106 -> 4,200 steps/s against keeping those batches on the
+  // register-direct kernel of the time)
+  if (all_bwd && gemm_bwdp_supports(gb)) return bwdp_cfg(gb);
+  // the rest (hidden < 64, ragged dims, mixed batches): the LDS-tiled kernel,
+  // or the small kernel for a batch carrying the width-1 head dot (an
+  // epilogue the LDS-tiled kernel does not have)
+  return dot ? 0 : 1;
 }
 
 static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {

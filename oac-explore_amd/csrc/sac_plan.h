@@ -148,7 +148,7 @@ int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long
 // not kept.)
 inline bool big_direct_ok(const SacPlan& p) {
   // gemm_fwd's rank-Da continuation reads [obs | act] as one span of the row
-  return (p.c.kind == OAC_KIND_SAC || p.c.kind == OAC_KIND_PARTICLE) && p.cfg == 2 && fwd2_on() &&
+  return (p.c.kind == OAC_KIND_SAC || p.c.kind == OAC_KIND_PARTICLE) && p.cfg == kCfgLargeBatch &&
          p.c.hidden >= 64 &&
          p.c.row_stride % 4 == 0 && p.c.row_stride / 4 <= 256 &&
          p.c.off_act == p.c.off_obs + p.c.obs_dim;

@@ -117,7 +117,7 @@ static void layout_workspace(SacPlan& p) {
 // epilogue is the head backward) instead of a GEMM launch and a row launch.
 static bool head_bwd_fused_big() { return true; }
 static bool qdot(const SacPlan& p) {
-  return (p.cfg == 0 || p.cfg == 2) && p.c.q_out == 1 && (p.c.hidden + 31) / 32 <= 16;
+  return (p.cfg == 0 || p.cfg == kCfgLargeBatch) && p.c.q_out == 1 && (p.c.hidden + 31) / 32 <= 16;
 }
 static GemmTask q_l1(SacPlan& p, const float* in, const float* net, float* out, int qv) {
   const oac_sac_config& c = p.c;
@@ -195,11 +195,9 @@ static void add_critic_l1(SacPlan& p, GemmBatch& gb) {
 // layer 1 -- which needs exactly those post-step weights -- then reads them
 // from the shadow and runs inside the critic layer-0 dW launch (whose side
 // blocks copy the shadow into the parameters) instead of a launch of its own:
-// one launch fewer on the step's chain.  OAC_MINQ_MERGE=0 keeps the separate
-// launch (A/B runs).
+// one launch fewer on the step's chain.
 static bool minq_merged(const SacPlan& p) {
-  static const bool on = [] { const char* e = getenv("OAC_MINQ_MERGE"); return !e || atoi(e) != 0; }();
-  return on && can_fuse_adam(p) && p.ws[W_QSHADOW].rows > 0;
+  return can_fuse_adam(p) && p.ws[W_QSHADOW].rows > 0;
 }
 
 // -min Q backward to layer 1 with post-step weights (critic i's layer 1 and
@@ -242,16 +240,7 @@ static GemmTask critic_dw0(SacPlan& p, int i, int c0, int n, bool bias) {
 // Adam + Polyak of both critics then runs as side blocks of the policy-head
 // launch (nothing in it or later in the step reads the critic's layer 0).
 // Not with a next-step prefetch: its critic forward reads the post-step
-// layer 0 in the dL/da launch.  OAC_DW0_DEFER=0 keeps the layer-0 dW + Adam
-// in the layer-0 launch.
-static bool inline_rows_on() {
-  static const bool on = [] { const char* e = getenv("OAC_INLINE_ROWS"); return !e || atoi(e) != 0; }();
-  return on;
-}
-static bool defer_dw0_on() {
-  static const bool on = [] { const char* e = getenv("OAC_DW0_DEFER"); return !e || atoi(e) != 0; }();
-  return on;
-}
+// layer 0 in the dL/da launch.
 static void add_dw0_side_adam(SacPlan& p, GemmBatch& gb) {
   for (int k = 0; k < gb.ntasks; ++k) gb.t[k].no_adam = 1;   // (the policy's gradients)
   const oac_sac_layout& L = p.L;
@@ -358,7 +347,7 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
       // captured launch would replay this step's indices)
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       if (p.inline_ok && B <= kInlineRows && hipStreamIsCapturing(s, &cs) == hipSuccess &&
-          cs == hipStreamCaptureStatusNone && inline_rows_on())
+          cs == hipStreamCaptureStatusNone)
         g.inl = p.inline_rows;
       if (flags & OAC_STEP_DEVICE_EPS) {
         g.eps1 = p.E1(); g.eps2 = p.E2(); g.n_eps = B * Da;
@@ -428,7 +417,7 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
 // us: eight blocks each redoing the row math and the h2 pass; not kept.)
 static bool wl_in_targets(const SacPlan& p) {
   const oac_sac_config& c = p.c;
-  return c.kind == OAC_KIND_SAC && c.q_out == 1 && p.cfg == 2 && bwdp_on() &&
+  return c.kind == OAC_KIND_SAC && c.q_out == 1 && p.cfg == kCfgLargeBatch &&
          p.sp_ql.kchunk == 256 && p.sp_ql.S * 256 == c.batch && c.hidden % 32 == 0;
 }
 
@@ -541,7 +530,7 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
   }
   {  // critic backward, layer 0 (input = [obs | act] contiguous in the row)
     GemmBatch gb{};
-    const bool dfr = defer && fused && minq_merged(p);   // (defer_dw0_on)
+    const bool dfr = defer && fused && minq_merged(p);
     for (int i = 0; i < 2; ++i)
       add(gb, dfr ? critic_dw0(p, i, Do, Da, true) : critic_dw0(p, i, 0, Dq, true));
     if (dfr) {   // critic 1's obs columns: gradient only (their Adam: the policy-head launch)
@@ -698,7 +687,7 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
   if (phase0(p, flags, s, gather_n, ahead && p.slot > 0)) return 1;
   const bool split = !fused && split_adam_on(p);
   const bool pf = ahead && i + 1 < n && p.slot + 1 < kXSlots;
-  const bool defer = !pf && defer_dw0_on();
+  const bool defer = !pf;
   if (phase1(p, s, fused, 0, split, defer)) return 1;
   if (!fused && !split && phase2_adam(p, s, 0)) return 1;
   if (phase2(p, s, fused, pf ? p.W(OAC_WS_BATCH) + (long)(p.slot + 1) * c_batch_rows(p) : nullptr,
@@ -839,6 +828,7 @@ static int validate(const oac_sac_config* c) {
   }
   if (c->row_stride % 4 != 0) { set_error("row_stride must be a multiple of 4"); return 1; }
   if (c->world_size < 1) { set_error("world_size must be >= 1"); return 1; }
+  if (c->gemm_cfg < -1 || c->gemm_cfg > 2) { set_error("gemm_cfg must be -1, 0, 1 or 2"); return 1; }
   if (c->off_act != c->off_obs + c->obs_dim) { set_error("row layout: act must follow obs"); return 1; }
   if (c->off_obs < 0 || c->off_next_obs + c->obs_dim > c->row_stride ||
       c->off_act + c->act_dim > c->row_stride || c->off_rew >= c->row_stride ||
@@ -851,8 +841,8 @@ static int validate(const oac_sac_config* c) {
 
 static void plan_splits(SacPlan& p) {
   const oac_sac_config& c = p.c;
-  p.cfg = c.gemm_cfg >= 0 ? c.gemm_cfg : (c.batch >= 1024 ? large_batch_cfg() : 0);
-  const int tm = gemm_tile_m(p.cfg), tn = gemm_tile_n(p.cfg);
+  p.cfg = c.gemm_cfg >= 0 ? c.gemm_cfg : (c.batch >= 1024 ? kCfgLargeBatch : 0);
+  const int tm = split_tile_m(p.cfg), tn = split_tile_n(p.cfg);
   auto tiles = [&](int M, int N) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); };
   const int H = c.hidden, Dq = c.obs_dim + c.act_dim, Do = c.obs_dim, Da = c.act_dim;
   const int nq = (c.kind == OAC_KIND_SAC) ? 2 : 1;
@@ -862,7 +852,7 @@ static void plan_splits(SacPlan& p) {
   p.sp_ph = choose_split(c.batch, tiles(2 * Da, H + 1), p.cfg);
   p.sp_p1 = choose_split(c.batch, tiles(H, H + 1), p.cfg);
   p.sp_p0 = choose_split(c.batch, tiles(H, Do + 1), p.cfg);
-  if (p.cfg == 2 && bwdp_on()) {   // the large-batch dW products run on gemm_bwdp.hip
+  if (p.cfg == kCfgLargeBatch) {   // the large-batch dW products run on gemm_bwdp.hip
     auto t64 = [](int M, int Nx) { return ((M + 63) / 64) * ((Nx + 63) / 64); };
     p.sp_q1 = choose_split_pipe(c.batch, nq * (t64(H, H) + t64(c.q_out, H)));
     p.sp_ql = p.sp_q1;
@@ -1145,11 +1135,8 @@ int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags,
   // as the step graph, but one hipGraphLaunch per step cost more than the
   // host's 12 launch calls (same-box A/B, the bench line: B=256 10,443-10,491
   // -> 11,015-11,049 steps/s, B=4096 3,688-3,696 -> 3,740-3,749, configs[4]
-  // 4,878-4,897 -> 5,028-5,035).  OAC_DROPIN_GRAPH=1: the graph launch.
-  static const bool direct_launch = [] { const char* e = getenv("OAC_DROPIN_GRAPH"); return !e || atoi(e) == 0; }();
-  return oac_sac_step_n(h, flags | OAC_STEP_GATHER | (direct_launch ? 0 : OAC_STEP_USE_GRAPH) |
-                               (hr ? kStepHostIdx : 0), 1,
-                        stream);
+  // 4,878-4,897 -> 5,028-5,035).
+  return oac_sac_step_n(h, flags | OAC_STEP_GATHER | (hr ? kStepHostIdx : 0), 1, stream);
 }
 
 int oac_sac_step_phase(oac_sac* h, int phase, int flags, void* stream) {

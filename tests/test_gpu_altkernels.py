@@ -1,7 +1,6 @@
 """The large-batch kernels the default per-launch choice does not pick
 (plan_common.h launch_cfg), each in a child process whose environment forces
-it: the register-direct forward / backward GEMMs (OAC_FWD2=0 OAC_BWDP=0:
-gemm_big.hip), the pipelined forward on 128x128 tiles with a
+it: the pipelined forward on 128x128 tiles with a
 3-stage ring (OAC_FWD2_TILE=128,128) and the pipelined backward on 128x64 /
 128x128 tiles or 64x64 on a 3-stage ring (OAC_BWDP_CFG=9 / 11 / 10), and the step-structure fallbacks
 (OAC_SPLIT_ADAM=0, OAC_DH2_TARGETS=0).  Each runs the ragged large-batch parity
@@ -17,7 +16,6 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 VARIANTS = {
-    "register_direct": {"OAC_FWD2": "0", "OAC_BWDP": "0"},
     "fwd_128x128_bwd_128x64": {"OAC_FWD2_TILE": "128,128", "OAC_BWDP_CFG": "9"},
     "fwd_64x64_nb3_bwd_128x128": {"OAC_FWD2_TILE": "64,64", "OAC_FWD2_NB": "3", "OAC_BWDP_CFG": "11"},
     # the backward 64x64 tiles on the 3-stage ring (the default is the 2-stage one, cfg 12)

@@ -114,9 +114,7 @@ def test_particle_large_batch_matches_oracle(B):
     4096) on the large-batch kernels (the LDS-DMA pipelined forward and
     backward GEMMs, gemm_fwd.hip / gemm_bwdp.hip, incl. the post-step critic
     layer 0 on a~ as a rank-R continuation; narrow products on the small-tile
-    kernel; OAC_FWD2=0 / OAC_BWDP=0 in the environment move the products to
-    the register-direct kernel, gemm_big.hip, for A/B runs of
-    this test): one step against the fp32 CPU oracle on the same inputs and
+    kernel): one step against the fp32 CPU oracle on the same inputs and
     eps: 1e-5 on every gradient tensor, on the post-step parameters (Adam's
     sign band aside, parity.compare_post), the Adam moments, the target
     critic after Polyak, log-alpha and its gradient, and the K head losses."""

@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--events", type=int, default=1, help="record an event between steps")
+    ap.add_argument("--idle-ms", type=float, default=0.0,
+                    help="host sleep between the warm-up's synchronize and the window")
     a = ap.parse_args()
     sys.argv = [sys.argv[0]]
     args = bench.parse()
@@ -42,15 +44,17 @@ def main():
 
     out = []
     for w in range(a.windows):
-        for _ in range(a.warmup):
-            step()
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
         for e in evs:   # torch creates the HIP event on its first record: not inside the window
             e.record()
         host = []
-        gc.collect()
+        gc.collect()    # (before the warm-up, as bench.py: it leaves the host caches cold)
         gc.disable()
+        for _ in range(a.warmup):
+            step()
         torch.cuda.synchronize()
+        if a.idle_ms:
+            time.sleep(a.idle_ms * 1e-3)
         t0 = time.perf_counter()
         if a.events:
             evs[0].record()
