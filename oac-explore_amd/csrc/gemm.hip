@@ -16,8 +16,11 @@
 // double-buffered LDS).  Waves tile the output as WM x WN, and WK > 1 splits
 // the K loop across waves (for the small-M/N stages of a batch-256 step),
 // reduced through LDS in fixed order (deterministic).
+#include <cstring>
+
 #include "oac_common.h"
 #include "adam_common.h"
+#include "kernels.h"
 
 namespace oac {
 
@@ -344,11 +347,13 @@ __global__ void __launch_bounds__(256) gemm_grouped_kernel(const GemmBatch batch
 // 64x64x16 variants measured 0.6-1.02x and were retired.)
 using CfgLarge = GemmCfg<64, 64, 32, 2, 2, 1>;
 
-hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s);
+hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCache* bc = nullptr,
+                           int pos = -1);
 int gemm_fwd_tile_m(int cfg);
 int gemm_fwd_tile_n(int cfg);
 
-hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s);
+hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCache* bc = nullptr,
+                            int pos = -1);
 int gemm_bwdp_tile_m(int cfg);
 int gemm_bwdp_tile_n(int cfg);
 
@@ -364,7 +369,8 @@ int gemm_tile_n(int cfg) {
 }
 
 void gemm_small_finalize(GemmBatch& b);
-hipError_t gemm_small_launch(const GemmBatch& b, hipStream_t s);
+hipError_t gemm_small_launch(const GemmBatch& b, hipStream_t s, BatchCache* bc, int pos);
+
 
 // Fills tile_begin / tiles_n / total_tiles for a tile configuration.
 void gemm_batch_finalize(GemmBatch& b, int cfg) {
@@ -385,7 +391,7 @@ void gemm_batch_finalize(GemmBatch& b, int cfg) {
   b.total_tiles = tiles;
 }
 
-hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
+hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCache* bc, int pos) {
   if (b.total_tiles <= 0) return hipSuccess;
   if (b.side_adam > 0 && (cfg < 9 || cfg > 12)) return hipErrorInvalidValue;   // side Adam: gemm_bwdp only
   // rows read through the direct gather's index slot (a_rows) and the side
@@ -395,15 +401,15 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   bool gathers = b.rg.ring != nullptr;
   for (int i = 0; i < b.ntasks; ++i) gathers = gathers || b.t[i].a_rows;
   if (gathers && cfg != 0 && (cfg < 6 || cfg > 8)) return hipErrorInvalidValue;
-  if (cfg == 0) return gemm_small_launch(b, s);
+  if (cfg == 0) return gemm_small_launch(b, s, bc, pos);
   if (b.fuse_adam) return hipErrorInvalidValue;   // fused optimizer: small-batch kernel only
   for (int i = 0; i < b.ntasks; ++i) {             // dual products / head backward: small kernel
     if (b.t[i].K2 > 0 || b.t[i].epi == EPI_HEAD_BWD) return hipErrorInvalidValue;
     // the width-1 head dot: small kernel or gemm_fwd (6-8)
     if (b.t[i].epi == EPI_BIAS_RELU_DOT && (cfg < 6 || cfg > 8)) return hipErrorInvalidValue;
   }
-  if (cfg >= 9) return gemm_bwdp_launch(b, cfg, s);
-  if (cfg >= 6) return gemm_fwd_launch(b, cfg, s);
+  if (cfg >= 9) return gemm_bwdp_launch(b, cfg, s, bc, pos);
+  if (cfg >= 6) return gemm_fwd_launch(b, cfg, s, bc, pos);
   if (cfg != 1) return hipErrorInvalidValue;
   OAC_LAUNCH(gemm_grouped_kernel<CfgLarge>, dim3(b.total_tiles), dim3(256), 0, s, b);
   return hipGetLastError();

@@ -30,7 +30,8 @@
 namespace oac {
 
 #ifdef OAC_PIPE_CLOCK
-#define gemm_bwdp_kernel gemm_bwdp_kernel_clk   // distinct from the library's kernel of the same name
+#define gemm_bwdp_kernel gemm_bwdp_kernel_clk   // distinct from the library's kernels of the same names
+#define gemm_bwdp_kernel_dev gemm_bwdp_kernel_dev_clk
 #endif
 
 enum PKind { PK_KC = 0, PK_KC_R1 = 1, PK_MN = 2, PK_MN_R1 = 3 };
@@ -290,10 +291,9 @@ __device__ __forceinline__ void bwdp_tile(const GemmBatch& batch, int ti, int lo
 }
 
 template <int BM, int BN, int NB>
-__global__ void __launch_bounds__(256)
-gemm_bwdp_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
-                 const GemmBatch batch) {
-  __shared__ __attribute__((aligned(16))) float lds[BwdG<BM, BN, NB>::LDS];
+__device__ __forceinline__ void gemm_bwdp_body(int total_tiles, int tb1, int tb2, int tb3, int tb4,
+                                               int tb5, int tb6, int tb7, const GemmBatch& batch,
+                                               float* lds) {
   if (batch.publish && blockIdx.x == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
   const int side0 = batch.side_first ? 0 : total_tiles;   // side workgroups: the flat Adam
@@ -319,6 +319,22 @@ gemm_bwdp_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, i
   }
 }
 
+template <int BM, int BN, int NB>
+__global__ void __launch_bounds__(256)
+gemm_bwdp_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
+                 const GemmBatch batch) {
+  __shared__ __attribute__((aligned(16))) float lds[BwdG<BM, BN, NB>::LDS];
+  gemm_bwdp_body<BM, BN, NB>(total_tiles, tb1, tb2, tb3, tb4, tb5, tb6, tb7, batch, lds);
+}
+// the batch in device memory (kernels.h BatchCache)
+template <int BM, int BN, int NB>
+__global__ void __launch_bounds__(256)
+gemm_bwdp_kernel_dev(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
+                     const GemmBatchG* __restrict__ bp) {
+  __shared__ __attribute__((aligned(16))) float lds[BwdG<BM, BN, NB>::LDS];
+  gemm_bwdp_body<BM, BN, NB>(total_tiles, tb1, tb2, tb3, tb4, tb5, tb6, tb7, *(const GemmBatch*)bp, lds);
+}
+
 // a backward batch this kernel takes: dX (A k-contiguous, B n-contiguous) or dW
 // (both batch-major) products, plain or rank-1-mask A, STORE / MASK / GRAD
 // epilogues, no second product; a rank-1 factor indexed by k fits the LDS
@@ -341,15 +357,20 @@ bool gemm_bwdp_supports(const GemmBatch& b) {
 int gemm_bwdp_tile_m(int cfg) { return cfg == 10 || cfg == 12 ? 64 : 128; }
 int gemm_bwdp_tile_n(int cfg) { return cfg == 11 ? 128 : 64; }
 
-hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s) {
+hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCache* bc = nullptr, int pos = -1) {
   if (b.total_tiles <= 0) return hipSuccess;
   if (!gemm_bwdp_supports(b)) return hipErrorInvalidValue;
   int tb[8];
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
+  const GemmBatch* d = bc ? bc->get(b, pos, s) : nullptr;
 #define OAC_BWDP(C_, BM_, BN_, NB_) \
   if (cfg == C_) { \
-    OAC_LAUNCH((gemm_bwdp_kernel<BM_, BN_, NB_>), dim3(b.total_tiles + b.side_adam), dim3(256), 0, s, b.total_tiles, \
-               tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
+    if (d) \
+      OAC_LAUNCH((gemm_bwdp_kernel_dev<BM_, BN_, NB_>), dim3(b.total_tiles + b.side_adam), dim3(256), 0, s, \
+                 b.total_tiles, tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], (const GemmBatchG*)d); \
+    else \
+      OAC_LAUNCH((gemm_bwdp_kernel<BM_, BN_, NB_>), dim3(b.total_tiles + b.side_adam), dim3(256), 0, s, \
+                 b.total_tiles, tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
     return hipGetLastError(); }
   // cfg 12: 64x64 tiles on a 2-stage ring (36 KB of LDS: four workgroups per CU)
   OAC_BWDP(9, 128, 64, 3) OAC_BWDP(10, 64, 64, 3) OAC_BWDP(11, 128, 128, 3) OAC_BWDP(12, 64, 64, 2)

@@ -32,7 +32,8 @@
 namespace oac {
 
 #ifdef OAC_PIPE_CLOCK
-#define gemm_fwd_kernel gemm_fwd_kernel_clk   // distinct from the library's kernel of the same name
+#define gemm_fwd_kernel gemm_fwd_kernel_clk   // distinct from the library's kernels of the same names
+#define gemm_fwd_kernel_dev gemm_fwd_kernel_dev_clk
 #endif
 
 template <int BM, int BN>
@@ -190,15 +191,15 @@ __device__ __forceinline__ void fwd_gather_side(const RowGather& g, int sb, int 
       if (r >= g.B) break;
       const float4* src = reinterpret_cast<const float4*>(g.replay) + (long)src_row[k] * n4;
       float4* dst = reinterpret_cast<float4*>(g.out) + (long)r * n4;
-      float4 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const long i = lane + 64 * u;
-        v[u] = src[i < n4 ? i : 0];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (lane + 64 * u < n4) dst[lane + 64 * u] = v[u];
+      // four named registers, not an array: the array form went through
+      // scratch (80 bytes of private segment, a store and a reload per float4)
+      const long c0 = lane, c1 = lane + 64, c2 = lane + 128, c3 = lane + 192;
+      const float4 v0 = src[c0 < n4 ? c0 : 0], v1 = src[c1 < n4 ? c1 : 0];
+      const float4 v2 = src[c2 < n4 ? c2 : 0], v3 = src[c3 < n4 ? c3 : 0];
+      if (c0 < n4) dst[c0] = v0;
+      if (c1 < n4) dst[c1] = v1;
+      if (c2 < n4) dst[c2] = v2;
+      if (c3 < n4) dst[c3] = v3;
     }
   }
   if (!g.eps1) return;
@@ -209,12 +210,11 @@ __device__ __forceinline__ void fwd_gather_side(const RowGather& g, int sb, int 
 }
 
 template <int BM, int BN, int NB>
-__global__ void __launch_bounds__(256)
-gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
-                const GemmBatch batch) {
+__device__ __forceinline__ void gemm_fwd_body(int total_tiles, int tb1, int tb2, int tb3, int tb4,
+                                              int tb5, int tb6, int tb7, const GemmBatch& batch,
+                                              float* lds) {
   using G = FwdG<BM, BN>;
   constexpr int WM = G::WM, WN = G::WN;
-  __shared__ __attribute__((aligned(16))) float lds[NB * G::STAGE];
   if (batch.publish && blockIdx.x == 0 && threadIdx.x == 0)
     publish_step_consts(batch.publish, batch.pub_beta1, batch.pub_beta2);
   if ((int)blockIdx.x >= total_tiles) {   // side workgroups of a direct gather (GemmBatch::rg)
@@ -260,6 +260,22 @@ gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
   PIPE_CLK(31);
 }
 
+template <int BM, int BN, int NB>
+__global__ void __launch_bounds__(256)
+gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
+                const GemmBatch batch) {
+  __shared__ __attribute__((aligned(16))) float lds[NB * FwdG<BM, BN>::STAGE];
+  gemm_fwd_body<BM, BN, NB>(total_tiles, tb1, tb2, tb3, tb4, tb5, tb6, tb7, batch, lds);
+}
+// the batch in device memory (kernels.h BatchCache)
+template <int BM, int BN, int NB>
+__global__ void __launch_bounds__(256)
+gemm_fwd_kernel_dev(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
+                    const GemmBatchG* __restrict__ bp) {
+  __shared__ __attribute__((aligned(16))) float lds[NB * FwdG<BM, BN>::STAGE];
+  gemm_fwd_body<BM, BN, NB>(total_tiles, tb1, tb2, tb3, tb4, tb5, tb6, tb7, *(const GemmBatch*)bp, lds);
+}
+
 // forward batches this kernel takes: both operands k-contiguous, plain A, no
 // split, no second product, the forward epilogues of the register-direct
 // kernel; a_rows tasks (the direct gather) with the batch's RowGather, whose
@@ -303,7 +319,7 @@ int gemm_fwd_tile_n(int cfg) {
   return v ? v : cfg == 6 ? 128 : 64;
 }
 
-hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s) {
+hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCache* bc = nullptr, int pos = -1) {
   if (b.total_tiles <= 0) return hipSuccess;
   if (!gemm_fwd_supports(b)) return hipErrorInvalidValue;
   int tb[8];
@@ -315,10 +331,15 @@ hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s) {
   static const int nb_env = [] { const char* e = getenv("OAC_FWD2_NB"); return e ? atoi(e) : 0; }();
   const int nb = (nb_env == 2 || nb_env == 3) ? nb_env : (bm == 128 && bn == 64) ? 2 : 3;
   const int grid = b.total_tiles + b.rg.blocks;
+  const GemmBatch* d = bc ? bc->get(b, pos, s) : nullptr;
 #define OAC_FWD(BM_, BN_, NB_) \
   if (bm == BM_ && bn == BN_ && nb == NB_) { \
-    OAC_LAUNCH((gemm_fwd_kernel<BM_, BN_, NB_>), dim3(grid), dim3(256), 0, s, b.total_tiles, \
-               tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
+    if (d) \
+      OAC_LAUNCH((gemm_fwd_kernel_dev<BM_, BN_, NB_>), dim3(grid), dim3(256), 0, s, b.total_tiles, \
+                 tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], (const GemmBatchG*)d); \
+    else \
+      OAC_LAUNCH((gemm_fwd_kernel<BM_, BN_, NB_>), dim3(grid), dim3(256), 0, s, b.total_tiles, \
+                 tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
     return hipGetLastError(); }
   OAC_FWD(128, 128, 3) OAC_FWD(128, 64, 3) OAC_FWD(64, 128, 3) OAC_FWD(64, 64, 3)
   OAC_FWD(128, 128, 2) OAC_FWD(128, 64, 2) OAC_FWD(64, 64, 2)

@@ -443,7 +443,12 @@ void gemm_small_finalize(GemmBatch& b) {
   b.total_tiles = tiles;
 }
 
-hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
+// (bc / pos: the launch records in device memory, kernels.h BatchCache -- not
+// taken here: at B=256 the small kernel's launches measured the same either way,
+// some launches 0.3-0.6 us faster and others as much slower, where the
+// pipelined large-batch kernels gained, tools/gpu_r5_t14.sh)
+hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s, BatchCache* bc = nullptr, int pos = -1) {
+  (void)bc; (void)pos;
   if (b0.total_tiles <= 0) return hipSuccess;
   GemmBatch b = b0;
   for (int i = 0; i < b.ntasks; ++i)   // second products: plain unsplit dX tasks
@@ -464,7 +469,9 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s) {
   }
   const int grid = b.total_tiles + b.adam_blocks + (b.rg.ring ? b.rg.blocks : 0);
   const GemmHead h = gemm_head(b);
-  if (b.rg.inl && b.rg.ring && b.rg.B <= kInlineRows && ((nw == 16 && gpw == 4) || (nw == 8 && gpw == 5))) {
+  const bool inl = b.rg.inl && b.rg.ring && b.rg.B <= kInlineRows &&
+                   ((nw == 16 && gpw == 4) || (nw == 8 && gpw == 5));
+  if (inl) {
     InlineRows ir;
     std::memcpy(ir.r, b.rg.inl, sizeof(int) * b.rg.B);
     if (nw == 16)

@@ -1,5 +1,7 @@
 // Kernel argument structs and launch helpers shared by the plan builders.
 #pragma once
+#include <cstring>
+#include <vector>
 #include "oac_common.h"
 
 namespace oac {
@@ -309,9 +311,74 @@ hipError_t launch_det_head_backward(const DetHeadBwdArgs& a, hipStream_t s);
 struct LogpSumArgs { const float* logp; int B; float target_entropy; AlphaState* alpha; };
 hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s);
 
+// Launch records in device memory.  A plan's launches pass the same GemmBatch
+// step after step; read by value from the kernel arguments, every workgroup's
+// first dependent load (its task record) goes to memory the host wrote for
+// that launch, where a record the GPU read before is served by its caches
+// (tools/micro/kernarg_micro: 304-byte record, chains of 11 launches of 256
+// workgroups, 3.37 -> 2.93 us per launch).  The cache keeps each distinct
+// batch a plan launches at a position of its step in a device slot, uploaded
+// once (stream-ordered, before its first launch) and never rewritten, so a
+// captured graph may keep the pointer; a batch the cache cannot hold (slots
+// or variants per position exhausted) is passed by value as before.
+struct BatchCache {
+  static constexpr int kSlots = 512;       // 1.4 MB of device memory
+  static constexpr int kPerPosition = 16;  // distinct batches per launch position
+  char* dev = nullptr;
+  char* host = nullptr;   // pinned mirror: the uploads' sources, never rewritten
+  int used = 0;
+  bool failed = false;
+  std::vector<std::vector<int>> at;   // launch position -> slots of the batches seen there
+  long long hits = 0, misses = 0;
+  // device copy of b (bytewise identical), or null (pass b by value)
+  const GemmBatch* get(const GemmBatch& b, int pos, hipStream_t s);
+  ~BatchCache();
+};
+
+inline const GemmBatch* BatchCache::get(const GemmBatch& b, int pos, hipStream_t s) {
+  if (failed || pos < 0) return nullptr;
+  constexpr size_t sz = sizeof(GemmBatch);
+  if (!dev) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;   // (no allocation under capture)
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    if (hipMalloc(&dev, kSlots * sz) != hipSuccess) { dev = nullptr; failed = true; return nullptr; }
+    if (hipHostMalloc(&host, kSlots * sz, 0) != hipSuccess) {
+      (void)hipFree(dev); dev = nullptr; host = nullptr; failed = true; return nullptr;
+    }
+  }
+  if ((int)at.size() <= pos) at.resize(pos + 1);
+  for (int slot : at[pos])
+    if (std::memcmp(host + slot * sz, &b, sz) == 0) {
+      ++hits;
+      return reinterpret_cast<const GemmBatch*>(dev + slot * sz);
+    }
+  ++misses;
+  if (used >= kSlots || (int)at[pos].size() >= kPerPosition) return nullptr;
+  // no upload into a stream capture (the copy would become a graph node of
+  // its own): a captured launch of a batch not seen before takes it by value
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  const int slot = used;
+  std::memcpy(host + slot * sz, &b, sz);
+  if (hipMemcpyAsync(dev + slot * sz, host + slot * sz, sz, hipMemcpyHostToDevice, s) != hipSuccess) {
+    failed = true;
+    return nullptr;
+  }
+  ++used;
+  at[pos].push_back(slot);
+  return reinterpret_cast<const GemmBatch*>(dev + slot * sz);
+}
+
+inline BatchCache::~BatchCache() {
+  if (dev) (void)hipFree(dev);
+  if (host) (void)hipHostFree(host);
+}
+
+
 // launchers (defined in the .hip files)
 void gemm_batch_finalize(GemmBatch& b, int cfg);
-hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s);
+hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCache* bc = nullptr,
+                             int pos = -1);
 int gemm_tile_m(int cfg);
 int gemm_tile_n(int cfg);
 

@@ -145,6 +145,12 @@ struct GemmBatch {
   RowGather rg;              // rg.ring != null: direct row gather (small kernel only)
 };
 
+// A launch's GemmBatch read from device memory (kernels.h BatchCache) through a
+// pointer declared global: through a generic one the compiler cannot tell that
+// the operand pointers loaded from the record are global, and every operand
+// access becomes a flat load
+typedef __attribute__((address_space(1))) GemmBatch GemmBatchG;
+
 // ---------------------------------------------------------------------------
 // Device-resident step state (read by every kernel of a step; advanced by the
 // last block of the step's final kernel, so the launch sequence is static and

@@ -23,6 +23,7 @@ struct Split { int S, kchunk; };
 
 struct PlanBase {
   int cfg = 0;  // gemm tile config
+  BatchCache bcache;   // the launches' GemmBatch records in device memory (kernels.h)
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   hipStream_t graph_stream = nullptr;
@@ -277,7 +278,7 @@ static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {
               gb.t[i].a_kc, gb.t[i].b_kc, gb.t[i].a_mode, gb.t[i].epi, gb.t[i].ksplit);
     fprintf(stderr, "\n");
   }
-  TIMED(p, K_GEMM, s, OAC_HIP_CHECK(gemm_batch_launch(gb, cfg, s)));
+  TIMED(p, K_GEMM, s, OAC_HIP_CHECK(gemm_batch_launch(gb, cfg, s, &p.bcache, p.launches)));
   p.launches++;
   return 0;
 }

@@ -88,9 +88,14 @@ __device__ __forceinline__ void target_row_load(const CriticTargetArgs& p, int r
       for (int t = 0; t < 16; ++t)   // unconditional (all in flight), coalesced over rows
         x.pv[k][t] = pp[(long)min(t, p.n_part - 1) * p.B];
     }
-  } else {
+  } else {   // (every element assigned on both paths: a partly assigned
+             // array kept two of them in scratch across the merge)
 #pragma unroll
-    for (int k = 0; k < QV_COUNT; ++k) x.pv[k][0] = p.q[k][rc];
+    for (int k = 0; k < QV_COUNT; ++k) {
+      x.pv[k][0] = p.q[k][rc];
+#pragma unroll
+      for (int t = 1; t < 16; ++t) x.pv[k][t] = 0.f;
+    }
   }
 #pragma unroll
   for (int k = 0; k < QV_COUNT; ++k) x.pb[k] = p.n_part > 0 ? p.part_bias[k][0] : 0.f;

@@ -16,10 +16,7 @@
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
   printf("%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
 
-namespace oac {
-void gemm_batch_finalize(GemmBatch& b, int cfg);
-hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s);
-}
+#include "../../oac-explore_amd/csrc/kernels.h"
 #ifdef OAC_PIPE_CLOCK
 #include "../../oac-explore_amd/csrc/gemm_bwdp.hip"
 #endif
