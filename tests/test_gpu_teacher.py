@@ -193,7 +193,10 @@ def _check(errs, left_out, name, s):
     assert not bad, (name, s, sorted(bad.items(), key=lambda kv: -kv[1])[:10])
 
 
-@pytest.mark.parametrize("name", ["sac_humanoid", "sac_humanoid_b4096"])
+# every SAC fixture: each config flag (no alpha tuning, target period 2, the
+# small / stress / RiverSwim dims) through the step's fused paths at 1e-5
+@pytest.mark.parametrize("name", ["sac_humanoid", "sac_humanoid_b4096", "sac_small", "sac_stress",
+                                  "sac_noalpha", "sac_riverswim", "sac_period2"])
 def test_sac_teacher_forced_every_step(name):
     meta, g = parity.load(name)
     tr = sac_trainer_for(meta)
@@ -238,7 +241,8 @@ def test_sac_teacher_forced_every_step(name):
         _check(errs, left_out, name, s)
 
 
-@pytest.mark.parametrize("name", ["poac_ant", "poac_ant_b4096"])
+@pytest.mark.parametrize("name", ["poac_ant", "poac_ant_b4096", "poac_small", "poac_counts",
+                                  "poac_nobias", "poac_period2"])
 def test_particle_teacher_forced_every_step(name):
     from test_gpu_particle import particle_trainer_for
     meta, g = parity.load(name)
