@@ -87,6 +87,28 @@ def test_graph_replay_is_bitwise_equal_to_direct_launches():
     assert torch.equal(outs[0], outs[1])
 
 
+def test_large_batch_graph_replay_with_device_records_is_bitwise():
+    """B=4096 (the large-batch kernels, whose GemmBatch records live in device
+    memory once a plan has launched them, kernels.h BatchCache): direct
+    launches; a graph captured after direct steps filled the cache (the
+    captured launches keep the device records' pointers); a graph captured on
+    the first call (nothing cached, nothing uploaded under capture: by-value
+    records) -- all three bitwise equal."""
+    meta, g = parity.load("sac_humanoid_b4096")
+    n = min(3, meta["steps"])
+    outs = []
+    for mode in ("direct", "graph_after_direct", "graph_first"):
+        tr = sac_trainer_for(meta, use_graph=(mode == "graph_first"))
+        for s in range(n):
+            if mode == "graph_after_direct" and s == 1:
+                tr.use_graph = True
+            tr.train_from_torch(batch_from(meta, g[f"s{s}/idx"]), eps1=g[f"s{s}/eps1"],
+                                eps2=g[f"s{s}/eps2"])
+        outs.append(torch.cat([tr.params, tr.targets, tr.adam_m, tr.adam_v, tr.alpha_state]).cpu())
+    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[2])
+
+
 def test_device_gather_step_equals_host_batch_step():
     """ReplayBuffer.random_batch -> DeviceBatch -> in-step gather gives the
     same result as the reference-format numpy batch."""
