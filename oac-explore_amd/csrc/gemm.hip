@@ -401,6 +401,10 @@ hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCa
   bool gathers = b.rg.ring != nullptr;
   for (int i = 0; i < b.ntasks; ++i) gathers = gathers || b.t[i].a_rows;
   if (gathers && cfg != 0 && (cfg < 6 || cfg > 8)) return hipErrorInvalidValue;
+  for (int i = 0; i < b.ntasks; ++i)   // folded reductions (GemmTask::fold): the small kernel only,
+    if (b.t[i].fold && (cfg != 0 || b.t[i].ksplit > 1 || b.t[i].b_ones || b.t[i].a_kc ||
+                        b.t[i].a_mode != A_RANK1_MASK || b.t[i].epi != EPI_GRAD))   // unsplit
+      return hipErrorInvalidValue;
   if (cfg == 0) return gemm_small_launch(b, s, bc, pos);
   if (b.fuse_adam) return hipErrorInvalidValue;   // fused optimizer: small-batch kernel only
   for (int i = 0; i < b.ntasks; ++i) {             // dual products / head backward: small kernel

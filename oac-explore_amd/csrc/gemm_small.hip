@@ -34,12 +34,52 @@ __device__ long long g_gs_clock[4096 * 8];
 #define GS_STAGE(i)
 #endif
 
+// GemmTask::fold's per-lane sums (row m = lane & 31 over the k of this lane's
+// k-groups): inside the k loop at 16 waves (105 -> 119 VGPRs, four waves per
+// SIMD either way); below that in a pass of its own after the k loop, whose
+// operands come back from the cache -- accumulating in the 8-wave k loop took
+// that kernel from 123 to 137 VGPRs, past the 128 of two workgroups per CU
+struct FoldAcc { float rs, gs, ss; };
+__device__ __forceinline__ void fold_add(FoldAcc& fa, const Lane& la, int k, int k_hi, float a,
+                                         float x, float y) {
+  const bool kin = k < k_hi;
+  fa.rs += a;                                // the k loop's A value (fix1)
+  fa.gs += (la.valid && kin) ? y * x : 0.f;  // s[k] x(k, m)
+  fa.ss += kin ? y : 0.f;                    // s[k]
+}
 // acc += A[m0.., k_lo..k_hi) . B[k_lo..k_hi), n0..]  for this wave's k-groups
 // arow >= 0: this lane's A row is buffer row arow (the direct gather's index,
 // loaded by the caller ahead of everything else)
-template <int NW, int AK, int BK, int GPW = (NW >= 16 ? 4 : 5)>
+template <int NW>
+__device__ __forceinline__ FoldAcc fold_pass(const GemmTask& t, int m0, int k_lo, int k_hi) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l32 = lane & 31, half = lane >> 5;
+  const Lane la = lane_init<OP_MN_R1>(m0 + l32, t.M, false, t.a_mask, t.ld_mask, t.a_s, t.a_v);
+  const int g_lo = k_lo >> 3, g_hi = (k_hi + 7) >> 3, kmax = k_hi - 1;
+  FoldAcc fa{0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int g0 = g_lo + wave; g0 < g_hi; g0 += 2 * NW) {   // two groups in flight
+    float x0[4], y0[4], x1[4], y1[4];
+    const int kb0 = 8 * g0 + 4 * half, kb1 = kb0 + 8 * NW;
+    const bool two = g0 + NW < g_hi;
+    load4<OP_MN_R1>(la, kb0, kmax, x0, y0);
+    if (two) load4<OP_MN_R1>(la, kb1, kmax, x1, y1);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      fold_add(fa, la, kb0 + c, k_hi, fix1<OP_MN_R1>(la, kb0 + c, k_hi, x0[c], y0[c]), x0[c], y0[c]);
+    if (two) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        fold_add(fa, la, kb1 + c, k_hi, fix1<OP_MN_R1>(la, kb1 + c, k_hi, x1[c], y1[c]), x1[c], y1[c]);
+    }
+  }
+  return fa;
+}
+
+template <int NW, int AK, int BK, int GPW = (NW >= 16 ? 4 : 5), bool FOLD = false>
 __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
-                                       floatx16& acc, int arow = -1) {
+                                       floatx16& acc, int arow, FoldAcc& fa) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
   const int l32 = lane & 31;
@@ -74,20 +114,23 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
           const float a = fix1<AK>(la, kb + c, k_hi, ax[j][c], ay[j][c]);
           const float b = fix1<BK>(lb, kb + c, k_hi, bx[j][c], by[j][c]);
           acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+          if constexpr (FOLD) fold_add(fa, la, kb + c, k_hi, a, ax[j][c], ay[j][c]);
         }
       }
   }
 }
 
-template <int NW, int GPW>
+template <int NW, int GPW, bool FOLDK>
 __device__ __forceinline__ void k_dispatch(const GemmTask& t, int m0, int n0, int k_lo, int k_hi,
-                                           floatx16& acc, int arow) {
+                                           floatx16& acc, int arow, bool fold, FoldAcc& fa) {
   const bool r1 = t.a_mode == A_RANK1_MASK;
-  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW>(t, m0, n0, k_lo, k_hi, acc, arow);   // forward
-  else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dX
-  else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dX, rank-1 seed
-  else if (!r1)                k_loop<NW, OP_MN, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);      // dW
-  else                         k_loop<NW, OP_MN_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc);   // dW, rank-1 seed
+  if (t.a_kc && t.b_kc)        k_loop<NW, OP_KC, OP_KC, GPW>(t, m0, n0, k_lo, k_hi, acc, arow, fa);   // forward
+  else if (t.a_kc && !r1)      k_loop<NW, OP_KC, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc, -1, fa);      // dX
+  else if (t.a_kc)             k_loop<NW, OP_KC_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc, -1, fa);   // dX, rank-1 seed
+  else if (!r1)                k_loop<NW, OP_MN, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc, -1, fa);      // dW
+  else if (FOLDK && NW >= 16 && fold)
+    k_loop<NW, OP_MN_R1, OP_MN, GPW, FOLDK>(t, m0, n0, k_lo, k_hi, acc, -1, fa);   // dW + fold
+  else                         k_loop<NW, OP_MN_R1, OP_MN, GPW>(t, m0, n0, k_lo, k_hi, acc, -1, fa);   // dW, rank-1 seed
 }
 
 // Epilogue operands of one output element, loaded before the k loop so their
@@ -195,15 +238,45 @@ static GemmHead gemm_head(const GemmBatch& b) {
 // one workgroup's share of a launch: block `bid` of the batch (the kernel
 // below passes blockIdx.x; tools/micro/persist_micro.hip runs several batches
 // in one persistent launch with a grid barrier between them)
-template <int NW>
+template <int NW, bool FOLDK = false>
 struct SmallLds {
   static constexpr int RED = NW * 16 * 64;   // partial tiles: NW x 16 regs x 64 lanes
-  static constexpr int N = RED > 2 * 32 * 65 ? RED : 2 * 32 * 65;   // reused for the epilogue operands
+  static constexpr int FOLD = RED > 2 * 32 * 65 ? RED : 2 * 32 * 65;   // (before: the epilogue operands)
+  static constexpr int N = FOLD + (FOLDK ? NW * 65 : 0);   // + the fold's per-wave sums [rs 32 | gs 32 | ss 1]
 };
+
+// GemmTask::fold: one folded gradient element's value -> the gradient arena,
+// and with the fused optimizer its Adam (+ Polyak) on the prefetched p, m, v, t
+// (as epi_one's EPI_GRAD elements)
+struct FoldIn { float p, m, v, t; };
+__device__ __forceinline__ FoldIn fold_prefetch(const GemmBatch& batch, const float* g) {
+  FoldIn x{0.f, 0.f, 0.f, 0.f};
+  const long i = g - batch.adam.g;
+  x.p = batch.adam.p[i]; x.m = batch.adam.m[i]; x.v = batch.adam.v[i];
+  if (batch.adam.target) x.t = batch.adam.target[i];
+  return x;
+}
+__device__ __forceinline__ void fold_store(const GemmBatch& batch, const AdamConsts& ac, bool adam,
+                                           float* g, float val, FoldIn x) {
+  *g = val;
+  if (!adam) return;
+  const long i = g - batch.adam.g;
+  float p = x.p, m = x.m, v = x.v;
+  adam1(ac, p, val, m, v);
+  (batch.adam.p_out ? batch.adam.p_out : batch.adam.p)[i] = p;
+  if (!batch.adam.preview) {
+    batch.adam.m[i] = m; batch.adam.v[i] = v;
+    if (ac.polyak) batch.adam.target[i] = polyak1(ac, x.t, p);
+  }
+}
 
 constexpr int kGatherU = 4;   // float4s per lane of a side block's row copy (rows <= 1 KB)
 
-template <int NW, int GPW>
+// FOLDK: the kernel that takes GemmTask::fold tasks (a variant of its own, so
+// the other launches keep the registers and schedule of the plain kernel:
+// with the fold in every kernel, launches without a fold task came out
+// 0.2-0.4 us slower)
+template <int NW, int GPW, bool FOLDK = false>
 __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int publish, int tb1,
                                                  int tb2, int tb3, int tb4, int tb5, int tb6,
                                                  int tb7, const GemmBatch& batch, float* red,
@@ -318,21 +391,54 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     const int r = e >> 6, l = e & 63;
     xin[i] = epi_prefetch(batch, t, m0 + (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), n0 + (l & 31));
   }
+  // GemmTask::fold (first column block): thread f < 32 finishes row m0 + f's
+  // bias-column and width-1-layer sums, thread 32 (tile m0 = 0) the seed sum
+  const bool fold = FOLDK && t.fold && n0 == 0;   // (workgroup-uniform)
+  const bool fold_adam = fold && batch.fuse_adam && !t.no_adam;
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-  k_dispatch<NW, GPW>(t, m0, n0, k_lo, k_hi, acc, arow);
+  FoldAcc fa{0.f, 0.f, 0.f};
+  k_dispatch<NW, GPW, FOLDK>(t, m0, n0, k_lo, k_hi, acc, arow, fold, fa);
+  if constexpr (FOLDK && NW < 16)
+    if (fold) fa = fold_pass<NW>(t, m0, k_lo, k_hi);
+  // the folded elements' optimizer operands, requested now: their latency
+  // behind the LDS reduction (held across the k loop they cost registers)
+  FoldIn fb{}, fw{};
+  if (fold_adam && threadIdx.x < 33) {
+    const int fm = min(m0 + (int)threadIdx.x, t.M - 1);
+    fb = fold_prefetch(batch, threadIdx.x < 32 ? t.bias_grad + fm : t.C2 + t.ldc2);
+    fw = fold_prefetch(batch, t.C2 + fm);
+  }
+
   if (t.K2 > 0) {   // second product into the same accumulator (unsplit dX tasks only)
     GemmTask t2 = t;
     t2.A = t.A2; t2.B = t.B2; t2.K = t.K2;
-    k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc);
+    k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc, -1, fa);
   }
 
   GS_STAGE(2);
   // fixed-order split-K reduction through LDS
 #pragma unroll
   for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = acc[r];
+  float* fred = red + SmallLds<NW, FOLDK>::FOLD;
+  if (fold) {   // the two halves' k, then one slot per wave
+    fa.rs += __shfl_xor(fa.rs, 32);
+    fa.gs += __shfl_xor(fa.gs, 32);
+    fa.ss += __shfl_xor(fa.ss, 32);
+    if (lane < 32) { fred[wave * 65 + lane] = fa.rs; fred[wave * 65 + 32 + lane] = fa.gs; }
+    if (lane == 0) fred[wave * 65 + 64] = fa.ss;
+  }
   __syncthreads();
+  float fsum_a = 0.f, fsum_b = 0.f;   // (waves in order)
+  if (fold && threadIdx.x < 33) {
+    const int f = threadIdx.x;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      fsum_a += fred[w * 65 + (f < 32 ? f : 64)];
+      if (f < 32) fsum_b += fred[w * 65 + 32 + f];
+    }
+  }
   float vals[PER];
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
@@ -378,18 +484,25 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
       if (nt == 0 && m < t.M) t.C2[(long)(n0 >> 5) * t.ldc2 + m] = x;   // tile-major
     }
   }
+  if (fold && threadIdx.x < 32 && m0 + (int)threadIdx.x < t.M) {
+    const int m = m0 + threadIdx.x;
+    fold_store(batch, ac, fold_adam, t.bias_grad + m, fsum_a, fb);
+    fold_store(batch, ac, fold_adam, t.C2 + m, fsum_b, fw);
+  } else if (fold && threadIdx.x == 32 && m0 == 0) {
+    fold_store(batch, ac, fold_adam, t.C2 + t.ldc2, fsum_a, fb);
+  }
   if (batch.fuse_adam && !batch.adam.no_book && bid == 0 && threadIdx.x == 0)
     step_bookkeeping(batch.adam.state, batch.adam.alpha, batch.adam.advance);
   GS_STAGE(4);
 }
 
-template <int NW, int GPW>
+template <int NW, int GPW, bool FOLDK = false>
 __global__ void __launch_bounds__(64 * NW)
 gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6,
                   int tb7, const GemmBatch batch) {
-  __shared__ __attribute__((aligned(16))) float red[SmallLds<NW>::N];
-  gemm_small_block<NW, GPW>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6, tb7,
-                            batch, red);
+  __shared__ __attribute__((aligned(16))) float red[SmallLds<NW, FOLDK>::N];
+  gemm_small_block<NW, GPW, FOLDK>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6,
+                                   tb7, batch, red);
 }
 
 // The direct drop-in layer-0 launch with the step's B <= 256 indices in the
@@ -471,6 +584,9 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s, BatchCache* bc 
   const GemmHead h = gemm_head(b);
   const bool inl = b.rg.inl && b.rg.ring && b.rg.B <= kInlineRows &&
                    ((nw == 16 && gpw == 4) || (nw == 8 && gpw == 5));
+  bool has_fold = false;
+  for (int i = 0; i < b.ntasks; ++i) has_fold = has_fold || b.t[i].fold;
+  if (has_fold && inl) return hipErrorInvalidValue;   // (no fold task in a row-gathering launch)
   if (inl) {
     InlineRows ir;
     std::memcpy(ir.r, b.rg.inl, sizeof(int) * b.rg.B);
@@ -481,6 +597,16 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s, BatchCache* bc 
       OAC_LAUNCH((gemm_small_kernel_inl<8, 5>), dim3(grid), dim3(64 * 8), 0, s, h.total_tiles, h.publish,
                  h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b, ir);
     return hipGetLastError();
+  }
+  if (has_fold) {   // the fold kernels: the default wave / k-group pairs only
+#define OAC_GSF(NW_, G_) \
+    if (nw == NW_ && gpw == G_) { \
+      OAC_LAUNCH((gemm_small_kernel<NW_, G_, true>), dim3(grid), dim3(64 * NW_), 0, s, h.total_tiles, \
+                 h.publish, h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b); \
+      return hipGetLastError(); }
+    OAC_GSF(1, 5) OAC_GSF(2, 5) OAC_GSF(4, 5) OAC_GSF(8, 5) OAC_GSF(16, 4)
+#undef OAC_GSF
+    return hipErrorInvalidValue;
   }
 #define OAC_GS(NW_, G_) \
   if (nw == NW_ && gpw == G_) { \

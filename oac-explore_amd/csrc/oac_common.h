@@ -60,6 +60,12 @@ struct GemmTask {
   int R;         // rank of the EPI_BIAS_RANK_RELU update
   int ksplit;    // K chunks (EPI_GRAD only); chunk = kchunk (multiple of 64)
   int kchunk;
+  // small kernel, rank-1-seeded dW (A = s[k] v[m] [x(k, m) > 0]) unsplit:
+  // the tiles of the first column block also reduce, per output row m, the
+  // bias column sum_k A(m, k) into bias_grad[m] (b_ones off: no ones-column
+  // tiles) and the seed's width-1 layer gradient sum_k s[k] x(k, m) into
+  // C2[m], and the m0 = 0 tile sum_k s[k] into C2[ldc2] (that layer's bias)
+  int fold;
   long slab_stride;
   int tile_begin;
   int tiles_n;

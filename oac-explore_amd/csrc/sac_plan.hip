@@ -509,12 +509,21 @@ static int phase1(SacPlan& p, hipStream_t s, bool fused, int part = 0, bool spli
     const int dh1[2] = {W_DH1Q1, W_DH1Q2};
     float* gq = grad_q(p);
     const long gs = q_group(p);
+    // small batch, unsplit: the layer-1 bias column and the width-1 last layer
+    // (dW = dq^T h2, its bias sum dq) folded into the layer-1 dW tiles of the
+    // first column block, which load dq and h2 as the rank-1 seed's factors
+    // anyway (GemmTask::fold): 290 -> 256 tiles, one round of 16-wave workgroups
+    const bool fold = p.cfg == 0 && !wl_in_targets(p) && p.sp_q1.S == 1 && p.sp_ql.S == 1;
     for (int i = 0; i < 2; ++i) {
       float* g = gq + i * L.q_size;   // critic i's block in the gradient (slab) layout
       GemmTask t = t_dw(nullptr, 0, H, B, p.W(h1[i]), H, H, g + L.q_fc1_w, g + L.q_fc1_b, gs, p.sp_q1);
       set_rank1(t, p.W(dq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
+      if (fold) {
+        t.N = H; t.b_ones = 0; t.fold = 1;   // bias_grad keeps the layer-1 bias gradient
+        t.C2 = g + L.q_last_w; t.ldc2 = (long)L.q_last_b - (long)L.q_last_w;
+      }
       add(gb, t);
-      if (!wl_in_targets(p))   // (else the targets kernel wrote these slabs)
+      if (!wl_in_targets(p) && !fold)   // (else the targets kernel or the fold wrote these)
         add(gb, t_dw(p.W(dq[i]), 1, 1, B, p.W(h2[i]), H, H, g + L.q_last_w, g + L.q_last_b, gs, p.sp_ql));
       GemmTask d = t_dx(nullptr, 0, B, H, qs[i] + L.q_fc1_w, H, H, p.W(dh1[i]), H, p.W(h1[i]), H);
       set_rank1(d, p.W(dq[i]), qs[i] + L.q_last_w, p.W(h2[i]), H);
