@@ -1,6 +1,6 @@
 #!/bin/bash
-# round 5: the critic layer-1 backward with the bias column and the width-1
-# last layer folded into its dW tiles (290 -> 256 tiles) -- parity first,
+# round 5: A/B of the current tree against the previous build (liboac_amd_prev.so):
+# parity first,
 # then interleaved A/B against the previous build
 mkdir -p gpurun_out
 crash() { case $1 in 124|134|137|139) echo "GPU step ended with $1: stopping"; exit $1;; esac; }
