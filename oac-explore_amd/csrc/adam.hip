@@ -15,18 +15,47 @@
 
 namespace oac {
 
+// LANES threads per float4: with split-K slabs (9 <= S <= 32) each lane sums
+// one chunk of 8 slabs (slab_chunk), lane 0 adds the chunk sums in chunk
+// order -- the same bits as one thread per element (adam_flat_elem), with
+// every slab load of the element in flight at once across the lanes and 4x
+// the workgroups: configs[4]'s critic / policy Adam (100k parameters, 32
+// slabs) ran as 98 workgroups, one float4 and four dependent chunk rounds per
+// thread
+template <int LANES>
 __global__ void __launch_bounds__(256) adam_flat_kernel(AdamArgs a) {
   const AdamConsts c = adam_consts(a.state, a.advance, a.lr, a.beta1, a.beta2, a.eps, a.target,
                                    a.tau, a.period);
   const long n4 = a.n >> 2;
-  const long stride = (long)gridDim.x * 256;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) adam_flat_elem(c, a, i);
+  if (LANES == 1) {
+    const long stride = (long)gridDim.x * 256;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n4; i += stride) adam_flat_elem(c, a, i);
+  } else {
+    const int q = threadIdx.x % LANES;
+    const long stride = (long)gridDim.x * (256 / LANES);
+    for (long i0 = (long)blockIdx.x * (256 / LANES); i0 < n4; i0 += stride) {
+      const long i = i0 + threadIdx.x / LANES;   // (uniform trip count: every lane shuffles)
+      const long ic = i < n4 ? i : n4 - 1;
+      const int S = slab_count(a, ic);
+      const int nc = (S + kSlabChunk - 1) / kSlabChunk;   // <= LANES (launcher: S2 <= S)
+      float4 p = q < nc ? slab_chunk(a, ic, q, S) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 g = p;
+#pragma unroll
+      for (int j = 1; j < LANES; ++j) {   // chunk sums in chunk order, at lane 0 of the group
+        float4 r;
+        r.x = __shfl(p.x, (threadIdx.x & 63) - q + j); r.y = __shfl(p.y, (threadIdx.x & 63) - q + j);
+        r.z = __shfl(p.z, (threadIdx.x & 63) - q + j); r.w = __shfl(p.w, (threadIdx.x & 63) - q + j);
+        if (j < nc) add4(g, r);
+      }
+      if (q == 0 && i < n4) adam_flat_finish(c, a, i, g, true);
+    }
+  }
   if (a.reduce_only || a.no_book) return;
   step_bookkeeping(a.state, a.alpha, a.advance);
 }
 
-static int adam_blocks(long n) {
-  long b = (n + 255) / 256;
+static int adam_blocks(long n, int per_block) {
+  long b = (n + per_block - 1) / per_block;
   if (b > 2048) b = 2048;
   if (b < 1) b = 1;
   return (int)b;
@@ -34,7 +63,12 @@ static int adam_blocks(long n) {
 
 hipError_t launch_adam(const AdamArgs& a, hipStream_t s) {
   if (a.n & 3) return hipErrorInvalidValue;   // arena ranges are 16-byte multiples
-  OAC_LAUNCH(adam_flat_kernel, dim3(adam_blocks((a.n + 3) >> 2)), dim3(256), 0, s, a);
+  const long n4 = (a.n + 3) >> 2;
+  const bool slabs = a.S > 1 || a.gslab != a.g;
+  if (slabs && a.S > kSlabChunk && a.S <= kSlabChunk * kSlabLanes)
+    OAC_LAUNCH(adam_flat_kernel<kSlabLanes>, dim3(adam_blocks(n4, 256 / kSlabLanes)), dim3(256), 0, s, a);
+  else
+    OAC_LAUNCH(adam_flat_kernel<1>, dim3(adam_blocks(n4, 256)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

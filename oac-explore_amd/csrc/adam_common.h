@@ -108,38 +108,58 @@ __device__ __forceinline__ void adam_float4(const AdamConsts& c, const AdamArgs&
   }
 }
 
-// float4 i of a flat range: the split-K slabs summed in fixed order 0 .. S-1
-// (written back to g), optionally scaled, then Adam (+ Polyak) -- the body of
-// adam_flat_kernel (adam.hip) and of the large-batch GEMMs' side workgroups
-__device__ __forceinline__ void adam_flat_elem(const AdamConsts& c, const AdamArgs& a, long i) {
-  float4 g;
-  if (a.S > 1 || a.gslab != a.g) {
-    // the loads of 8 slabs are issued together (a one-slab-per-iteration loop
-    // waited out S dependent round trips: B=4096, S=32 -> ~11 us per launch)
-    const float4* gs = reinterpret_cast<const float4*>(a.gslab) + i;
-    const long st4 = a.slab_stride >> 2;
-    g = gs[0];
-    int k = 1;
-#pragma unroll 1
-    for (; k + 8 <= a.S; k += 8) {
-      float4 x[8];
+// The split-K slabs of float4 i summed in a fixed order that depends on the
+// element alone: chunks of kSlabChunk consecutive slabs, each summed in slab
+// order, then the chunk sums in chunk order -- so one thread per element (the
+// side workgroups, adam_flat_elem) and kSlabLanes lanes per element, one chunk
+// each (adam_flat_kernel), give the same bits.
+constexpr int kSlabChunk = 8;
+constexpr int kSlabLanes = 4;   // lanes per element in adam_flat_kernel (S <= 32)
+__device__ __forceinline__ int slab_count(const AdamArgs& a, long i) {
+  const long x = 4 * i;
+  return (x >= a.s2_lo && x < a.s2_hi) ? min(a.S2, a.S) : a.S;
+}
+__device__ __forceinline__ float4 slab_chunk(const AdamArgs& a, long i, int c, int S) {
+  const float4* gs = reinterpret_cast<const float4*>(a.gslab) + i;
+  const long st4 = a.slab_stride >> 2;
+  const int k0 = c * kSlabChunk, k1 = min(S, k0 + kSlabChunk);
+  float4 x[kSlabChunk];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) x[j] = gs[(long)(k + j) * st4];
+  for (int j = 0; j < kSlabChunk; ++j)   // every load of the chunk in flight together
+    if (k0 + j < k1) x[j] = gs[(long)(k0 + j) * st4];
+  float4 g = x[0];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { g.x += x[j].x; g.y += x[j].y; g.z += x[j].z; g.w += x[j].w; }
-    }
-#pragma unroll 1
-    for (; k < a.S; ++k) {
-      const float4 x = gs[(long)k * st4];
-      g.x += x.x; g.y += x.y; g.z += x.z; g.w += x.w;
-    }
-    reinterpret_cast<float4*>(a.g)[i] = g;
-  } else {
-    g = reinterpret_cast<const float4*>(a.g)[i];
-  }
+  for (int j = 1; j < kSlabChunk; ++j)
+    if (k0 + j < k1) { g.x += x[j].x; g.y += x[j].y; g.z += x[j].z; g.w += x[j].w; }
+  return g;
+}
+__device__ __forceinline__ void add4(float4& g, const float4& p) {
+  g.x += p.x; g.y += p.y; g.z += p.z; g.w += p.w;
+}
+
+// the reduced gradient (written back to g), optionally scaled, then Adam (+
+// Polyak): the body of adam_flat_kernel and of the large-batch GEMMs' side
+// workgroups
+__device__ __forceinline__ void adam_flat_finish(const AdamConsts& c, const AdamArgs& a, long i,
+                                                 float4 g, bool reduced) {
+  if (reduced) reinterpret_cast<float4*>(a.g)[i] = g;
   if (a.reduce_only) return;
   if (a.gscale != 1.f) { g.x *= a.gscale; g.y *= a.gscale; g.z *= a.gscale; g.w *= a.gscale; }
   adam_float4(c, a, i, g);
+}
+
+// float4 i of a flat range, one thread (slab order: slab_chunk)
+__device__ __forceinline__ void adam_flat_elem(const AdamConsts& c, const AdamArgs& a, long i) {
+  if (a.S > 1 || a.gslab != a.g) {
+    const int S = slab_count(a, i);
+    float4 g = slab_chunk(a, i, 0, S);
+    const int nc = (S + kSlabChunk - 1) / kSlabChunk;
+#pragma unroll 1
+    for (int ch = 1; ch < nc; ++ch) add4(g, slab_chunk(a, i, ch, S));
+    adam_flat_finish(c, a, i, g, true);
+  } else {
+    adam_flat_finish(c, a, i, reinterpret_cast<const float4*>(a.g)[i], false);
+  }
 }
 
 // side workgroup `blk` of `nblk` (256 threads each): the flat ranges of
@@ -153,6 +173,7 @@ __device__ __forceinline__ void adam_side_block(const GemmBatch& b, int blk, int
     AdamArgs r = a;
     const long off = b.seg_off[sgi];
     r.p += off; r.g += off; r.m += off; r.v += off; r.gslab += off;
+    r.s2_lo -= off; r.s2_hi -= off;
     if (r.target) r.target += off;
     const long n4 = b.seg_n[sgi] >> 2;
     for (long i = (long)blk * 256 + threadIdx.x; i < n4; i += stride) adam_flat_elem(c, r, i);

@@ -86,7 +86,10 @@ struct AdamArgs {
   float* p; float* g; float* m; float* v; long n;
   // split-K gradient slabs shaped like the arena range: g = sum_s gslab[s*stride + i]
   // (written back to g); gslab == g with S == 1 reads g directly
-  const float* gslab; int S; long slab_stride;
+  const float* gslab; int S; int S2; long slab_stride;
+  // elements [s2_lo, s2_hi) of the range (16-byte aligned) hold only S2 < S
+  // slabs (a layer split fewer ways than the group's widest; S2 = 0: none)
+  long s2_lo, s2_hi;
   float* target; float tau; int period;   // target != null -> Polyak after the step
   double lr, beta1, beta2, eps;
   StepState* state;

@@ -73,6 +73,12 @@ inline AdamArgs critic_adam(SacPlan& p, int reduce_only, AlphaState* commit) {
   a.gslab = reduce_only < 0 ? a.g : grad_q(p);
   a.S = reduce_only < 0 ? 1 : p.S_q;
   a.slab_stride = q_group(p);
+  // one critic: its layer 1 (and the last layer when split no wider) reads only
+  // its own slabs (configs[4]: 16 of the group's 32)
+  if (a.S > 1 && p.L.n_critics == 1 && p.sp_q1.S < a.S) {
+    a.S2 = p.sp_q1.S; a.s2_lo = p.L.q_fc1_w;
+    a.s2_hi = p.sp_ql.S <= p.sp_q1.S ? p.L.q_size : p.L.q_last_w;
+  }
   a.target = p.b.targets; a.tau = c.tau; a.period = c.target_update_period;
   a.lr = c.qf_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
   a.state = p.state(); a.advance = 0; a.alpha = commit;
@@ -92,6 +98,10 @@ inline AdamArgs policy_adam(SacPlan& p, int reduce_only, AlphaState* commit) {
   a.gslab = reduce_only < 0 ? a.g : grad_p(p);
   a.S = reduce_only < 0 ? 1 : p.S_p;
   a.slab_stride = p_group(p);
+  if (a.S > 1 && p.sp_p1.S < a.S) {   // policy layer 1 (and the heads when split no wider)
+    a.S2 = p.sp_p1.S; a.s2_lo = p.L.pol_fc1_w;
+    a.s2_hi = p.sp_ph.S <= p.sp_p1.S ? p.L.pol_size : p.L.pol_head_w;
+  }
   a.lr = c.policy_lr; a.beta1 = c.beta1; a.beta2 = c.beta2; a.eps = c.adam_eps;
   a.state = p.state(); a.advance = 1; a.alpha = commit;
   a.gscale = reduce_only < 0 ? 1.f / (float)c.world_size : 1.f;

@@ -275,6 +275,7 @@ int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long
     AdamArgs r = a;
     r.p += off[i]; r.g += off[i]; r.m += off[i]; r.v += off[i];
     r.gslab += off[i];
+    r.s2_lo -= off[i]; r.s2_hi -= off[i];
     if (r.target) r.target += off[i];
     r.n = n[i];
     r.no_book = (book && i == 0) ? 0 : 1;

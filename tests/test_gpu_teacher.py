@@ -14,9 +14,13 @@ targets, log-alpha (gradient and value) and the losses are compared.
 
 Allowances, each reported by the test: elements of a post-step parameter
 whose gradient is within fp32 rounding of 0 (Adam moves them by ~lr * sign,
-bounded by 2.5 lr); at most two rows of a critic hidden-layer gradient
-whose ReLU pre-activation sits within fp32 rounding of 0 for some sample
-(parity.relu_boundary_units), as in test_gpu_dp.py; and, for a SAC critic's
+bounded by 2.5 lr); at most two rows of a critic or policy hidden-layer
+gradient whose ReLU pre-activation sits within fp32 rounding of 0 for some
+sample (parity.relu_boundary_units), as in test_gpu_dp.py (the policy's on
+the observations: sac_humanoid_b4096 step 2 has a policy layer-0 unit at
+6.7e-7 rms of 0 that takes the other sign under the chunked slab order of the
+round-5 Adam launch, tools/diag_teacher_flip.py -- one fc0 row off, 2.2e-3);
+and, for a SAC critic's
 first layer, the layer-1 mask flips, which reach every fc0 row
 (_flip_adjusted: the (sample, unit) entries where the GPU's own saved layer-1
 activations -- the masks its backward used, workspace views h2q1 / h2q2 --
@@ -203,7 +207,7 @@ def test_sac_teacher_forced_every_step(name):
     lr = meta["lr"]
     for s in range(meta["steps"]):
         orc = sac_oracle_from_gpu(tr, meta)
-        pre = {grp: _np_sd(getattr(tr, grp)) for grp in ("qf1", "qf2")}
+        pre = {grp: _np_sd(getattr(tr, grp)) for grp in ("qf1", "qf2", "policy")}
         batch = batch_from(meta, g[f"s{s}/idx"])
         e1, e2 = g[f"s{s}/eps1"], g[f"s{s}/eps2"]
         tr.end_epoch(s)
@@ -213,6 +217,7 @@ def test_sac_teacher_forced_every_step(name):
         out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
         x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
         allowed = {grp: _boundary_rows(x0, pre[grp]) for grp in ("qf1", "qf2")}
+        allowed["policy"] = _boundary_rows(batch["observations"], pre["policy"])
         B = x0.shape[0]
         dqs = {grp: 2.0 * (orc.S[c]["q"] - orc.S["y"]) / B for grp, c in (("qf1", "c1"), ("qf2", "c2"))}
         errs, left_out = {}, {}
@@ -251,6 +256,7 @@ def test_particle_teacher_forced_every_step(name):
     for s in range(meta["steps"]):
         orc = poac_oracle_from_gpu(tr, meta)
         pre = _np_sd(tr.qfs[0])
+        pre_p = _np_sd(tr.policy)
         batch = batch_from(meta, g[f"s{s}/idx"])
         e1, e2 = g[f"s{s}/eps1"], g[f"s{s}/eps2"]
         tr.end_epoch(s)
@@ -258,7 +264,7 @@ def test_particle_teacher_forced_every_step(name):
         torch.cuda.synchronize()
         out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
         x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
-        allowed = {"qf": _boundary_rows(x0, pre)}
+        allowed = {"qf": _boundary_rows(x0, pre), "policy": _boundary_rows(batch["observations"], pre_p)}
         errs, left_out = {}, {}
         for grp, mod, order, opt, P in (("policy", tr.policy, PARAM_ORDER_POLICY, orc.opt_p, orc.P),
                                         ("qf", tr.qfs[0], PARAM_ORDER_Q, orc.opt_q, orc.Q)):
