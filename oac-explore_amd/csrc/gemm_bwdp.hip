@@ -302,7 +302,7 @@ __device__ __forceinline__ void gemm_bwdp_body(int total_tiles, int tb1, int tb2
     adam_side_block(batch, blockIdx.x - side0, batch.side_adam);
     return;
   }
-  const int bid = xcd_tile(blockIdx.x - tile0, total_tiles);
+  const int bid = xcd_tile_rr(blockIdx.x - tile0, total_tiles);
   int ti = 0;
   ti = bid >= tb1 ? 1 : ti; ti = bid >= tb2 ? 2 : ti; ti = bid >= tb3 ? 3 : ti;
   ti = bid >= tb4 ? 4 : ti; ti = bid >= tb5 ? 5 : ti; ti = bid >= tb6 ? 6 : ti;

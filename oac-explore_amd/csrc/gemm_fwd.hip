@@ -221,7 +221,7 @@ __device__ __forceinline__ void gemm_fwd_body(int total_tiles, int tb1, int tb2,
     fwd_gather_side(batch.rg, blockIdx.x - total_tiles, gridDim.x - total_tiles);
     return;
   }
-  const int bid = xcd_tile(blockIdx.x, total_tiles);
+  const int bid = xcd_tile_rr(blockIdx.x, total_tiles);
   // the direct gather's index slot (the A rows of the a_rows tasks)
   const int* rows = batch.rg.ring && batch.rg.slots > 0
                         ? batch.rg.ring + (long)(batch.rg.state->batch_counter % batch.rg.slots) * batch.rg.B

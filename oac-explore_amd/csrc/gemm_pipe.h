@@ -57,4 +57,18 @@ __device__ __forceinline__ int xcd_tile(int bid, int n) {
   return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (bid >> 3);
 }
 
+// The same dispatch, chunks of kXcdChunk consecutive tiles (a row block's
+// column tiles: the same X rows) dealt round-robin over the XCDs: each XCD
+// gets every task's share instead of a contiguous range of tasks, so tasks of
+// unequal work (the critic layer 0's rank continuation) do not pile onto two
+// XCDs.  Tiles [0, T), T = the largest multiple of 8 chunks, go by chunks; the
+// tail keeps its id (bijective for any grid size).
+constexpr int kXcdChunk = 4;
+__device__ __forceinline__ int xcd_tile_rr(int bid, int n) {
+  const int T = n / (8 * kXcdChunk) * (8 * kXcdChunk);
+  if (bid >= T) return bid;
+  const int x = bid & 7, j = bid >> 3;
+  return ((j / kXcdChunk) * 8 + x) * kXcdChunk + j % kXcdChunk;
+}
+
 }  // namespace oac

@@ -1,0 +1,18 @@
+#!/bin/bash
+# round 5: large-batch tiles dealt to the XCDs in round-robin chunks of a row
+# block (every XCD a share of every task): forward kernel only (fwdrr) and
+# forward + backward (cur) -- parity of cur, then A/B against the previous build
+mkdir -p gpurun_out
+crash() { case $1 in 124|134|137|139) echo "GPU step ended with $1: stopping"; exit $1;; esac; }
+T="--timeout 240 --timeout-method thread -p no:cacheprovider"
+timeout -k 10 700 python -u -m pytest tests/test_gpu_teacher.py tests/test_gpu_particle.py tests/test_gpu_parity.py tests/test_gpu_altkernels.py -x -q $T > gpurun_out/r5_t25_tests.log 2>&1
+rc=$?; crash $rc; tail -3 gpurun_out/r5_t25_tests.log; [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/r5_t25_tests.log | head -20; exit $rc; }
+L=$PWD/oac-explore_amd/oac_amd
+for r in 1 2; do for v in prev fwdrr cur; do
+  if [ $v = cur ]; then unset OAC_LIB; else export OAC_LIB=$L/liboac_amd_$v.so; fi
+  timeout -k 10 120 python tools/launch_times.py --batch 4096 --poac --rate-steps 600 > gpurun_out/r5_t25_poac_$v.txt 2>&1; rc=$?; crash $rc
+  echo "$v poac: $(grep drop-in gpurun_out/r5_t25_poac_$v.txt | cut -c1-60)"
+  timeout -k 10 120 python tools/launch_times.py --batch 4096 --rate-steps 600 > gpurun_out/r5_t25_b4096_$v.txt 2>&1; rc=$?; crash $rc
+  echo "$v b4096: $(grep drop-in gpurun_out/r5_t25_b4096_$v.txt | cut -c1-60)"
+done; done
+for v in prev fwdrr cur; do echo "== $v"; paste gpurun_out/r5_t25_b4096_$v.txt gpurun_out/r5_t25_poac_$v.txt | grep launch | tr -s ' ' | cut -c1-90; done
