@@ -90,6 +90,11 @@ static inline Split choose_split(int K, int tiles, int cfg) {
 static inline Split choose_split_pipe(int K, int tiles) {
   tiles = std::max(1, tiles);
   int S = std::max(1, std::min(K / 256, 768 / tiles));
+  // a power of two (equal chunks of a power-of-two batch): B=4096 SAC critic
+  // layer 0 dW 13 -> 8 splits, 26.0 -> 24.4 us, 3,884 -> 3,918 steps/s (same
+  // box after the round-robin XCD mapping; 10 and 6 splits: 30-31 us); the
+  // other launches of the measured configs already were
+  while (S & (S - 1)) S &= S - 1;
   // a small dW (configs[4]'s 256 x 119 critic layer 0: 8 tiles) would leave
   // CUs idle: chunks down to 128 rows until one workgroup per CU
   if (S * tiles < 256) S = std::max(S, std::min(K / 128, (256 + tiles - 1) / tiles));
