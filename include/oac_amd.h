@@ -144,6 +144,9 @@ enum oac_ws_buffer {
   OAC_WS_H2Q1, OAC_WS_H2Q2,            /* SAC: the critics' second hidden layer on (obs, a) [B, H]
                                           after the ReLU -- the masks their backward used (parity
                                           checks; 0 rows for the other kinds) */
+  OAC_WS_H1P, OAC_WS_H2P,              /* SAC / P-OAC: the policy's hidden layers on obs [B, H]
+                                          after the ReLU -- the masks the policy backward used
+                                          (parity checks; 0 rows for the other kinds) */
   OAC_WS_COUNT_PUBLIC
 };
 
@@ -267,6 +270,11 @@ int oac_sac_trace(oac_sac* h, int reset);
 int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows, int64_t* cols);
 /* number of kernel launches of one step (for the launch/graph accounting) */
 int oac_sac_launch_count(oac_sac* h);
+/* the device launch-record cache (no reference counterpart; diagnostics):
+   out[0] records uploaded, out[1] launch positions seen, out[2] hits, out[3]
+   misses.  Positions are launch indices within one step, so both stay
+   bounded however many steps run (<= 512 records, <= 64 positions). */
+int oac_sac_cache_stats(oac_sac* h, int64_t* out);
 /* bench instrumentation: with timing enabled, steps run as direct launches
  * bracketed by hipEvents; read_timing returns (and resets) the summed device
  * milliseconds and launch counts per kernel kind: 0 grouped GEMM, 1 row

@@ -20,6 +20,7 @@
 #include "gemm_operand.h"
 
 #include <algorithm>
+#include <cstddef>
 #include <cstring>
 
 namespace oac {
@@ -512,9 +513,18 @@ struct InlineRows { int r[kInlineRows]; };
 // (read in place in the kernel-argument segment: taking the address of the
 // by-value argument made the compiler copy its 1 KB into every thread's
 // scratch -- 1,028 bytes of private segment, that launch 11.7 -> 45.8 us)
-constexpr size_t kInlineRowsOff =
-    (9 * sizeof(int) + alignof(GemmBatch) - 1) / alignof(GemmBatch) * alignof(GemmBatch) +
-    sizeof(GemmBatch);
+// The kernel-argument segment lays the arguments out as this struct does
+// (each at its own alignment, in order): it mirrors gemm_small_kernel_inl's
+// parameter list, which must change with it.
+struct InlineKernArgs {
+  int total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6, tb7;
+  GemmBatch batch;
+  InlineRows ir;
+};
+constexpr size_t kInlineRowsOff = offsetof(InlineKernArgs, ir);
+static_assert(offsetof(InlineKernArgs, batch) % alignof(GemmBatch) == 0 &&
+                  kInlineRowsOff == offsetof(InlineKernArgs, batch) + sizeof(GemmBatch),
+              "inline rows must follow the batch argument directly");
 template <int NW, int GPW>
 __global__ void __launch_bounds__(64 * NW)
 gemm_small_kernel_inl(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5,

@@ -324,6 +324,7 @@ hipError_t launch_logp_sum(const LogpSumArgs& a, hipStream_t s);
 struct BatchCache {
   static constexpr int kSlots = 512;       // 1.4 MB of device memory
   static constexpr int kPerPosition = 16;  // distinct batches per launch position
+  static constexpr int kPositions = 64;    // launch positions per step (a step has <= 20)
   char* dev = nullptr;
   char* host = nullptr;   // pinned mirror: the uploads' sources, never rewritten
   int used = 0;
@@ -336,7 +337,9 @@ struct BatchCache {
 };
 
 inline const GemmBatch* BatchCache::get(const GemmBatch& b, int pos, hipStream_t s) {
-  if (failed || pos < 0) return nullptr;
+  // a position past kPositions means the caller never reset its launch index
+  // (it must be the launch's index within ONE step): no record, by value
+  if (failed || pos < 0 || pos >= kPositions) return nullptr;
   constexpr size_t sz = sizeof(GemmBatch);
   if (!dev) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;   // (no allocation under capture)

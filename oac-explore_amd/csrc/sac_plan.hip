@@ -714,6 +714,9 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
 }
 
 static int step_phase(SacPlan& p, int phase, int flags, hipStream_t s) {
+  // the launch index keys the device launch records (BatchCache): it counts
+  // the launches of ONE step, so a phase-0 call starts it again
+  if (phase == 0) p.launches = 0;
   if (p.c.kind == OAC_KIND_PARTICLE) return particle_step_phase(p, phase, flags, s);
   if (has_target_policy(p.c.kind)) return det_step_phase(p, phase, flags, s);
   switch (phase) {
@@ -1065,7 +1068,12 @@ int32_t* oac_sac_host_ring(oac_sac* h) { return h ? h->plan.host_ring : nullptr;
 // entering the chunk again (one lap later) waits for it.  A batch counter that
 // does not advance by one (another path of the trainer stepped in between, or
 // a restore) drains every reader enqueued so far: the slots are then all free.
-static int stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream, bool host_read) {
+// inline: the indices may also travel in the next direct step's layer-0 kernel
+// arguments -- only for oac_sac_step_host_idx's own step, which follows at
+// once (a public staging call may be followed by other stagings, or by a
+// caller's graph that never clears the flag; those read the host slot)
+static int stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stream, bool host_read,
+                          bool inline_ok = false) {
   if (!h) { set_error("null handle"); return 1; }
   SacPlan& p = h->plan;
   if (!p.host_ring) { set_error("oac_sac_set_host_ring first"); return 1; }
@@ -1104,7 +1112,7 @@ static int stage_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, void* stre
     dst[i] = (int32_t)v;
   }
   p.inline_ok = false;
-  if (p.rows_direct && B <= kInlineRows) {   // the direct step passes them as kernel arguments
+  if (inline_ok && p.rows_direct && B <= kInlineRows) {   // the direct step passes them as kernel arguments
     std::memcpy(p.inline_rows, dst, sizeof(int32_t) * B);
     p.inline_ok = true;
   }
@@ -1140,7 +1148,7 @@ int oac_sac_step_host_idx(oac_sac* h, const int64_t* idx, int64_t bc, int flags,
     return 0;
   }
   const bool hr = h->plan.idx_host;
-  if (stage_host_idx(h, idx, bc, stream, hr || h->plan.rows_direct)) return 1;
+  if (stage_host_idx(h, idx, bc, stream, hr || h->plan.rows_direct, true)) return 1;
   // the one-step drop-in call issues its launches directly: the same kernels
   // as the step graph, but one hipGraphLaunch per step cost more than the
   // host's 12 launch calls (same-box A/B, the bench line: B=256 10,443-10,491
@@ -1180,6 +1188,11 @@ int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows
   int id = which;
   if (which == OAC_WS_H2Q1 || which == OAC_WS_H2Q2)   // aliases of the SAC layout's buffers
     id = h->plan.c.kind == OAC_KIND_SAC ? (which == OAC_WS_H2Q1 ? W_H2Q1 : W_H2Q2) : which;
+  // the policy's hidden layers on obs: the first two internal buffers of the
+  // SAC and P-OAC layouts (W_H1P, W_H2P / X_H1P, X_H2P)
+  if (which == OAC_WS_H1P || which == OAC_WS_H2P)
+    id = (h->plan.c.kind == OAC_KIND_SAC || h->plan.c.kind == OAC_KIND_PARTICLE)
+             ? (which == OAC_WS_H1P ? W_H1P : W_H2P) : which;
   const WsBuf& w = h->plan.ws[id];
   *offset = w.off; *rows = w.rows; *cols = w.cols;
   if (which == OAC_WS_BATCH || which == OAC_WS_EPS1 || which == OAC_WS_EPS2)
@@ -1188,6 +1201,13 @@ int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows
 }
 
 int oac_sac_launch_count(oac_sac* h) { return h ? h->plan.launches : 0; }
+
+int oac_sac_cache_stats(oac_sac* h, int64_t* out) {
+  if (!h || !out) { set_error("null argument"); return 1; }
+  const BatchCache& c = h->plan.bcache;
+  out[0] = c.used; out[1] = (int64_t)c.at.size(); out[2] = c.hits; out[3] = c.misses;
+  return 0;
+}
 
 int oac_sac_set_timing(oac_sac* h, int enable) {
   if (!h) { set_error("null handle"); return 1; }

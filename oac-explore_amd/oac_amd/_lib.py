@@ -37,7 +37,9 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
 WS = {name: i for i, name in enumerate([
     "batch", "eps1", "eps2", "head1", "head2", "act1", "act2", "logp1", "logp2",
     "q1", "q2", "qn1", "qn2", "tq1", "tq2", "y", "sqe1", "sqe2", "qnew", "counts",
-    "head3", "act3", "logp_part", "h2q1", "h2q2"])}
+    "head3", "act3", "logp_part", "h2q1", "h2q2", "h1p", "h2p"])}
+# diagnostic views a library build may predate (skipped when it rejects the id)
+WS_OPTIONAL = ("h1p", "h2p")
 
 
 class SacConfig(ctypes.Structure):
@@ -115,6 +117,7 @@ _SIGS = {
                                               ctypes.POINTER(ctypes.c_int64),
                                               ctypes.POINTER(ctypes.c_int64)]),
     "oac_sac_launch_count": (ctypes.c_int, [ctypes.c_void_p]),
+    "oac_sac_cache_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "oac_sac_set_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "oac_sac_read_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),

@@ -226,8 +226,11 @@ class _ArenaTrainer(object):
         views = {}
         for name, wid in _lib.WS.items():
             off, r, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
-            check(L.oac_sac_workspace_view(h, wid, ctypes.byref(off), ctypes.byref(r),
-                                           ctypes.byref(c)))
+            rc = L.oac_sac_workspace_view(h, wid, ctypes.byref(off), ctypes.byref(r),
+                                          ctypes.byref(c))
+            if rc and name in _lib.WS_OPTIONAL:
+                continue
+            check(rc)
             views[name] = ws[off.value:off.value + r.value * c.value].view(r.value, c.value)
         p = _Plan(h, ws, views, key)
         self._plans[key] = p
