@@ -141,12 +141,10 @@ def policy_forward(obs, p, eps, deterministic=False):
                 logp=logp, eps=eps, u=u, var=var)
 
 
-def policy_backward(c, p, ga, G):
-    """Gradients of  sum(ga * a) + sum(G * logp)  w.r.t. the policy params.
-
-    ga: [B,Da] upstream grad on the tanh action, G: [B,1] upstream grad on
-    log_prob.  Derivatives of policies.py:154-160,179-190,275-279 (clamp passes
-    the gradient where LOG_SIG_MIN <= x <= LOG_SIG_MAX)."""
+def policy_head_grads(c, ga, G):
+    """Upstream gradients on the two heads' outputs (mean, raw log_std) of
+    sum(ga * a) + sum(G * logp): policies.py:154-160,179-190,275-279 (clamp
+    passes the gradient where LOG_SIG_MIN <= x <= LOG_SIG_MAX)."""
     a, std, u, var, eps = c["a"], c["std"], c["u"], c["var"], c["eps"]
     da = ga + G * (2 * a / (1 - a * a + TANH_EPS))
     dz = da * (1 - a * a) - G * (u / var)
@@ -154,6 +152,15 @@ def policy_backward(c, p, ga, G):
     dstd = dz * eps + G * (u * u * std / (var * var) - 1.0 / std)
     dls = dstd * std
     dls = dls * ((c["ls_raw"] >= LOG_SIG_MIN) & (c["ls_raw"] <= LOG_SIG_MAX))
+    return dmean, dls
+
+
+def policy_backward(c, p, ga, G):
+    """Gradients of  sum(ga * a) + sum(G * logp)  w.r.t. the policy params.
+
+    ga: [B,Da] upstream grad on the tanh action, G: [B,1] upstream grad on
+    log_prob (policy_head_grads), then the trunk's backward."""
+    dmean, dls = policy_head_grads(c, ga, G)
     hs = c["hs"]
     L = len(hs) - 1
     g = {}
@@ -333,6 +340,7 @@ class SACOracle:
         da = q_input_grad(c1n, gq * sel1, self.Q1)[:, Do:] \
             + q_input_grad(c2n, gq * (1 - sel1), self.Q2)[:, Do:]
         G = (S["alpha"] / B) * torch.ones_like(pf["logp"])
+        S["pol_up"] = (da, G)   # the policy backward's upstream gradients (parity checks)
         gp = policy_backward(pf, self.P, da, G)
         order = list(self.P.keys())
         self.pol_flat, views = self._flat(gp, order)
@@ -354,7 +362,8 @@ class SACOracle:
                          policy_loss=S["policy_loss"], alpha=S["alpha"],
                          alpha_loss=S["alpha_loss"], y=S["y"], q1=S["c1"]["q"],
                          q2=S["c2"]["q"], logp=S["pf"]["logp"], logp2=S["pf2"]["logp"],
-                         a=S["pf"]["a"], a2=S["pf2"]["a"], stats=stats)
+                         a=S["pf"]["a"], a2=S["pf2"]["a"], stats=stats,
+                         pf=S["pf"], pol_up=S["pol_up"])
         return self.last
 
     def _stats(self, q1, q2, y, pf, q_new, l1, l2, alpha, alpha_loss):
@@ -455,7 +464,8 @@ class ParticleOACOracle:
         self.last = dict(grads=dict(policy=gp, qf=gq, log_alpha=g_la), qf_losses=losses,
                          qf_loss=losses.sum(), policy_loss=policy_loss, alpha=alpha,
                          alpha_loss=alpha_loss, sorted_qs=sorted_qs, y=y, tq=tq,
-                         policy_mean=pf["mean"], policy_log_std=pf["log_std"])
+                         policy_mean=pf["mean"], policy_log_std=pf["log_std"],
+                         pf=pf, pol_up=(da, G))
         return self.last
 
 

@@ -13,6 +13,34 @@ import torch.multiprocessing as mp
 import parity
 from fixtures_lib import sac_params, synthetic_transitions
 
+def _spawn(target, args_of, world=1, n_get=1, timeout=240):
+    """Start ``world`` spawned workers target(*args_of(rank, port, q)), read
+    ``n_get`` results BEFORE joining (a worker blocks in q.put until its
+    message -- a state larger than the pipe's buffer -- is read), each read
+    bounded by ``timeout`` (a worker that dies without putting fails the test
+    instead of hanging it), then join and check every exit code."""
+    import queue as _queue
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=args_of(r, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        got = [q.get(timeout=timeout) for _ in range(n_get)]
+    except _queue.Empty:
+        for p in procs:
+            p.join(timeout=5)
+        raise AssertionError(("no result from a worker", [p.exitcode for p in procs]))
+    for p in procs:
+        p.join(timeout=timeout)
+        assert p.exitcode == 0, p.exitcode
+    return got
+
+
 pytestmark = pytest.mark.gpu
 
 Do, Da, H, BL, STEPS = 11, 3, 32, 32, 3
@@ -123,19 +151,7 @@ def test_dp_trainer_two_ranks_equals_single_gpu_on_global_batch(kind):
     alpha all-reduce between them, synchronous over gloo) -- the library code
     only the world > 1 RCCL step runs otherwise."""
     world = 2
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, kind)) for r in range(world)]
-    for p in procs:
-        p.start()
-    got = q.get()
-    for p in procs:
-        p.join(timeout=300)
-        assert p.exitcode == 0
+    got, = _spawn(_worker, lambda r, port, q: (r, world, port, q, kind), world)
     tr = _trainer(False, "sac" if kind == "sac_overlap" else kind)
     for step, (batch, e1, e2) in enumerate(_inputs(world)):
         if kind in ("goac", "ptrain"):
@@ -209,17 +225,7 @@ def test_dp_rccl_graph_capture_single_rank_equals_single_gpu(teardown, overlap, 
     transport="library": no graph -- the library issues the three RCCL
     all-reduces itself on its own communicator between its launches (the
     split schedule on its side stream), checked through the plan's trace."""
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
-    p = ctx.Process(target=_nccl_worker, args=(port, q, teardown, overlap, transport))
-    p.start()
-    p.join(timeout=150)
-    assert p.exitcode == 0, p.exitcode
-    got, n = q.get()
+    (got, n), = _spawn(_nccl_worker, lambda r, port, q: (port, q, teardown, overlap, transport))
     if transport == "torch":
         assert n == 1   # one captured graph
     else:
@@ -291,19 +297,7 @@ def test_dp_humanoid_b4096_two_ranks_equals_single_gpu_and_oracle():
     from gpu_helpers import module_tensors
     from oracle import sac_oracle as so
     world = 2
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_h_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    dp_grads0, dp_state = q.get()
-    for p in procs:
-        p.join(timeout=300)
-        assert p.exitcode == 0
+    (dp_grads0, dp_state), = _spawn(_h_worker, lambda r, port, q: (r, world, port, q), world)
     inputs = _h_inputs(world)
     tr = _h_trainer(False)
     single_grads0 = None
@@ -419,17 +413,7 @@ def test_dp_rccl_dropin_step_graph_equals_single_gpu(overlap, transport):
     attached to the handle and each train() is one library call (staging +
     graph launch); 140 steps across the staging ring's wrap equal the
     single-process drop-in step."""
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
-    p = ctx.Process(target=_nccl_dropin_worker, args=(port, q, overlap, transport))
-    p.start()
-    p.join(timeout=150)
-    assert p.exitcode == 0, p.exitcode
-    got, n_attached = q.get()
+    (got, n_attached), = _spawn(_nccl_dropin_worker, lambda r, port, q: (port, q, overlap, transport))
     assert n_attached == 1
     want = _dropin_loop(_trainer(False))
     assert parity.rel_err(got, want) < 1e-6, parity.rel_err(got, want)
@@ -441,20 +425,7 @@ def test_dp_dropin_loop_equals_device_index_path():
     world = 2
     got = {}
     for dropin in (True, False):
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-        s.close()
-        ctx = mp.get_context("spawn")
-        q = ctx.SimpleQueue()
-        procs = [ctx.Process(target=_dropin_worker, args=(r, world, port, q, dropin))
-                 for r in range(world)]
-        for p in procs:
-            p.start()
-        got[dropin] = q.get()
-        for p in procs:
-            p.join(timeout=300)
-            assert p.exitcode == 0
+        got[dropin], = _spawn(_dropin_worker, lambda r, port, q: (r, world, port, q, dropin), world)
     assert np.array_equal(got[True], got[False])
 
 
@@ -523,20 +494,8 @@ def test_dp_humanoid_b4096_two_ranks_split_schedule_dropin_equals_single_gpu_and
     from oac_amd._lib import TRACE
     from oracle import sac_oracle as so
     world, steps = 2, 2
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
-    procs = [ctx.Process(target=_h_dropin_worker, args=(r, world, port, q, steps, overlap))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    got = dict((m[0], m[1:]) for m in (q.get(), q.get()))
-    for p in procs:
-        p.join(timeout=300)
-        assert p.exitcode == 0
+    got = dict((m[0], m[1:]) for m in _spawn(
+        _h_dropin_worker, lambda r, port, q: (r, world, port, q, steps, overlap), world, n_get=2))
     dp_grads0, dp_state = got[0][1], got[0][2]
     for r in range(world):
         tr_bits = got[r][3]
@@ -598,7 +557,7 @@ def test_dp_humanoid_b4096_two_ranks_split_schedule_dropin_equals_single_gpu_and
             assert e < 1e-5, (grp, name, e)
 
 
-def _nccl_h_worker(port, q, B, steps):
+def _nccl_h_worker(port, q, B, steps, overlap):
     import faulthandler
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
@@ -612,7 +571,7 @@ def _nccl_h_worker(port, q, B, steps):
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     from oac_amd import _lib
-    tr = _h_trainer(True, force_collectives=True, force_overlap=True)
+    tr = _h_trainer(True, force_collectives=True, force_overlap=overlap)
     rb, _ = _h_replay(7)
     np.random.seed(3)
     for _ in range(steps):
@@ -626,30 +585,23 @@ def _nccl_h_worker(port, q, B, steps):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("overlap", [False, True])
 @pytest.mark.parametrize("B", [256, 4096])
-def test_dp_rccl_humanoid_split_schedule_dropin_equals_single_gpu(B):
+def test_dp_rccl_humanoid_split_schedule_dropin_equals_single_gpu(B, overlap):
     """The 8-GPU step's code over RCCL at one rank, Humanoid dims at the
     headline batch (256) and configs[3]'s (4096): the library's own
-    communicator, the three all-reduces issued between its launches, the
-    alpha exchange on the side stream beside phase 4 -- through the drop-in
-    call, against the single-process drop-in step on the same replay, index
-    stream and Philox eps."""
+    communicator, the three all-reduces issued between its launches --
+    in line (overlap False: the world > 1 default, dp.py) or with the alpha
+    exchange on the side stream beside phase 4 (overlap True) -- through the
+    drop-in call, against the single-process drop-in step on the same
+    replay, index stream and Philox eps."""
     from oac_amd._lib import TRACE
     steps = 24
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
-    p = ctx.Process(target=_nccl_h_worker, args=(port, q, B, steps))
-    p.start()
-    got, bits = q.get()   # (before the join: the state does not fit the pipe's buffer)
-    p.join(timeout=200)
-    assert p.exitcode == 0, p.exitcode
+    (got, bits), = _spawn(_nccl_h_worker, lambda r, port, q: (port, q, B, steps, overlap))
     want_bits = ("direct",) if B == 256 else BIG_BRANCHES
-    missing = [b for b in want_bits + ("exchange", "split_phase1") if not bits & TRACE[b]]
+    missing = [b for b in want_bits + ("exchange",) if not bits & TRACE[b]]
     assert not missing and not bits & TRACE["fused"], (missing, bits)
+    assert bool(bits & TRACE["split_phase1"]) == overlap, bits
     tr = _h_trainer(False)
     rb, _ = _h_replay(7)
     np.random.seed(3)

@@ -14,19 +14,25 @@ targets, log-alpha (gradient and value) and the losses are compared.
 
 Allowances, each reported by the test: elements of a post-step parameter
 whose gradient is within fp32 rounding of 0 (Adam moves them by ~lr * sign,
-bounded by 2.5 lr); at most two rows of a critic or policy hidden-layer
-gradient whose ReLU pre-activation sits within fp32 rounding of 0 for some
-sample (parity.relu_boundary_units), as in test_gpu_dp.py (the policy's on
-the observations: sac_humanoid_b4096 step 2 has a policy layer-0 unit at
-6.7e-7 rms of 0 that takes the other sign under the chunked slab order of the
-round-5 Adam launch, tools/diag_teacher_flip.py -- one fc0 row off, 2.2e-3);
-and, for a SAC critic's
-first layer, the layer-1 mask flips, which reach every fc0 row
-(_flip_adjusted: the (sample, unit) entries where the GPU's own saved layer-1
-activations -- the masks its backward used, workspace views h2q1 / h2q2 --
-disagree in sign with the oracle's are listed, each is asserted to sit within
-3e-5 rms of 0, the oracle's fc0 reference is corrected by exactly those
-entries, and the result is gated at 1e-5).
+bounded by 2.5 lr); at most two rows of a critic hidden-layer gradient whose
+ReLU pre-activation sits within fp32 rounding of 0 for some sample
+(parity.relu_boundary_units), as in test_gpu_dp.py; for a SAC critic's first
+layer, the layer-1 mask flips, which reach every fc0 row (_flip_adjusted: the
+(sample, unit) entries where the GPU's own saved layer-1 activations -- the
+masks its backward used, workspace views h2q1 / h2q2 -- disagree in sign with
+the oracle's are listed, each is asserted to sit within 3e-5 rms of 0, the
+oracle's fc0 reference is corrected by exactly those entries, and the result
+is gated at 1e-5); and the same rule for BOTH hidden layers of the policy
+(_policy_flip_adjusted, workspace views h1p / h2p), with no policy row left
+out (sac_humanoid_b4096 step 2 has a policy layer-0 unit at 6.7e-7 rms of 0
+that takes the other sign under the chunked slab order of the round-5 Adam
+launch, tools/diag_teacher_flip.py).
+
+The drop-in tests (test_*_dropin_teacher_forced) do the same on the call path
+the bench times -- ReplayBuffer.random_batch + trainer.train, i.e. host
+indices staged into the step's first launch, device Philox eps, the deferred
+layer-0 Adam -- reading each step's eps back from the plan's workspace and
+checking the in-step gather against the replay rows bit for bit.
 
 Reference: trainer/trainer.py:126-280 (SAC), trainer/particle_trainer_oac.py:
 169-363 (P-OAC), torch-1.4 Adam (trainer/trainer.py:75-91).
@@ -159,11 +165,69 @@ def _flip_adjusted(gref, cache, dq, q, opt, lr, gpu_h2, tol=3e-5):
     return out, [d[0] for d in sel]
 
 
-def _compare_group(errs, left_out, tr, mod, grp, order, opt, P, grads, lr, allowed, flip=None):
+def _policy_flip_adjusted(gref, pf, up, p, opt, lr, gpu_h1, gpu_h2, tol=3e-5):
+    """Policy trunk references under the GPU's own ReLU masks.
+
+    The critics' rule (_flip_adjusted) for both hidden layers of the policy:
+    the (layer, sample, unit) entries where the GPU's saved activations on
+    obs (workspace views h1p / h2p: the masks its policy backward used)
+    disagree in sign with the oracle's are listed, each must sit within
+    ``tol`` rms of 0, and the fc0 / fc1 references are recomputed in float64
+    under the GPU's masks (the heads' upstream gradients ``up`` = (dL/da,
+    dL/dlogp) and the pre-step weights ``p`` as the oracle had them); the
+    difference is added to the oracle's fp32 gradients and m, v and the
+    post-step parameters follow through torch-1.4 Adam.  A flipped entry's
+    activation is within rounding of 0 either way, so the heads' gradients
+    are unchanged.  Returns ({pn: (g, m, v, P)}, flipped entries)."""
+    f64 = lambda t: (t.double().numpy() if torch.is_tensor(t) else np.asarray(t, np.float64))
+    x, h1, h2 = (f64(pf["hs"][i]) for i in range(3))
+    W0, b0, W1, b1 = (f64(p[k]) for k in ("fc0.weight", "fc0.bias", "fc1.weight", "fc1.bias"))
+    pre = (x @ W0.T + b0, h1 @ W1.T + b1)
+    mo = (f64(pf["hs"][1]) > 0, f64(pf["hs"][2]) > 0)
+    mg = (np.asarray(gpu_h1) > 0, np.asarray(gpu_h2) > 0)
+    flips = []
+    for l in range(2):
+        rms = np.sqrt(np.mean(pre[l] * pre[l]))
+        fl = np.argwhere(mo[l] != mg[l])
+        far = [(l, int(s_), int(u), float(abs(pre[l][s_, u]) / rms)) for s_, u in fl
+               if abs(pre[l][s_, u]) >= tol * rms]
+        assert not far, ("policy masks differ away from 0 (layer, sample, unit, |pre| / rms)",
+                         far[:8])
+        flips += [(l, int(s_), int(u)) for s_, u in fl]
+    if not flips:
+        return {}, []
+    dmean, dls = so.policy_head_grads(pf, *up)
+    dh2 = f64(dmean) @ f64(p["last_fc.weight"]) + f64(dls) @ f64(p["last_fc_log_std.weight"])
+
+    def trunk(m1, m2):
+        d1 = dh2 * m2
+        d0 = (d1 @ W1) * m1
+        return {"fc0.weight": d0.T @ x, "fc0.bias": d0.sum(0),
+                "fc1.weight": d1.T @ h1, "fc1.bias": d1.sum(0)}
+
+    go, gg = trunk(*mo), trunk(*mg)
+    out = {}
+    t = opt.t
+    bc1, bc2 = 1 - opt.b1 ** t, 1 - opt.b2 ** t
+    for pn in go:
+        g = gref[pn].double().numpy()
+        dg = gg[pn] - go[pn]
+        m = opt.m[pn].double().numpy() + (1 - opt.b1) * dg
+        v = opt.v[pn].double().numpy() + (1 - opt.b2) * (2 * g * dg + dg * dg)
+        P = np.asarray(p[pn], np.float64) - (lr / bc1) * m / (np.sqrt(v) / np.sqrt(bc2) + opt.eps)
+        out[pn] = (g + dg, m, v, P)
+    return out, flips
+
+
+def _compare_group(errs, left_out, tr, mod, grp, order, opt, P, grads, lr, allowed, flip=None,
+                   pflip=None):
     """Gradient, Adam m / v and post-step errors of one module's parameters
     (ReLU-boundary rows as allowed; with ``flip`` = (forward cache, dq,
     pre-step params, the GPU's layer-1 activations) a critic's fc0
-    references take the GPU's layer-1 mask flips, _flip_adjusted)."""
+    references take the GPU's layer-1 mask flips, _flip_adjusted; with
+    ``pflip`` = (policy forward cache, upstream gradients, pre-step params,
+    the GPU's h1 / h2) the policy's fc0 / fc1 take its mask flips,
+    _policy_flip_adjusted)."""
     gv = module_tensors(tr, mod, tr.grads)
     mv = module_tensors(tr, mod, tr.adam_m)
     vv = module_tensors(tr, mod, tr.adam_v)
@@ -176,6 +240,12 @@ def _compare_group(errs, left_out, tr, mod, grp, order, opt, P, grads, lr, allow
         if flips:
             refs.update(adj)
             left_out[f"{grp}/layer-1 mask flips (sample, unit)"] = flips
+    if pflip is not None:
+        pfc, up, p, g1, g2 = pflip
+        adj, flips = _policy_flip_adjusted(grads, pfc, up, p, opt, lr, g1, g2)
+        if flips:
+            refs.update(adj)
+            left_out[f"{grp}/mask flips (layer, sample, unit)"] = flips
     for pn in order:
         gref, mref, vref, pref = refs[pn]
         e, bad = parity.rel_err_rows(gv[pn].cpu().numpy(), gref, allowed.get(pn, []))
@@ -197,6 +267,48 @@ def _check(errs, left_out, name, s):
     assert not bad, (name, s, sorted(bad.items(), key=lambda kv: -kv[1])[:10])
 
 
+def _views(tr, *names):
+    return [tr._last_plan.views[n].cpu().numpy() for n in names]
+
+
+def _sac_compare(tr, orc, out, pre, batch, meta, name, s):
+    """Every tensor of one SAC step against the oracle's step on the GPU's
+    pre-step state (gate TOL; allowances in the module docstring)."""
+    lr = meta["lr"]
+    h2g = dict(zip(("qf1", "qf2"), _views(tr, "h2q1", "h2q2")))
+    h1p, h2p = _views(tr, "h1p", "h2p")
+    x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
+    allowed = {grp: _boundary_rows(x0, pre[grp]) for grp in ("qf1", "qf2")}
+    B = x0.shape[0]
+    dqs = {grp: 2.0 * (orc.S[c]["q"] - orc.S["y"]) / B for grp, c in (("qf1", "c1"), ("qf2", "c2"))}
+    errs, left_out = {}, {}
+    for grp, mod, order, opt, P in (("policy", tr.policy, PARAM_ORDER_POLICY, orc.opt_p, orc.P),
+                                    ("qf1", tr.qf1, PARAM_ORDER_Q, orc.opt_q1, orc.Q1),
+                                    ("qf2", tr.qf2, PARAM_ORDER_Q, orc.opt_q2, orc.Q2)):
+        _compare_group(errs, left_out, tr, mod, grp, order, opt, P, out["grads"][grp], lr,
+                       allowed.get(grp, {}),
+                       (orc.S["c" + grp[-1]], dqs[grp], pre[grp], h2g[grp])
+                       if grp in dqs else None,
+                       (out["pf"], out["pol_up"], pre["policy"], h1p, h2p)
+                       if grp == "policy" else None)
+    for grp, mod, T in (("target_qf1", tr.target_qf1, orc.T1),
+                        ("target_qf2", tr.target_qf2, orc.T2)):
+        for pn, t in mod.state_dict().items():
+            errs[f"post/{grp}/{pn}"] = parity.rel_err(t.cpu().numpy(), T[pn].numpy())
+    if meta["auto_alpha"]:
+        a = tr.alpha_state.cpu().numpy()
+        errs["grad/log_alpha"] = parity.rel_err(a[5:6], out["grads"]["log_alpha"].numpy())
+        errs["post/log_alpha"] = parity.rel_err(a[0:1], orc.log_alpha.numpy())
+        errs["adam/log_alpha"] = parity.rel_err(a[1:3], np.concatenate(
+            [orc.opt_a.m["log_alpha"].numpy(), orc.opt_a.v["log_alpha"].numpy()]))
+    st = tr.get_diagnostics()
+    for k in ("QF1 Loss", "QF2 Loss", "Q Loss", "Policy Loss", "Alpha", "Alpha Loss",
+              "Log Pis Mean", "Q Targets Mean", "Q1 Predictions Mean"):
+        if k in out["stats"]:
+            errs[f"stat/{k}"] = parity.rel_err(st[k], out["stats"][k])
+    _check(errs, left_out, name, s)
+
+
 # every SAC fixture: each config flag (no alpha tuning, target period 2, the
 # small / stress / RiverSwim dims) through the step's fused paths at 1e-5
 @pytest.mark.parametrize("name", ["sac_humanoid", "sac_humanoid_b4096", "sac_small", "sac_stress",
@@ -204,7 +316,6 @@ def _check(errs, left_out, name, s):
 def test_sac_teacher_forced_every_step(name):
     meta, g = parity.load(name)
     tr = sac_trainer_for(meta)
-    lr = meta["lr"]
     for s in range(meta["steps"]):
         orc = sac_oracle_from_gpu(tr, meta)
         pre = {grp: _np_sd(getattr(tr, grp)) for grp in ("qf1", "qf2", "policy")}
@@ -213,37 +324,91 @@ def test_sac_teacher_forced_every_step(name):
         tr.end_epoch(s)
         tr.train_from_torch(batch, eps1=e1, eps2=e2)
         torch.cuda.synchronize()
-        h2g = {grp: tr._last_plan.views["h2q" + grp[-1]].cpu().numpy() for grp in ("qf1", "qf2")}
         out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
-        x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
-        allowed = {grp: _boundary_rows(x0, pre[grp]) for grp in ("qf1", "qf2")}
-        allowed["policy"] = _boundary_rows(batch["observations"], pre["policy"])
-        B = x0.shape[0]
-        dqs = {grp: 2.0 * (orc.S[c]["q"] - orc.S["y"]) / B for grp, c in (("qf1", "c1"), ("qf2", "c2"))}
-        errs, left_out = {}, {}
-        for grp, mod, order, opt, P in (("policy", tr.policy, PARAM_ORDER_POLICY, orc.opt_p, orc.P),
-                                        ("qf1", tr.qf1, PARAM_ORDER_Q, orc.opt_q1, orc.Q1),
-                                        ("qf2", tr.qf2, PARAM_ORDER_Q, orc.opt_q2, orc.Q2)):
-            _compare_group(errs, left_out, tr, mod, grp, order, opt, P, out["grads"][grp], lr,
-                           allowed.get(grp, {}),
-                           (orc.S["c" + grp[-1]], dqs[grp], pre[grp], h2g[grp])
-                           if grp in dqs else None)
-        for grp, mod, T in (("target_qf1", tr.target_qf1, orc.T1),
-                            ("target_qf2", tr.target_qf2, orc.T2)):
-            for pn, t in mod.state_dict().items():
-                errs[f"post/{grp}/{pn}"] = parity.rel_err(t.cpu().numpy(), T[pn].numpy())
-        if meta["auto_alpha"]:
-            a = tr.alpha_state.cpu().numpy()
-            errs["grad/log_alpha"] = parity.rel_err(a[5:6], out["grads"]["log_alpha"].numpy())
-            errs["post/log_alpha"] = parity.rel_err(a[0:1], orc.log_alpha.numpy())
-            errs["adam/log_alpha"] = parity.rel_err(a[1:3], np.concatenate(
-                [orc.opt_a.m["log_alpha"].numpy(), orc.opt_a.v["log_alpha"].numpy()]))
-        st = tr.get_diagnostics()
-        for k in ("QF1 Loss", "QF2 Loss", "Q Loss", "Policy Loss", "Alpha", "Alpha Loss",
-                  "Log Pis Mean", "Q Targets Mean", "Q1 Predictions Mean"):
-            if k in out["stats"]:
-                errs[f"stat/{k}"] = parity.rel_err(st[k], out["stats"][k])
-        _check(errs, left_out, name, s)
+        _sac_compare(tr, orc, out, pre, batch, meta, name, s)
+
+
+# ------------------------------------------------- the timed call path itself
+def _replay_for(meta):
+    """The fixture's replay (fixtures_lib.synthetic_transitions, seed 0) in an
+    oac_amd.ReplayBuffer on the GPU."""
+    from oac_amd import ReplayBuffer
+    from fixtures_lib import synthetic_transitions
+    from gpu_helpers import Space
+    n = meta["n_replay"]
+    rb = ReplayBuffer(n, Space(meta["obs_dim"]), Space(meta["act_dim"]), device="cuda:0")
+    d = synthetic_transitions(n, meta["obs_dim"], meta["act_dim"], seed=0)
+    rb.add_paths([dict(observations=d["observations"], actions=d["actions"],
+                       rewards=d["rewards"], next_observations=d["next_observations"],
+                       terminals=d["terminals"])])
+    return rb
+
+
+def _dropin_step(tr, rb, meta):
+    """One rl_algorithm.py:160-167 call (random_batch, then train) on the
+    drop-in path; returns the step's indices, host batch and the eps the
+    step drew (read back from the plan's workspace).  The batch the step
+    gathered must equal the replay rows at those indices bit for bit."""
+    B = meta["B"]
+    batch = rb.random_batch(B)
+    idx = np.array(batch.host_indices, copy=True)
+    batch["buffer"] = rb                      # rl_algorithm.py:166
+    n0 = tr._n_train_steps_total
+    tr.train(batch)
+    torch.cuda.synchronize()
+    assert tr._n_train_steps_total == n0 + 1
+    plan = tr._last_plan
+    assert plan is tr._dropin[(B, rb._storage.data_ptr())], "not the drop-in plan"
+    e1, e2 = (plan.views[k].cpu().numpy().copy() for k in ("eps1", "eps2"))
+    row = rb._storage.shape[1]
+    got = plan.views["batch"][:, :row].cpu().numpy()
+    assert np.array_equal(got, rb._storage[torch.as_tensor(idx, device=rb._storage.device)]
+                          .cpu().numpy()), "in-step gather differs from the replay rows"
+    return idx, batch_from(meta, idx), e1, e2
+
+
+@pytest.mark.parametrize("name", ["sac_humanoid", "sac_humanoid_b4096"])
+def test_sac_dropin_teacher_forced(name):
+    """The bench's timed call (rb.random_batch(B) + tr.train(batch):
+    oac_sac_step_host_idx -- indices in the first launch's arguments or the
+    host slot, device Philox eps, the deferred layer-0 Adam) at the
+    fixture's dims, every step at 1e-5 against the oracle on the GPU's own
+    pre-step state.  Reference: rl_algorithm.py:160-167, trainer.py:126-224."""
+    meta, _ = parity.load(name)
+    tr = sac_trainer_for(meta)
+    rb = _replay_for(meta)
+    np.random.seed(5)
+    for s in range(3):
+        orc = sac_oracle_from_gpu(tr, meta)
+        pre = {grp: _np_sd(getattr(tr, grp)) for grp in ("qf1", "qf2", "policy")}
+        tr.end_epoch(s)
+        idx, batch, e1, e2 = _dropin_step(tr, rb, meta)
+        assert np.all(np.isfinite(e1)) and np.std(e1) > 0.5, "eps not drawn by the step"
+        out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
+        _sac_compare(tr, orc, out, pre, batch, meta, name + "/dropin", s)
+
+
+def _particle_compare(tr, orc, out, pre, pre_p, batch, meta, name, s):
+    lr, K = meta["lr"], meta["K"]
+    h1p, h2p = _views(tr, "h1p", "h2p")
+    x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
+    allowed = {"qf": _boundary_rows(x0, pre)}
+    errs, left_out = {}, {}
+    for grp, mod, order, opt, P in (("policy", tr.policy, PARAM_ORDER_POLICY, orc.opt_p, orc.P),
+                                    ("qf", tr.qfs[0], PARAM_ORDER_Q, orc.opt_q, orc.Q)):
+        _compare_group(errs, left_out, tr, mod, grp, order, opt, P, out["grads"][grp], lr,
+                       allowed.get(grp, {}), None,
+                       (out["pf"], out["pol_up"], pre_p, h1p, h2p) if grp == "policy" else None)
+    for pn, t in tr.tfs[0].state_dict().items():
+        errs[f"post/tf/{pn}"] = parity.rel_err(t.cpu().numpy(), orc.T[pn].numpy())
+    a = tr.alpha_state.cpu().numpy()
+    errs["grad/log_alpha"] = parity.rel_err(a[5:6], out["grads"]["log_alpha"].numpy())
+    errs["post/log_alpha"] = parity.rel_err(a[0:1], orc.log_alpha.numpy())
+    st = tr.get_diagnostics()
+    for i in range(K):
+        errs[f"stat/QF{i} Loss"] = parity.rel_err(st[f"QF{i} Loss"], float(out["qf_losses"][i]))
+    errs["stat/Policy Loss"] = parity.rel_err(st["Policy Loss"], float(out["policy_loss"]))
+    _check(errs, left_out, name, s)
 
 
 @pytest.mark.parametrize("name", ["poac_ant", "poac_ant_b4096", "poac_small", "poac_counts",
@@ -252,35 +417,37 @@ def test_particle_teacher_forced_every_step(name):
     from test_gpu_particle import particle_trainer_for
     meta, g = parity.load(name)
     tr = particle_trainer_for(meta)
-    lr, K = meta["lr"], meta["K"]
     for s in range(meta["steps"]):
         orc = poac_oracle_from_gpu(tr, meta)
-        pre = _np_sd(tr.qfs[0])
-        pre_p = _np_sd(tr.policy)
+        pre, pre_p = _np_sd(tr.qfs[0]), _np_sd(tr.policy)
         batch = batch_from(meta, g[f"s{s}/idx"])
         e1, e2 = g[f"s{s}/eps1"], g[f"s{s}/eps2"]
         tr.end_epoch(s)
         tr.train_from_torch(batch, eps1=e1, eps2=e2)
         torch.cuda.synchronize()
         out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
-        x0 = np.concatenate([batch["observations"], batch["actions"]], 1)
-        allowed = {"qf": _boundary_rows(x0, pre), "policy": _boundary_rows(batch["observations"], pre_p)}
-        errs, left_out = {}, {}
-        for grp, mod, order, opt, P in (("policy", tr.policy, PARAM_ORDER_POLICY, orc.opt_p, orc.P),
-                                        ("qf", tr.qfs[0], PARAM_ORDER_Q, orc.opt_q, orc.Q)):
-            _compare_group(errs, left_out, tr, mod, grp, order, opt, P, out["grads"][grp], lr,
-                           allowed.get(grp, {}))
-        for pn, t in tr.tfs[0].state_dict().items():
-            errs[f"post/tf/{pn}"] = parity.rel_err(t.cpu().numpy(), orc.T[pn].numpy())
-        a = tr.alpha_state.cpu().numpy()
-        errs["grad/log_alpha"] = parity.rel_err(a[5:6], out["grads"]["log_alpha"].numpy())
-        errs["post/log_alpha"] = parity.rel_err(a[0:1], orc.log_alpha.numpy())
-        st = tr.get_diagnostics()
-        for i in range(K):
-            errs[f"stat/QF{i} Loss"] = parity.rel_err(st[f"QF{i} Loss"],
-                                                      float(out["qf_losses"][i]))
-        errs["stat/Policy Loss"] = parity.rel_err(st["Policy Loss"], float(out["policy_loss"]))
-        _check(errs, left_out, name, s)
+        _particle_compare(tr, orc, out, pre, pre_p, batch, meta, name, s)
+
+
+def test_particle_dropin_teacher_forced():
+    """BASELINE configs[4] (K=10 shared-head critic, Ant-v2 dims, B=4096) on
+    the bench's timed call (random_batch + train: host indices read by the
+    step's first launch, device Philox eps), every step at 1e-5 against the
+    oracle on the GPU's own pre-step state.  Reference:
+    trainer/particle_trainer_oac.py:169-363, rl_algorithm.py:160-167."""
+    from test_gpu_particle import particle_trainer_for
+    meta, _ = parity.load("poac_ant_b4096")
+    tr = particle_trainer_for(meta)
+    rb = _replay_for(meta)
+    np.random.seed(6)
+    for s in range(2):
+        orc = poac_oracle_from_gpu(tr, meta)
+        pre, pre_p = _np_sd(tr.qfs[0]), _np_sd(tr.policy)
+        tr.end_epoch(s)
+        idx, batch, e1, e2 = _dropin_step(tr, rb, meta)
+        assert np.all(np.isfinite(e1)) and np.std(e1) > 0.5, "eps not drawn by the step"
+        out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
+        _particle_compare(tr, orc, out, pre, pre_p, batch, meta, "poac_ant_b4096/dropin", s)
 
 
 # ------------------------------------------------- mid-training-state goldens
