@@ -936,11 +936,12 @@ def main():
         if not args.no_cpu_baseline and world == 1:   # the CPU baseline is an N=1 figure
             out["cpu_baseline"] = cpu_baseline(args)
             if big is not None:      # configs[2]: the same step at batch 4096
-                out["b4096"]["cpu_baseline"] = cpu_baseline(args, steps=4, warmup=2, all_runs=0,
+                # runs of >= 2 s: ~5 steps/s at one thread
+                out["b4096"]["cpu_baseline"] = cpu_baseline(args, steps=11, warmup=2, all_runs=0,
                                                             B=4096)
             if "poac_ant_b4096" in out:   # configs[4]: P-OAC K=10, Ant dims, batch 4096
-                out["poac_ant_b4096"]["cpu_baseline"] = cpu_baseline(
-                    args, steps=8, warmup=2, all_runs=0, kind="poac", B=4096, dims=(111, 8, 256))
+                out["poac_ant_b4096"]["cpu_baseline"] = cpu_baseline(   # (~12.7 steps/s: >= 2 s runs)
+                    args, steps=26, warmup=2, all_runs=0, kind="poac", B=4096, dims=(111, 8, 256))
         print(json.dumps(out), flush=True)
     if dp:
         # the trainer's teardown (its captured step graphs hold RCCL kernels),

@@ -409,6 +409,32 @@ int oac_policy_eval(const float* net, const int64_t* offsets, int obs_dim, int a
 const char* oac_last_error(void);
 int oac_abi_version(void);
 
+/* Kernel / schedule choices that are not the default, for A/B measurements
+   and the alternative-kernel parity tests (no reference counterpart).  The
+   library reads no environment variable: a process sets a choice with
+   oac_tuning_set (0 = the default) before it creates the plans that use it.
+   Returns 1 for an unknown key. */
+enum oac_tuning_key {
+  OAC_TUNE_BWDP_CFG = 0,     /* large-batch backward tile config: 9-14 (default: 12, 64x64 2-stage) */
+  OAC_TUNE_FWD_TILE_M,       /* large-batch forward tile rows: 64 / 128 (default: per launch) */
+  OAC_TUNE_FWD_TILE_N,       /* large-batch forward tile columns: 64 / 128 */
+  OAC_TUNE_FWD_NB,           /* large-batch forward LDS ring depth: 2 / 3 */
+  OAC_TUNE_SPLIT_ADAM,       /* 1: side-workgroup Adam (default), -1: one Adam launch per group */
+  OAC_TUNE_DH2_TARGETS,      /* 1: P-OAC rank-K dX in the targets kernel (default), -1: own GEMM */
+  OAC_TUNE_HEAD_CC,          /* policy-head column chunks per row block (default: by batch) */
+  OAC_TUNE_SPLITS_Q1,        /* forced split-K counts of the dW products (0: sized by the plan) */
+  OAC_TUNE_SPLITS_Q0,
+  OAC_TUNE_SPLITS_PH,
+  OAC_TUNE_SPLITS_P1,
+  OAC_TUNE_SPLITS_P0,
+  OAC_TUNE_DEBUG_CFG,        /* 1: print each GEMM launch's config and tasks to stderr */
+  OAC_TUNE_RING_PREFETCH,    /* -1: the device-ring path without the next step's critic-side
+                                forward inside the policy backward (the layer-0 Adam deferred
+                                instead, as on the drop-in path) */
+  OAC_TUNE_COUNT
+};
+int oac_tuning_set(int key, int value);
+
 #ifdef __cplusplus
 }
 #endif

@@ -37,6 +37,9 @@ namespace oac {
 enum PKind { PK_KC = 0, PK_KC_R1 = 1, PK_MN = 2, PK_MN_R1 = 3 };
 
 constexpr int kVec = 1024;   // LDS floats for a rank-1 factor indexed by k
+// consecutive tile ids per XCD: a dW's 16 (m, n) tiles of one K chunk (256 x
+// 256 at 64 x 64), a dX's 4 row blocks of 4 column tiles
+constexpr int kBwdXcdChunk = 16;
 
 template <int BM, int BN, int NB = kFBuf>
 struct BwdG {
@@ -76,20 +79,35 @@ struct PSrc {
       }
     }
   }
-  // stage kst .. kst + 31 into dst (an operand image of the stage)
-  __device__ __forceinline__ void issue(int kst, int k_hi, float* dst, int wave) const {
+  // Stages are issued in order, kst = k0, k0 + 32, ...: each lane keeps the
+  // source of its next stage and advances it by one stage per issue (a 64-bit
+  // add, not the multiply by ld the row index would take), and only a stage
+  // that reaches past k_hi takes the clamped addresses (rows k >= k_hi read
+  // row kst as a stand-in: the fix-ups zero them).
+  const float* cur[P];
+  __device__ __forceinline__ void start(int k0) {
 #pragma unroll
-    for (int q = 0; q < P; ++q) {
-      const float* src;
-      if (KC) {
-        const int k = kst + off[q];
-        src = row[q] + (k < k_hi ? k : kst);
-      } else {
-        const int k = kst + off[q];
-        src = row[q] + (long)(k < k_hi ? k : kst) * ld;
-      }
+    for (int q = 0; q < P; ++q) cur[q] = KC ? row[q] + k0 + off[q] : row[q] + (long)(k0 + off[q]) * ld;
+  }
+  // piece q of stage kst .. kst + 31 into dst (an operand image of the stage)
+  __device__ __forceinline__ void issue_one(int q, int kst, int k_hi, float* dst, int wave) const {
+    if (kst + kFK <= k_hi) {   // (wave-uniform)
+      glds16(cur[q], dst + (wave * P + q) * 256);
+    } else {
+      const int k = kst + off[q];
+      const float* src = KC ? row[q] + (k < k_hi ? k : kst) : row[q] + (long)(k < k_hi ? k : kst) * ld;
       glds16(src, dst + (wave * P + q) * 256);
     }
+  }
+  __device__ __forceinline__ void advance() {
+#pragma unroll
+    for (int q = 0; q < P; ++q) cur[q] += KC ? (long)kFK : (long)kFK * ld;
+  }
+  // the whole stage
+  __device__ __forceinline__ void issue(int kst, int k_hi, float* dst, int wave) {
+#pragma unroll
+    for (int q = 0; q < P; ++q) issue_one(q, kst, k_hi, dst, wave);
+    advance();
   }
 };
 
@@ -128,6 +146,8 @@ __device__ __forceinline__ void bwdp_pipe(const GemmTask& t, int m0, int n0, int
   PSrc<false, BN> sb;
   sa.init(AR1 ? t.a_mask : t.A, AR1 ? t.ld_mask : t.lda, m0, t.M, wave, lane);
   sb.init(t.B, t.ldb, n0, nx, wave, lane);
+  sa.start(kb0);
+  sb.start(kb0);
   const int ar = (wave >> 1) * (BM / 2) + l32, br = (wave & 1) * (BN / 2) + l32;
   // the ring's first two stages are in flight before the rank-1 factors are
   // requested, so their round trips overlap (the factors' waits also cover
@@ -244,8 +264,12 @@ __device__ __forceinline__ void bwdp_tile(const GemmBatch& batch, int ti, int lo
   GemmTask t = batch.t[ti];
   int k_lo = 0, k_hi = t.K;
   if (t.ksplit > 1) {
-    const int split = local % t.ksplit;
-    local /= t.ksplit;
+    // split-major: the (m, n) tiles of one K chunk have consecutive ids, so
+    // the XCD mapping (xcd_tile_rr) puts tiles that share that chunk's rows
+    // of both operands on one XCD, where its L2 serves the re-reads
+    const int per = ((t.M + BM - 1) / BM) * t.tiles_n;
+    const int split = local / per;
+    local -= split * per;
     k_lo = split * t.kchunk;
     k_hi = min(t.K, k_lo + t.kchunk);
     t.C += (long)split * t.slab_stride;
@@ -302,7 +326,7 @@ __device__ __forceinline__ void gemm_bwdp_body(int total_tiles, int tb1, int tb2
     adam_side_block(batch, blockIdx.x - side0, batch.side_adam);
     return;
   }
-  const int bid = xcd_tile_rr(blockIdx.x - tile0, total_tiles);
+  const int bid = xcd_tile_rr<kBwdXcdChunk>(blockIdx.x - tile0, total_tiles);
   int ti = 0;
   ti = bid >= tb1 ? 1 : ti; ti = bid >= tb2 ? 2 : ti; ti = bid >= tb3 ? 3 : ti;
   ti = bid >= tb4 ? 4 : ti; ti = bid >= tb5 ? 5 : ti; ti = bid >= tb6 ? 6 : ti;
@@ -319,8 +343,11 @@ __device__ __forceinline__ void gemm_bwdp_body(int total_tiles, int tb1, int tb2
   }
 }
 
+// waves per SIMD the registers must allow so that the 2-stage ring's LDS sets
+// the workgroups per CU: 64x64 tiles (36 KB) four, 128x64 (52 KB) three,
+// 128x128 (68 KB) two
 template <int BM, int BN, int NB>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, NB == 2 ? (BM == 128 && BN == 128 ? 2 : BM == 128 ? 3 : 4) : 1)
 gemm_bwdp_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                  const GemmBatch batch) {
   __shared__ __attribute__((aligned(16))) float lds[BwdG<BM, BN, NB>::LDS];
@@ -328,7 +355,7 @@ gemm_bwdp_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, i
 }
 // the batch in device memory (kernels.h BatchCache)
 template <int BM, int BN, int NB>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, NB == 2 ? (BM == 128 && BN == 128 ? 2 : BM == 128 ? 3 : 4) : 1)
 gemm_bwdp_kernel_dev(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                      const GemmBatchG* __restrict__ bp) {
   __shared__ __attribute__((aligned(16))) float lds[BwdG<BM, BN, NB>::LDS];
@@ -355,7 +382,7 @@ bool gemm_bwdp_supports(const GemmBatch& b) {
 }
 
 int gemm_bwdp_tile_m(int cfg) { return cfg == 10 || cfg == 12 ? 64 : 128; }
-int gemm_bwdp_tile_n(int cfg) { return cfg == 11 ? 128 : 64; }
+int gemm_bwdp_tile_n(int cfg) { return cfg == 11 || cfg == 13 ? 128 : 64; }
 
 hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCache* bc = nullptr, int pos = -1) {
   if (b.total_tiles <= 0) return hipSuccess;
@@ -374,6 +401,7 @@ hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCac
     return hipGetLastError(); }
   // cfg 12: 64x64 tiles on a 2-stage ring (36 KB of LDS: four workgroups per CU)
   OAC_BWDP(9, 128, 64, 3) OAC_BWDP(10, 64, 64, 3) OAC_BWDP(11, 128, 128, 3) OAC_BWDP(12, 64, 64, 2)
+  OAC_BWDP(13, 128, 128, 2) OAC_BWDP(14, 128, 64, 2)
 #undef OAC_BWDP
   return hipErrorInvalidValue;
 }

@@ -260,8 +260,11 @@ __device__ __forceinline__ void gemm_fwd_body(int total_tiles, int tb1, int tb2,
   PIPE_CLK(31);
 }
 
+// waves per SIMD the registers must allow so that the 2-stage ring's LDS, not
+// the VGPRs, sets the workgroups per CU (128x64: 48 KB -> three; 128x128:
+// 64 KB -> two; 64x64: four)
 template <int BM, int BN, int NB>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, NB == 2 ? (BM == 128 && BN == 128 ? 2 : BM == 128 ? 3 : 4) : 1)
 gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                 const GemmBatch batch) {
   __shared__ __attribute__((aligned(16))) float lds[NB * FwdG<BM, BN>::STAGE];
@@ -269,7 +272,7 @@ gemm_fwd_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, in
 }
 // the batch in device memory (kernels.h BatchCache)
 template <int BM, int BN, int NB>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, NB == 2 ? (BM == 128 && BN == 128 ? 2 : BM == 128 ? 3 : 4) : 1)
 gemm_fwd_kernel_dev(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                     const GemmBatchG* __restrict__ bp) {
   __shared__ __attribute__((aligned(16))) float lds[NB * FwdG<BM, BN>::STAGE];
@@ -300,22 +303,14 @@ bool gemm_fwd_supports(const GemmBatch& b) {
 }
 
 // Tiles by gemm_cfg: 6 = 128 x 128, 7 = 128 x 64, 8 = 64 x 64 (plan_common.h
-// launch_cfg picks one per launch).  OAC_FWD2_TILE = "BM,BN" forces one tile
-// for every forward launch (tile sweeps: tools/gpu_fwd3.sh).
-static int fwd_env(int which) {
-  static const char* e = getenv("OAC_FWD2_TILE");
-  if (!e) return 0;
-  if (which == 0) return atoi(e);
-  const char* c = e;
-  while (*c && *c != ',') ++c;
-  return *c ? atoi(c + 1) : 0;
-}
+// launch_cfg picks one per launch).  OAC_TUNE_FWD_TILE_M / _N force one tile
+// for every forward launch (tile sweeps).
 int gemm_fwd_tile_m(int cfg) {
-  static const int v = fwd_env(0);
+  const int v = tuning(OAC_TUNE_FWD_TILE_M);
   return v ? v : cfg == 8 ? 64 : 128;
 }
 int gemm_fwd_tile_n(int cfg) {
-  static const int v = fwd_env(1);
+  const int v = tuning(OAC_TUNE_FWD_TILE_N);
   return v ? v : cfg == 6 ? 128 : 64;
 }
 
@@ -327,8 +322,8 @@ hipError_t gemm_fwd_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCach
   const int bm = gemm_fwd_tile_m(cfg), bn = gemm_fwd_tile_n(cfg);
   // LDS ring depth: 2 for 128x64 tiles (48 KB: three workgroups per CU;
   // B=4096 SAC layer 0, 768 tiles, 65.6 -> 61.1 us), 3 otherwise (128x128 is
-  // register-bound to one workgroup per CU either way); OAC_FWD2_NB forces one
-  static const int nb_env = [] { const char* e = getenv("OAC_FWD2_NB"); return e ? atoi(e) : 0; }();
+  // register-bound to one workgroup per CU either way); OAC_TUNE_FWD_NB forces one
+  const int nb_env = tuning(OAC_TUNE_FWD_NB);
   const int nb = (nb_env == 2 || nb_env == 3) ? nb_env : (bm == 128 && bn == 64) ? 2 : 3;
   const int grid = b.total_tiles + b.rg.blocks;
   const GemmBatch* d = bc ? bc->get(b, pos, s) : nullptr;

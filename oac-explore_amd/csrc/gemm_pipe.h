@@ -64,11 +64,12 @@ __device__ __forceinline__ int xcd_tile(int bid, int n) {
 // XCDs.  Tiles [0, T), T = the largest multiple of 8 chunks, go by chunks; the
 // tail keeps its id (bijective for any grid size).
 constexpr int kXcdChunk = 4;
+template <int C = kXcdChunk>
 __device__ __forceinline__ int xcd_tile_rr(int bid, int n) {
-  const int T = n / (8 * kXcdChunk) * (8 * kXcdChunk);
+  const int T = n / (8 * C) * (8 * C);
   if (bid >= T) return bid;
   const int x = bid & 7, j = bid >> 3;
-  return ((j / kXcdChunk) * 8 + x) * kXcdChunk + j % kXcdChunk;
+  return ((j / C) * 8 + x) * C + j % C;
 }
 
 }  // namespace oac

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/oac_amd.h"
+
 namespace oac {
 
 // ---------------------------------------------------------------------------
@@ -208,6 +210,11 @@ struct AlphaState {
 
 namespace oac {
 void set_error(const char* fmt, ...);
+
+// the process's non-default kernel / schedule choices (oac_tuning_set; all 0
+// = the defaults)
+extern int g_tuning[OAC_TUNE_COUNT];
+inline int tuning(int key) { return g_tuning[key]; }
 
 // Kernel-exact timing (bench instrumentation, never inside a graph): when
 // g_ext_timing.start is set, the next OAC_LAUNCH records the pair on the

@@ -67,9 +67,9 @@ void particle_layout_workspace(SacPlan& p) {
 
 // ------------------------------------------------------------------ phases
 // the critic's backward into its last hidden layer inside the targets kernel
-// (rank-K dX of the K-output head; OAC_DH2_TARGETS=0 keeps its GEMM launch)
+// (rank-K dX of the K-output head; OAC_TUNE_DH2_TARGETS = -1 keeps its GEMM launch)
 static bool dh2_in_targets(const SacPlan& p) {
-  static const bool v = [] { const char* e = getenv("OAC_DH2_TARGETS"); return !e || atoi(e) != 0; }();
+  const bool v = tuning(OAC_TUNE_DH2_TARGETS) >= 0;
   return v && (p.c.hidden & 3) == 0;
 }
 

@@ -235,9 +235,9 @@ static inline int bwdp_cfg(const GemmBatch& gb) {
   // -> 33.0, -min Q dX 20.7 -> 19.0), and on a 2-stage ring (cfg 12: 36 KB of
   // LDS, four workgroups per CU instead of three, bitwise the same) critic
   // layer 0 dW 33.6 -> 30.2, layer 1 38.7 -> 37.8, the rest equal (round 3)
-  static const int forced = [] { const char* e = getenv("OAC_BWDP_CFG"); return e ? atoi(e) : 0; }();
+  const int forced = tuning(OAC_TUNE_BWDP_CFG);
   (void)gb;
-  return (forced >= 9 && forced <= 12) ? forced : 12;
+  return (forced >= 9 && forced <= 14) ? forced : 12;
 }
 
 static inline int launch_cfg(int cfg, const GemmBatch& gb) {
@@ -275,8 +275,7 @@ static inline int launch_cfg(int cfg, const GemmBatch& gb) {
 static inline int run_gemm(PlanBase& p, GemmBatch& gb, hipStream_t s) {
   const int cfg = launch_cfg(p.cfg, gb);
   gemm_batch_finalize(gb, cfg);
-  static const bool dbg = getenv("OAC_DEBUG_CFG") != nullptr;
-  if (dbg) {
+  if (tuning(OAC_TUNE_DEBUG_CFG)) {
     fprintf(stderr, "launch %d cfg %d tiles %d:", p.launches, cfg, gb.total_tiles);
     for (int i = 0; i < gb.ntasks; ++i)
       fprintf(stderr, " [M%d N%d K%d akc%d bkc%d r1%d epi%d S%d]", gb.t[i].M, gb.t[i].N, gb.t[i].K,

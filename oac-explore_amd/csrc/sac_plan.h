@@ -138,9 +138,9 @@ inline const int* gather_idx(const SacPlan& p, int flags) {
 // launch -- the critic's layer 1 + last layer beside its layer-0 dW, the
 // critic's layer 0 beside the -min Q dX to layer 1, the policy's layer 1 +
 // heads beside its layer-0 dW; only the policy's layer 0 keeps a launch.
-// OAC_SPLIT_ADAM=0: one Adam launch per group (A/B runs).
+// OAC_TUNE_SPLIT_ADAM = -1: one Adam launch per group (A/B runs).
 inline bool split_adam_on(const SacPlan& p) {
-  static const bool v = [] { const char* e = getenv("OAC_SPLIT_ADAM"); return !e || atoi(e) != 0; }();
+  const bool v = tuning(OAC_TUNE_SPLIT_ADAM) >= 0;
   return v && p.cfg != 0 && p.c.world_size == 1 && !can_fuse_adam(p);
 }
 // Attach the ranges [off[i], off[i] + n[i]) of `a` to batch gb as side

@@ -27,6 +27,8 @@ namespace oac {
 
 static thread_local char g_err[1024] = "";
 thread_local ExtTiming g_ext_timing;
+int g_tuning[OAC_TUNE_COUNT] = {};
+
 void set_error(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -292,7 +294,7 @@ int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long
 // (114 VGPRs: 4 waves per SIMD) run as a single round -- two chunks of 128
 // columns made 1,024 workgroups and two rounds (B=4096: 24.4 us)
 static int head_col_chunks(int B, int H) {
-  static const int forced = [] { const char* e = getenv("OAC_HEAD_CC"); return e ? atoi(e) : 0; }();
+  const int forced = tuning(OAC_TUNE_HEAD_CC);
   if (forced > 0) return forced;
   return B >= 1024 ? std::max(1, (H + 255) / 256) : std::max(1, (H + 63) / 64);
 }
@@ -693,7 +695,7 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
   const int gather_n = p.slot == 0 ? std::min(kXSlots, n - i) : 0;
   // steps after the first of a gather batch had their critic-side forward
   // issued inside the previous step's policy backward (small-batch path)
-  const bool ahead = p.cfg == 0 && (flags & OAC_STEP_GATHER);
+  const bool ahead = p.cfg == 0 && (flags & OAC_STEP_GATHER) && tuning(OAC_TUNE_RING_PREFETCH) >= 0;
   if (phase0(p, flags, s, gather_n, ahead && p.slot > 0)) return 1;
   const bool split = !fused && split_adam_on(p);
   const bool pf = ahead && i + 1 < n && p.slot + 1 < kXSlots;
@@ -814,6 +816,12 @@ extern "C" {
 const char* oac_last_error(void) { return g_err; }
 int oac_abi_version(void) { return OAC_ABI_VERSION; }
 
+int oac_tuning_set(int key, int value) {
+  if (key < 0 || key >= OAC_TUNE_COUNT) { set_error("unknown tuning key %d", key); return 1; }
+  g_tuning[key] = value;
+  return 0;
+}
+
 static int validate(const oac_sac_config* c) {
   if (!c) { set_error("null config"); return 1; }
   if (c->kind != OAC_KIND_SAC && c->kind != OAC_KIND_PARTICLE && c->kind != OAC_KIND_GAUSS &&
@@ -879,10 +887,11 @@ static void plan_splits(SacPlan& p) {
     p.sp_p1 = choose_split_pipe(c.batch, t64(H, H));
     p.sp_p0 = choose_split_pipe(c.batch, t64(H, Do));
   }
-  // OAC_SPLITS="q1,q0,ph,p1,p0": forced split counts (0 = keep), tuning runs
-  if (const char* e = getenv("OAC_SPLITS")) {
-    int v[5] = {0, 0, 0, 0, 0};
-    sscanf(e, "%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4]);
+  // forced split counts (OAC_TUNE_SPLITS_*; 0 = keep), tuning runs
+  {
+    const int v[5] = {tuning(OAC_TUNE_SPLITS_Q1), tuning(OAC_TUNE_SPLITS_Q0),
+                      tuning(OAC_TUNE_SPLITS_PH), tuning(OAC_TUNE_SPLITS_P1),
+                      tuning(OAC_TUNE_SPLITS_P0)};
     Split* sp[5] = {&p.sp_q1, &p.sp_q0, &p.sp_ph, &p.sp_p1, &p.sp_p0};
     const int bk = p.cfg == 0 ? 64 : 32;
     for (int i = 0; i < 5; ++i)

@@ -10,7 +10,8 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 # OAC_LIB: another in-tree build of the same library (same-box A/B runs of a
 # kernel change, e.g. tools/ab_lib.sh); the default is the package's own
-LIB_PATH = os.environ.get("OAC_LIB") or os.path.join(HERE, "liboac_amd.so")
+_DEFAULT_LIB = os.path.join(HERE, "liboac_amd.so")
+LIB_PATH = os.environ.get("OAC_LIB") or _DEFAULT_LIB
 
 OAC_KIND_SAC = 0
 OAC_KIND_PARTICLE = 1
@@ -38,6 +39,26 @@ WS = {name: i for i, name in enumerate([
     "batch", "eps1", "eps2", "head1", "head2", "act1", "act2", "logp1", "logp2",
     "q1", "q2", "qn1", "qn2", "tq1", "tq2", "y", "sqe1", "sqe2", "qnew", "counts",
     "head3", "act3", "logp_part", "h2q1", "h2q2", "h1p", "h2p"])}
+# non-default kernel / schedule choices (enum oac_tuning_key; A/B runs and the
+# alternative-kernel parity tests): set_tuning(bwdp_cfg=9, ...) before the
+# trainers that should use them create their plans; 0 restores a default
+TUNE = {name: i for i, name in enumerate([
+    "bwdp_cfg", "fwd_tile_m", "fwd_tile_n", "fwd_nb", "split_adam", "dh2_targets", "head_cc",
+    "splits_q1", "splits_q0", "splits_ph", "splits_p1", "splits_p0", "debug_cfg",
+    "ring_prefetch"])}
+
+
+def set_tuning(**kw):
+    for k, v in kw.items():
+        check(lib().oac_tuning_set(TUNE[k], int(v)))
+
+
+def set_tuning_spec(spec):
+    """set_tuning from "key=value,key=value" (tools' A/B scripts)."""
+    if spec:
+        set_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in spec.split(",") if kv)})
+
+
 # diagnostic views a library build may predate (skipped when it rejects the id)
 WS_OPTIONAL = ("h1p", "h2p")
 
@@ -118,6 +139,7 @@ _SIGS = {
                                               ctypes.POINTER(ctypes.c_int64)]),
     "oac_sac_launch_count": (ctypes.c_int, [ctypes.c_void_p]),
     "oac_sac_cache_stats": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "oac_tuning_set": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "oac_sac_set_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "oac_sac_read_timing": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
@@ -199,6 +221,8 @@ def lib():
     import torch  # noqa: F401  (HIP runtime first)
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in _SIGS.items():
+        if LIB_PATH != _DEFAULT_LIB and not hasattr(L, name):
+            continue   # an OAC_LIB A/B build of an older tree: its entry points only
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

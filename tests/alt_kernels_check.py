@@ -1,6 +1,6 @@
-"""Run by tests/test_gpu_altkernels.py in a child process whose environment
-selects a non-default large-batch kernel (the kernel choice is read once per
-process): the ragged large-batch parity cases of test_gpu_ragged.py (B = 1029
+"""Run by tests/test_gpu_altkernels.py in a child process that selects a
+non-default large-batch kernel (OAC_TEST_TUNING -> oac_tuning_set): the
+ragged large-batch parity cases of test_gpu_ragged.py (B = 1029
 / 1100, hidden 48 / 80) for all four trainers against the fp32 CPU oracle."""
 import os
 import sys
@@ -12,6 +12,10 @@ for p in (ROOT, os.path.join(ROOT, "oac-explore_amd"), HERE):
         sys.path.insert(0, p)
 
 import test_gpu_ragged as tr  # noqa: E402
+from oac_amd import _lib  # noqa: E402
+
+# the kernel / schedule choice of this child (oac_tuning_set), from the parent
+_lib.set_tuning_spec(os.environ.get("OAC_TEST_TUNING", ""))
 
 
 def main():

@@ -2,7 +2,7 @@
 steps (B = 1100, hidden 48 / 80) of SACTrainer and ParticleTrainerOAC with
 fixed batches and eps; the trainers' params / targets / Adam moments are
 written to the .npz path given on the command line.  The parent compares the
-side-workgroup Adam (OAC_SPLIT_ADAM, the SAC step) against one Adam
+side-workgroup Adam (tuning split_adam, the SAC step) against one Adam
 launch per group: the same adam_flat_elem on the same slabs, so bit for bit."""
 import os
 import sys
@@ -19,6 +19,10 @@ import torch  # noqa: E402
 from fixtures_lib import sac_params  # noqa: E402
 from gpu_helpers import Space, producers  # noqa: E402
 import test_gpu_ragged as tr  # noqa: E402
+from oac_amd import _lib  # noqa: E402
+
+# the kernel / schedule choice of this child (oac_tuning_set), from the parent
+_lib.set_tuning_spec(os.environ.get("OAC_TEST_TUNING", ""))
 
 
 def _run(trainer, Do, Da, B, seed):

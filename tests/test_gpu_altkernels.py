@@ -1,10 +1,12 @@
 """The large-batch kernels the default per-launch choice does not pick
-(plan_common.h launch_cfg), each in a child process whose environment forces
-it: the pipelined forward on 128x128 tiles with a
-3-stage ring (OAC_FWD2_TILE=128,128) and the pipelined backward on 128x64 /
-128x128 tiles or 64x64 on a 3-stage ring (OAC_BWDP_CFG=9 / 11 / 10), and the step-structure fallbacks
-(OAC_SPLIT_ADAM=0, OAC_DH2_TARGETS=0).  Each runs the ragged large-batch parity
-cases (tests/alt_kernels_check.py) against the fp32 CPU oracle at 1e-5."""
+(plan_common.h launch_cfg), each in a child process that forces it through
+oac_tuning_set (OAC_TEST_TUNING="key=value,..." read by the child script):
+the pipelined forward on 128x128 tiles with a 3-stage ring and the pipelined
+backward on 128x64 / 128x128 tiles (3-stage and 2-stage rings) or 64x64 on a
+3-stage ring (bwdp_cfg 9 / 11 / 13 / 14 / 10), and the step-structure
+fallbacks (one Adam launch per group, the P-OAC rank-K dX as a GEMM).  Each
+runs the ragged large-batch parity cases (tests/alt_kernels_check.py) against
+the fp32 CPU oracle at 1e-5."""
 import os
 import subprocess
 import sys
@@ -16,19 +18,22 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 VARIANTS = {
-    "fwd_128x128_bwd_128x64": {"OAC_FWD2_TILE": "128,128", "OAC_BWDP_CFG": "9"},
-    "fwd_64x64_nb3_bwd_128x128": {"OAC_FWD2_TILE": "64,64", "OAC_FWD2_NB": "3", "OAC_BWDP_CFG": "11"},
+    "fwd_128x128_bwd_128x64": "fwd_tile_m=128,fwd_tile_n=128,bwdp_cfg=9",
+    "fwd_64x64_nb3_bwd_128x128": "fwd_tile_m=64,fwd_tile_n=64,fwd_nb=3,bwdp_cfg=11",
     # the backward 64x64 tiles on the 3-stage ring (the default is the 2-stage one, cfg 12)
-    "bwd_64x64_nb3": {"OAC_BWDP_CFG": "10"},
+    "bwd_64x64_nb3": "bwdp_cfg=10",
+    # the backward 128x128 / 128x64 tiles on the 2-stage ring
+    "bwd_128x128_nb2": "bwdp_cfg=13",
+    "bwd_128x64_nb2": "bwdp_cfg=14",
     # the step-structure fallbacks: one Adam launch per group, the P-OAC
     # rank-K dX as its own GEMM launch
-    "adam_launches_dh2_gemm": {"OAC_SPLIT_ADAM": "0", "OAC_DH2_TARGETS": "0"},
+    "adam_launches_dh2_gemm": "split_adam=-1,dh2_targets=-1",
 }
 
 
 @pytest.mark.parametrize("name", list(VARIANTS))
 def test_alternative_large_batch_kernels_match_oracle(name):
-    env = dict(os.environ, **VARIANTS[name])
+    env = dict(os.environ, OAC_TEST_TUNING=VARIANTS[name])
     r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "alt_kernels_check.py")], env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, f"{name}: rc {r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
@@ -43,16 +48,16 @@ def test_side_workgroup_adam_is_bitwise_the_adam_launch(tmp_path):
     along as a control)."""
     import numpy as np
     outs = {}
-    for name, env in {"side": {"OAC_SPLIT_ADAM": "1", "OAC_DH2_TARGETS": "0"},
-                      "launch": {"OAC_SPLIT_ADAM": "0", "OAC_DH2_TARGETS": "0"},
-                      # and the policy head on two 128-column chunks per row
-                      # block (recomputed heads, 2 pairs per wave): the same
-                      # arithmetic per output, so bitwise too
-                      "head_cc2": {"OAC_SPLIT_ADAM": "1", "OAC_DH2_TARGETS": "0",
-                                   "OAC_HEAD_CC": "2"}}.items():
+    for name, spec in {"side": "split_adam=1,dh2_targets=-1",
+                       "launch": "split_adam=-1,dh2_targets=-1",
+                       # and the policy head on two 128-column chunks per row
+                       # block (recomputed heads, 2 pairs per wave): the same
+                       # arithmetic per output, so bitwise too
+                       "head_cc2": "split_adam=1,dh2_targets=-1,head_cc=2"}.items():
         out = str(tmp_path / f"{name}.npz")
         r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "split_adam_check.py"), out],
-                           env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
+                           env=dict(os.environ, OAC_TEST_TUNING=spec), capture_output=True,
+                           text=True, timeout=240)
         assert r.returncode == 0, f"{name}: rc {r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
         outs[name] = np.load(out)
     a = outs["side"]

@@ -180,3 +180,43 @@ def test_host_read_dropin_mixed_paths_across_ring_wrap():
     sa, sb = _state(a), _state(b)
     assert np.isfinite(sa).all()
     assert np.array_equal(sa, sb)
+
+
+def test_eager_phase_calls_keep_launch_records_bounded():
+    """oac_sac_step_phase (the torch-transport data-parallel path) at a
+    large batch: every step's launches reuse their device launch records
+    (kernels.h BatchCache, keyed by the launch's index within one step), so
+    100 eager steps add no records after the first and the positions stay
+    those of one step."""
+    import ctypes
+    from oac_amd import SACTrainer, _lib
+    Bb = 1024
+    pp, qp = producers(sac_params(Do, Da, [64, 64], 3, pi_init_w=0.2, q_init_w=0.1))
+    tr = SACTrainer(pp, qp, action_space=Space(Da), discount=0.99, reward_scale=1.0,
+                    policy_lr=1e-3, qf_lr=1e-3, soft_target_tau=5e-3, device="cuda:0", seed=7)
+    d = synthetic_transitions(Bb, Do, Da, seed=1)
+    tr.train_from_torch(d)   # the plan, with this batch and Philox eps in its workspace
+    torch.cuda.synchronize()
+    plan = tr._last_plan
+    L = _lib.lib()
+    sp = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    st = (ctypes.c_int64 * 4)()
+
+    def stats():
+        _lib.check(L.oac_sac_cache_stats(plan.handle, st))
+        return list(st)
+
+    def step():
+        for ph in (0, 1, 2, 3):
+            _lib.check(L.oac_sac_step_phase(plan.handle, ph, _lib.OAC_STEP_DEVICE_EPS, sp))
+
+    step()
+    torch.cuda.synchronize()
+    used0, pos0, _, _ = stats()
+    for _ in range(100):
+        step()
+    torch.cuda.synchronize()
+    used, pos, hits, misses = stats()
+    print("launch records: used %d positions %d hits %d misses %d" % (used, pos, hits, misses))
+    assert used == used0 and pos == pos0 and 0 < pos <= 32 and used <= 64
+    assert torch.isfinite(tr.params).all()

@@ -26,6 +26,9 @@ def main():
     sys.argv = [sys.argv[0], "--no-cpu-baseline", "--batch", str(a.batch)]
     import bench
     from oac_amd import _lib
+    # OAC_TUNE="key=value,...": non-default kernel choices (oac_tuning_set)
+    if hasattr(_lib.lib(), "oac_tuning_set"):   # (older A/B builds read OAC_* env switches)
+        _lib.set_tuning_spec(os.environ.get("OAC_TUNE", ""))
     args = bench.parse()
     dev = torch.device("cuda", 0)
     if a.poac:   # the trainer and replay of bench.poac_ant_leg

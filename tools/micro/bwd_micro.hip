@@ -143,6 +143,30 @@ int main(int argc, char** argv) {
     bs.push_back(g); names.push_back("policy L0 dW");
     fl.push_back(2.0 * H * (Do + 1) * B);
   }
+  {  // configs[4] (P-OAC, Ant dims, K = 10 heads): critic layer-0 dW over [obs | act]
+     // beside the K-head last layer's dW (its 10 rows in one 64-row tile)
+    const int Do4 = 111, Da4 = 8, K4 = 10, RS4 = 240;
+    GemmBatch g; memset(&g, 0, sizeof(g));
+    g.t[g.ntasks++] = t_dw(dh1, H, H, B, X, RS4, Do4 + Da4, 32);
+    g.t[g.ntasks++] = t_dw(dh2, K4, K4, B, h2, H, H, 16);
+    bs.push_back(g); names.push_back("poac L0 dW + K-head dW");
+    fl.push_back(2.0 * H * (Do4 + Da4 + 1) * B + 2.0 * K4 * (H + 1) * B);
+  }
+  // concurrency probe: the critic layer-1 dW (rank-1 seeded, 16 K chunks)
+  // alone at 1 / 2 / 3 / 4 copies = 256 / 512 / 768 / 1,024 workgroups, so
+  // one launch fills 1 / 2 / 3 / 4 workgroups per CU: the per-stage cycles
+  // show whether a stage is bound by the workgroup's own latency chain (flat)
+  // or by a resource the co-resident workgroups share (growing with them)
+  static char nm[4][48];
+  for (int copies = 1; copies <= 4; ++copies) {
+    GemmBatch g; memset(&g, 0, sizeof(g));
+    for (int i = 0; i < copies; ++i) {
+      GemmTask t = t_dw(nullptr, 0, H, B, h1, H, H, 16); rank1(t, dq, wl, h2, H); g.t[g.ntasks++] = t;
+    }
+    snprintf(nm[copies - 1], 48, "occupancy: dW1 x%d (%d wgs)", copies, 256 * copies);
+    bs.push_back(g); names.push_back(nm[copies - 1]);
+    fl.push_back(copies * 2.0 * H * (H + 1) * B);
+  }
   int bad = 0;
   for (size_t k = 0; k < bs.size(); ++k) {
     const double t5 = run(bs[k], cfg_ref, s, 30);

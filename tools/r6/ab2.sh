@@ -15,11 +15,11 @@ for r in $(seq 1 ${ROUNDS:-2}); do
   done
   for vc in $STEP; do
     v=${vc%%:*}; c=${vc##*:}
-    OAC_BWDP_CFG=$c OAC_LIB=$R/tools/r6/libs/$v/liboac_amd.so timeout -k 10 150 python tools/launch_times.py --batch 4096 --rate-steps 600 > $O/s_${v}_${c}_$r.txt 2>&1; crash $?
+    OAC_BWDP_CFG=$c OAC_TUNE=bwdp_cfg=$c OAC_LIB=$R/tools/r6/libs/$v/liboac_amd.so timeout -k 10 150 python tools/launch_times.py --batch 4096 --rate-steps 600 > $O/s_${v}_${c}_$r.txt 2>&1; crash $?
     echo "b4096 $v cfg$c r$r: $(grep drop-in $O/s_${v}_${c}_$r.txt | cut -c1-60)"
     grep "launch " $O/s_${v}_${c}_$r.txt | awk '{printf "%s ", $4}'; echo
     if [ -n "$POAC" ]; then
-      OAC_BWDP_CFG=$c OAC_LIB=$R/tools/r6/libs/$v/liboac_amd.so timeout -k 10 150 python tools/launch_times.py --batch 4096 --poac --rate-steps 600 > $O/p_${v}_${c}_$r.txt 2>&1; crash $?
+      OAC_BWDP_CFG=$c OAC_TUNE=bwdp_cfg=$c OAC_LIB=$R/tools/r6/libs/$v/liboac_amd.so timeout -k 10 150 python tools/launch_times.py --batch 4096 --poac --rate-steps 600 > $O/p_${v}_${c}_$r.txt 2>&1; crash $?
       echo "poac $v cfg$c r$r: $(grep drop-in $O/p_${v}_${c}_$r.txt | cut -c1-60)"
       grep "launch " $O/p_${v}_${c}_$r.txt | awk '{printf "%s ", $4}'; echo
     fi
