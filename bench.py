@@ -919,8 +919,11 @@ def main():
         if world == 1 and not args.no_extras:
             out["launches"] = launch_breakdown(tr, rb, B)
             out["hbm_subkernels"] = standalone_hbm(rb, device)
+            # (the device-ring path, train_from_ring, is no longer a default
+            # leg: in the drop-in step's form it runs ~8 % below the drop-in
+            # loop -- 11,100 against 12,000 steps/s on one box, round 6,
+            # tools/r6/ring_ab.sh; `--mode ring` times it)
             if args.mode == "dropin":
-                out["ring"] = ring_timing(tr, stream, rb, B)
                 if not dp:
                     try:
                         out["dp1"] = dp1_leg(args, rb, device, B, value)

@@ -428,9 +428,12 @@ enum oac_tuning_key {
   OAC_TUNE_SPLITS_P1,
   OAC_TUNE_SPLITS_P0,
   OAC_TUNE_DEBUG_CFG,        /* 1: print each GEMM launch's config and tasks to stderr */
-  OAC_TUNE_RING_PREFETCH,    /* -1: the device-ring path without the next step's critic-side
-                                forward inside the policy backward (the layer-0 Adam deferred
-                                instead, as on the drop-in path) */
+  OAC_TUNE_RING_DIRECT,      /* -1: the device-ring small-batch path through a gather launch per
+                                8 steps instead of each step's layer-0 launch reading its rows
+                                through the device index ring (the drop-in path's form) */
+  OAC_TUNE_RING_PREFETCH,    /* 1: on that gather-launch path, the next step's critic-side
+                                forward inside the policy backward (instead of the deferred
+                                layer-0 Adam) */
   OAC_TUNE_COUNT
 };
 int oac_tuning_set(int key, int value);

@@ -36,6 +36,9 @@ namespace oac {
 
 enum PKind { PK_KC = 0, PK_KC_R1 = 1, PK_MN = 2, PK_MN_R1 = 3 };
 
+#ifndef OAC_NOPA_GUARD
+#define OAC_NOPA_GUARD
+#endif
 constexpr int kVec = 1024;   // LDS floats for a rank-1 factor indexed by k
 // consecutive tile ids per XCD: a dW's 16 (m, n) tiles of one K chunk (256 x
 // 256 at 64 x 64), a dX's 4 row blocks of 4 column tiles
@@ -91,7 +94,7 @@ struct PSrc {
   }
   // piece q of stage kst .. kst + 31 into dst (an operand image of the stage)
   __device__ __forceinline__ void issue_one(int q, int kst, int k_hi, float* dst, int wave) const {
-    if (kst + kFK <= k_hi) {   // (wave-uniform)
+    if (OAC_NOPA_GUARD kst + kFK <= k_hi) {   // (wave-uniform)
       glds16(cur[q], dst + (wave * P + q) * 256);
     } else {
       const int k = kst + off[q];

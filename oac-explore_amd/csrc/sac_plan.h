@@ -24,6 +24,7 @@ struct SacPlan : PlanBase {
   Split sp_q0, sp_q1, sp_ql, sp_p0, sp_p1, sp_ph;
   int S_q = 1, S_p = 1;   // slab counts per group (max over the group's dW tasks)
   int slot = 0;           // batch / eps slot of the step being issued
+  bool ring_direct = false;   // device-ring step: layer 0 reads its rows through the index ring
   // the step being issued gathers directly at large batch (phase0 sets it;
   // phase1's fresh-action critic launch then carries the batch copy)
   bool direct_big = false;

@@ -307,8 +307,8 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
   float* X = p.X();
   // direct drop-in step: the layer-0 launch reads the batch rows through the
   // host-written index slot and its side blocks do the gather's copy + eps
-  const bool direct = p.rows_direct && p.cfg == 0 && gather_n == 1 && !critic_done &&
-                      (flags & OAC_STEP_GATHER) && p.b.ring_slots > 0;
+  const bool direct = (p.rows_direct || p.ring_direct) && p.cfg == 0 && gather_n == 1 &&
+                      !critic_done && (flags & OAC_STEP_GATHER) && p.b.ring_slots > 0;
   // the same at large batch: the LDS-DMA forward kernel stages layer 0's rows
   // straight from the replay through the step's index slot, and side
   // workgroups of that launch copy the batch and draw eps (gemm_fwd.hip;
@@ -344,7 +344,8 @@ static int phase0(SacPlan& p, int flags, hipStream_t s, int gather_n = 1, bool c
     if (direct) {
       for (int i = 0; i < gb.ntasks; ++i) gb.t[i].a_rows = 1;
       RowGather& g = gb.rg;
-      g.ring = p.host_ring; g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
+      g.ring = p.rows_direct ? p.host_ring : gather_idx(p, flags);
+      g.slots = p.b.ring_slots; g.B = B; g.state = p.state();
       g.replay = p.b.replay; g.row_stride = RS; g.out = X;
       // the staged indices in the kernel arguments (not under capture: a
       // captured launch would replay this step's indices)
@@ -691,11 +692,20 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
   p.launches = 0;
   const bool fused = can_fuse_adam(p);
   if (fused) p.trace |= OAC_TRACE_FUSED;
-  p.slot = i % kXSlots;
-  const int gather_n = p.slot == 0 ? std::min(kXSlots, n - i) : 0;
+  // the small-batch device-ring step in the drop-in step's form: its layer-0
+  // launch reads the rows through the device index ring (side blocks copy the
+  // batch and draw eps), no gather launch, no prefetch; same-box A/B against
+  // the gather launch per 8 steps with the next step's critic forward inside
+  // the policy backward: see DESIGN.md section 5
+  p.ring_direct = p.cfg == 0 && !p.rows_direct && (flags & OAC_STEP_GATHER) &&
+                  p.c.kind == OAC_KIND_SAC && p.b.ring_slots > 0 && tuning(OAC_TUNE_RING_DIRECT) >= 0;
+  p.slot = p.ring_direct ? 0 : i % kXSlots;
+  const int gather_n = p.ring_direct ? 1 : p.slot == 0 ? std::min(kXSlots, n - i) : 0;
   // steps after the first of a gather batch had their critic-side forward
-  // issued inside the previous step's policy backward (small-batch path)
-  const bool ahead = p.cfg == 0 && (flags & OAC_STEP_GATHER) && tuning(OAC_TUNE_RING_PREFETCH) >= 0;
+  // issued inside the previous step's policy backward (small-batch path;
+  // measured slower than deferring the layer-0 Adam: off unless tuned on)
+  const bool ahead = !p.ring_direct && p.cfg == 0 && (flags & OAC_STEP_GATHER) &&
+                     tuning(OAC_TUNE_RING_PREFETCH) > 0;
   if (phase0(p, flags, s, gather_n, ahead && p.slot > 0)) return 1;
   const bool split = !fused && split_adam_on(p);
   const bool pf = ahead && i + 1 < n && p.slot + 1 < kXSlots;
@@ -712,6 +722,7 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
     p.launches++;
   }
   p.slot = 0;
+  p.ring_direct = false;
   return 0;
 }
 

@@ -45,7 +45,7 @@ WS = {name: i for i, name in enumerate([
 TUNE = {name: i for i, name in enumerate([
     "bwdp_cfg", "fwd_tile_m", "fwd_tile_n", "fwd_nb", "split_adam", "dh2_targets", "head_cc",
     "splits_q1", "splits_q0", "splits_ph", "splits_p1", "splits_p0", "debug_cfg",
-    "ring_prefetch"])}
+    "ring_direct", "ring_prefetch"])}
 
 
 def set_tuning(**kw):

@@ -49,6 +49,24 @@ def test_ring_steps_independent_of_call_split():
     np.testing.assert_array_equal(a, c)
 
 
+@pytest.mark.parametrize("prefetch", [0, 1])
+def test_ring_direct_rows_equal_the_gather_launch_path(prefetch):
+    """The small-batch ring step's default form -- layer 0 reading its rows
+    through the device index ring, side blocks copying the batch and drawing
+    eps (the drop-in step's form) -- against the gather launch per 8 steps
+    (tuning ring_direct=-1), with and without the next step's critic forward
+    inside the policy backward (ring_prefetch): bitwise equal states."""
+    from oac_amd import _lib
+    a = _run([16, 8, 4, 2, 1, 1])
+    try:
+        _lib.set_tuning(ring_direct=-1, ring_prefetch=prefetch)
+        b = _run([16, 8, 4, 2, 1, 1])
+    finally:
+        _lib.set_tuning(ring_direct=0, ring_prefetch=0)
+    assert np.isfinite(a).all()
+    np.testing.assert_array_equal(a, b)
+
+
 # ------------------------------------------- counts=True trainers on the ring
 def _counts_trainer(kind):
     from fixtures_lib import goac_params, ptrain_params

@@ -69,14 +69,21 @@ static void rank1(GemmTask& t, const float* s, const float* v, const float* mask
   t.a_mode = A_RANK1_MASK; t.a_s = s; t.a_v = v; t.a_mask = mask; t.ld_mask = ldm;
 }
 
+// OAC_MICRO_DEVREC=1: the launch records in device memory (kernels.h
+// BatchCache), as the trainers' plans pass them (gemm_bwdp_kernel_dev)
+static BatchCache g_bc;
+static int g_pos = 0;
+static const bool g_devrec = getenv("OAC_MICRO_DEVREC") != nullptr;
 static double run(const GemmBatch& b0, int cfg, hipStream_t s, int reps) {
   GemmBatch b = b0;
   gemm_batch_finalize(b, cfg);
-  CK(gemm_batch_launch(b, cfg, s));
+  const int pos = g_pos++;
+  BatchCache* bc = g_devrec ? &g_bc : nullptr;
+  CK(gemm_batch_launch(b, cfg, s, bc, pos));
   CK(hipStreamSynchronize(s));
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   CK(hipEventRecord(e0, s));
-  for (int i = 0; i < reps; ++i) CK(gemm_batch_launch(b, cfg, s));
+  for (int i = 0; i < reps; ++i) CK(gemm_batch_launch(b, cfg, s, bc, pos));
   CK(hipEventRecord(e1, s)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1));
   return 1e3 * ms / reps;
