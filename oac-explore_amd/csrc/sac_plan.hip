@@ -905,13 +905,15 @@ static void plan_splits(SacPlan& p) {
                       tuning(OAC_TUNE_SPLITS_P0)};
     Split* sp[5] = {&p.sp_q1, &p.sp_q0, &p.sp_ph, &p.sp_p1, &p.sp_p0};
     const int bk = p.cfg == 0 ? 64 : 32;
+    bool forced = false;
     for (int i = 0; i < 5; ++i)
       if (v[i] > 0) {
         int kc = (c.batch + v[i] - 1) / v[i];
         kc = ((kc + bk - 1) / bk) * bk;
         *sp[i] = Split{(c.batch + kc - 1) / kc, kc};
+        forced = true;
       }
-    p.sp_ql = p.sp_q1;
+    if (forced) p.sp_ql = p.sp_q1;   // (only then: the plan's own sp_ql choice stands otherwise)
   }
   p.S_q = std::max(std::max(p.sp_q0.S, p.sp_q1.S), p.sp_ql.S);
   p.S_p = std::max(std::max(p.sp_p0.S, p.sp_p1.S), p.sp_ph.S);
