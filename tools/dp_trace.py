@@ -40,6 +40,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--show", default=None)
+    ap.add_argument("--overlap", action="store_true",
+                    help="the alpha exchange on the side stream (force_overlap)")
     a = ap.parse_args()
     if a.show:
         show(a.show)
@@ -70,7 +72,7 @@ def main():
                                     reward_scale=1.0, policy_lr=3e-4, qf_lr=3e-4,
                                     soft_target_tau=5e-3, target_update_period=1,
                                     use_automatic_entropy_tuning=True, device=dev, seed=2,
-                                    force_collectives=True) as tr:
+                                    force_collectives=True, force_overlap=a.overlap) as tr:
             np.random.seed(1)
             run = bench.dropin_run(tr, rb, args.batch)
             run(a.steps)

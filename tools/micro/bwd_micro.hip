@@ -164,14 +164,14 @@ int main(int argc, char** argv) {
   // one launch fills 1 / 2 / 3 / 4 workgroups per CU: the per-stage cycles
   // show whether a stage is bound by the workgroup's own latency chain (flat)
   // or by a resource the co-resident workgroups share (growing with them)
-  static char nm[4][48];
-  for (int copies = 1; copies <= 4; ++copies) {
+  static char nm[8][48];
+  for (int copies : {1, 2, 3, 4, 6, 8}) {
     GemmBatch g; memset(&g, 0, sizeof(g));
     for (int i = 0; i < copies; ++i) {
       GemmTask t = t_dw(nullptr, 0, H, B, h1, H, H, 16); rank1(t, dq, wl, h2, H); g.t[g.ntasks++] = t;
     }
     snprintf(nm[copies - 1], 48, "occupancy: dW1 x%d (%d wgs)", copies, 256 * copies);
-    bs.push_back(g); names.push_back(nm[copies - 1]);
+    bs.push_back(g); names.push_back(nm[copies - 1]);   // (x6 / x8: 1.5 / 2 rounds)
     fl.push_back(copies * 2.0 * H * (H + 1) * B);
   }
   int bad = 0;
