@@ -665,10 +665,10 @@ def _launches(tr):
     return _lib.lib().oac_sac_launch_count(tr._last_plan.handle)
 
 
-def rocprof_gemm_avg(key, round_dir="r05"):
+def rocprof_gemm_avg(key, round_dir="r06"):
     """(average GEMM launch us, path) from the committed rocprofv3 summary of
     this workload (tools/prof_summary.py output), or None."""
-    for rd in (round_dir, "r04"):   # the newest round's summary, else the previous one
+    for rd in (round_dir, "r05"):   # the newest round's summary, else the previous one
         path = os.path.join("profiles", rd, {256: "b256", 4096: "b4096"}.get(key, str(key))
                             + "_gemm_avg.txt")
         try:
