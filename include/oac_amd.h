@@ -265,6 +265,7 @@ int oac_rccl_allreduce(void* rccl, float* buf, int64_t n, void* stream);
 #define OAC_TRACE_SPLIT_PHASE1  32   /* phase 1 issued as 4 + 5 (the overlapped alpha exchange) */
 #define OAC_TRACE_FUSED         64   /* the single-process fused-Adam step */
 #define OAC_TRACE_EXCHANGE      128  /* data-parallel exchanges issued through the hook */
+#define OAC_TRACE_LA_ADAM       256  /* large batch: policy layer-0 Adam by last arrival (no launch) */
 int oac_sac_trace(oac_sac* h, int reset);
 
 int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows, int64_t* cols);
@@ -415,7 +416,7 @@ int oac_abi_version(void);
    oac_tuning_set (0 = the default) before it creates the plans that use it.
    Returns 1 for an unknown key. */
 enum oac_tuning_key {
-  OAC_TUNE_BWDP_CFG = 0,     /* large-batch backward tile config: 9-14 (default: 12, 64x64 2-stage) */
+  OAC_TUNE_BWDP_CFG = 0,     /* large-batch backward tile config: 9-15, 17 (default: 12, 64x64 2-stage) */
   OAC_TUNE_FWD_TILE_M,       /* large-batch forward tile rows: 64 / 128 (default: per launch) */
   OAC_TUNE_FWD_TILE_N,       /* large-batch forward tile columns: 64 / 128 */
   OAC_TUNE_FWD_NB,           /* large-batch forward LDS ring depth: 2 / 3 */
@@ -434,6 +435,8 @@ enum oac_tuning_key {
   OAC_TUNE_RING_PREFETCH,    /* 1: on that gather-launch path, the next step's critic-side
                                 forward inside the policy backward (instead of the deferred
                                 layer-0 Adam) */
+  OAC_TUNE_LA_ADAM,          /* 1: the large-batch SAC step's policy layer-0 Adam by the last
+                                arrival of each dW tile (no Adam launch) */
   OAC_TUNE_COUNT
 };
 int oac_tuning_set(int key, int value);

@@ -97,6 +97,7 @@ __device__ __forceinline__ void epi_run(const GemmTask& t, int mw, int nw,
           case EPI_STORE: t.C[o] = v; break;
           case EPI_GRAD:
             if (t.b_ones && n == N - 1) t.bias_grad[m] = v;
+            else if (t.wt) __hip_atomic_store(t.C + o, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else t.C[o] = v;
             break;
           case EPI_BIAS: t.C[o] = v + bias; break;

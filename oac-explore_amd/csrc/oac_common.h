@@ -79,6 +79,7 @@ struct GemmTask {
   const float* ex[6];   // extra epilogue operands (EPI_HEAD_BWD)
   int a_rows;           // small kernel: A (and U) row m is row batch.rg rows[m] of the buffer
   int no_adam;          // EPI_GRAD in a fused-Adam batch: store the gradient only (another group's)
+  int wt;               // EPI_GRAD: write-through (agent-scope) stores, read by a last arrival
 };
 
 struct StepState;
@@ -107,6 +108,7 @@ struct AdamArgs {
 };
 
 constexpr int kMaxTasks = 8;
+constexpr int kLaTickets = 4096;   // GemmBatch::la_ticket entries
 
 // The layer-0 launch of a direct drop-in step (small kernel, sac_plan phase0):
 // the batch's rows are read straight from the replay through the host-written
@@ -153,6 +155,16 @@ struct GemmBatch {
   // side_first: the side workgroups are blockIdx [0, side_adam) (a multiple
   // of 8, so every tile keeps its XCD), dispatched ahead of the tiles.
   int side_adam, side_book, side_first;
+  // Last-arrival optimizer (gemm_bwdp.hip, la_adam != 0): the split-K dW
+  // tasks marked wt store their slabs write-through, and the workgroup that
+  // finishes a dW tile last (an agent-scope ticket per (m, n) tile in
+  // la_ticket[tile_begin + tile], re-armed by that workgroup) sums the
+  // tile's t.ksplit slabs in adam_flat_kernel's fixed order and applies
+  // `adam` (+ Polyak) to the tile's elements -- the group's Adam launch for
+  // those elements, without the launch; la_book: the (0, 0) tile's last
+  // arrival also does the adam.state / adam.alpha bookkeeping
+  unsigned* la_ticket;        // kLaTickets of them (a launch's tiles: at most that many)
+  int la_adam, la_book;
   RowGather rg;              // rg.ring != null: direct row gather (small kernel only)
 };
 

@@ -237,7 +237,7 @@ static inline int bwdp_cfg(const GemmBatch& gb) {
   // layer 0 dW 33.6 -> 30.2, layer 1 38.7 -> 37.8, the rest equal (round 3)
   const int forced = tuning(OAC_TUNE_BWDP_CFG);
   (void)gb;
-  return (forced >= 9 && forced <= 14) ? forced : 12;
+  return (forced >= 9 && forced <= 17 && forced != 16) ? forced : 12;
 }
 
 static inline int launch_cfg(int cfg, const GemmBatch& gb) {

@@ -13,6 +13,7 @@ constexpr int kMaxWs = 128;
 // kXSlots consecutive steps (slot i % kXSlots is step i's batch)
 constexpr int kXSlots = 8;
 // split-K weight-gradient slabs shaped like the critic / policy arena ranges
+constexpr int WS_TICKETS = kMaxWs - 3;   // last-arrival Adam tickets (GemmBatch::la_ticket), zeroed
 constexpr int WS_GSLAB_Q = kMaxWs - 2;
 constexpr int WS_GSLAB_P = kMaxWs - 1;
 
@@ -24,7 +25,8 @@ struct SacPlan : PlanBase {
   Split sp_q0, sp_q1, sp_ql, sp_p0, sp_p1, sp_ph;
   int S_q = 1, S_p = 1;   // slab counts per group (max over the group's dW tasks)
   int slot = 0;           // batch / eps slot of the step being issued
-  bool ring_direct = false;   // device-ring step: layer 0 reads its rows through the index ring
+  bool ring_direct = false;
+  bool la_now = false;        // run_step: the policy layer-0 Adam by last arrival (no Adam launch)   // device-ring step: layer 0 reads its rows through the index ring
   // the step being issued gathers directly at large batch (phase0 sets it;
   // phase1's fresh-action critic launch then carries the batch copy)
   bool direct_big = false;
@@ -143,6 +145,12 @@ inline const int* gather_idx(const SacPlan& p, int flags) {
 inline bool split_adam_on(const SacPlan& p) {
   const bool v = tuning(OAC_TUNE_SPLIT_ADAM) >= 0;
   return v && p.cfg != 0 && p.c.world_size == 1 && !can_fuse_adam(p);
+}
+// With the split Adam: the policy layer 0's own Adam by the last arrival of
+// each of its dW tiles (GemmBatch::la_adam) instead of the step's last launch.
+// OAC_TUNE_LA_ADAM = 1 (A/B runs).
+inline bool la_adam_on(const SacPlan& p) {
+  return tuning(OAC_TUNE_LA_ADAM) > 0 && p.cfg == kCfgLargeBatch && p.c.world_size == 1;
 }
 // Attach the ranges [off[i], off[i] + n[i]) of `a` to batch gb as side
 // workgroups when gb runs on gemm_bwdp; otherwise launch them now, one Adam

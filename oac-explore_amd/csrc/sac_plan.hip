@@ -100,6 +100,7 @@ static void layout_workspace(SacPlan& p) {
   if (can_fuse_adam(p)) set(W_QSHADOW, 1, p.L.n_critics * p.L.q_size);   // (same indexing as the group)
   if (p.S_q > 1) set(WS_GSLAB_Q, p.S_q, p.L.n_critics * p.L.q_size);
   if (p.S_p > 1) set(WS_GSLAB_P, p.S_p, p.L.pol_size);
+  if (p.cfg == kCfgLargeBatch) set(WS_TICKETS, 1, kLaTickets);
   int64_t off = 0;
   for (int i = 0; i < kMaxWs; ++i) {
     p.ws[i].off = off;
@@ -256,7 +257,7 @@ static void add_dw0_side_adam(SacPlan& p, GemmBatch& gb) {
 int side_adam(SacPlan& p, GemmBatch& gb, const AdamArgs& a, int nseg, const long* off,
               const long* n, bool book, hipStream_t s) {
   const int cfg = launch_cfg(p.cfg, gb);
-  if (cfg >= 9 && cfg <= 12 && nseg <= 2) {
+  if (((cfg >= 9 && cfg <= 12) || cfg == 15 || cfg == 17) && nseg <= 2) {
     // one float4 per thread, dispatched after the tiles (B=4096 SAC, same
     // box: one Adam launch per group 3,429 steps/s; side blocks after the
     // tiles, 32 per launch 3,186 -- the side work became the launch's tail --,
@@ -678,6 +679,17 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
       AdamArgs a = policy_adam(p, 0, nullptr);
       a.S = std::max(p.sp_p1.S, p.sp_ph.S);
       if (side_adam(p, gb, a, 1, off, n, false, s)) return 1;
+      // and layer 0's own Adam by its tiles' last arrivals (GemmBatch::la_adam),
+      // when this launch runs on gemm_bwdp with the side workgroups attached
+      // (gb.adam is then the policy group's; otherwise run_step launches it)
+      if (p.la_now && gb.side_adam == 0) p.la_now = false;
+      if (p.la_now) {
+        p.trace |= OAC_TRACE_LA_ADAM;
+        gb.t[0].wt = 1;
+        gb.la_adam = 1;
+        gb.la_book = 1;   // (the side workgroups do none)
+        gb.la_ticket = reinterpret_cast<unsigned*>(p.W(WS_TICKETS));
+      }
     }
     if (run_gemm(p, gb, s)) return 1;
   }
@@ -708,6 +720,7 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
                      tuning(OAC_TUNE_RING_PREFETCH) > 0;
   if (phase0(p, flags, s, gather_n, ahead && p.slot > 0)) return 1;
   const bool split = !fused && split_adam_on(p);
+  p.la_now = split && la_adam_on(p);
   const bool pf = ahead && i + 1 < n && p.slot + 1 < kXSlots;
   const bool defer = !pf;
   if (phase1(p, s, fused, 0, split, defer)) return 1;
@@ -715,12 +728,13 @@ static int run_step(SacPlan& p, int flags, hipStream_t s, int i = 0, int n = 1) 
   if (phase2(p, s, fused, pf ? p.W(OAC_WS_BATCH) + (long)(p.slot + 1) * c_batch_rows(p) : nullptr,
              split, defer))
     return 1;
-  if (!fused) {
+  if (!fused && !p.la_now) {
     AdamArgs a = policy_adam(p, 0, nullptr);
     if (split) { a.n = p.L.pol_fc1_w; a.S = p.sp_p0.S; }   // layer 0; the rest ran beside the layer-0 dW
     TIMED(p, K_ADAM, s, OAC_HIP_CHECK(launch_adam(a, s)));
     p.launches++;
   }
+  p.la_now = false;
   p.slot = 0;
   p.ring_direct = false;
   return 0;

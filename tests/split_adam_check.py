@@ -38,13 +38,15 @@ def _run(trainer, Do, Da, B, seed):
 
 def main(out):
     from oac_amd import ParticleTrainerOAC, SACTrainer
-    res = {}
+    res, trace = {}, {}
     for Do, Da, H, B in [(7, 5, 48, 1100), (13, 6, 80, 1029)]:
         pp, qp = producers(sac_params(Do, Da, [H, H], 3, pi_init_w=0.2, q_init_w=0.1))
         sac = SACTrainer(pp, qp, action_space=Space(Da), policy_lr=3e-4, qf_lr=3e-4,
                          soft_target_tau=5e-3, use_automatic_entropy_tuning=True)
         for k, v in _run(sac, Do, Da, B, 11).items():
             res[f"sac_{H}_{k}"] = v
+        # the step's trace bits (not compared: the parent checks the path taken)
+        trace[f"sac_{H}"] = _lib.lib().oac_sac_trace(sac._last_plan.handle, 1)
         K = 7
         pp, qp = producers(sac_params(Do, Da, [H, H], 3, q_out=K, pi_init_w=0.2, q_init_w=0.1,
                                       q_last_bias=np.linspace(0.0, 30.0, K)),
@@ -56,7 +58,7 @@ def main(out):
         for k, v in _run(poac, Do, Da, B, 21).items():
             res[f"poac_{H}_{k}"] = v
     np.savez(out, **res)
-    print("ok", len(res), flush=True)
+    print("ok", len(res), "trace", " ".join(f"{k}={v}" for k, v in sorted(trace.items())), flush=True)
 
 
 if __name__ == "__main__":
