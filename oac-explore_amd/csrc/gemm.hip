@@ -394,7 +394,7 @@ void gemm_batch_finalize(GemmBatch& b, int cfg) {
 hipError_t gemm_batch_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCache* bc, int pos) {
   if (b.total_tiles <= 0) return hipSuccess;
   if (b.side_adam > 0 && (cfg < 9 || cfg > 17)) return hipErrorInvalidValue;   // side Adam: gemm_bwdp only
-  if (b.la_adam && (cfg < 9 || cfg > 17 || b.total_tiles > kLaTickets))   // last-arrival Adam: the same
+  if (b.la_adam && (cfg != 12 || b.total_tiles > kLaTickets))   // last-arrival Adam: gemm_bwdp cfg 12
     return hipErrorInvalidValue;
   // rows read through the direct gather's index slot (a_rows) and the side
   // workgroups that copy the batch / draw eps (rg): only the small kernel and

@@ -436,7 +436,7 @@ __device__ __forceinline__ void la_tail(const GemmBatch& batch, const GemmTask& 
   if (batch.la_book && tile == 0 && threadIdx.x == 0) step_bookkeeping_lead(a.state, a.alpha, a.advance);
 }
 
-template <int BM, int BN, int AK, int NB, int FK, bool SWP>
+template <int BM, int BN, int AK, int NB, int FK, bool SWP, bool LA>
 __device__ __forceinline__ void bwdp_tile(const GemmBatch& batch, int ti, int local, float* lds) {
   using G = BwdG<BM, BN, NB, FK>;
   constexpr int WM = G::WM, WN = G::WN;
@@ -487,19 +487,19 @@ __device__ __forceinline__ void bwdp_tile(const GemmBatch& batch, int ti, int lo
         const float s = bsum[i] + __shfl_xor(bsum[i], 32);
         const int m = mw + 32 * i + lane;
         if (lane < 32 && m < t.M) {
-          if (t.wt) __hip_atomic_store(t.bias_grad + m, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (LA) __hip_atomic_store(t.bias_grad + m, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else t.bias_grad[m] = s;
         }
       }
     }
   }
-  rd_epilogue<WM, WN, kEpiBwd>(t, mw, nw, acc, false);
-  if (batch.la_adam && t.wt) la_tail<BM, BN>(batch, t, local, m0, n0, nx, grad_ones, c0, bg0);
+  rd_epilogue<WM, WN, kEpiBwd, LA>(t, mw, nw, acc, false);
+  if (LA && t.epi == EPI_GRAD) la_tail<BM, BN>(batch, t, local, m0, n0, nx, grad_ones, c0, bg0);
   PIPE_CLK(30);
   PIPE_CLK(31);
 }
 
-template <int BM, int BN, int NB, int FK, bool SWP>
+template <int BM, int BN, int NB, int FK, bool SWP, bool LA = false>
 __device__ __forceinline__ void gemm_bwdp_body(int total_tiles, int tb1, int tb2, int tb3, int tb4,
                                                int tb5, int tb6, int tb7, const GemmBatch& batch,
                                                float* lds) {
@@ -521,30 +521,31 @@ __device__ __forceinline__ void gemm_bwdp_body(int total_tiles, int tb1, int tb2
   const int local = bid - t.tile_begin;
   const int ak = (t.a_kc ? PK_KC : PK_MN) + (t.a_mode == A_RANK1_MASK ? 1 : 0);
   switch (ak) {
-    case PK_KC: bwdp_tile<BM, BN, PK_KC, NB, FK, SWP>(batch, ti, local, lds); break;
-    case PK_KC_R1: bwdp_tile<BM, BN, PK_KC_R1, NB, FK, SWP>(batch, ti, local, lds); break;
-    case PK_MN: bwdp_tile<BM, BN, PK_MN, NB, FK, SWP>(batch, ti, local, lds); break;
-    default: bwdp_tile<BM, BN, PK_MN_R1, NB, FK, SWP>(batch, ti, local, lds); break;
+    case PK_KC: bwdp_tile<BM, BN, PK_KC, NB, FK, SWP, LA>(batch, ti, local, lds); break;
+    case PK_KC_R1: bwdp_tile<BM, BN, PK_KC_R1, NB, FK, SWP, LA>(batch, ti, local, lds); break;
+    case PK_MN: bwdp_tile<BM, BN, PK_MN, NB, FK, SWP, LA>(batch, ti, local, lds); break;
+    default: bwdp_tile<BM, BN, PK_MN_R1, NB, FK, SWP, LA>(batch, ti, local, lds); break;
   }
 }
 
 // waves per SIMD the registers must allow so that the ring's LDS sets the
 // workgroups per CU (BwdG::OCC; the software-pipelined loop: 64x64 only): 64x64 tiles on a 2-stage 32-deep ring or a
 // 4-stage 16-deep one (36 KB) four, 128x64 (52 KB) three, 128x128 (68 KB) two
-template <int BM, int BN, int NB, int FK, bool SWP>
+template <int BM, int BN, int NB, int FK, bool SWP, bool LA = false>
 __global__ void __launch_bounds__(256, (SWP ? 4 : BwdG<BM, BN, NB, FK>::OCC))
 gemm_bwdp_kernel(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                  const GemmBatch batch) {
   __shared__ __attribute__((aligned(16))) float lds[BwdG<BM, BN, NB, FK>::LDS];
-  gemm_bwdp_body<BM, BN, NB, FK, SWP>(total_tiles, tb1, tb2, tb3, tb4, tb5, tb6, tb7, batch, lds);
+  gemm_bwdp_body<BM, BN, NB, FK, SWP, LA>(total_tiles, tb1, tb2, tb3, tb4, tb5, tb6, tb7, batch, lds);
 }
 // the batch in device memory (kernels.h BatchCache)
-template <int BM, int BN, int NB, int FK, bool SWP>
+template <int BM, int BN, int NB, int FK, bool SWP, bool LA = false>
 __global__ void __launch_bounds__(256, (SWP ? 4 : BwdG<BM, BN, NB, FK>::OCC))
 gemm_bwdp_kernel_dev(int total_tiles, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6, int tb7,
                      const GemmBatchG* __restrict__ bp) {
   __shared__ __attribute__((aligned(16))) float lds[BwdG<BM, BN, NB, FK>::LDS];
-  gemm_bwdp_body<BM, BN, NB, FK, SWP>(total_tiles, tb1, tb2, tb3, tb4, tb5, tb6, tb7, *(const GemmBatch*)bp, lds);
+  gemm_bwdp_body<BM, BN, NB, FK, SWP, LA>(total_tiles, tb1, tb2, tb3, tb4, tb5, tb6, tb7, *(const GemmBatch*)bp,
+                                          lds);
 }
 
 // a backward batch this kernel takes: dX (A k-contiguous, B n-contiguous) or dW
@@ -575,15 +576,23 @@ hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCac
   int tb[8];
   for (int i = 0; i < 8; ++i) tb[i] = i < b.ntasks ? b.t[i].tile_begin : 0x7fffffff;
   const GemmBatch* d = bc ? bc->get(b, pos, s) : nullptr;
-#define OAC_BWDP(C_, BM_, BN_, NB_, FK_, SWP_) \
+#define OAC_BWDP_LA(C_, BM_, BN_, NB_, FK_, SWP_, LA_) \
   if (cfg == C_) { \
     if (d) \
-      OAC_LAUNCH((gemm_bwdp_kernel_dev<BM_, BN_, NB_, FK_, SWP_>), dim3(b.total_tiles + b.side_adam), dim3(256), 0, s, \
-                 b.total_tiles, tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], (const GemmBatchG*)d); \
+      OAC_LAUNCH((gemm_bwdp_kernel_dev<BM_, BN_, NB_, FK_, SWP_, LA_>), dim3(b.total_tiles + b.side_adam), \
+                 dim3(256), 0, s, b.total_tiles, tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], \
+                 (const GemmBatchG*)d); \
     else \
-      OAC_LAUNCH((gemm_bwdp_kernel<BM_, BN_, NB_, FK_, SWP_>), dim3(b.total_tiles + b.side_adam), dim3(256), 0, s, \
-                 b.total_tiles, tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
+      OAC_LAUNCH((gemm_bwdp_kernel<BM_, BN_, NB_, FK_, SWP_, LA_>), dim3(b.total_tiles + b.side_adam), \
+                 dim3(256), 0, s, b.total_tiles, tb[1], tb[2], tb[3], tb[4], tb[5], tb[6], tb[7], b); \
     return hipGetLastError(); }
+#define OAC_BWDP(C_, BM_, BN_, NB_, FK_, SWP_) OAC_BWDP_LA(C_, BM_, BN_, NB_, FK_, SWP_, false)
+  // the last-arrival Adam: its own instance of the default tiles (the
+  // write-through stores and the tail stay out of every other kernel)
+  if (b.la_adam) {
+    OAC_BWDP_LA(12, 64, 64, 2, 32, false, true)
+    return hipErrorInvalidValue;
+  }
   // cfg 12: 64x64 tiles on a 2-stage ring (36 KB of LDS: four workgroups per CU)
   // cfg 15: 64x64 tiles on a 4-stage 16-deep ring (the LDS of cfg 12, three
   // stages in flight instead of one); cfg 17: cfg 12 software-pipelined
@@ -593,6 +602,7 @@ hipError_t gemm_bwdp_launch(const GemmBatch& b, int cfg, hipStream_t s, BatchCac
   OAC_BWDP(13, 128, 128, 2, 32, false) OAC_BWDP(14, 128, 64, 2, 32, false)
   OAC_BWDP(15, 64, 64, 4, 16, false) OAC_BWDP(17, 64, 64, 2, 32, true)
 #undef OAC_BWDP
+#undef OAC_BWDP_LA
   return hipErrorInvalidValue;
 }
 

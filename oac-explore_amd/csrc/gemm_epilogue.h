@@ -51,7 +51,7 @@ __device__ __forceinline__ float rows_sum16(const float (&x)[16], int lane) {
   return d + __shfl_xor(d, 1, 32);
 }
 
-template <int WM, int WN, int EPI, bool FULL>
+template <int WM, int WN, int EPI, bool FULL, bool WT = false>
 __device__ __forceinline__ void epi_run(const GemmTask& t, int mw, int nw,
                                         const floatx16 (&acc)[WM][WN], bool second) {
   const int lane = threadIdx.x & 63;
@@ -97,7 +97,7 @@ __device__ __forceinline__ void epi_run(const GemmTask& t, int mw, int nw,
           case EPI_STORE: t.C[o] = v; break;
           case EPI_GRAD:
             if (t.b_ones && n == N - 1) t.bias_grad[m] = v;
-            else if (t.wt) __hip_atomic_store(t.C + o, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (WT) __hip_atomic_store(t.C + o, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             else t.C[o] = v;
             break;
           case EPI_BIAS: t.C[o] = v + bias; break;
@@ -125,13 +125,13 @@ __device__ __forceinline__ void epi_run(const GemmTask& t, int mw, int nw,
   }
 }
 
-template <int WM, int WN, int EPI>
+template <int WM, int WN, int EPI, bool WT = false>
 __device__ __forceinline__ void epi_dispatch(const GemmTask& t, int mw, int nw,
                                              const floatx16 (&acc)[WM][WN], bool second) {
   if (mw + 32 * WM <= t.M && nw + 32 * WN <= t.N)
-    epi_run<WM, WN, EPI, true>(t, mw, nw, acc, second);
+    epi_run<WM, WN, EPI, true, WT>(t, mw, nw, acc, second);
   else
-    epi_run<WM, WN, EPI, false>(t, mw, nw, acc, second);
+    epi_run<WM, WN, EPI, false, WT>(t, mw, nw, acc, second);
 }
 
 // KINDS: bit mask (1 << Epi) of the epilogue kinds a kernel instantiates
@@ -139,11 +139,12 @@ constexpr unsigned kEpiAll = 0xffu;
 constexpr unsigned kEpiFwd = (1u << EPI_STORE) | (1u << EPI_BIAS) | (1u << EPI_BIAS_RELU) |
                              (1u << EPI_BIAS_RANK_RELU) | (1u << EPI_BIAS_RELU_DOT);
 
-template <int WM, int WN, unsigned KINDS = kEpiAll>
+// WT: EPI_GRAD stores write-through (the last-arrival Adam's batches)
+template <int WM, int WN, unsigned KINDS = kEpiAll, bool WT = false>
 __device__ __forceinline__ void rd_epilogue(const GemmTask& t, int mw, int nw,
                                             const floatx16 (&acc)[WM][WN], bool second) {
 #define OAC_EPI_CASE(E) \
-  case E: if (KINDS & (1u << E)) epi_dispatch<WM, WN, E>(t, mw, nw, acc, second); break;
+  case E: if (KINDS & (1u << E)) epi_dispatch<WM, WN, E, WT>(t, mw, nw, acc, second); break;
   switch (t.epi) {
     OAC_EPI_CASE(EPI_STORE) OAC_EPI_CASE(EPI_GRAD) OAC_EPI_CASE(EPI_BIAS) OAC_EPI_CASE(EPI_BIAS_RELU)
     OAC_EPI_CASE(EPI_BIAS_RANK_RELU) OAC_EPI_CASE(EPI_ADD_RELU) OAC_EPI_CASE(EPI_MASK)

@@ -79,7 +79,6 @@ struct GemmTask {
   const float* ex[6];   // extra epilogue operands (EPI_HEAD_BWD)
   int a_rows;           // small kernel: A (and U) row m is row batch.rg rows[m] of the buffer
   int no_adam;          // EPI_GRAD in a fused-Adam batch: store the gradient only (another group's)
-  int wt;               // EPI_GRAD: write-through (agent-scope) stores, read by a last arrival
 };
 
 struct StepState;
@@ -155,8 +154,8 @@ struct GemmBatch {
   // side_first: the side workgroups are blockIdx [0, side_adam) (a multiple
   // of 8, so every tile keeps its XCD), dispatched ahead of the tiles.
   int side_adam, side_book, side_first;
-  // Last-arrival optimizer (gemm_bwdp.hip, la_adam != 0): the split-K dW
-  // tasks marked wt store their slabs write-through, and the workgroup that
+  // Last-arrival optimizer (gemm_bwdp.hip, la_adam != 0): the batch's
+  // split-K dW tasks store their slabs write-through, and the workgroup that
   // finishes a dW tile last (an agent-scope ticket per (m, n) tile in
   // la_ticket[tile_begin + tile], re-armed by that workgroup) sums the
   // tile's t.ksplit slabs in adam_flat_kernel's fixed order and applies

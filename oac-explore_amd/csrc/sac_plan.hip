@@ -685,7 +685,6 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
       if (p.la_now && gb.side_adam == 0) p.la_now = false;
       if (p.la_now) {
         p.trace |= OAC_TRACE_LA_ADAM;
-        gb.t[0].wt = 1;
         gb.la_adam = 1;
         gb.la_book = 1;   // (the side workgroups do none)
         gb.la_ticket = reinterpret_cast<unsigned*>(p.W(WS_TICKETS));
