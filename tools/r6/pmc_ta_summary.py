@@ -22,7 +22,11 @@ for key in sorted(acc):
     for k in ("TA_BUSY_avr", "TA_BUSY_max", "TD_BUSY_avr", "TD_BUSY_max"):
         if k in c:
             line += f"  {k}={c[k] / gui:.2f}"
-    for k in ("TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "SQ_INSTS_VMEM_RD"):
+    for k in ("TCP_TOTAL_CACHE_ACCESSES_sum", "TCP_TCC_READ_REQ_sum", "SQ_INSTS_VMEM_RD",
+              "SQC_ICACHE_HITS", "SQC_ICACHE_MISSES", "SQC_ICACHE_MISSES_DUPLICATE",
+              "TCC_HIT_sum", "TCC_MISS_sum", "TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum"):
         if k in c:
             line += f"  {k}={c[k]:.3g}"
+    if "TCC_HIT_sum" in c:
+        line += f"  hit_rate={c['TCC_HIT_sum'] / max(1.0, c['TCC_HIT_sum'] + c['TCC_MISS_sum']):.3f}"
     print(line)
