@@ -85,3 +85,36 @@ def test_product_path_has_no_fallback(monkeypatch, tmp_path):
             src = open(os.path.join(pkg, f)).read()
             assert not re.search(r"^\s*(from|import)\s+oracle\b", src, flags=re.M), f
             assert "sac_oracle" not in src, f
+
+
+def _header_enum(prefix, end):
+    """The members of a C enum in include/oac_amd.h, in order (prefix-named)."""
+    src = open(os.path.join(ROOT, "include", "oac_amd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"\b(" + prefix + r"[A-Z0-9_]+)\b\s*(?:=\s*\d+)?\s*,", src)
+    return [n for n in dict.fromkeys(names) if n != end]
+
+
+def test_tuning_keys_match_the_header_and_reject_unknown():
+    """oac_amd._lib.TUNE names every oac_tuning_key in the header's order;
+    oac_tuning_set takes each key (0 = the default) and rejects one past the
+    end with a message (host-only: no GPU call)."""
+    from oac_amd import _lib
+    keys = _header_enum("OAC_TUNE_", "OAC_TUNE_COUNT")
+    assert keys and len(keys) == len(_lib.TUNE)
+    py = sorted(_lib.TUNE, key=_lib.TUNE.get)
+    assert [k.lower() for k in (n[len("OAC_TUNE_"):] for n in keys)] == py
+    L = _lib.lib()
+    for name in py:
+        _lib.set_tuning(**{name: 0})
+    assert L.oac_tuning_set(len(py), 1) != 0
+    assert b"tuning key" in L.oac_last_error()
+
+
+def test_trace_bits_match_the_header():
+    """oac_amd._lib.TRACE carries every OAC_TRACE_* bit the header defines."""
+    from oac_amd import _lib
+    src = open(os.path.join(ROOT, "include", "oac_amd.h")).read()
+    bits = {n[len("OAC_TRACE_"):].lower(): int(v)
+            for n, v in re.findall(r"#define\s+(OAC_TRACE_[A-Z0-9_]+)\s+(\d+)", src)}
+    assert bits == _lib.TRACE
