@@ -22,8 +22,39 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
+
+def _pin_host_threads(per_rank=8):
+    """Keep this rank's host threads on `per_rank` fixed cores of the ones it
+    may use (rank r: the r-th slice, by LOCAL_RANK), set before torch starts
+    its threads so they all inherit it.  The timed loop is host-issued
+    launches; left to migrate, the driver-shaped line spread 11,064-11,416
+    steps/s over six runs on one box, pinned 11,491-11,544
+    (tools/r6/variance.sh).  Not in the `--gpus N` launcher process (its
+    ranks take their own slices) and not with --no-pin; returns the cores the
+    process had (the CPU baseline's all-cores leg runs on them)."""
+    argv = sys.argv[1:]
+    gpus = 1
+    for i, a in enumerate(argv):
+        v = a.split("=", 1)[1] if a.startswith("--gpus=") else (
+            argv[i + 1] if a == "--gpus" and i + 1 < len(argv) else None)
+        if v is not None and v.isdigit():
+            gpus = int(v)
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+    if "--no-pin" in argv or ("WORLD_SIZE" not in os.environ and gpus > 1):
+        return allowed
+    lr = int(os.environ.get("LOCAL_RANK", "0") or 0)
+    if len(allowed) >= per_rank * (lr + 1):
+        os.sched_setaffinity(0, allowed[per_rank * lr:per_rank * (lr + 1)])
+    return allowed
+
+
+_HOST_CPUS = _pin_host_threads()
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "oac-explore_amd"))
@@ -52,6 +83,8 @@ def parse():
     ap.add_argument("--hidden", type=int, default=256)
     ap.add_argument("--replay", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pin", action="store_true",
+                    help="leave the host threads unpinned (bench.py pins each rank to 8 cores)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the exploration and g-oac legs (profiling runs: keeps the "
                          "per-kernel statistics to the headline step)")
@@ -457,6 +490,17 @@ def kernel_timing(tr, rb, B, n, seed=12345):
                            avg_us=1e3 * ms[k] / max(cnt[k], 1)) for k in range(4)}
 
 
+def unpin_host_threads():
+    """Every thread of this process back on the cores it started with."""
+    if not _HOST_CPUS:
+        return
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            os.sched_setaffinity(int(tid), _HOST_CPUS)
+        except OSError:
+            pass
+
+
 def cpu_threads_all():
     """All cores this process may run on (len(os.sched_getaffinity(0)), capped
     by OMP_NUM_THREADS where the host sets it: the GPU box's CPU share)."""
@@ -465,7 +509,7 @@ def cpu_threads_all():
     return (min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n), n
 
 
-def cpu_baseline(args, runs=5, steps=300, warmup=20, all_runs=1, kind="sac", B=None,
+def cpu_baseline(args, runs=5, steps=300, warmup=20, all_runs=3, kind="sac", B=None,
                  dims=None):
     """The reference's PyTorch-CPU step restated on torch autograd
     (oracle/sac_autograd.py: the reference's forward ops, backward() and the
@@ -529,7 +573,7 @@ def cpu_baseline(args, runs=5, steps=300, warmup=20, all_runs=1, kind="sac", B=N
         T, aff = cpu_threads_all()
         allc, all_rates = median_rate(T, all_runs)
         out["all_cores"] = dict(value=round(allc, 2), cores=T, affinity_cpus=aff, runs=all_rates,
-                                sample=sample + f", {all_runs} run(s), {T} threads")
+                                sample=sample + f", median of {all_runs} run(s), {T} threads")
     torch.set_num_threads(1)
     return out
 
@@ -937,6 +981,7 @@ def main():
                 if not args.no_cpu_baseline:
                     out[kind]["cpu_baseline"] = recipe_cpu_baseline(kind, args)
         if not args.no_cpu_baseline and world == 1:   # the CPU baseline is an N=1 figure
+            unpin_host_threads()   # (its all-cores leg: every core the process had)
             out["cpu_baseline"] = cpu_baseline(args)
             if big is not None:      # configs[2]: the same step at batch 4096
                 # runs of >= 2 s: ~5 steps/s at one thread
