@@ -85,6 +85,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pin", action="store_true",
                     help="leave the host threads unpinned (bench.py pins each rank to 8 cores)")
+    ap.add_argument("--cpu-baseline-only", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the exploration and g-oac legs (profiling runs: keeps the "
                          "per-kernel statistics to the headline step)")
@@ -816,8 +817,28 @@ def launcher_selftest(args):
     dist.destroy_process_group()
 
 
+def cpu_baseline_fresh(args, **kw):
+    """cpu_baseline in a fresh, unpinned process: its thread pools (torch's,
+    the BLAS library's) must size themselves on every core this process
+    started with, which the pinned timed process's pools may not (its
+    all-cores leg measured 78-103 steps/s against 127-131 unpinned on one
+    box, tools/r6/cpu_pin_check.sh)."""
+    import subprocess
+    unpin_host_threads()
+    argv = [a for a in sys.argv[1:] if a != "--no-pin"]
+    r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__)] + argv +
+                       ["--no-pin", "--cpu-baseline-only", json.dumps(kw)],
+                       capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu baseline process: rc {r.returncode}: {r.stderr[-500:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def main():
     args = parse()
+    if args.cpu_baseline_only is not None:   # (cpu_baseline_fresh's child: no GPU work)
+        print(json.dumps(cpu_baseline(args, **json.loads(args.cpu_baseline_only))), flush=True)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # started as `python bench.py --gpus N` (no torchrun): become the launcher
         ngpu = visible_gpu_count() if not args.selftest_launcher else args.gpus
@@ -981,15 +1002,14 @@ def main():
                 if not args.no_cpu_baseline:
                     out[kind]["cpu_baseline"] = recipe_cpu_baseline(kind, args)
         if not args.no_cpu_baseline and world == 1:   # the CPU baseline is an N=1 figure
-            unpin_host_threads()   # (its all-cores leg: every core the process had)
-            out["cpu_baseline"] = cpu_baseline(args)
+            out["cpu_baseline"] = cpu_baseline_fresh(args)
             if big is not None:      # configs[2]: the same step at batch 4096
                 # runs of >= 2 s: ~5 steps/s at one thread
-                out["b4096"]["cpu_baseline"] = cpu_baseline(args, steps=11, warmup=2, all_runs=0,
-                                                            B=4096)
+                out["b4096"]["cpu_baseline"] = cpu_baseline_fresh(args, steps=11, warmup=2, all_runs=0,
+                                                                  B=4096)
             if "poac_ant_b4096" in out:   # configs[4]: P-OAC K=10, Ant dims, batch 4096
-                out["poac_ant_b4096"]["cpu_baseline"] = cpu_baseline(   # (~12.7 steps/s: >= 2 s runs)
-                    args, steps=26, warmup=2, all_runs=0, kind="poac", B=4096, dims=(111, 8, 256))
+                out["poac_ant_b4096"]["cpu_baseline"] = cpu_baseline_fresh(   # (~12.7 steps/s: >= 2 s runs)
+                    args, steps=26, warmup=2, all_runs=0, kind="poac", B=4096, dims=[111, 8, 256])
         print(json.dumps(out), flush=True)
     if dp:
         # the trainer's teardown (its captured step graphs hold RCCL kernels),
