@@ -23,13 +23,14 @@ import sys
 import time
 
 
-def _pin_host_threads(per_rank=8):
+def _pin_host_threads(per_rank=4):
     """Keep this rank's host threads on `per_rank` fixed cores of the ones it
     may use (rank r: the r-th slice, by LOCAL_RANK), set before torch starts
     its threads so they all inherit it.  The timed loop is host-issued
     launches; left to migrate, the driver-shaped line spread 11,064-11,416
-    steps/s over six runs on one box, pinned 11,491-11,544
-    (tools/r6/variance.sh).  Not in the `--gpus N` launcher process (its
+    steps/s over six runs on one box, pinned to 8 cores 11,491-11,544
+    (tools/r6/variance.sh); 2 / 4 / 8 / 16 cores measured 11,536 / 11,526 /
+    11,491 / 11,420 (means of three, tools/r6/pinsize.sh).  Not in the `--gpus N` launcher process (its
     ranks take their own slices) and not with --no-pin; returns the cores the
     process had (the CPU baseline's all-cores leg runs on them)."""
     argv = sys.argv[1:]
@@ -84,7 +85,7 @@ def parse():
     ap.add_argument("--replay", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pin", action="store_true",
-                    help="leave the host threads unpinned (bench.py pins each rank to 8 cores)")
+                    help="leave the host threads unpinned (bench.py pins each rank to 4 cores)")
     ap.add_argument("--cpu-baseline-only", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the exploration and g-oac legs (profiling runs: keeps the "
