@@ -32,7 +32,7 @@ def _pin_host_threads(per_rank=4):
     (tools/r6/variance.sh); 2 / 4 / 8 / 16 cores measured 11,536 / 11,526 /
     11,491 / 11,420 (means of three, tools/r6/pinsize.sh).  Not in the `--gpus N` launcher process (its
     ranks take their own slices) and not with --no-pin; returns the cores the
-    process had (the CPU baseline's all-cores leg runs on them)."""
+    process had (the CPU baselines' fresh process starts on them)."""
     argv = sys.argv[1:]
     gpus = 1
     for i, a in enumerate(argv):
@@ -52,7 +52,9 @@ def _pin_host_threads(per_rank=4):
     return allowed
 
 
-_HOST_CPUS = _pin_host_threads()
+# (as the benchmark process only: a process that imports bench -- the tests,
+# tools/launch_times.py -- keeps its threads where they are)
+_HOST_CPUS = _pin_host_threads() if __name__ == "__main__" else None
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
