@@ -1,12 +1,16 @@
-// Large-batch backward products on the LDS-DMA pipeline (gemm_cfg 9 / 10 /
-// 11: 128x64 / 64x64 / 128x128 workgroup tiles): dX = dY W (dY k-contiguous,
-// possibly a rank-1 seed s[m] v[k] through a ReLU mask; W n-contiguous) and
-// dW = dY^T [X | 1] (both operands batch-major, dY possibly rank-1 masked),
-// split-K slabs as the other kernels write them.
+// Large-batch backward products on the LDS-DMA pipeline: dX = dY W (dY
+// k-contiguous, possibly a rank-1 seed s[m] v[k] through a ReLU mask; W
+// n-contiguous) and dW = dY^T [X | 1] (both operands batch-major, dY possibly
+// rank-1 masked), split-K slabs as the other kernels write them.  Tile
+// configurations (gemm_cfg): 12 = 64x64 tiles on a 2-stage ring (the
+// default), 9 / 10 / 11 = 128x64 / 64x64 / 128x128 on 3-stage rings, 13 / 14 =
+// 128x128 / 128x64 on 2-stage rings, 15 = 64x64 with 16-deep stages on a
+// 4-stage ring, 17 = cfg 12 software-pipelined; cfg 12 with the last-arrival
+// Adam (GemmBatch::la_adam) is an instance of its own.
 //
 // Same pipeline as the forward kernel (gemm_pipe.h, gemm_fwd.hip): 2 x 2 waves
-// of (BM/2) x (BN/2) v_mfma_f32_32x32x2_f32 blocks, 32-deep K stages in a
-// three-stage LDS ring filled by global_load_lds_dwordx4.  A k-contiguous
+// of (BM/2) x (BN/2) v_mfma_f32_32x32x2_f32 blocks, FK-deep K stages (32, or
+// 16) in an NB-stage LDS ring filled by global_load_lds_dwordx4.  A k-contiguous
 // operand is staged as in the forward kernel ([row][32 k], 16-byte chunks
 // swizzled by the row, one ds_read_b128 per 4 k); a batch-major operand as
 // the rows of its k range ([32 k][BM or BN], lane-linear: one 1-KB LDS-DMA
