@@ -26,6 +26,7 @@
 namespace oac {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 #ifdef OAC_STAGE_CLOCK   // per-stage wall clock of thread 0 of each block (tools/micro only)
 __device__ long long g_gs_clock[4096 * 8];
@@ -277,7 +278,24 @@ constexpr int kGatherU = 4;   // float4s per lane of a side block's row copy (ro
 // the other launches keep the registers and schedule of the plain kernel:
 // with the fold in every kernel, launches without a fold task came out
 // 0.2-0.4 us slower)
-template <int NW, int GPW, bool FOLDK = false>
+// one 16x16 tile of the head's dX over KS k-steps of 4: A from the dhead rows
+// in LDS (arow: the lane's row at its k-group; zeros past 2N), B the lane's
+// prefetched weights (k-step order, a fixed order per output)
+template <int KS>
+__device__ __forceinline__ floatx4 hd_mfma(const float* arow, const float (&hb)[12]) {
+  float a[KS];
+#pragma unroll
+  for (int st = 0; st < KS; ++st) a[st] = arow[4 * st];
+  floatx4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int st = 0; st < KS; ++st) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[st], hb[st], c, 0, 0, 0);
+  return c;
+}
+
+// HD2: the kernel that takes EPI_HEAD_BWD tasks with the head's dX chunk
+// (GemmTask::C2; its own instance, as FOLDK, so the other launches keep
+// their registers and schedule)
+template <int NW, int GPW, bool FOLDK = false, bool HD2 = false>
 __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int publish, int tb1,
                                                  int tb2, int tb3, int tb4, int tb5, int tb6,
                                                  int tb7, const GemmBatch& batch, float* red,
@@ -399,6 +417,33 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  // EPI_HEAD_BWD with C2: the head's dX for the task's R hidden columns from
+  // this tile's own dhead rows, as v_mfma_f32_16x16x4_f32 tiles (lane l:
+  // A[l&15][k=l>>4], B[k=l>>4][l&15]; D reg r: row 4*(l>>4)+r, col l&15):
+  // wave w takes row tile w & 1 and column tile w >> 1 (R <= 8 NW).  Its B
+  // operands (the head weights, 2N <= 48 k) and the ReLU mask of its outputs
+  // are requested now, their latency behind the k loop.
+  constexpr int kHdS = 12;   // k-steps of 4 (2N <= 48)
+  const bool hd = HD2 && t.epi == EPI_HEAD_BWD && t.C2 != nullptr;   // (workgroup-uniform)
+  float hb[HD2 ? kHdS : 1], hm[4];
+  if constexpr (HD2) {
+    if (hd) {
+      const int l16 = lane & 15, g4 = lane >> 4, n2 = 2 * t.N;
+      const int col = (wave >> 1) * 16 + l16;
+      const bool cv = col < t.R;
+#pragma unroll
+      for (int st = 0; st < kHdS; ++st) {
+        const int k = 4 * st + g4;
+        hb[st] = (cv && k < n2) ? t.U[(long)k * t.ldu + col] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 16 * (wave & 1) + 4 * g4 + r;
+        hm[r] = (cv && m < t.M) ? t.aux[(long)m * t.ld_aux + col] : 0.f;
+      }
+    }
+  }
+
   FoldAcc fa{0.f, 0.f, 0.f};
   k_dispatch<NW, GPW, FOLDK>(t, m0, n0, k_lo, k_hi, acc, arow, fold, fa);
   if constexpr (FOLDK && NW < 16)
@@ -417,7 +462,6 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     t2.A = t.A2; t2.B = t.B2; t2.K = t.K2;
     k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc, -1, fa);
   }
-
   GS_STAGE(2);
   // fixed-order split-K reduction through LDS
 #pragma unroll
@@ -469,6 +513,52 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     ac = adam_consts(batch.adam.state, batch.adam.advance, batch.adam.lr, batch.adam.beta1,
                      batch.adam.beta2, batch.adam.eps, batch.adam.target, batch.adam.tau,
                      batch.adam.period);
+  if constexpr (HD2) {
+    if (hd) {   // the head backward, then its dX columns
+      __syncthreads();   // (every wave's reads of the partial tiles are done: the LDS is reused)
+      constexpr int kDh = 65;   // dhead row stride in LDS (odd: a column read is conflict-free)
+      float* dh = red;          // [32][kDh]: dmean | dls_raw of the tile's rows
+      const int N = t.N;
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int e = threadIdx.x + i * 64 * NW;
+        const int r = e >> 6, l = e & 63;
+        const int mt = (r & 3) + 8 * (r >> 2) + 4 * (l >> 5), nt = l & 31;
+        const int m = m0 + mt, n = n0 + nt;
+        float dmean = 0.f, dls = 0.f;
+        if (m < t.M && n < N) {
+          const EpiIn x = xin[i];
+          tanh_gauss_backward(vals[i], x.xb, x.xa, x.am, x.av, x.at, x.s * (1.f / (float)t.M), dmean,
+                              dls);
+          if (!t.dup) {
+            const long o = (long)m * t.ldc + n;
+            t.C[o] = dmean;
+            t.C[o + N] = dls;
+          }
+        }
+        if (n < N) { dh[mt * kDh + n] = dmean; dh[mt * kDh + N + n] = dls; }
+      }
+      for (int e = threadIdx.x; e < 32 * 64; e += 64 * NW)   // k past 2N: zeros (fixed-length MFMA runs)
+        if ((e & 63) >= 2 * N) dh[(e >> 6) * kDh + (e & 63)] = 0.f;
+      __syncthreads();
+      const int l16 = lane & 15, g4 = lane >> 4, ksteps = (2 * N + 3) >> 2;
+      const int rt = 16 * (wave & 1), col = (wave >> 1) * 16 + l16;
+      if ((wave >> 1) * 16 < t.R) {   // (wave-uniform)
+        const float* arow = dh + (rt + l16) * kDh + g4;
+        const floatx4 c = ksteps <= 8 ? hd_mfma<8>(arow, hb) : hd_mfma<12>(arow, hb);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float mk = hm[r];
+          asm volatile("" : "+v"(mk));   // (the mask's wait here, after the MFMAs, not at its load)
+          const int m = m0 + rt + 4 * g4 + r;
+          if (col < t.R && m < t.M) t.C2[(long)m * t.ldc2 + col] = mk > 0.f ? c[r] : 0.f;
+        }
+      }
+      if (batch.fuse_adam && !batch.adam.no_book && bid == 0 && threadIdx.x == 0)
+        step_bookkeeping(batch.adam.state, batch.adam.alpha, batch.adam.advance);
+      return;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int e = threadIdx.x + i * 64 * NW;
@@ -497,13 +587,14 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   GS_STAGE(4);
 }
 
-template <int NW, int GPW, bool FOLDK = false>
+template <int NW, int GPW, bool FOLDK = false, bool HD2 = false>
 __global__ void __launch_bounds__(64 * NW)
 gemm_small_kernel(int total_tiles, int publish, int tb1, int tb2, int tb3, int tb4, int tb5, int tb6,
                   int tb7, const GemmBatch batch) {
+  static_assert(!HD2 || (NW >= 8 && SmallLds<NW, FOLDK>::N >= 32 * 65), "HD2: 8+ waves, dhead in LDS");
   __shared__ __attribute__((aligned(16))) float red[SmallLds<NW, FOLDK>::N];
-  gemm_small_block<NW, GPW, FOLDK>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5, tb6,
-                                   tb7, batch, red);
+  gemm_small_block<NW, GPW, FOLDK, HD2>(blockIdx.x, total_tiles, publish, tb1, tb2, tb3, tb4, tb5,
+                                        tb6, tb7, batch, red);
 }
 
 // The direct drop-in layer-0 launch with the step's B <= 256 indices in the
@@ -578,8 +669,8 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s, BatchCache* bc 
     if (b.t[i].K2 > 0 && (b.t[i].ksplit > 1 || !b.t[i].a_kc || b.t[i].b_kc ||
                           b.t[i].a_mode != A_PLAIN))
       return hipErrorInvalidValue;
-  const int nw = b.force_nw > 0 ? b.force_nw : gemm_small_waves(b);
-  const int gpw = b.force_gpw > 0 ? b.force_gpw : (nw >= 16 ? 4 : 5);
+  int nw = b.force_nw > 0 ? b.force_nw : gemm_small_waves(b);
+  int gpw = b.force_gpw > 0 ? b.force_gpw : (nw >= 16 ? 4 : 5);
   b.adam_blocks = 0;
   if (b.fuse_adam) {
     long n4 = 0;
@@ -594,9 +685,38 @@ hipError_t gemm_small_launch(const GemmBatch& b0, hipStream_t s, BatchCache* bc 
   const GemmHead h = gemm_head(b);
   const bool inl = b.rg.inl && b.rg.ring && b.rg.B <= kInlineRows &&
                    ((nw == 16 && gpw == 4) || (nw == 8 && gpw == 5));
-  bool has_fold = false;
-  for (int i = 0; i < b.ntasks; ++i) has_fold = has_fold || b.t[i].fold;
+  bool has_fold = false, has_hd = false;
+  for (int i = 0; i < b.ntasks; ++i) {
+    has_fold = has_fold || b.t[i].fold;
+    const GemmTask& t = b.t[i];
+    if (t.epi == EPI_HEAD_BWD && t.C2) {   // the head's dX chunk: dhead and the weights in LDS
+      if (t.N > 24 || t.R < 1 || t.R > 256 || t.tiles_n != 1 || t.ksplit > 1)
+        return hipErrorInvalidValue;
+      has_hd = true;
+    }
+  }
   if (has_fold && inl) return hipErrorInvalidValue;   // (no fold task in a row-gathering launch)
+  if (has_hd && (has_fold || inl)) return hipErrorInvalidValue;
+  if (has_hd) {   // the head-dX kernels: 8 or 16 waves (a thread's share of the chunk)
+    // (a 16-column tile per wave, NW / 2 waves per row tile -> R <= 8 NW)
+    int rmax = 0;
+    for (int i = 0; i < b.ntasks; ++i)
+      if (b.t[i].epi == EPI_HEAD_BWD && b.t[i].C2) rmax = std::max(rmax, b.t[i].R);
+    if (b0.force_nw <= 0 && (nw < 8 || (nw < 16 && rmax > 8 * nw))) {
+      nw = rmax > 64 ? 16 : 8;
+      gpw = b0.force_gpw > 0 ? b0.force_gpw : (nw >= 16 ? 4 : 5);
+    }
+    if (rmax > 8 * nw) return hipErrorInvalidValue;
+    if (nw == 16 && gpw == 4)
+      OAC_LAUNCH((gemm_small_kernel<16, 4, false, true>), dim3(grid), dim3(64 * 16), 0, s, h.total_tiles,
+                 h.publish, h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b);
+    else if (nw == 8 && gpw == 5)
+      OAC_LAUNCH((gemm_small_kernel<8, 5, false, true>), dim3(grid), dim3(64 * 8), 0, s, h.total_tiles,
+                 h.publish, h.tb1, h.tb2, h.tb3, h.tb4, h.tb5, h.tb6, h.tb7, b);
+    else
+      return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (inl) {
     InlineRows ir;
     std::memcpy(ir.r, b.rg.inl, sizeof(int) * b.rg.B);

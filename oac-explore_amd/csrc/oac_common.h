@@ -33,7 +33,11 @@ enum Epi : int {
                           // ones column); both offset by split*slab_stride
   EPI_HEAD_BWD = 8,       // acc = dL/da (N = act_dim): tanh-Gaussian head backward
                           // (policy_math.h) -> C[m*ldc + n] = dmean, C[m*ldc + N + n]
-                          // = dls_raw; ex[] = act, std, u, eps, head, &alpha (small kernel)
+                          // = dls_raw; ex[] = act, std, u, eps, head, &alpha (small kernel).
+                          // C2 set: the head's dX follows in the same workgroup,
+                          // C2[m*ldc2 + c] = [aux[m*ld_aux + c] > 0] sum_k dhead[m, k] U[k*ldu + c]
+                          // for the R columns c at C2 / aux / U (one column chunk of
+                          // the hidden layer; dup: the dhead stores are another task's)
   EPI_BIAS_RELU_DOT = 7,  // C = relu(acc + bias[n]) and, per row, the partial
                           // dot of this 32-column tile with aux[n] (a width-1
                           // output layer): C2[(n0/32)*ldc2 + m]  (small kernel)
@@ -76,6 +80,9 @@ struct GemmTask {
   const float* A2;
   const float* B2;
   int K2;
+  int dup;              // EPI_HEAD_BWD with C2: the tiles recompute another task's dhead for
+                        // their column chunk of the head's dX and store only that (here: the
+                        // padding after K2, the record keeps its 304 bytes)
   const float* ex[6];   // extra epilogue operands (EPI_HEAD_BWD)
   int a_rows;           // small kernel: A (and U) row m is row batch.rg rows[m] of the buffer
   int no_adam;          // EPI_GRAD in a fused-Adam batch: store the gradient only (another group's)

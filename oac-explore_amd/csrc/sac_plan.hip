@@ -586,6 +586,21 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
   return 0;
 }
 
+// The small-batch step's policy-head dX (dh2 = dhead W_head (x) [h2 > 0], K =
+// 2 Da) in the dL/da launch: that launch's head-backward tiles hold whole
+// dhead rows, so each finishes dh2 for its rows, as MFMA tiles after the
+// head backward (GemmTask::C2, gemm_small.hip HD2).  Each row block runs once
+// per 64-column chunk of the hidden layer, the copies (dup) recomputing dL/da
+// and storing only their dh2 columns: four workgroups finish a row block's
+// dh2 in parallel (one workgroup for all 256 columns spent ~1 us of MFMA
+// issue alone).  The head
+// dW, which then needs nothing the policy layer-1 backward produces, joins
+// that launch: one launch fewer on the chain.
+static bool head_dh2(const SacPlan& p, const float* prefetch) {
+  return p.cfg == 0 && !prefetch && p.c.act_dim <= 24 && p.c.hidden <= 6 * 64 &&
+         tuning(OAC_TUNE_HEAD_DH2) >= 0;
+}
+
 // prefetch: batch of the next step (its critic-side forward rides on this
 // step's policy-backward launches, small-batch path only), or null
 static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch = nullptr,
@@ -601,6 +616,7 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
   const bool merged = fused && minq_merged(p);   // (then the critic layer-0 dW launch ran it)
   const bool dfr = defer && merged && !prefetch;
   const float* qa = dfr ? p.W(W_QSHADOW) : q1;   // critic 1's post-step layer 0 (critic 2: + q_size)
+  const bool hd2 = head_dh2(p, prefetch);
   if (!merged) {  // -min Q backward to layer 1 with post-step weights, pre-step masks
     GemmBatch gb{};
     const float* const qs[2] = {q1, q2};
@@ -624,7 +640,20 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     t.ex[0] = p.W(OAC_WS_ACT1); t.ex[1] = p.W(W_STD1); t.ex[2] = p.W(W_U1);
     t.ex[3] = p.E1(); t.ex[4] = p.W(OAC_WS_HEAD1);
     t.ex[5] = c.auto_alpha ? &p.alpha()->alpha : nullptr;
-    add(gb, t);
+    if (hd2) {   // the head-backward tiles, once per 64-column chunk of dh2
+      for (int c0 = 0; c0 < H; c0 += 64) {
+        GemmTask u = t;
+        u.C2 = p.W(W_DH2P) + c0; u.ldc2 = H;
+        u.aux = p.W(W_H2P) + c0; u.ld_aux = H;
+        u.U = pol + L.pol_head_w + c0; u.ldu = H;
+        u.R = std::min(64, H - c0);
+        u.dup = c0 > 0;
+        add(gb, u);
+      }
+      p.trace |= OAC_TRACE_HEAD_DH2;
+    } else {
+      add(gb, t);
+    }
     if (prefetch && merged) add_critic_l0(p, gb, prefetch);
     if (prefetch) add_target_l0(p, gb, prefetch);
     if (dfr) add(gb, critic_dw0(p, 1, 0, Do, false));   // critic 2's obs columns: gradient only
@@ -646,22 +675,25 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
       p.launches++;
     }
   }
-  {  // policy heads: dW_head slab, dh2
+  {  // policy heads: dW_head slab, dh2 (hd2: the dL/da launch ran dh2, and
+     // the head dW shares the policy layer-1 backward's launch)
     GemmBatch gb{};
     float* gp = grad_p(p);
     add(gb, t_dw(p.W(W_DHEAD), 2 * Da, 2 * Da, B, p.W(W_H2P), H, H, gp + L.pol_head_w,
                  gp + L.pol_head_b, L.pol_size, p.sp_ph));
-    add(gb, t_dx(p.W(W_DHEAD), 2 * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(W_DH2P), H, p.W(W_H2P), H));
-    if (prefetch) add_critic_l1(p, gb);
-    if (dfr) add_dw0_side_adam(p, gb);   // both critics' layer 0 (+ bias): Adam + Polyak
-    if (run_gemm(p, gb, s)) return 1;
-  }
-  {  // policy layer 1
-    GemmBatch gb{};
-    float* gp = grad_p(p);
+    if (!hd2) {
+      add(gb, t_dx(p.W(W_DHEAD), 2 * Da, B, 2 * Da, pol + L.pol_head_w, H, H, p.W(W_DH2P), H,
+                   p.W(W_H2P), H));
+      if (prefetch) add_critic_l1(p, gb);
+      if (dfr) add_dw0_side_adam(p, gb);   // both critics' layer 0 (+ bias): Adam + Polyak
+      if (run_gemm(p, gb, s)) return 1;
+      gb = GemmBatch{};
+    }
+    // policy layer 1
     add(gb, t_dw(p.W(W_DH2P), H, H, B, p.W(W_H1P), H, H, gp + L.pol_fc1_w, gp + L.pol_fc1_b,
                  L.pol_size, p.sp_p1));
     add(gb, t_dx(p.W(W_DH2P), H, B, H, pol + L.pol_fc1_w, H, H, p.W(W_DH1P), H, p.W(W_H1P), H));
+    if (hd2 && dfr) add_dw0_side_adam(p, gb);   // (after every task: they store gradients only)
     if (run_gemm(p, gb, s)) return 1;
   }
   {  // policy layer 0

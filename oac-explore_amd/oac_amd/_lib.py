@@ -28,7 +28,7 @@ OAC_DP_OVERLAP = 2
 
 # oac_sac_trace bits
 TRACE = dict(direct=1, direct_big=2, batch_copy=4, qdot=8, wl_targets=16, split_phase1=32,
-             fused=64, exchange=128, la_adam=256)
+             fused=64, exchange=128, la_adam=256, head_dh2=512)
 
 # oac_allreduce_fn: int (*)(void* ctx, float* buf, int64_t n, void* stream)
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
@@ -45,7 +45,7 @@ WS = {name: i for i, name in enumerate([
 TUNE = {name: i for i, name in enumerate([
     "bwdp_cfg", "fwd_tile_m", "fwd_tile_n", "fwd_nb", "split_adam", "dh2_targets", "head_cc",
     "splits_q1", "splits_q0", "splits_ph", "splits_p1", "splits_p0", "debug_cfg",
-    "ring_direct", "ring_prefetch", "la_adam"])}
+    "ring_direct", "ring_prefetch", "la_adam", "head_dh2"])}
 
 
 def set_tuning(**kw):

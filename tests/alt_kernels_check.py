@@ -1,7 +1,9 @@
 """Run by tests/test_gpu_altkernels.py in a child process that selects a
 non-default large-batch kernel (OAC_TEST_TUNING -> oac_tuning_set): the
 ragged large-batch parity cases of test_gpu_ragged.py (B = 1029
-/ 1100, hidden 48 / 80) for all four trainers against the fp32 CPU oracle."""
+/ 1100, hidden 48 / 80) for all four trainers against the fp32 CPU oracle
+(OAC_TEST_SHAPES=small: the small-batch SAC cases instead, for a
+small-batch step choice)."""
 import os
 import sys
 
@@ -19,9 +21,12 @@ _lib.set_tuning_spec(os.environ.get("OAC_TEST_TUNING", ""))
 
 
 def main():
-    shapes = [s for s in tr.SHAPES if s[3] >= 1024]
-    for fn in (tr.test_sac_ragged, tr.test_particle_oac_ragged, tr.test_goac_ragged,
-               tr.test_ptrain_ragged):
+    # OAC_TEST_SHAPES=small: the small-batch SAC shapes (a small-kernel step choice)
+    small = os.environ.get("OAC_TEST_SHAPES") == "small"
+    shapes = [s for s in tr.SHAPES if (s[3] < 1024) == small]
+    fns = (tr.test_sac_ragged,) if small else (tr.test_sac_ragged, tr.test_particle_oac_ragged,
+                                               tr.test_goac_ragged, tr.test_ptrain_ragged)
+    for fn in fns:
         for s in shapes:
             fn(*s)
             print(f"ok {fn.__name__}{s}", flush=True)

@@ -47,6 +47,18 @@ def test_alternative_large_batch_kernels_match_oracle(name):
     assert r.stdout.count("ok ") == 8, r.stdout
 
 
+def test_head_dx_launch_small_batch_matches_oracle():
+    """The small-batch step with the policy-head dX in a launch of its own
+    (head_dh2=-1; the default runs it in the dL/da launch's epilogue and the
+    head dW beside the policy layer-1 backward), on the ragged small-batch SAC
+    shapes against the oracle."""
+    env = dict(os.environ, OAC_TEST_TUNING="head_dh2=-1", OAC_TEST_SHAPES="small")
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "alt_kernels_check.py")], env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, f"rc {r.returncode}\n{r.stdout[-3000:]}\n{r.stderr[-3000:]}"
+    assert r.stdout.count("ok ") == 4, r.stdout
+
+
 def test_side_workgroup_adam_is_bitwise_the_adam_launch(tmp_path):
     """Large-batch side-workgroup Adam (GemmBatch::side_adam; the SAC step)
     against one Adam launch per group, and the policy head's column-chunk

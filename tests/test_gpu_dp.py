@@ -598,7 +598,7 @@ def test_dp_rccl_humanoid_split_schedule_dropin_equals_single_gpu(B, overlap):
     from oac_amd._lib import TRACE
     steps = 24
     (got, bits), = _spawn(_nccl_h_worker, lambda r, port, q: (port, q, B, steps, overlap))
-    want_bits = ("direct",) if B == 256 else BIG_BRANCHES
+    want_bits = ("direct", "head_dh2") if B == 256 else BIG_BRANCHES
     missing = [b for b in want_bits + ("exchange",) if b != "split_phase1" and not bits & TRACE[b]]
     assert not missing and not bits & TRACE["fused"], (missing, bits)
     assert bool(bits & TRACE["split_phase1"]) == overlap, bits

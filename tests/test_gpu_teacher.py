@@ -386,6 +386,10 @@ def test_sac_dropin_teacher_forced(name):
         assert np.all(np.isfinite(e1)) and np.std(e1) > 0.5, "eps not drawn by the step"
         out = orc.step(so.NumpyReplay.to_torch(batch), e1, e2)
         _sac_compare(tr, orc, out, pre, batch, meta, name + "/dropin", s)
+    from oac_amd._lib import TRACE, lib
+    bits = lib().oac_sac_trace(tr._last_plan.handle, 1)
+    if meta["B"] <= 256:   # the headline step's form: fused Adam, the head's dX in the dL/da launch
+        assert bits & TRACE["fused"] and bits & TRACE["head_dh2"], bits
 
 
 def _particle_compare(tr, orc, out, pre, pre_p, batch, meta, name, s):
