@@ -266,7 +266,7 @@ int oac_rccl_allreduce(void* rccl, float* buf, int64_t n, void* stream);
 #define OAC_TRACE_FUSED         64   /* the single-process fused-Adam step */
 #define OAC_TRACE_EXCHANGE      128  /* data-parallel exchanges issued through the hook */
 #define OAC_TRACE_LA_ADAM       256  /* large batch: policy layer-0 Adam by last arrival (no launch) */
-#define OAC_TRACE_HEAD_DH2      512  /* small batch: the head's dX in the dL/da launch, head dW with policy layer 1 */
+#define OAC_TRACE_HEAD_DH2      512  /* the head's dX in the dL/da launch, head dW with policy layer 1 */
 int oac_sac_trace(oac_sac* h, int reset);
 
 int oac_sac_workspace_view(oac_sac* h, int which, int64_t* offset, int64_t* rows, int64_t* cols);
@@ -438,9 +438,10 @@ enum oac_tuning_key {
                                 layer-0 Adam) */
   OAC_TUNE_LA_ADAM,          /* 1: the large-batch SAC step's policy layer-0 Adam by the last
                                 arrival of each dW tile (no Adam launch) */
-  OAC_TUNE_HEAD_DH2,         /* -1: the small-batch step's policy-head dX in the head-dW launch
-                                instead of in the dL/da launch's epilogue (the default, which
-                                merges the head dW into the policy layer-1 backward launch) */
+  OAC_TUNE_HEAD_DH2,         /* -1: the small-batch SAC step's policy-head dX in the head-dW
+                                launch instead of in the dL/da launch's epilogue (the default,
+                                which merges the head dW into the policy layer-1 backward
+                                launch); 2: the epilogue form at large batch too */
   OAC_TUNE_COUNT
 };
 int oac_tuning_set(int key, int value);

@@ -422,27 +422,28 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
   // A[l&15][k=l>>4], B[k=l>>4][l&15]; D reg r: row 4*(l>>4)+r, col l&15):
   // wave w takes row tile w & 1 and column tile w >> 1 (R <= 8 NW).  Its B
   // operands (the head weights, 2N <= 48 k) and the ReLU mask of its outputs
-  // are requested now, their latency behind the k loop.
+  // are requested ahead: before the k loop on 16 waves (122 VGPRs), after it
+  // on 8 (held across the 8-wave loop they took it to 141, one workgroup per CU)
   constexpr int kHdS = 12;   // k-steps of 4 (2N <= 48)
   const bool hd = HD2 && t.epi == EPI_HEAD_BWD && t.C2 != nullptr;   // (workgroup-uniform)
   float hb[HD2 ? kHdS : 1], hm[4];
-  if constexpr (HD2) {
-    if (hd) {
-      const int l16 = lane & 15, g4 = lane >> 4, n2 = 2 * t.N;
-      const int col = (wave >> 1) * 16 + l16;
-      const bool cv = col < t.R;
+  auto hd_prefetch = [&]() {
+    const int l16 = lane & 15, g4 = lane >> 4, n2 = 2 * t.N;
+    const int col = (wave >> 1) * 16 + l16;
+    const bool cv = col < t.R;
 #pragma unroll
-      for (int st = 0; st < kHdS; ++st) {
-        const int k = 4 * st + g4;
-        hb[st] = (cv && k < n2) ? t.U[(long)k * t.ldu + col] : 0.f;
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + 16 * (wave & 1) + 4 * g4 + r;
-        hm[r] = (cv && m < t.M) ? t.aux[(long)m * t.ld_aux + col] : 0.f;
-      }
+    for (int st = 0; st < kHdS; ++st) {
+      const int k = 4 * st + g4;
+      hb[st] = (cv && k < n2) ? t.U[(long)k * t.ldu + col] : 0.f;
     }
-  }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + 16 * (wave & 1) + 4 * g4 + r;
+      hm[r] = (cv && m < t.M) ? t.aux[(long)m * t.ld_aux + col] : 0.f;
+    }
+  };
+  if constexpr (HD2 && NW >= 16)
+    if (hd) hd_prefetch();
 
   FoldAcc fa{0.f, 0.f, 0.f};
   k_dispatch<NW, GPW, FOLDK>(t, m0, n0, k_lo, k_hi, acc, arow, fold, fa);
@@ -462,6 +463,8 @@ __device__ __forceinline__ void gemm_small_block(int bid, int total_tiles, int p
     t2.A = t.A2; t2.B = t.B2; t2.K = t.K2;
     k_loop<NW, OP_KC, OP_MN, GPW>(t2, m0, n0, 0, t.K2, acc, -1, fa);
   }
+  if constexpr (HD2 && NW < 16)
+    if (hd) hd_prefetch();
   GS_STAGE(2);
   // fixed-order split-K reduction through LDS
 #pragma unroll

@@ -35,6 +35,9 @@ VARIANTS = {
     "adam_launches_dh2_gemm": "split_adam=-1,dh2_targets=-1",
     # the SAC policy layer 0's Adam by the last arrival of each dW tile
     "last_arrival_adam": "la_adam=1",
+    # the policy-head dX in the dL/da launch's epilogue at large batch too
+    # (the small-batch default; at large batch it is a launch of its own)
+    "head_dx_epilogue": "head_dh2=2",
 }
 
 
