@@ -97,6 +97,13 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
   const int g_lo = k_lo >> 3;                 // k_lo is a multiple of 8 (kchunk % 8 == 0)
   const int g_hi = (k_hi + 7) >> 3;
   const int kmax = k_hi - 1;
+  // direct rows (the drop-in layer-0 launch: random replay rows, from HBM):
+  // the A fragment of the wave's first group of its second pass, requested
+  // with the first pass's loads, so that pass waits on one row fetch, not two
+  const int g_pf = g_lo + wave + kGPW * NW;
+  const bool pf = (AK == OP_KC) && arow >= 0 && g_pf < g_hi;   // (wave-uniform)
+  float px[4] = {0.f, 0.f, 0.f, 0.f}, py[4];
+  if (pf) load4<AK>(la, 8 * g_pf + 4 * half, kmax, px, py);
 #pragma unroll 1
   for (int g0 = g_lo + wave; g0 < g_hi; g0 += kGPW * NW) {
     float ax[kGPW][4], ay[kGPW][4], bx[kGPW][4], by[kGPW][4];
@@ -105,7 +112,12 @@ __device__ __forceinline__ void k_loop(const GemmTask& t, int m0, int n0, int k_
       if (g0 + j * NW < g_hi) {
         const int kb = 8 * (g0 + j * NW) + 4 * half;
         load4<BK>(lb, kb, kmax, bx[j], by[j]);   // B first: it never waits on a row index
-        load4<AK>(la, kb, kmax, ax[j], ay[j]);
+        if (j == 0 && pf && g0 == g_pf) {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) ax[j][c] = px[c];
+        } else {
+          load4<AK>(la, kb, kmax, ax[j], ay[j]);
+        }
       }
 #pragma unroll
     for (int j = 0; j < kGPW; ++j)

@@ -602,7 +602,7 @@ static bool head_dh2(const SacPlan& p, const float* prefetch) {
   // 14.4; 3,939 -> 3,888 steps/s, tools/r7/big.sh -- on by tuning value 2)
   const int v = tuning(OAC_TUNE_HEAD_DH2);
   return (p.cfg == 0 || (p.cfg == kCfgLargeBatch && v == 2)) && v != -1 && !prefetch &&
-         p.c.act_dim <= 24 && p.c.hidden <= 6 * 64;
+         p.c.act_dim <= 24 && p.c.hidden <= 6 * 64 && (v < 16 || p.c.hidden <= 6 * v);
 }
 
 // prefetch: batch of the next step (its critic-side forward rides on this
@@ -645,12 +645,14 @@ static int phase2(SacPlan& p, hipStream_t s, bool fused, const float* prefetch =
     t.ex[3] = p.E1(); t.ex[4] = p.W(OAC_WS_HEAD1);
     t.ex[5] = c.auto_alpha ? &p.alpha()->alpha : nullptr;
     if (hd2) {   // the head-backward tiles, once per 64-column chunk of dh2
-      for (int c0 = 0; c0 < H; c0 += 64) {
+      const int tv = tuning(OAC_TUNE_HEAD_DH2);   // (a chunk width of 16 .. 128: A/B runs)
+      const int cw = (tv >= 16 && tv <= 128 && tv % 16 == 0) ? tv : 64;
+      for (int c0 = 0; c0 < H; c0 += cw) {
         GemmTask u = t;
         u.C2 = p.W(W_DH2P) + c0; u.ldc2 = H;
         u.aux = p.W(W_H2P) + c0; u.ld_aux = H;
         u.U = pol + L.pol_head_w + c0; u.ldu = H;
-        u.R = std::min(64, H - c0);
+        u.R = std::min(cw, H - c0);
         u.dup = c0 > 0;
         add(gb, u);
       }
