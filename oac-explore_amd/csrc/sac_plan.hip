@@ -599,7 +599,7 @@ static int phase2_adam(SacPlan& p, hipStream_t s, int dp) {
 static bool head_dh2(const SacPlan& p, const float* prefetch) {
   // (at large batch it measured slower: B=4096, the dL/da launch's 128 row
   // blocks x 4 chunks 8.4 -> 16.7 us, the merged launch 17.1 us against 7.3 +
-  // 14.4; 3,939 -> 3,888 steps/s, tools/r7/big.sh -- on by tuning value 2)
+  // 14.4; 3,939 -> 3,888 steps/s, tools/r6s2/big.sh -- on by tuning value 2)
   const int v = tuning(OAC_TUNE_HEAD_DH2);
   return (p.cfg == 0 || (p.cfg == kCfgLargeBatch && v == 2)) && v != -1 && !prefetch &&
          p.c.act_dim <= 24 && p.c.hidden <= 6 * 64 && (v < 16 || p.c.hidden <= 6 * v);

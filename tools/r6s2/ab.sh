@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of tuning specs on the B=256 per-launch times and drop-in rate:
-# tools/r7/ab.sh "spec1" "spec2" ... (empty string = default), two rounds.
+# tools/r6s2/ab.sh "spec1" "spec2" ... (empty string = default), two rounds.
 O=$PWD/gpurun_out/r7
 mkdir -p $O
 TAG=${TAG:-ab}
