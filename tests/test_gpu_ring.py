@@ -55,14 +55,18 @@ def test_ring_direct_rows_equal_the_gather_launch_path(prefetch):
     through the device index ring, side blocks copying the batch and drawing
     eps (the drop-in step's form) -- against the gather launch per 8 steps
     (tuning ring_direct=-1), with and without the next step's critic forward
-    inside the policy backward (ring_prefetch): bitwise equal states."""
+    inside the policy backward (ring_prefetch): bitwise equal states.  The
+    prefetch form keeps the policy-head dX in a launch of its own (its own
+    summation order), so its direct-rows counterpart is run that way too
+    (head_dh2=-1)."""
     from oac_amd import _lib
-    a = _run([16, 8, 4, 2, 1, 1])
     try:
+        _lib.set_tuning(head_dh2=-1 if prefetch else 0)
+        a = _run([16, 8, 4, 2, 1, 1])
         _lib.set_tuning(ring_direct=-1, ring_prefetch=prefetch)
         b = _run([16, 8, 4, 2, 1, 1])
     finally:
-        _lib.set_tuning(ring_direct=0, ring_prefetch=0)
+        _lib.set_tuning(ring_direct=0, ring_prefetch=0, head_dh2=0)
     assert np.isfinite(a).all()
     np.testing.assert_array_equal(a, b)
 
