@@ -13,6 +13,9 @@
 //   load per lane per 4 MFMAs; other layouts load one dword per lane per MFMA
 //   (coalesced across the 32 lanes of a half-wave).  The next group's loads
 //   are issued before the current group's MFMAs (register double buffer).
+// * The dL/da launch's head-backward tiles (EPI_HEAD_BWD with C2, the HD2
+//   instance) go on from their dhead rows to a 64-column chunk of the head's
+//   dX as v_mfma_f32_16x16x4_f32 tiles: one launch fewer in the step.
 #include "oac_common.h"
 #include "kernels.h"
 #include "adam_common.h"
@@ -286,10 +289,6 @@ __device__ __forceinline__ void fold_store(const GemmBatch& batch, const AdamCon
 
 constexpr int kGatherU = 4;   // float4s per lane of a side block's row copy (rows <= 1 KB)
 
-// FOLDK: the kernel that takes GemmTask::fold tasks (a variant of its own, so
-// the other launches keep the registers and schedule of the plain kernel:
-// with the fold in every kernel, launches without a fold task came out
-// 0.2-0.4 us slower)
 // one 16x16 tile of the head's dX over KS k-steps of 4: A from the dhead rows
 // in LDS (arow: the lane's row at its k-group; zeros past 2N), B the lane's
 // prefetched weights (k-step order, a fixed order per output)
@@ -304,6 +303,10 @@ __device__ __forceinline__ floatx4 hd_mfma(const float* arow, const float (&hb)[
   return c;
 }
 
+// FOLDK: the kernel that takes GemmTask::fold tasks (a variant of its own, so
+// the other launches keep the registers and schedule of the plain kernel:
+// with the fold in every kernel, launches without a fold task came out
+// 0.2-0.4 us slower)
 // HD2: the kernel that takes EPI_HEAD_BWD tasks with the head's dX chunk
 // (GemmTask::C2; its own instance, as FOLDK, so the other launches keep
 // their registers and schedule)
